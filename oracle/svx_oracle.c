@@ -1,0 +1,283 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY. NOT PART OF THE PRODUCT.
+ *
+ * Plain-C, scalar, fp64 restatement of the thien/stereo.vision hot path, used
+ * exclusively as the CHECKER by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg. The product path (stereo.vision_amd/svx + libsvx.so) never
+ * links, loads or calls this file.
+ *
+ * Parity: pinned against tests/golden/* — fixtures produced by running the
+ * reference's own Python functions (tests/golden/make_golden.py, container
+ * only) — and against the SURVEY.md §8c digests.
+ *
+ * Every function cites the reference line it restates (paths relative to the
+ * reference repo root). Build: oracle/Makefile → oracle/_build/libsvx_oracle.so
+ * with -O2 -ffp-contract=off so no operation is fused behind our back.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+typedef struct { double f, B, cw, ch; } svo_camera;
+
+/* ------------------------------------------------------------------------
+ * Synthetic frame generator. Counter based: the value of a
+ * pixel depends only on (frame id, y, x), so host and device agree.
+ * --------------------------------------------------------------------- */
+static inline uint64_t svo_mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static inline int64_t floordiv(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) q -= 1;
+    return q;
+}
+
+void svo_synth_frame(int64_t frame_id, int H, int W, uint8_t* disp, uint8_t* bgr) {
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W; ++x) {
+            uint64_t idx = ((uint64_t)frame_id * (uint64_t)H + (uint64_t)y) * (uint64_t)W + (uint64_t)x;
+            uint64_t r = svo_mix64(idx + 0x5EED000000000001ull);
+            uint64_t r2 = svo_mix64(idx + 0x5EED000000000002ull);
+            int64_t t = floordiv(3 * (int64_t)(y - 200), 5) + (int64_t)((r >> 8) & 7) - 3;
+            if (t < 0) t = 0;
+            if (t > 254) t = 254;
+            int d = (int)(t & ~1ll);
+            if ((r & 0xFF) < 38) d = 0;
+            disp[(size_t)y * W + x] = (uint8_t)d;
+            if (bgr) {
+                uint8_t* px = bgr + ((size_t)y * W + x) * 3;
+                if (y >= 262) {
+                    px[0] = (uint8_t)(110 + (r2 & 3));
+                    px[1] = (uint8_t)(100 + ((r2 >> 2) & 3));
+                    px[2] = (uint8_t)(90 + ((r2 >> 4) & 3));
+                } else {
+                    px[0] = (uint8_t)(r2 & 255);
+                    px[1] = (uint8_t)((r2 >> 8) & 255);
+                    px[2] = (uint8_t)((r2 >> 16) & 255);
+                }
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * a1: projectDisparityTo3d — functions.py:178-198.
+ * Grid: y in range(0, H-1, step), x in range(0, W-1, step) (:185-186; the
+ * reference hard-codes step 2). d == 0 skipped (:188). fp64:
+ *   Z = (f*B)/d ; X = ((x-cw)*Z)/f ; Y = ((y-ch)*Z)/f      (:191-193)
+ * rgb row = (bgr[..,2], bgr[..,1], bgr[..,0])             (:195)
+ * Returns N; xyz is N x 3, rgb (optional) N x 3, src (optional) N x 2 (y, x).
+ * --------------------------------------------------------------------- */
+int64_t svo_project(const uint8_t* disp, int H, int W, int64_t ld_disp,
+                    const uint8_t* bgr, int64_t ld_bgr, int step, const svo_camera* cam,
+                    double* xyz, uint8_t* rgb, int32_t* src) {
+    const double f = cam->f, B = cam->B;
+    const double fB = f * B;
+    int64_t n = 0;
+    for (int y = 0; y < H - 1; y += step) {
+        for (int x = 0; x < W - 1; x += step) {
+            const uint8_t d = disp[(int64_t)y * ld_disp + x];
+            if (d == 0) continue;
+            const double Z = fB / (double)d;
+            const double X = (((double)x - cam->cw) * Z) / f;
+            const double Y = (((double)y - cam->ch) * Z) / f;
+            xyz[3 * n + 0] = X;
+            xyz[3 * n + 1] = Y;
+            xyz[3 * n + 2] = Z;
+            if (rgb && bgr) {
+                const uint8_t* px = bgr + (int64_t)y * ld_bgr + 3 * (int64_t)x;
+                rgb[3 * n + 0] = px[2];
+                rgb[3 * n + 1] = px[1];
+                rgb[3 * n + 2] = px[0];
+            }
+            if (src) { src[2 * n] = y; src[2 * n + 1] = x; }
+            ++n;
+        }
+    }
+    return n;
+}
+
+/* Dense variant: every grid point, (0,0,0) where d == 0. Output planes are
+ * Hg x pitch (row-major); columns >= Wg are written as 0. Used to check the
+ * dense K1 output of the batched API. */
+void svo_project_dense(const uint8_t* disp, int H, int W, int step, const svo_camera* cam,
+                       int pitch, double* X, double* Y, double* Z) {
+    const double f = cam->f, fB = cam->f * cam->B;
+    const int Hg = (H - 1 + step - 1) / step, Wg = (W - 1 + step - 1) / step;
+    for (int gy = 0; gy < Hg; ++gy) {
+        for (int gx = 0; gx < pitch; ++gx) {
+            double vx = 0, vy = 0, vz = 0;
+            if (gx < Wg) {
+                const int y = gy * step, x = gx * step;
+                const uint8_t d = disp[(int64_t)y * W + x];
+                if (d) {
+                    vz = fB / (double)d;
+                    vx = (((double)x - cam->cw) * vz) / f;
+                    vy = (((double)y - cam->ch) * vz) / f;
+                }
+            }
+            X[(int64_t)gy * pitch + gx] = vx;
+            Y[(int64_t)gy * pitch + gx] = vy;
+            Z[(int64_t)gy * pitch + gx] = vz;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * a7: project3DPointsTo2DImagePoints — functions.py:201-209 (fp64):
+ *   x = ((X*f)/Z) + cw ; y = ((Y*f)/Z) + ch
+ * --------------------------------------------------------------------- */
+void svo_backproject(const double* xyz, int64_t n, int64_t ld, const svo_camera* cam, double* xy) {
+    for (int64_t i = 0; i < n; ++i) {
+        const double X = xyz[i * ld], Y = xyz[i * ld + 1], Z = xyz[i * ld + 2];
+        xy[2 * i] = ((X * cam->f) / Z) + cam->cw;
+        xy[2 * i + 1] = ((Y * cam->f) / Z) + cam->ch;
+    }
+}
+
+/* a8: np.array(planePoints, np.int32) — stereovision.py:112: C truncation. */
+static inline int32_t trunc_i32(double v) { return (int32_t)v; }
+
+/* ------------------------------------------------------------------------
+ * a2: calculatePointErrors — functions.py:300-312.
+ *   nrm = sqrt(a*a + b*b + c*c)         (:307, left-to-right)
+ *   dist = |(P . abc) - 1| / nrm         (:310)
+ * The dot goes through BLAS in the reference; the order below is the one
+ * OpenBLAS produces bit-for-bit (checked by tests against the golden dist
+ * values). Only the keep mask (a3) is a parity claim.
+ * --------------------------------------------------------------------- */
+static inline double plane_norm(const double* abc) {
+    return sqrt(abc[0] * abc[0] + abc[1] * abc[1] + abc[2] * abc[2]);
+}
+static inline double plane_dist(double X, double Y, double Z, const double* abc, double nrm) {
+    const double dot = fma(Z, abc[2], fma(X, abc[0], Y * abc[1]));
+    return fabs((dot - 1.0) / nrm);
+}
+void svo_point_errors(const double* xyz, int64_t n, int64_t ld, const double* abc, double* dist) {
+    const double nrm = plane_norm(abc);
+    for (int64_t i = 0; i < n; ++i)
+        dist[i] = plane_dist(xyz[i * ld], xyz[i * ld + 1], xyz[i * ld + 2], abc, nrm);
+}
+
+/* ------------------------------------------------------------------------
+ * a4: BGRtoHSVHue + colorsys.rgb_to_hsv — functions.py:73-78 (inputs are
+ * numpy uint8 scalars). Key str(round(h,3)) <-> integer bin rint(h*1000):
+ *   rc,gc,bc = (mx-c)/(mx-mn)   (fp64 true division of exact integers)
+ *   h = bc-gc | (2+rc)-bc | (4+gc)-rc   ; h = (h/6) mod 1 (numpy floor-mod)
+ *   bin = rint(h*1000) (numpy round = multiply, rint half-even, divide)
+ * Grey (mx == mn) returns hue 0.0 -> bin 0.
+ * --------------------------------------------------------------------- */
+int svo_hue_bin(int r, int g, int b) {
+    int mx = r, mn = r;
+    if (g > mx) mx = g;
+    if (b > mx) mx = b;
+    if (g < mn) mn = g;
+    if (b < mn) mn = b;
+    if (mx == mn) return 0;
+    const double rng = (double)(mx - mn);
+    const double rc = (double)(mx - r) / rng;
+    const double gc = (double)(mx - g) / rng;
+    const double bc = (double)(mx - b) / rng;
+    double h;
+    if (r == mx) h = bc - gc;
+    else if (g == mx) h = (2.0 + rc) - bc;
+    else h = (4.0 + gc) - rc;
+    h = h / 6.0;
+    double m = fmod(h, 1.0);
+    if (m != 0.0) {
+        if (m < 0.0) m += 1.0;
+    } else {
+        m = 0.0;
+    }
+    return (int)nearbyint(m * 1000.0);
+}
+
+/* Full 2^24 LUT, index R<<16 | G<<8 | B (SURVEY.md §8c digest). */
+void svo_hue_lut(int16_t* lut) {
+    for (int r = 0; r < 256; ++r)
+        for (int g = 0; g < 256; ++g)
+            for (int b = 0; b < 256; ++b)
+                lut[(r << 16) | (g << 8) | b] = (int16_t)svo_hue_bin(r, g, b);
+}
+
+/* ------------------------------------------------------------------------
+ * Back-projection delta tables: the int32 of the fp64 round trip
+ * x -> X -> x' depends only on (x, d) (resp. (y, d)), so
+ *   dx[d][x] = trunc(((X(x,d)*f)/Z(d)) + cw) - x     in {-1, 0}
+ * d = 0 column is 0. Layout [d][coord] (256 x W, 256 x H).
+ * --------------------------------------------------------------------- */
+void svo_delta_tables(int H, int W, const svo_camera* cam, int8_t* dx, int8_t* dy) {
+    const double f = cam->f, fB = cam->f * cam->B;
+    for (int d = 0; d < 256; ++d) {
+        const double Z = d ? fB / (double)d : 0.0;
+        for (int x = 0; x < W; ++x) {
+            int8_t v = 0;
+            if (d) {
+                const double X = (((double)x - cam->cw) * Z) / f;
+                v = (int8_t)(trunc_i32(((X * f) / Z) + cam->cw) - x);
+            }
+            dx[d * W + x] = v;
+        }
+        for (int y = 0; y < H; ++y) {
+            int8_t v = 0;
+            if (d) {
+                const double Y = (((double)y - cam->ch) * Z) / f;
+                v = (int8_t)(trunc_i32(((Y * f) / Z) + cam->ch) - y);
+            }
+            dy[d * H + y] = v;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * The whole per-frame chain (stereovision.py:84,97-113):
+ *   project (a1) -> errors (a2) -> keep dist < point_thr (a3, order kept)
+ *   -> hue histogram of kept (a5) -> keep hist[bin] > hist_thr (a6)
+ *   -> back-project (a7) -> int32 trunc (a8)
+ * Outputs (caller sized to the grid count):
+ *   counts[3]   = N_valid, N_kept, N_kept2
+ *   hist[1024]  = per-bin count over the plane-kept points (bins 0..999)
+ *   xyz2 (N_kept2 x 3, fp64), pts (N_kept2 x 2 int32), src2 (N_kept2 x 2: y,x)
+ * --------------------------------------------------------------------- */
+int svo_pipeline_frame(const uint8_t* disp, const uint8_t* bgr, int H, int W, int step,
+                       const svo_camera* cam, const double* abc, double point_thr, int hist_thr,
+                       int64_t* counts, uint32_t* hist, double* xyz2, int32_t* pts, int32_t* src2,
+                       double* scratch_xyz, uint8_t* scratch_rgb, int32_t* scratch_src,
+                       uint8_t* scratch_keep, int16_t* scratch_bin) {
+    const int64_t n = svo_project(disp, H, W, W, bgr, (int64_t)W * 3, step, cam,
+                                  scratch_xyz, scratch_rgb, scratch_src);
+    const double nrm = plane_norm(abc);
+    int64_t n1 = 0;
+    memset(hist, 0, 1024 * sizeof(uint32_t));
+    for (int64_t i = 0; i < n; ++i) {
+        const double dd = plane_dist(scratch_xyz[3 * i], scratch_xyz[3 * i + 1],
+                                     scratch_xyz[3 * i + 2], abc, nrm);
+        scratch_keep[i] = dd < point_thr;
+        if (scratch_keep[i]) {
+            const int bin = svo_hue_bin(scratch_rgb[3 * i], scratch_rgb[3 * i + 1], scratch_rgb[3 * i + 2]);
+            scratch_bin[i] = (int16_t)bin;
+            hist[bin] += 1;
+            ++n1;
+        }
+    }
+    int64_t n2 = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!scratch_keep[i]) continue;
+        if (!((int64_t)hist[scratch_bin[i]] > (int64_t)hist_thr)) continue;
+        const double X = scratch_xyz[3 * i], Y = scratch_xyz[3 * i + 1], Z = scratch_xyz[3 * i + 2];
+        if (xyz2) { xyz2[3 * n2] = X; xyz2[3 * n2 + 1] = Y; xyz2[3 * n2 + 2] = Z; }
+        pts[2 * n2] = trunc_i32(((X * cam->f) / Z) + cam->cw);
+        pts[2 * n2 + 1] = trunc_i32(((Y * cam->f) / Z) + cam->ch);
+        if (src2) { src2[2 * n2] = scratch_src[2 * i]; src2[2 * n2 + 1] = scratch_src[2 * i + 1]; }
+        ++n2;
+    }
+    counts[0] = n;
+    counts[1] = n1;
+    counts[2] = n2;
+    return 0;
+}
