@@ -1,0 +1,148 @@
+/*
+ * svx — MI355X-native disparity -> 3D point-cloud hot path (C ABI).
+ *
+ * Drop-in boundary for thien/stereo.vision. The reference has no native/FFI
+ * API: its boundary is the Python module `functions`, whose attributes
+ * stereovision.py resolves at call time (stereovision.py:3, :84-113). The
+ * Python binding (stereo.vision_amd/svx/_abi.py, ctypes) binds exactly these
+ * symbols and re-exposes the reference's signatures (svx/dropin.py).
+ *
+ * Conventions
+ *   - every entry point returns 0 on success, a negative SV_E* code on error;
+ *     sv_last_error() gives a thread-local message. The Python wrapper raises
+ *     RuntimeError(message), which lands in the reference's own try/except
+ *     (stereovision.py:92-126) exactly like a reference exception would.
+ *   - host buffers are allocated by the caller; device buffers are owned by
+ *     the library (sv_batch) and stay resident in HBM.
+ *   - the "host" entry points (sv_project_frame, sv_backproject,
+ *     sv_pipeline_frame) are synchronous: they return after the D2H copy.
+ *   - plain pointers and sizes only; no torch / no C++ types.
+ */
+#ifndef SVX_H
+#define SVX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SV_OK 0
+#define SV_E_ARG -1     /* bad argument / unsupported shape                */
+#define SV_E_HIP -2     /* HIP runtime error                               */
+#define SV_E_CAP -3     /* caller's output capacity too small              */
+#define SV_E_STATE -4   /* not initialised / wrong object                  */
+#define SV_E_COMM -5    /* RCCL error                                      */
+#define SV_E_DEVICE -6  /* a kernel reported an internal failure (timeout) */
+
+/* functions.py:15,19,21,22 — focal length (px), baseline (m), image centre. */
+typedef struct { double f, B, cw, ch; } sv_camera;
+/* Plane a*X + b*Y + c*Z = 1 (functions.py:267, consumed at :300-312). */
+typedef struct { double a, b, c; } sv_plane;
+
+/* ---- library / device ------------------------------------------------- */
+const char* sv_version(void);
+const char* sv_last_error(void);
+int sv_device_count(int* n);
+int sv_init(int device);                 /* select + warm the device          */
+
+/* ---- drop-in (host buffers, synchronous) -------------------------------- */
+
+/* Replaces functions.py:178-198 projectDisparityTo3d(disparity, max_disparity,
+ * rgb=[]). Grid y in range(0,H-1,step) x range(0,W-1,step), raster order,
+ * d == 0 skipped, fp64 X,Y,Z bit-identical to the reference arithmetic.
+ * bgr may be NULL (the `rgb=[]` case, stereovision.py:85); out_rgb receives
+ * (R,G,B) = bgr[...,2], bgr[...,1], bgr[...,0] (functions.py:195).
+ * cap = rows available in out_xyz/out_rgb; *out_n = rows written. */
+int sv_project_frame(const uint8_t* disp, int H, int W, int64_t ld_disp,
+                     const uint8_t* bgr, int64_t ld_bgr, int step, const sv_camera* cam,
+                     double* out_xyz, uint8_t* out_rgb, int64_t cap, int64_t* out_n);
+
+/* Replaces functions.py:201-209 project3DPointsTo2DImagePoints(points):
+ * x = ((X*f)/Z)+cw, y = ((Y*f)/Z)+ch in fp64, bit-identical. xyz rows have
+ * stride ld (>= 3) doubles; out_xy is n x 2. */
+int sv_backproject(const double* xyz, int64_t n, int64_t ld, const sv_camera* cam, double* out_xy);
+
+/* Fused chain of stereovision.py:84,97-113 for one host frame: projection ->
+ * calculatePointErrors (functions.py:300-312) -> computePlanarThreshold
+ * (:314-323) -> calculateColourHistogram (:215-226) -> filterPointsByHistogram
+ * (:228-230) -> back-projection + int32 trunc (stereovision.py:111-113).
+ * out_counts[3] = N_valid, N_kept, N_kept2; out_hist[1024] = hue-bin counts of
+ * the plane-kept points (bin k <-> key str(k/1000)); out_xyz (cap x 3, fp32,
+ * NULL ok) and out_pts (cap x 2 int32) hold the N_kept2 surviving points in
+ * reference order. Requires W % 8 == 0. */
+int sv_pipeline_frame(const uint8_t* disp, const uint8_t* bgr, int H, int W, int step,
+                      const sv_camera* cam, const sv_plane* plane, double point_thr, int hist_thr,
+                      int64_t* out_counts, uint32_t* out_hist, float* out_xyz, int32_t* out_pts,
+                      int64_t cap);
+
+/* ---- batched, device-resident API ------------- */
+typedef struct sv_batch sv_batch;
+
+/* frames x H x W uint8 disparity (+ frames x H x W x 3 BGR if with_bgr) in
+ * HBM. W % 8 == 0. Dense outputs: 3 fp32 planes (X, Y, Z) of
+ * frames x Hg x pitch, pitch = round_up(Wg, 4); Z == 0 marks d == 0 / pad. */
+int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr,
+                    int with_points, sv_batch** out);
+int sv_batch_destroy(sv_batch* b);
+int sv_batch_info(const sv_batch* b, int64_t* out8); /* Hg, Wg, pitch, Ng, bytes, frames, H, W */
+/* K1 launch shape: grid_cap = max workgroups (0 = one quad per lane, no
+ * grid-stride), nontemporal = 1 for non-temporal (streaming) stores. */
+int sv_batch_tune(sv_batch* b, int grid_cap, int nontemporal);
+
+/* Counter-based synthetic frames for global frame ids first..first+frames-1
+ * (SURVEY §8d), generated on the device: inputs never cross PCIe. */
+int sv_batch_synth(sv_batch* b, int64_t first_frame_id);
+/* Upload one host frame (tests / real data). bgr may be NULL. */
+int sv_batch_upload(sv_batch* b, int frame, const uint8_t* disp, const uint8_t* bgr);
+
+/* K1: dense projection of every frame (configs 2/3). Asynchronous on the
+ * batch stream unless sync != 0. */
+int sv_batch_project(sv_batch* b, const sv_camera* cam, int sync);
+
+/* K2+K3: plane threshold + hue histogram + stable compaction + int32
+ * back-projection for every frame (config 4). chunk = frames per
+ * histogram/compaction wave (0 = library default). */
+int sv_batch_pipeline(sv_batch* b, const sv_camera* cam, const sv_plane* plane,
+                      double point_thr, int hist_thr, int chunk, int sync);
+
+int sv_batch_sync(sv_batch* b);
+/* ms of the last sv_batch_project / sv_batch_pipeline, from HIP events
+ * recorded on the batch stream around the kernels. which: 0 = project,
+ * 1 = pipeline. */
+int sv_batch_last_ms(sv_batch* b, int which, float* ms);
+/* Sum of the per-launch durations (HIP events on the batch stream around each
+ * K1 launch / each pipeline call) since the last reset, and their count.
+ * Synchronises the batch stream. */
+int sv_batch_timing(sv_batch* b, int which, double* total_ms, int64_t* count);
+int sv_batch_timing_reset(sv_batch* b);
+
+/* Read back. */
+int sv_batch_read_dense(sv_batch* b, int frame, float* X, float* Y, float* Z);
+int sv_batch_read_counts(sv_batch* b, int64_t* counts /* frames x 3 */);
+int sv_batch_read_hist(sv_batch* b, int frame, uint32_t* hist /* 1024 */);
+int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64_t cap, int64_t* n);
+
+/* ---- verification helpers (device computes, host compares) -------------- */
+/* Hue bin of all 2^24 colours, index R<<16|G<<8|B (for exhaustive tests). */
+int sv_hue_lut(int device, int16_t* out_lut);
+/* Back-projection delta tables as computed on the device: dx[d][x], dy[d][y]. */
+int sv_delta_tables(int device, int H, int W, const sv_camera* cam, int8_t* dx, int8_t* dy);
+/* Regenerate one synthetic frame on the device and copy it back. */
+int sv_synth_frame(int device, int64_t frame_id, int H, int W, uint8_t* disp, uint8_t* bgr);
+
+/* ---- multi-GPU: RCCL over xGMI ----------------------------- */
+typedef struct sv_comm sv_comm;
+#define SV_UNIQUE_ID_BYTES 128
+int sv_comm_unique_id(uint8_t* out_id /* SV_UNIQUE_ID_BYTES */);
+int sv_comm_init(int nranks, int rank, const uint8_t* id, int device, sv_comm** out);
+int sv_comm_destroy(sv_comm* c);
+/* Broadcast the plane coefficients from root over RCCL (device buffer). */
+int sv_comm_broadcast_plane(sv_comm* c, sv_plane* inout, int root);
+/* Sum int64 counters over ranks (reporting only). */
+int sv_comm_allreduce_i64(sv_comm* c, int64_t* inout, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVX_H */

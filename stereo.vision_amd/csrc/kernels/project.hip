@@ -1,0 +1,296 @@
+// Projection kernels (gfx950).
+//
+//  * synth_kernel            — counter-based synthetic frames, on device
+//  * project_dense_kernel    — K1: every grid pixel -> fp32 X,Y,Z planes (configs 2/3)
+//  * project_compact_f64     — drop-in projectDisparityTo3d (functions.py:178-198):
+//                              fp64, raster-ordered compaction of the d>0 pixels
+//  * backproject_f64_kernel  — drop-in project3DPointsTo2DImagePoints (functions.py:201-209)
+//
+// K1 is a pure HBM stream: 1 B of disparity in, 12 B of fp32 XYZ out per grid
+// point. One lane owns one "quad" (4 consecutive grid points of a row): a
+// 4-byte (step 1) or 8-byte (step 2) disparity load and three 16-byte stores,
+// one per plane, so every wave-instruction writes 1 KiB contiguous.
+#include "../svx_launch.h"
+
+namespace svx {
+
+// ---------------------------------------------------------------------------
+// Synthetic frames: one lane per 4 pixels (dword of disparity, 3 dwords BGR).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_kernel(uint8_t* __restrict__ disp, uint8_t* __restrict__ bgr,
+                                                    int H, int W, int frames, int64_t first_frame) {
+    const int64_t quads = (int64_t)frames * H * (W / 4);
+    for (int64_t g = blockIdx.x * 256ll + threadIdx.x; g < quads; g += (int64_t)gridDim.x * 256) {
+        const int64_t px0 = g * 4;
+        const int64_t fl = px0 / ((int64_t)H * W);
+        const int64_t rem = px0 - fl * H * W;
+        const int y = (int)(rem / W);
+        const int x0 = (int)(rem - (int64_t)y * W);
+        uint32_t dw = 0;
+        uint32_t c[3] = {0, 0, 0};
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t idx = ((uint64_t)(first_frame + fl) * H + y) * W + (x0 + k);
+            const uint64_t r = mix64(idx + 0x5EED000000000001ull);
+            const uint64_t r2 = mix64(idx + 0x5EED000000000002ull);
+            // floor((3*(y-200))/5) with Python floor semantics
+            const int num = 3 * (y - 200);
+            int t = (num >= 0) ? num / 5 : -((-num + 4) / 5);
+            t += (int)((r >> 8) & 7) - 3;
+            t = t < 0 ? 0 : (t > 254 ? 254 : t);
+            uint32_t d = (uint32_t)(t & ~1);
+            if ((r & 0xFF) < 38) d = 0;
+            dw |= d << (8 * k);
+            uint32_t B, G, R;
+            if (y >= 262) {
+                B = 110 + (uint32_t)(r2 & 3);
+                G = 100 + (uint32_t)((r2 >> 2) & 3);
+                R = 90 + (uint32_t)((r2 >> 4) & 3);
+            } else {
+                B = (uint32_t)(r2 & 255);
+                G = (uint32_t)((r2 >> 8) & 255);
+                R = (uint32_t)((r2 >> 16) & 255);
+            }
+            const int o = 3 * k;
+            c[(o + 0) >> 2] |= B << (8 * ((o + 0) & 3));
+            c[(o + 1) >> 2] |= G << (8 * ((o + 1) & 3));
+            c[(o + 2) >> 2] |= R << (8 * ((o + 2) & 3));
+        }
+        reinterpret_cast<uint32_t*>(disp)[g] = dw;
+        if (bgr) {
+            uint32_t* cb = reinterpret_cast<uint32_t*>(bgr) + 3 * g;
+            cb[0] = c[0];
+            cb[1] = c[1];
+            cb[2] = c[2];
+        }
+    }
+}
+
+hipError_t launch_synth(const KParams& p, uint8_t* disp, uint8_t* bgr, int frames,
+                        int64_t first_frame, hipStream_t s) {
+    const int64_t quads = (int64_t)frames * p.H * (p.W / 4);
+    int64_t blocks = (quads + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, s, disp, bgr, p.H, p.W,
+                       frames, first_frame);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K1: dense projection. Z = fB/d, X = (x-cw)*B/d, Y = (y-ch)*B/d in fp32
+// (B/d = Z/f; rcp has <= 1 ulp error: |rel err| < 2^-21 vs the fp64 reference,
+// far inside the 1e-5 contract). d == 0 and pad columns (gx >= Wg) -> 0.
+// ---------------------------------------------------------------------------
+template <int STEP>
+__device__ __forceinline__ void load_disp_quad(const uint8_t* row, int q, uint32_t (&d)[4]) {
+    if constexpr (STEP == 1) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(row + 4 * q);
+        d[0] = w & 0xFF; d[1] = (w >> 8) & 0xFF; d[2] = (w >> 16) & 0xFF; d[3] = w >> 24;
+    } else {
+        const uint2 w = *reinterpret_cast<const uint2*>(row + 8 * q);
+        d[0] = w.x & 0xFF; d[1] = (w.x >> 16) & 0xFF; d[2] = w.y & 0xFF; d[3] = (w.y >> 16) & 0xFF;
+    }
+}
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ void store4(float* p, float a, float b, float c, float d) {
+    const v4f v = {a, b, c, d};
+    if constexpr (NT) {
+        __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
+    } else {
+        *reinterpret_cast<v4f*>(p) = v;
+    }
+}
+
+template <int STEP, bool NT>
+__global__ __launch_bounds__(256) void project_dense_kernel(const uint8_t* __restrict__ disp,
+                                                            float* __restrict__ X, float* __restrict__ Y,
+                                                            float* __restrict__ Z, uint32_t total_quads,
+                                                            KParams p) {
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < total_quads; g += stride) {
+        const uint32_t row = g / (uint32_t)p.Q;
+        const int q = (int)(g - row * (uint32_t)p.Q);
+        const uint32_t fl = row / (uint32_t)p.Hg;
+        const int gy = (int)(row - fl * (uint32_t)p.Hg);
+        const int y = gy * STEP;
+        const uint8_t* drow = disp + (int64_t)fl * p.frame_px + (int64_t)y * p.W;
+        uint32_t d[4];
+        load_disp_quad<STEP>(drow, q, d);
+        const float yc = (float)((double)y - p.ch);
+        float ox[4], oy[4], oz[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int gx = 4 * q + k;
+            const float xc = (float)((double)(gx * STEP) - p.cw);
+            const float r = __builtin_amdgcn_rcpf((float)d[k]);
+            const float K = p.B32 * r;
+            const bool ok = (d[k] != 0) && (gx < p.Wg);
+            ox[k] = ok ? xc * K : 0.0f;
+            oy[k] = ok ? yc * K : 0.0f;
+            oz[k] = ok ? p.fB32 * r : 0.0f;
+        }
+        const size_t o = (size_t)g * 4;
+        store4<NT>(X + o, ox[0], ox[1], ox[2], ox[3]);
+        store4<NT>(Y + o, oy[0], oy[1], oy[2], oy[3]);
+        store4<NT>(Z + o, oz[0], oz[1], oz[2], oz[3]);
+    }
+}
+
+hipError_t launch_project_dense(const KParams& p, const uint8_t* disp, float* X, float* Y, float* Z,
+                                int frames, int grid_cap, int nontemporal, hipStream_t s) {
+    const uint64_t total = (uint64_t)frames * (uint64_t)p.frame_quads;
+    if (total >= (1ull << 32)) return hipErrorInvalidValue;
+    uint64_t blocks = (total + 255) / 256;
+    if (grid_cap > 0 && blocks > (uint64_t)grid_cap) blocks = grid_cap;
+    const dim3 grid((unsigned)blocks), block(256);
+    const uint32_t t = (uint32_t)total;
+    if (p.step == 1) {
+        if (nontemporal)
+            hipLaunchKernelGGL((project_dense_kernel<1, true>), grid, block, 0, s, disp, X, Y, Z, t, p);
+        else
+            hipLaunchKernelGGL((project_dense_kernel<1, false>), grid, block, 0, s, disp, X, Y, Z, t, p);
+    } else if (p.step == 2) {
+        if (nontemporal)
+            hipLaunchKernelGGL((project_dense_kernel<2, true>), grid, block, 0, s, disp, X, Y, Z, t, p);
+        else
+            hipLaunchKernelGGL((project_dense_kernel<2, false>), grid, block, 0, s, disp, X, Y, Z, t, p);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Drop-in projection (functions.py:178-198): fp64, bit-identical arithmetic,
+// raster-ordered compaction of d > 0 across workgroups (decoupled look-back).
+// Tile = 1024 consecutive grid points (256 lanes x 4). Any H, W, step.
+// ---------------------------------------------------------------------------
+constexpr int kCompactTile = 1024;
+
+int project_compact_tiles(const KParams& p) {
+    const int64_t ng = (int64_t)p.Hg * p.Wg;
+    return (int)((ng + kCompactTile - 1) / kCompactTile);
+}
+
+__global__ __launch_bounds__(256) void project_compact_f64_kernel(
+    const uint8_t* __restrict__ disp, int64_t ld_disp, const uint8_t* __restrict__ bgr, int64_t ld_bgr,
+    double* __restrict__ xyz, uint8_t* __restrict__ rgb, uint64_t* status, uint32_t* ticket,
+    uint32_t* count, uint32_t* err, int tiles, KParams p) {
+    __shared__ uint32_t sh_tile, sh_excl;
+    __shared__ uint32_t sh_wave[4];
+    const int tid = threadIdx.x;
+    if (tid == 0) sh_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int tile = (int)sh_tile;
+    const int64_t ng = (int64_t)p.Hg * p.Wg;
+    const int64_t i0 = (int64_t)tile * kCompactTile + 4 * tid;
+    uint32_t dv[4];
+    int gyv[4], gxv[4];
+    uint32_t mask = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = i0 + k;
+        dv[k] = 0;
+        gyv[k] = gxv[k] = 0;
+        if (i < ng) {
+            const int gy = (int)(i / p.Wg);
+            const int gx = (int)(i - (int64_t)gy * p.Wg);
+            gyv[k] = gy;
+            gxv[k] = gx;
+            dv[k] = disp[(int64_t)gy * p.step * ld_disp + (int64_t)gx * p.step];
+            if (dv[k]) mask |= 1u << k;
+        }
+    }
+    const uint32_t cnt = __builtin_popcount(mask);
+    const uint32_t inc = wave_incl_scan(cnt);
+    const int wave = tid >> 6;
+    if (lane_id() == 63) sh_wave[wave] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t t = sh_wave[w];
+        wbase += (w < wave) ? t : 0u;
+        total += t;
+    }
+    if (wave == 0) {
+        uint32_t excl = 0;
+        if (tile == 0) {
+            if (tid == 0) publish(status, kFlagInc, total);
+        } else {
+            if (tid == 0) publish(status + tile, kFlagAgg, total);
+            excl = lookback(status, tile, err);
+            if (tid == 0) publish(status + tile, kFlagInc, excl + total);
+        }
+        if (tid == 0) {
+            sh_excl = excl;
+            if (tile == tiles - 1) *count = excl + total;
+        }
+    }
+    __syncthreads();
+    uint32_t o = sh_excl + wbase + inc - cnt;
+    const double fB = p.fB;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (!(mask & (1u << k))) continue;
+        const int y = gyv[k] * p.step, x = gxv[k] * p.step;
+        const double Zv = fB / (double)dv[k];
+        const double Xv = (((double)x - p.cw) * Zv) / p.f;
+        const double Yv = (((double)y - p.ch) * Zv) / p.f;
+        xyz[3 * (size_t)o + 0] = Xv;
+        xyz[3 * (size_t)o + 1] = Yv;
+        xyz[3 * (size_t)o + 2] = Zv;
+        if (rgb) {
+            const uint8_t* px = bgr + (int64_t)y * ld_bgr + 3 * (int64_t)x;
+            rgb[3 * (size_t)o + 0] = px[2];
+            rgb[3 * (size_t)o + 1] = px[1];
+            rgb[3 * (size_t)o + 2] = px[0];
+        }
+        ++o;
+    }
+}
+
+hipError_t launch_project_compact_f64(const KParams& p, const uint8_t* disp, int64_t ld_disp,
+                                      const uint8_t* bgr, int64_t ld_bgr, double* xyz, uint8_t* rgb,
+                                      uint64_t* status, uint32_t* ticket, uint32_t* count,
+                                      uint32_t* err, hipStream_t s) {
+    const int tiles = project_compact_tiles(p);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(project_compact_f64_kernel, dim3(tiles), dim3(256), 0, s, disp, ld_disp, bgr,
+                       ld_bgr, xyz, rgb, status, ticket, count, err, tiles, p);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Drop-in back-projection (functions.py:201-209), fp64, bit-identical.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void backproject_f64_kernel(const double* __restrict__ xyz, int64_t n,
+                                                              int64_t ld, double f, double cw, double ch,
+                                                              double* __restrict__ xy) {
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const double X = xyz[i * ld], Y = xyz[i * ld + 1], Z = xyz[i * ld + 2];
+        xy[2 * i] = ((X * f) / Z) + cw;
+        xy[2 * i + 1] = ((Y * f) / Z) + ch;
+    }
+}
+
+hipError_t launch_backproject_f64(const double* xyz, int64_t n, int64_t ld, double f, double cw,
+                                  double ch, double* xy, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(backproject_f64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, xyz, n, ld, f,
+                       cw, ch, xy);
+    return hipGetLastError();
+}
+
+}  // namespace svx

@@ -1,0 +1,671 @@
+// svx runtime: device/stream management, buffers, tables and the C ABI
+// declared in include/svx.h. Host-side C++ compiled by hipcc; every compute
+// step is a hand-written gfx950 kernel (kernels/*.hip). There is no CPU
+// compute path: if a kernel cannot run, the call fails with an error.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/svx.h"
+#include "svx_launch.h"
+
+using namespace svx;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(SV_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                              \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// per-device state
+// ---------------------------------------------------------------------------
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t want = n < 4096 ? 4096 : n + n / 4;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct Tables {
+    bool valid = false;
+    int H = 0, W = 0;
+    sv_camera cam{};
+    DevBuf dx, dy;
+};
+
+struct Device {
+    bool init = false;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    // drop-in scratch
+    DevBuf disp, bgr, xyz, rgb, ctrl, xy;
+    Tables tables;
+    sv_batch* frame_batch = nullptr;  // cached 1-frame batch for sv_pipeline_frame
+};
+
+constexpr int kMaxDev = 64;
+Device g_dev[kMaxDev];
+std::mutex g_init_mu;
+
+bool same_cam(const sv_camera& a, const sv_camera& b) {
+    return a.f == b.f && a.B == b.B && a.cw == b.cw && a.ch == b.ch;
+}
+
+int grid_len(int n, int step) { return n > 1 ? (n - 1 + step - 1) / step : 0; }
+
+KParams make_params(int H, int W, int step, const sv_camera& cam) {
+    KParams p;
+    std::memset(&p, 0, sizeof p);
+    p.H = H;
+    p.W = W;
+    p.step = step;
+    p.Hg = grid_len(H, step);
+    p.Wg = grid_len(W, step);
+    p.pitch = (p.Wg + 3) / 4 * 4;
+    p.Q = p.pitch / 4;
+    p.frame_quads = p.Hg * p.Q;
+    p.frame_px = (int64_t)H * W;
+    p.f = cam.f;
+    p.B = cam.B;
+    p.cw = cam.cw;
+    p.ch = cam.ch;
+    p.fB = cam.f * cam.B;  // functions.py:191 evaluates f*B in fp64
+    p.fB32 = (float)p.fB;
+    p.B32 = (float)cam.B;
+    p.dx_words = (W + 31) / 32;
+    p.dy_words = (H + 31) / 32;
+    return p;
+}
+
+void set_plane(KParams& p, const sv_plane& pl, double thr, int hist_thr) {
+    p.a = pl.a;
+    p.b = pl.b;
+    p.c = pl.c;
+    p.nrm = std::sqrt(pl.a * pl.a + pl.b * pl.b + pl.c * pl.c);  // functions.py:307
+    p.thr = thr;
+    p.a32 = (float)pl.a;
+    p.b32 = (float)pl.b;
+    p.c32 = (float)pl.c;
+    p.thr32 = (float)thr;
+    p.inv_nrm32 = (float)(1.0 / p.nrm);
+    p.guard32 = (float)(std::ldexp(1.0, -18) / p.nrm);
+    if (!std::isfinite(p.guard32)) p.guard32 = INFINITY;  // degenerate plane: always exact path
+    p.abs_a32 = (float)std::fabs(pl.a);
+    p.abs_b32 = (float)std::fabs(pl.b);
+    p.abs_cf32 = (float)(std::fabs(pl.c) * p.f);
+    p.hist_thr = hist_thr;
+}
+
+int dev_get(int device, Device** out) {
+    if (device < 0 || device >= kMaxDev) return fail(SV_E_ARG, "device %d out of range", device);
+    Device& d = g_dev[device];
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    if (!d.init) {
+        int n = 0;
+        HIP_TRY(hipGetDeviceCount(&n));
+        if (device >= n) return fail(SV_E_ARG, "device %d not present (%d visible)", device, n);
+        HIP_TRY(hipSetDevice(device));
+        HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+        d.init = true;
+    }
+    HIP_TRY(hipSetDevice(device));
+    *out = &d;
+    return SV_OK;
+}
+
+int current_device(int* dev) {
+    HIP_TRY(hipGetDevice(dev));
+    return SV_OK;
+}
+
+// Delta tables for (H, W, camera), built on the device in fp64 (tables.hip).
+int ensure_tables(Device& d, int H, int W, const sv_camera& cam, hipStream_t s) {
+    Tables& t = d.tables;
+    if (t.valid && t.H == H && t.W == W && same_cam(t.cam, cam)) return SV_OK;
+    KParams p = make_params(H, W, 1, cam);
+    HIP_TRY(t.dx.ensure(sizeof(uint32_t) * 256 * p.dx_words));
+    HIP_TRY(t.dy.ensure(sizeof(uint32_t) * 256 * p.dy_words));
+    HIP_TRY(launch_delta_tables(p, t.dx.as<uint32_t>(), t.dy.as<uint32_t>(), nullptr, nullptr, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    t.valid = true;
+    t.H = H;
+    t.W = W;
+    t.cam = cam;
+    return SV_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// batch object
+// ---------------------------------------------------------------------------
+struct sv_batch {
+    int device = 0;
+    int frames = 0, H = 0, W = 0, step = 1;
+    bool with_bgr = false;
+    KParams kp{};
+    int64_t Ng = 0;            // grid points per frame
+    int64_t dense_per_frame = 0;
+    hipStream_t stream = nullptr;
+    DevBuf disp, bgr, X, Y, Z, xyz, pts, hist, counts, status, ctrl;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float last_ms[2] = {0, 0};
+    bool have_ms[2] = {false, false};
+    int grid_cap = 0;          // K1 grid size cap (0 = one quad per lane)
+    int nontemporal = 0;       // K1 store flavour
+    // per-launch timing accumulator: event pairs recorded on the batch stream
+    std::vector<hipEvent_t> pool;
+    std::vector<std::pair<int, int>> pending[2];  // (start idx, end idx) per op kind
+    size_t pool_next = 0;
+    hipError_t timed_event(int* idx) {
+        if (pool_next == pool.size()) {
+            hipEvent_t e;
+            hipError_t r = hipEventCreate(&e);
+            if (r != hipSuccess) return r;
+            pool.push_back(e);
+        }
+        *idx = (int)pool_next++;
+        return hipEventRecord(pool[*idx], stream);
+    }
+};
+
+extern "C" {
+
+const char* sv_version(void) { return "svx 0.1.0 (gfx950)"; }
+
+const char* sv_last_error(void) { return g_err.c_str(); }
+
+// internal: lets comm.hip report into the same thread-local error slot
+int sv_comm_set_error(const char* msg) {
+    g_err = msg ? msg : "";
+    return 0;
+}
+
+int sv_device_count(int* n) {
+    if (!n) return fail(SV_E_ARG, "null out");
+    hipError_t e = hipGetDeviceCount(n);
+    if (e != hipSuccess) {
+        *n = 0;
+        return fail(SV_E_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    return SV_OK;
+}
+
+int sv_init(int device) {
+    Device* d;
+    return dev_get(device, &d);
+}
+
+// ---------------------------------------------------------------------------
+// drop-in: projectDisparityTo3d (functions.py:178-198)
+// ---------------------------------------------------------------------------
+int sv_project_frame(const uint8_t* disp, int H, int W, int64_t ld_disp, const uint8_t* bgr,
+                     int64_t ld_bgr, int step, const sv_camera* cam, double* out_xyz, uint8_t* out_rgb,
+                     int64_t cap, int64_t* out_n) {
+    if (!disp || !cam || !out_n || H < 0 || W < 0 || step < 1 || ld_disp < W)
+        return fail(SV_E_ARG, "sv_project_frame: bad arguments (H=%d W=%d step=%d)", H, W, step);
+    if (bgr && ld_bgr < 3ll * W) return fail(SV_E_ARG, "sv_project_frame: ld_bgr < 3*W");
+    *out_n = 0;
+    const KParams p = make_params(H, W, step, *cam);
+    if ((int64_t)p.Hg * p.Wg == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    const int tiles = project_compact_tiles(p);
+    const int64_t ng = (int64_t)p.Hg * p.Wg;
+    HIP_TRY(d->disp.ensure((size_t)H * W));
+    HIP_TRY(d->xyz.ensure(sizeof(double) * 3 * ng));
+    HIP_TRY(d->ctrl.ensure(sizeof(uint64_t) * (tiles + 2)));
+    HIP_TRY(hipMemcpy2DAsync(d->disp.p, W, disp, ld_disp, W, H, hipMemcpyHostToDevice, s));
+    const bool want_rgb = bgr && out_rgb;
+    if (want_rgb) {
+        HIP_TRY(d->bgr.ensure((size_t)H * W * 3));
+        HIP_TRY(d->rgb.ensure(3 * ng));
+        HIP_TRY(hipMemcpy2DAsync(d->bgr.p, 3 * (size_t)W, bgr, ld_bgr, 3 * (size_t)W, H,
+                                 hipMemcpyHostToDevice, s));
+    }
+    uint64_t* status = d->ctrl.as<uint64_t>();
+    uint32_t* small = reinterpret_cast<uint32_t*>(status + tiles);  // ticket, count, err
+    HIP_TRY(hipMemsetAsync(d->ctrl.p, 0, sizeof(uint64_t) * (tiles + 2), s));
+    HIP_TRY(launch_project_compact_f64(p, d->disp.as<uint8_t>(), W, want_rgb ? d->bgr.as<uint8_t>() : nullptr,
+                                       3ll * W, d->xyz.as<double>(), want_rgb ? d->rgb.as<uint8_t>() : nullptr,
+                                       status, small, small + 1, small + 2, s));
+    uint32_t hs[3];
+    HIP_TRY(hipMemcpyAsync(hs, small, sizeof hs, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (hs[2]) return fail(SV_E_DEVICE, "projection look-back timed out");
+    const int64_t n = hs[1];
+    if (n > cap) return fail(SV_E_CAP, "output capacity %lld < %lld points", (long long)cap, (long long)n);
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(out_xyz, d->xyz.p, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, s));
+        if (want_rgb) HIP_TRY(hipMemcpyAsync(out_rgb, d->rgb.p, 3 * n, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    *out_n = n;
+    return SV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// drop-in: project3DPointsTo2DImagePoints (functions.py:201-209)
+// ---------------------------------------------------------------------------
+int sv_backproject(const double* xyz, int64_t n, int64_t ld, const sv_camera* cam, double* out_xy) {
+    if (n < 0 || ld < 3 || !cam || (n > 0 && (!xyz || !out_xy)))
+        return fail(SV_E_ARG, "sv_backproject: bad arguments");
+    if (n == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    HIP_TRY(d->xyz.ensure(sizeof(double) * ld * n));
+    HIP_TRY(d->xy.ensure(sizeof(double) * 2 * n));
+    HIP_TRY(hipMemcpyAsync(d->xyz.p, xyz, sizeof(double) * ld * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_backproject_f64(d->xyz.as<double>(), n, ld, cam->f, cam->cw, cam->ch, d->xy.as<double>(), s));
+    HIP_TRY(hipMemcpyAsync(out_xy, d->xy.p, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// batch API
+// ---------------------------------------------------------------------------
+int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr, int with_points,
+                    sv_batch** out) {
+    if (!out) return fail(SV_E_ARG, "null out");
+    *out = nullptr;
+    if (frames < 1 || H < 2 || W < 8 || (W % 8) != 0 || (step != 1 && step != 2))
+        return fail(SV_E_ARG, "sv_batch_create: need frames>=1, H>=2, W%%8==0, step in {1,2} "
+                              "(frames=%d H=%d W=%d step=%d)", frames, H, W, step);
+    Device* d;
+    if (int rc = dev_get(device, &d)) return rc;
+    sv_batch* b = new sv_batch;
+    b->device = device;
+    b->frames = frames;
+    b->H = H;
+    b->W = W;
+    b->step = step;
+    b->with_bgr = with_bgr != 0;
+    sv_camera cam0{1, 1, 0, 0};
+    b->kp = make_params(H, W, step, cam0);
+    b->Ng = (int64_t)b->kp.Hg * b->kp.Wg;
+    b->dense_per_frame = (int64_t)b->kp.Hg * b->kp.pitch;
+    b->stream = d->stream;
+    const size_t px = (size_t)frames * H * W;
+    hipError_t e = b->disp.ensure(px);
+    if (e == hipSuccess && b->with_bgr) e = b->bgr.ensure(px * 3);
+    if (e == hipSuccess && with_points) {
+        e = b->xyz.ensure(sizeof(float) * 3 * (size_t)b->Ng * frames);
+        if (e == hipSuccess) e = b->pts.ensure(sizeof(int32_t) * 2 * (size_t)b->Ng * frames);
+    }
+    if (e == hipSuccess) e = b->hist.ensure(sizeof(uint32_t) * kBins * (size_t)frames);
+    if (e == hipSuccess) e = b->counts.ensure(sizeof(int64_t) * 4 * (size_t)frames);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
+    if (e != hipSuccess) {
+        sv_batch_destroy(b);
+        return fail(SV_E_HIP, "sv_batch_create: %s", hipGetErrorString(e));
+    }
+    *out = b;
+    return SV_OK;
+}
+
+int sv_batch_destroy(sv_batch* b) {
+    if (!b) return SV_OK;
+    (void)hipSetDevice(b->device);
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->hist, &b->counts,
+                      &b->status, &b->ctrl})
+        if (x->p) (void)hipFree(x->p);
+    for (auto& ev : b->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : b->pool) (void)hipEventDestroy(ev);
+    delete b;
+    return SV_OK;
+}
+
+int sv_batch_info(const sv_batch* b, int64_t* o) {
+    if (!b || !o) return fail(SV_E_ARG, "null");
+    o[0] = b->kp.Hg;
+    o[1] = b->kp.Wg;
+    o[2] = b->kp.pitch;
+    o[3] = b->Ng;
+    o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->pts.bytes);
+    o[5] = b->frames;
+    o[6] = b->H;
+    o[7] = b->W;
+    return SV_OK;
+}
+
+int sv_batch_tune(sv_batch* b, int grid_cap, int nontemporal) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    b->grid_cap = grid_cap;
+    b->nontemporal = nontemporal;
+    return SV_OK;
+}
+
+int sv_batch_synth(sv_batch* b, int64_t first_frame_id) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(launch_synth(b->kp, b->disp.as<uint8_t>(), b->with_bgr ? b->bgr.as<uint8_t>() : nullptr,
+                         b->frames, first_frame_id, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_upload(sv_batch* b, int frame, const uint8_t* disp, const uint8_t* bgr) {
+    if (!b || !disp || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "sv_batch_upload: bad args");
+    if (bgr && !b->with_bgr) return fail(SV_E_ARG, "batch created without bgr");
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t px = (size_t)b->H * b->W;
+    HIP_TRY(hipMemcpyAsync(b->disp.as<uint8_t>() + px * frame, disp, px, hipMemcpyHostToDevice, b->stream));
+    if (bgr)
+        HIP_TRY(hipMemcpyAsync(b->bgr.as<uint8_t>() + 3 * px * frame, bgr, 3 * px, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_project(sv_batch* b, const sv_camera* cam, int sync) {
+    if (!b || !cam) return fail(SV_E_ARG, "null");
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t plane = sizeof(float) * (size_t)b->dense_per_frame * b->frames;
+    HIP_TRY(b->X.ensure(plane));
+    HIP_TRY(b->Y.ensure(plane));
+    HIP_TRY(b->Z.ensure(plane));
+    KParams p = make_params(b->H, b->W, b->step, *cam);
+    int t0, t1;
+    HIP_TRY(hipEventRecord(b->ev[0], b->stream));
+    HIP_TRY(b->timed_event(&t0));
+    HIP_TRY(launch_project_dense(p, b->disp.as<uint8_t>(), b->X.as<float>(), b->Y.as<float>(), b->Z.as<float>(),
+                                 b->frames, b->grid_cap, b->nontemporal, b->stream));
+    HIP_TRY(b->timed_event(&t1));
+    HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+    b->pending[0].push_back({t0, t1});
+    b->have_ms[0] = true;
+    if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane* plane, double point_thr,
+                               int hist_thr, int chunk, int sync, Device* d) {
+    if (!b->with_bgr) return fail(SV_E_ARG, "pipeline needs a batch created with bgr");
+    KParams p = make_params(b->H, b->W, b->step, *cam);
+    set_plane(p, *plane, point_thr, hist_thr);
+    if (chunk <= 0) chunk = 16;
+    if (chunk > b->frames) chunk = b->frames;
+    const size_t cap = (size_t)b->Ng;
+    HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames));
+    HIP_TRY(b->pts.ensure(sizeof(int32_t) * 2 * cap * b->frames));
+    const int tiles = pipeline_tiles_per_frame(p);
+    HIP_TRY(b->status.ensure(sizeof(uint64_t) * (size_t)tiles * chunk));
+    HIP_TRY(b->ctrl.ensure(64));
+    if (int rc = ensure_tables(*d, b->H, b->W, *cam, b->stream)) return rc;
+    PipeBuffers bf;
+    bf.disp = b->disp.as<uint8_t>();
+    bf.bgr = b->bgr.as<uint8_t>();
+    bf.hist = b->hist.as<uint32_t>();
+    bf.counts = b->counts.as<int64_t>();
+    bf.status = b->status.as<uint64_t>();
+    bf.ticket = b->ctrl.as<uint32_t>();
+    bf.err = b->ctrl.as<uint32_t>() + 1;
+    bf.xyz = b->xyz.as<float>();
+    bf.pts = b->pts.as<int32_t>();
+    bf.dxbits = d->tables.dx.as<uint32_t>();
+    bf.dybits = d->tables.dy.as<uint32_t>();
+    bf.cap = (int64_t)cap;
+    int t0, t1;
+    HIP_TRY(hipEventRecord(b->ev[2], b->stream));
+    HIP_TRY(b->timed_event(&t0));
+    HIP_TRY(hipMemsetAsync(b->hist.p, 0, sizeof(uint32_t) * kBins * (size_t)b->frames, b->stream));
+    HIP_TRY(hipMemsetAsync(b->counts.p, 0, sizeof(int64_t) * 4 * (size_t)b->frames, b->stream));
+    HIP_TRY(hipMemsetAsync(b->ctrl.p, 0, 64, b->stream));
+    for (int f0 = 0; f0 < b->frames; f0 += chunk) {
+        const int n = (b->frames - f0) < chunk ? (b->frames - f0) : chunk;
+        HIP_TRY(launch_pipeline_chunk(p, bf, f0, n, b->stream));
+    }
+    HIP_TRY(b->timed_event(&t1));
+    HIP_TRY(hipEventRecord(b->ev[3], b->stream));
+    b->pending[1].push_back({t0, t1});
+    b->have_ms[1] = true;
+    if (sync) {
+        HIP_TRY(hipStreamSynchronize(b->stream));
+        uint32_t err = 0;
+        HIP_TRY(hipMemcpy(&err, bf.err, 4, hipMemcpyDeviceToHost));
+        if (err) return fail(SV_E_DEVICE, "pipeline look-back timed out");
+    }
+    return SV_OK;
+}
+
+int sv_batch_pipeline(sv_batch* b, const sv_camera* cam, const sv_plane* plane, double point_thr, int hist_thr,
+                      int chunk, int sync) {
+    if (!b || !cam || !plane) return fail(SV_E_ARG, "null");
+    Device* d;
+    if (int rc = dev_get(b->device, &d)) return rc;
+    return batch_pipeline_impl(b, cam, plane, point_thr, hist_thr, chunk, sync, d);
+}
+
+int sv_batch_sync(sv_batch* b) {
+    if (!b) return fail(SV_E_ARG, "null");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    if (b->ctrl.p) {
+        uint32_t err = 0;
+        HIP_TRY(hipMemcpy(&err, b->ctrl.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost));
+        if (err) return fail(SV_E_DEVICE, "pipeline look-back timed out");
+    }
+    return SV_OK;
+}
+
+int sv_batch_last_ms(sv_batch* b, int which, float* ms) {
+    if (!b || !ms || which < 0 || which > 1) return fail(SV_E_ARG, "bad args");
+    if (!b->have_ms[which]) return fail(SV_E_STATE, "no timing recorded");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipEventSynchronize(b->ev[2 * which + 1]));
+    HIP_TRY(hipEventElapsedTime(ms, b->ev[2 * which], b->ev[2 * which + 1]));
+    return SV_OK;
+}
+
+int sv_batch_timing(sv_batch* b, int which, double* total_ms, int64_t* count) {
+    if (!b || which < 0 || which > 1 || !total_ms || !count) return fail(SV_E_ARG, "bad args");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    double tot = 0;
+    for (auto& pr : b->pending[which]) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, b->pool[pr.first], b->pool[pr.second]));
+        tot += ms;
+    }
+    *total_ms = tot;
+    *count = (int64_t)b->pending[which].size();
+    return SV_OK;
+}
+
+int sv_batch_timing_reset(sv_batch* b) {
+    if (!b) return fail(SV_E_ARG, "null");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    b->pending[0].clear();
+    b->pending[1].clear();
+    b->pool_next = 0;
+    return SV_OK;
+}
+
+int sv_batch_read_dense(sv_batch* b, int frame, float* X, float* Y, float* Z) {
+    if (!b || frame < 0 || frame >= b->frames || !b->X.p) return fail(SV_E_ARG, "bad args / nothing projected");
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t n = (size_t)b->dense_per_frame, off = n * frame;
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    if (X) HIP_TRY(hipMemcpy(X, b->X.as<float>() + off, n * 4, hipMemcpyDeviceToHost));
+    if (Y) HIP_TRY(hipMemcpy(Y, b->Y.as<float>() + off, n * 4, hipMemcpyDeviceToHost));
+    if (Z) HIP_TRY(hipMemcpy(Z, b->Z.as<float>() + off, n * 4, hipMemcpyDeviceToHost));
+    return SV_OK;
+}
+
+int sv_batch_read_counts(sv_batch* b, int64_t* counts) {
+    if (!b || !counts) return fail(SV_E_ARG, "null");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    int64_t* tmp = new int64_t[4 * (size_t)b->frames];
+    hipError_t e = hipMemcpy(tmp, b->counts.p, sizeof(int64_t) * 4 * b->frames, hipMemcpyDeviceToHost);
+    if (e == hipSuccess)
+        for (int f = 0; f < b->frames; ++f)
+            for (int k = 0; k < 3; ++k) counts[3 * f + k] = tmp[4 * f + k];
+    delete[] tmp;
+    HIP_TRY(e);
+    return SV_OK;
+}
+
+int sv_batch_read_hist(sv_batch* b, int frame, uint32_t* hist) {
+    if (!b || !hist || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "bad args");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    HIP_TRY(hipMemcpy(hist, b->hist.as<uint32_t>() + (size_t)kBins * frame, 4 * kBins, hipMemcpyDeviceToHost));
+    return SV_OK;
+}
+
+int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64_t cap, int64_t* n) {
+    if (!b || !n || frame < 0 || frame >= b->frames || !b->pts.p) return fail(SV_E_ARG, "bad args");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    int64_t c[4];
+    HIP_TRY(hipMemcpy(c, b->counts.as<int64_t>() + 4 * (size_t)frame, sizeof c, hipMemcpyDeviceToHost));
+    *n = c[2];
+    if (c[2] > cap) return fail(SV_E_CAP, "capacity %lld < %lld", (long long)cap, (long long)c[2]);
+    const size_t base = (size_t)b->Ng * frame;
+    if (xyz && c[2]) HIP_TRY(hipMemcpy(xyz, b->xyz.as<float>() + 3 * base, 12 * c[2], hipMemcpyDeviceToHost));
+    if (pts && c[2]) HIP_TRY(hipMemcpy(pts, b->pts.as<int32_t>() + 2 * base, 8 * c[2], hipMemcpyDeviceToHost));
+    return SV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// fused one-frame chain (stereovision.py:84,97-113) through a cached batch
+// ---------------------------------------------------------------------------
+int sv_pipeline_frame(const uint8_t* disp, const uint8_t* bgr, int H, int W, int step, const sv_camera* cam,
+                      const sv_plane* plane, double point_thr, int hist_thr, int64_t* out_counts,
+                      uint32_t* out_hist, float* out_xyz, int32_t* out_pts, int64_t cap) {
+    if (!disp || !bgr || !cam || !plane || !out_counts)
+        return fail(SV_E_ARG, "sv_pipeline_frame: null argument");
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    sv_batch* b = d->frame_batch;
+    if (!b || b->H != H || b->W != W || b->step != step) {
+        if (b) sv_batch_destroy(b);
+        d->frame_batch = nullptr;
+        if (int rc = sv_batch_create(dev, 1, H, W, step, 1, 1, &b)) return rc;
+        d->frame_batch = b;
+    }
+    if (int rc = sv_batch_upload(b, 0, disp, bgr)) return rc;
+    if (int rc = batch_pipeline_impl(b, cam, plane, point_thr, hist_thr, 1, 1, d)) return rc;
+    if (int rc = sv_batch_read_counts(b, out_counts)) return rc;
+    if (out_hist)
+        if (int rc = sv_batch_read_hist(b, 0, out_hist)) return rc;
+    if (out_pts || out_xyz) {
+        int64_t n = 0;
+        if (int rc = sv_batch_read_points(b, 0, out_xyz, out_pts, cap, &n)) return rc;
+    }
+    return SV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// verification helpers
+// ---------------------------------------------------------------------------
+int sv_hue_lut(int device, int16_t* out_lut) {
+    if (!out_lut) return fail(SV_E_ARG, "null");
+    Device* d;
+    if (int rc = dev_get(device, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    DevBuf buf;
+    HIP_TRY(buf.ensure(sizeof(int16_t) << 24));
+    hipError_t e = launch_hue_lut(buf.as<int16_t>(), d->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out_lut, buf.p, sizeof(int16_t) << 24, hipMemcpyDeviceToHost, d->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    (void)hipFree(buf.p);
+    HIP_TRY(e);
+    return SV_OK;
+}
+
+int sv_delta_tables(int device, int H, int W, const sv_camera* cam, int8_t* dx, int8_t* dy) {
+    if (!cam || !dx || !dy || H < 1 || W < 1) return fail(SV_E_ARG, "bad args");
+    Device* d;
+    if (int rc = dev_get(device, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    KParams p = make_params(H, W, 1, *cam);
+    DevBuf bx, by, b8;
+    HIP_TRY(bx.ensure(4 * 256 * p.dx_words));
+    HIP_TRY(by.ensure(4 * 256 * p.dy_words));
+    HIP_TRY(b8.ensure(256 * (size_t)(H + W)));
+    int8_t* dx8 = b8.as<int8_t>();
+    int8_t* dy8 = dx8 + 256 * (size_t)W;
+    hipError_t e = launch_delta_tables(p, bx.as<uint32_t>(), by.as<uint32_t>(), dx8, dy8, d->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dx, dx8, 256 * (size_t)W, hipMemcpyDeviceToHost, d->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dy, dy8, 256 * (size_t)H, hipMemcpyDeviceToHost, d->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    (void)hipFree(bx.p);
+    (void)hipFree(by.p);
+    (void)hipFree(b8.p);
+    HIP_TRY(e);
+    return SV_OK;
+}
+
+int sv_synth_frame(int device, int64_t frame_id, int H, int W, uint8_t* disp, uint8_t* bgr) {
+    if (!disp || H < 1 || W < 4 || (W % 4)) return fail(SV_E_ARG, "bad args (W%%4 == 0 required)");
+    Device* d;
+    if (int rc = dev_get(device, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    sv_camera cam0{1, 1, 0, 0};
+    KParams p = make_params(H, W, 1, cam0);
+    DevBuf bd, bc;
+    HIP_TRY(bd.ensure((size_t)H * W));
+    HIP_TRY(bc.ensure((size_t)H * W * 3));
+    hipError_t e = launch_synth(p, bd.as<uint8_t>(), bc.as<uint8_t>(), 1, frame_id, d->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(disp, bd.p, (size_t)H * W, hipMemcpyDeviceToHost, d->stream);
+    if (e == hipSuccess && bgr) e = hipMemcpyAsync(bgr, bc.p, (size_t)H * W * 3, hipMemcpyDeviceToHost, d->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    (void)hipFree(bd.p);
+    (void)hipFree(bc.p);
+    HIP_TRY(e);
+    return SV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,176 @@
+// Device-side building blocks shared by the svx kernels (gfx950 / CDNA4).
+//
+// Exactness contract ("three bit-exactness traps"):
+//   * keep1 (dist < thr, functions.py:300-323): fp32 fast path with a rigorous
+//     per-point error bound; points inside the band are decided by the exact
+//     fp64 reference arithmetic. The mask is therefore bit-exact.
+//   * hue bin (functions.py:73-78 + colorsys): exact integer rational path;
+//     only exact rational ties (2q == den) run the fp64 colorsys emulation.
+//   * int32 back-projection (functions.py:201-209, stereovision.py:112): the
+//     fp64 round trip depends on (x,d) / (y,d) only -> 1-bit delta tables
+//     built once per camera in fp64 on the device.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace svx {
+
+constexpr int kWave = 64;
+constexpr int kBins = 1024;   // hue bins 0..999 used; padded to 1024
+
+// Everything a kernel needs, passed by value (kernarg segment, scalar loads).
+struct KParams {
+    int H, W, step, Hg, Wg, pitch, Q;   // Q = quads per grid row = pitch/4
+    int frame_quads;                    // Hg * Q
+    int64_t frame_px;                   // H * W
+    // camera (functions.py:15-22)
+    double f, B, cw, ch, fB;
+    float fB32, B32;
+    // plane (a*X+b*Y+c*Z = 1) and thresholds
+    double a, b, c, nrm, thr;
+    float a32, b32, c32, thr32, inv_nrm32, guard32;   // guard32 = 2^-18 / nrm
+    float abs_a32, abs_b32, abs_cf32;      // |a|, |b|, |c|*f (bound of |aX|+|bY|+|cZ| per unit K)
+    int hist_thr;
+    int dx_words, dy_words;                // words per d-row of the delta bit tables
+};
+
+// ---------------------------------------------------------------------------
+// Hue bin: integer bin k <-> reference key str(round(colorsys hue, 3)).
+// exact rational t = 1000*n/(6*rng) (n in [0, 6 rng)); fp64 only on exact ties.
+// ---------------------------------------------------------------------------
+__device__ __noinline__ int hue_bin_tie_f64(int r, int g, int b, int mx, int mn) {
+    // colorsys.rgb_to_hsv on numpy uint8 scalars, then numpy round(h, 3).
+    const double rng = (double)(mx - mn);
+    const double rc = (double)(mx - r) / rng;
+    const double gc = (double)(mx - g) / rng;
+    const double bc = (double)(mx - b) / rng;
+    double h;
+    if (r == mx) h = bc - gc;
+    else if (g == mx) h = (2.0 + rc) - bc;
+    else h = (4.0 + gc) - rc;
+    h = h / 6.0;
+    double m = fmod(h, 1.0);
+    if (m != 0.0) {
+        if (m < 0.0) m += 1.0;
+    } else {
+        m = 0.0;
+    }
+    return (int)rint(m * 1000.0);
+}
+
+__device__ __forceinline__ int hue_bin(int r, int g, int b) {
+    const int mx = max(r, max(g, b));
+    const int mn = min(r, min(g, b));
+    const int rng = mx - mn;
+    if (rng == 0) return 0;
+    int n;
+    if (r == mx) n = g - b;
+    else if (g == mx) n = 2 * rng + b - r;
+    else n = 4 * rng + r - g;
+    if (n < 0) n += 6 * rng;
+    // t = 500 n / (3 rng); num < 2^20, den <= 765: fp32 quotient + exact fixup
+    const int num = 500 * n, den = 3 * rng;
+    int q = (int)((float)num * __builtin_amdgcn_rcpf((float)den));
+    int rem = num - q * den;
+    if (rem < 0) { q -= 1; rem += den; }
+    if (rem >= den) { q += 1; rem -= den; }
+    const int two_rem = 2 * rem;
+    if (two_rem > den) return q + 1;
+    if (two_rem < den) return q;
+    return hue_bin_tie_f64(r, g, b, mx, mn);   // exact .5 tie: reference fp64 decides
+}
+
+// ---------------------------------------------------------------------------
+// Plane keep test (functions.py:300-323) for grid pixel (x, y) with d > 0.
+// K = B/d (fp32), xc = x - cw, yc = y - ch (exact in fp32).
+// ---------------------------------------------------------------------------
+__device__ __noinline__ bool keep1_f64(int x, int y, uint32_t d, const KParams& p) {
+    const double Z = p.fB / (double)d;
+    const double X = (((double)x - p.cw) * Z) / p.f;
+    const double Y = (((double)y - p.ch) * Z) / p.f;
+    const double dot = __builtin_fma(Z, p.c, __builtin_fma(X, p.a, Y * p.b));
+    return __builtin_fabs((dot - 1.0) / p.nrm) < p.thr;
+}
+
+__device__ __forceinline__ bool keep1(int x, int y, uint32_t d, float xc, float yc, float K,
+                                      float X, float Y, float Z, const KParams& p) {
+    const float dot = __builtin_fmaf(Z, p.c32, __builtin_fmaf(X, p.a32, Y * p.b32));
+    const float dist = __builtin_fabsf(dot - 1.0f) * p.inv_nrm32;
+    const float S = __builtin_fmaf(p.abs_a32, __builtin_fabsf(xc),
+                                   __builtin_fmaf(p.abs_b32, __builtin_fabsf(yc), p.abs_cf32)) * K;
+    const float G = (S + 1.0f) * p.guard32;
+    if (dist < p.thr32 - G) return true;
+    if (dist > p.thr32 + G) return false;
+    return keep1_f64(x, y, d, p);
+}
+
+// ---------------------------------------------------------------------------
+// Wave / block helpers (wave64).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, kWave);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Decoupled look-back (single-pass ordered compaction across workgroups).
+// Status word: [63:62] flag (0 not ready, 1 aggregate, 2 inclusive), [31:0] value.
+// One 8-byte granule per tile, written by ONE relaxed agent-scope (sc1) store
+// and read by relaxed agent-scope loads: the data is the flag (MI355X guide
+// §6 G16, form R2) — no separate payload, no fence needed.
+// Forward progress: tile ids come from an atomic ticket, so every tile a wave
+// waits on belongs to a workgroup that is already running.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kFlagAgg = 1ull << 62;
+constexpr uint64_t kFlagInc = 2ull << 62;
+
+__device__ __forceinline__ void publish(uint64_t* st, uint64_t flag, uint32_t v) {
+    __hip_atomic_store(st, flag | (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by ALL lanes of ONE wave. st points at this frame's tile 0.
+// Returns the exclusive prefix of `tile`. Sets *err on (impossible) timeout.
+__device__ uint32_t lookback(const uint64_t* st, int tile, uint32_t* err) {
+    const int lane = lane_id();
+    uint32_t excl = 0;
+    int j = tile - 1;
+    uint32_t spins = 0;
+    while (true) {
+        const int idx = j - lane;
+        uint64_t w = kFlagInc;  // before the frame start: inclusive 0
+        if (idx >= 0)
+            w = __hip_atomic_load(st + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t flag = (uint32_t)(w >> 62);
+        const uint64_t not_ready = __ballot(flag == 0);
+        const uint64_t incl = __ballot(flag == 2);
+        const int first_incl = incl ? __builtin_ctzll(incl) : 64;
+        const int first_nr = not_ready ? __builtin_ctzll(not_ready) : 64;
+        if (first_nr < first_incl) {
+            if (++spins > (1u << 24)) {  // bounded: never hang the device
+                if (lane == 0) atomicExch(err, 1u);
+                return excl;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        const uint32_t v = (lane <= first_incl) ? (uint32_t)w : 0u;
+        excl += wave_sum(v);
+        if (first_incl < 64) return excl;
+        j -= 64;
+    }
+}
+
+}  // namespace svx

@@ -1,0 +1,51 @@
+// Host-side launchers for the svx kernels (one TU per kernel family).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "svx_device.h"
+
+namespace svx {
+
+// kernels/project.hip -------------------------------------------------------
+hipError_t launch_synth(const KParams& p, uint8_t* disp, uint8_t* bgr, int frames,
+                        int64_t first_frame, hipStream_t s);
+// K1: dense fp32 projection. total_quads = frames * Hg * Q.
+hipError_t launch_project_dense(const KParams& p, const uint8_t* disp, float* X, float* Y, float* Z,
+                                int frames, int grid_cap, int nontemporal, hipStream_t s);
+// Drop-in projection: fp64 XYZ, compacted in raster order (any H, W, step).
+hipError_t launch_project_compact_f64(const KParams& p, const uint8_t* disp, int64_t ld_disp,
+                                      const uint8_t* bgr, int64_t ld_bgr, double* xyz, uint8_t* rgb,
+                                      uint64_t* status, uint32_t* ticket, uint32_t* count,
+                                      uint32_t* err, hipStream_t s);
+hipError_t launch_backproject_f64(const double* xyz, int64_t n, int64_t ld, double f, double cw,
+                                  double ch, double* xy, hipStream_t s);
+int project_compact_tiles(const KParams& p);
+
+// kernels/tables.hip --------------------------------------------------------
+hipError_t launch_hue_lut(int16_t* lut, hipStream_t s);
+// dx bits [256][dx_words], dy bits [256][dy_words]; optional int8 tables.
+hipError_t launch_delta_tables(const KParams& p, uint32_t* dxbits, uint32_t* dybits, int8_t* dx8,
+                               int8_t* dy8, hipStream_t s);
+
+// kernels/pipeline.hip ------------------------------------------------------
+struct PipeBuffers {
+    const uint8_t* disp;
+    const uint8_t* bgr;
+    uint32_t* hist;      // frames x 1024
+    int64_t* counts;     // frames x 4 (N_valid, N_kept, N_kept2, spare)
+    uint64_t* status;    // chunk x tiles look-back granules
+    uint32_t* ticket;
+    uint32_t* err;
+    float* xyz;          // frames x cap x 3
+    int32_t* pts;        // frames x cap x 2
+    const uint32_t* dxbits;
+    const uint32_t* dybits;
+    int64_t cap;         // points per frame (Ng)
+};
+int pipeline_tiles_per_frame(const KParams& p);
+int pipeline_slices_per_frame(const KParams& p);
+hipError_t launch_pipeline_chunk(const KParams& p, const PipeBuffers& b, int frame0, int frames,
+                                 hipStream_t s);
+
+}  // namespace svx

@@ -1,0 +1,112 @@
+"""ctypes binding of libsvx.so (include/svx.h).
+
+The product has exactly one compute path: the hand-written gfx950 kernels in
+libsvx.so. If the library is missing or has no device, every call raises —
+there is deliberately no CPU fallback.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libsvx.so")
+
+SV_UNIQUE_ID_BYTES = 128
+
+
+class SvxError(RuntimeError):
+    """A libsvx call failed (message from sv_last_error())."""
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("f", ctypes.c_double), ("B", ctypes.c_double),
+                ("cw", ctypes.c_double), ("ch", ctypes.c_double)]
+
+
+class Plane(ctypes.Structure):
+    _fields_ = [("a", ctypes.c_double), ("b", ctypes.c_double), ("c", ctypes.c_double)]
+
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+D = ctypes.c_double
+PI64 = ctypes.POINTER(ctypes.c_int64)
+PF = ctypes.POINTER(ctypes.c_float)
+
+# name -> argtypes (restype is int unless listed in _RESTYPE)
+SIGNATURES = {
+    "sv_version": [],
+    "sv_last_error": [],
+    "sv_device_count": [ctypes.POINTER(I)],
+    "sv_init": [I],
+    "sv_project_frame": [P, I, I, I64, P, I64, I, ctypes.POINTER(Camera), P, P, I64, PI64],
+    "sv_backproject": [P, I64, I64, ctypes.POINTER(Camera), P],
+    "sv_pipeline_frame": [P, P, I, I, I, ctypes.POINTER(Camera), ctypes.POINTER(Plane), D, I,
+                          P, P, P, P, I64],
+    "sv_batch_create": [I, I, I, I, I, I, I, ctypes.POINTER(P)],
+    "sv_batch_destroy": [P],
+    "sv_batch_info": [P, P],
+    "sv_batch_tune": [P, I, I],
+    "sv_batch_synth": [P, I64],
+    "sv_batch_upload": [P, I, P, P],
+    "sv_batch_project": [P, ctypes.POINTER(Camera), I],
+    "sv_batch_pipeline": [P, ctypes.POINTER(Camera), ctypes.POINTER(Plane), D, I, I, I],
+    "sv_batch_sync": [P],
+    "sv_batch_last_ms": [P, I, PF],
+    "sv_batch_timing": [P, I, ctypes.POINTER(D), PI64],
+    "sv_batch_timing_reset": [P],
+    "sv_batch_read_dense": [P, I, P, P, P],
+    "sv_batch_read_counts": [P, P],
+    "sv_batch_read_hist": [P, I, P],
+    "sv_batch_read_points": [P, I, P, P, I64, PI64],
+    "sv_hue_lut": [I, P],
+    "sv_delta_tables": [I, I, I, ctypes.POINTER(Camera), P, P],
+    "sv_synth_frame": [I, I64, I, I, P, P],
+    "sv_comm_unique_id": [P],
+    "sv_comm_init": [I, I, P, I, ctypes.POINTER(P)],
+    "sv_comm_destroy": [P],
+    "sv_comm_broadcast_plane": [P, ctypes.POINTER(Plane), I],
+    "sv_comm_allreduce_i64": [P, P, I],
+}
+_RESTYPE = {"sv_version": ctypes.c_char_p, "sv_last_error": ctypes.c_char_p}
+
+_lib = None
+
+
+def lib():
+    """The loaded libsvx.so (raises ImportError if it was never built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libsvx.so not found at {LIB_PATH}: build it with "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPE.get(name, ctypes.c_int)
+        _lib = l
+    return _lib
+
+
+def last_error():
+    msg = lib().sv_last_error()
+    return msg.decode() if msg else ""
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise SvxError(f"{name} failed ({rc}): {last_error()}")
+    return rc
+
+
+def ptr(a):
+    """data pointer of a numpy array (or None)."""
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    rc = lib().sv_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0

@@ -1,0 +1,168 @@
+"""Batched, device-resident API.
+
+Frames live in HBM for their whole life: generated on the device by the
+counter-based synthetic generator (or uploaded once), projected by K1 into
+dense fp32 X/Y/Z planes, or run through the plane/hue/compaction pipeline.
+Only the small per-frame results are copied back, on request.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi
+from .dropin import DEFAULT_CAMERA
+
+CAMERA = _abi.Camera(*DEFAULT_CAMERA)
+
+
+def synthetic_plane(f=DEFAULT_CAMERA[0], B=DEFAULT_CAMERA[1], ch=DEFAULT_CAMERA[3], horizon=200):
+    """SURVEY §8d plane matching the synthetic road (a*X + b*Y + c*Z = 1)."""
+    k = 0.6
+    return (0.0, k / B, -k * (horizon - ch) / (f * B))
+
+
+class Batch:
+    """`frames` x H x W disparity (+BGR) frames resident on one GPU."""
+
+    def __init__(self, frames, H=544, W=1024, step=1, with_bgr=True, with_points=False, device=0):
+        h = ctypes.c_void_p()
+        _abi.call("sv_batch_create", device, frames, H, W, step, int(with_bgr), int(with_points),
+                  ctypes.byref(h))
+        self._h = h
+        self.frames, self.H, self.W, self.step, self.device = frames, H, W, step, device
+        info = np.zeros(8, np.int64)
+        _abi.call("sv_batch_info", self._h, _abi.ptr(info))
+        self.Hg, self.Wg, self.pitch, self.Ng = (int(v) for v in info[:4])
+
+    # -- lifetime ---------------------------------------------------------------
+    def close(self):
+        if self._h:
+            _abi.call("sv_batch_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- inputs -------------------------------------------------------------------
+    def synth(self, first_frame_id=0):
+        _abi.call("sv_batch_synth", self._h, int(first_frame_id))
+
+    def upload(self, frame, disp, bgr=None):
+        disp = np.ascontiguousarray(disp, np.uint8)
+        if disp.shape != (self.H, self.W):
+            raise ValueError(f"disp shape {disp.shape} != {(self.H, self.W)}")
+        if bgr is not None:
+            bgr = np.ascontiguousarray(bgr, np.uint8)
+            if bgr.shape != (self.H, self.W, 3):
+                raise ValueError(f"bgr shape {bgr.shape} != {(self.H, self.W, 3)}")
+        _abi.call("sv_batch_upload", self._h, frame, _abi.ptr(disp), _abi.ptr(bgr))
+
+    def tune(self, grid_cap=0, nontemporal=0):
+        _abi.call("sv_batch_tune", self._h, int(grid_cap), int(nontemporal))
+
+    # -- compute -------------------------------------------------------------------
+    def project(self, camera=None, sync=True):
+        cam = camera or CAMERA
+        _abi.call("sv_batch_project", self._h, ctypes.byref(cam), int(sync))
+
+    def pipeline(self, plane=None, point_thr=0.05, hist_thr=10, camera=None, chunk=0, sync=True):
+        cam = camera or CAMERA
+        pl = _abi.Plane(*(plane if plane is not None else synthetic_plane()))
+        _abi.call("sv_batch_pipeline", self._h, ctypes.byref(cam), ctypes.byref(pl), float(point_thr),
+                  int(hist_thr), int(chunk), int(sync))
+
+    def sync(self):
+        _abi.call("sv_batch_sync", self._h)
+
+    def last_ms(self, which="project"):
+        ms = ctypes.c_float(0)
+        _abi.call("sv_batch_last_ms", self._h, 0 if which == "project" else 1, ctypes.byref(ms))
+        return float(ms.value)
+
+    def timing(self, which="project"):
+        """(total_ms, launches) of the per-launch event timings since reset_timing()."""
+        tot = ctypes.c_double(0)
+        cnt = ctypes.c_int64(0)
+        _abi.call("sv_batch_timing", self._h, 0 if which == "project" else 1, ctypes.byref(tot),
+                  ctypes.byref(cnt))
+        return float(tot.value), int(cnt.value)
+
+    def reset_timing(self):
+        _abi.call("sv_batch_timing_reset", self._h)
+
+    # -- outputs -------------------------------------------------------------------
+    def read_dense(self, frame):
+        shape = (self.Hg, self.pitch)
+        X, Y, Z = (np.empty(shape, np.float32) for _ in range(3))
+        _abi.call("sv_batch_read_dense", self._h, frame, _abi.ptr(X), _abi.ptr(Y), _abi.ptr(Z))
+        return X, Y, Z
+
+    def read_counts(self):
+        c = np.empty((self.frames, 3), np.int64)
+        _abi.call("sv_batch_read_counts", self._h, _abi.ptr(c))
+        return c
+
+    def read_hist(self, frame):
+        h = np.empty(1024, np.uint32)
+        _abi.call("sv_batch_read_hist", self._h, frame, _abi.ptr(h))
+        return h
+
+    def read_points(self, frame):
+        n = ctypes.c_int64(0)
+        cap = self.Ng
+        xyz = np.empty((cap, 3), np.float32)
+        pts = np.empty((cap, 2), np.int32)
+        _abi.call("sv_batch_read_points", self._h, frame, _abi.ptr(xyz), _abi.ptr(pts), cap, ctypes.byref(n))
+        k = n.value
+        return xyz[:k], pts[:k]
+
+
+def pipeline_frame(disp, bgr, step=2, plane=None, point_thr=0.05, hist_thr=10, camera=None):
+    """Fused chain for one host frame (sv_pipeline_frame). Returns dict like the oracle."""
+    disp = np.ascontiguousarray(disp, np.uint8)
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    H, W = disp.shape
+    hg = (H - 1 + step - 1) // step
+    wg = (W - 1 + step - 1) // step
+    cap = max(hg * wg, 1)
+    counts = np.zeros(3, np.int64)
+    hist = np.zeros(1024, np.uint32)
+    xyz = np.empty((cap, 3), np.float32)
+    pts = np.empty((cap, 2), np.int32)
+    cam = camera or CAMERA
+    pl = _abi.Plane(*(plane if plane is not None else synthetic_plane()))
+    _abi.call("sv_pipeline_frame", _abi.ptr(disp), _abi.ptr(bgr), H, W, step, ctypes.byref(cam),
+              ctypes.byref(pl), float(point_thr), int(hist_thr), _abi.ptr(counts), _abi.ptr(hist),
+              _abi.ptr(xyz), _abi.ptr(pts), cap)
+    n2 = int(counts[2])
+    return dict(counts=tuple(int(v) for v in counts), hist=hist, xyz2=xyz[:n2], pts=pts[:n2])
+
+
+def hue_lut(device=0):
+    lut = np.empty(1 << 24, np.int16)
+    _abi.call("sv_hue_lut", device, _abi.ptr(lut))
+    return lut
+
+
+def delta_tables(H=544, W=1024, camera=None, device=0):
+    dx = np.empty((256, W), np.int8)
+    dy = np.empty((256, H), np.int8)
+    cam = camera or CAMERA
+    _abi.call("sv_delta_tables", device, H, W, ctypes.byref(cam), _abi.ptr(dx), _abi.ptr(dy))
+    return dx, dy
+
+
+def synth_frame(frame_id, H=544, W=1024, device=0):
+    disp = np.empty((H, W), np.uint8)
+    bgr = np.empty((H, W, 3), np.uint8)
+    _abi.call("sv_synth_frame", device, int(frame_id), H, W, _abi.ptr(disp), _abi.ptr(bgr))
+    return disp, bgr

@@ -1,0 +1,134 @@
+"""Drop-in replacements for the reference's hot-path functions.
+
+The reference (thien/stereo.vision) has no plugin/FFI API: stereovision.py
+does ``import functions as f`` (stereovision.py:3) and resolves
+``f.projectDisparityTo3d`` etc. at call time (stereovision.py:84-111). The
+boundary is therefore the attributes of the ``functions`` module:
+
+    import functions, svx.dropin
+    svx.dropin.install(functions)      # loop.py / single_frame.py then run unchanged
+
+Signatures, argument meaning, return conventions and error behaviour follow the
+reference:
+
+* ``projectDisparityTo3d(disparity, max_disparity, rgb=[])`` (functions.py:178-198):
+  ``max_disparity`` is accepted and ignored (as in the reference); ``rgb`` is
+  used iff ``len(rgb) > 0``. Returns a ``list`` (a Sequence: ``random.sample``
+  in RANSAC needs one, functions.py:252,286) of rows supporting ``row[0..5]``
+  and ``row[:3]``; XYZ are ``np.float64`` bit-identical to the reference and
+  R,G,B are numpy scalars (np.float64), which keeps ``BGRtoHSVHue`` keys
+  identical (Python ints would not: SURVEY §0 trap 3).
+* ``project3DPointsTo2DImagePoints(points)`` (functions.py:201-209): returns
+  an (N, 2) float64 array that ``np.array(.., np.int32).reshape((-1,1,2))``
+  (stereovision.py:112-113) accepts, (0, 2) for no points.
+
+Failures raise ``RuntimeError`` (``SvxError``), which the reference's own
+``try/except`` at stereovision.py:92-126 handles like any reference error.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi
+
+# functions.py:15,19,21,22
+DEFAULT_CAMERA = (399.9745178222656, 0.2090607502, 474.5, 262.0)
+REFERENCE_STEP = 2   # functions.py:185-186 hard-codes the grid step
+
+_module = None       # the installed `functions` module (its constants are read per call)
+
+
+def _camera():
+    if _module is not None:
+        m = _module
+        return _abi.Camera(m.camera_focal_length_px, m.stereo_camera_baseline_m,
+                           m.image_centre_w, m.image_centre_h)
+    return _abi.Camera(*DEFAULT_CAMERA)
+
+
+def _as_u8(a, ndim, what):
+    arr = np.asarray(a)
+    if arr.dtype != np.uint8:
+        raise TypeError(f"{what} must be uint8 (as functions.disparity / cv2.imread produce), got {arr.dtype}")
+    if arr.ndim != ndim:
+        raise ValueError(f"{what} must have {ndim} dimensions, got shape {arr.shape}")
+    if arr.strides[-1] != arr.itemsize or (ndim == 3 and arr.strides[1] != 3):
+        arr = np.ascontiguousarray(arr)
+    return arr
+
+
+def project_frame(disparity, rgb=None, step=REFERENCE_STEP, camera=None):
+    """Array form: (xyz (N,3) float64, rgb (N,3) uint8 or None) in reference order."""
+    disp = _as_u8(disparity, 2, "disparity")
+    h, w = disp.shape
+    bgr = None
+    if rgb is not None and len(rgb) > 0:
+        bgr = _as_u8(rgb, 3, "rgb")
+        if bgr.shape[0] < h or bgr.shape[1] < w or bgr.shape[2] < 3:
+            raise IndexError(f"rgb shape {bgr.shape} smaller than disparity {disp.shape}")
+        if bgr.shape[2] != 3:
+            bgr = np.ascontiguousarray(bgr[:, :, :3])
+    hg = (h - 1 + step - 1) // step if h > 1 else 0
+    wg = (w - 1 + step - 1) // step if w > 1 else 0
+    cap = max(hg * wg, 1)
+    xyz = np.empty((cap, 3), np.float64)
+    out_rgb = np.empty((cap, 3), np.uint8) if bgr is not None else None
+    n = ctypes.c_int64(0)
+    cam = camera if camera is not None else _camera()
+    _abi.call("sv_project_frame", _abi.ptr(disp), h, w, disp.strides[0],
+              _abi.ptr(bgr), bgr.strides[0] if bgr is not None else 0, step, ctypes.byref(cam),
+              _abi.ptr(xyz), _abi.ptr(out_rgb), cap, ctypes.byref(n))
+    k = n.value
+    return xyz[:k], (out_rgb[:k] if out_rgb is not None else None)
+
+
+def projectDisparityTo3d(disparity, max_disparity, rgb=[]):  # noqa: N802,B006 (reference signature)
+    """functions.py:178-198 on the GPU. Returns a list of rows (see module doc)."""
+    xyz, rgbs = project_frame(disparity, rgb)
+    if rgbs is None:
+        rows = xyz
+    else:
+        rows = np.empty((len(xyz), 6), np.float64)
+        rows[:, :3] = xyz
+        rows[:, 3:] = rgbs
+    return list(rows)
+
+
+def project3DPointsTo2DImagePoints(points):  # noqa: N802
+    """functions.py:201-209 on the GPU: (N,2) float64 [x, y]."""
+    n = len(points)
+    if n == 0:
+        return np.zeros((0, 2), np.float64)
+    arr = points if isinstance(points, np.ndarray) else np.asarray(points)
+    arr = np.ascontiguousarray(arr, dtype=np.float64)
+    if arr.ndim != 2 or arr.shape[1] < 3:
+        raise ValueError(f"points must be rows of at least [X, Y, Z], got shape {arr.shape}")
+    out = np.empty((n, 2), np.float64)
+    cam = _camera()
+    _abi.call("sv_backproject", _abi.ptr(arr), n, arr.shape[1], ctypes.byref(cam), _abi.ptr(out))
+    return out
+
+
+# snake_case names used by BASELINE.json
+project_disparity_to_3d = projectDisparityTo3d
+project_3D_points_to_2D = project3DPointsTo2DImagePoints
+
+PATCHED = ("projectDisparityTo3d", "project3DPointsTo2DImagePoints")
+
+
+def install(functions_module):
+    """Patch the reference's `functions` module in place (stereovision.py resolves
+    f.<name> at call time, so performStereoVision picks the GPU path up)."""
+    global _module
+    _abi.lib()  # fail loudly now if libsvx is missing
+    _module = functions_module
+    for name in PATCHED:
+        setattr(functions_module, name, globals()[name])
+    functions_module.project_disparity_to_3d = projectDisparityTo3d
+    functions_module.project_3D_points_to_2D = project3DPointsTo2DImagePoints
+    return functions_module
+
+
+def uninstall():
+    global _module
+    _module = None
