@@ -6,22 +6,23 @@
 // points in reference (raster) order as fp32 XYZ + int32 (x,y) back-projection
 // (functions.py:201-209 + stereovision.py:112).
 //
-// The histogram must be complete before any point can be filtered, so each
-// chunk of frames takes two launches:
-//   pass 1  hist_kernel     frames x slices workgroups; LDS histogram (4 KB),
-//                           flushed with one global atomic per non-zero bin.
-//   pass 2  compact_kernel  one 4096-point tile per workgroup; wave ballot/scan
-//                           + LDS block scan inside the tile, decoupled
-//                           look-back across the tiles of a frame (tile ids
-//                           from an atomic ticket => forward progress).
-// A chunk is small enough (default 16 frames = 36 MB of input) that pass 2
-// re-reads its inputs from the 256 MB Infinity Cache rather than HBM.
+// The histogram must be complete before any point of a frame can be filtered,
+// so every frame is visited twice:
+//   pass 1  hist_tile     LDS histogram (4 KB) per 4096-point tile, flushed with
+//                         one global atomic per non-zero bin; N_valid, N_kept.
+//   pass 2  compact_tile  wave ballot/scan + LDS block scan inside the tile,
+//                         decoupled look-back across the tiles of a frame,
+//                         then fp32 XYZ + int32 (x,y) stores.
+// Frames go in chunks; launch c runs pass 2 of chunk c-1 together with pass 1
+// of chunk c (one ticketed grid), so a chunk's second read comes from the
+// 256 MB Infinity Cache shortly after its first, and there are chunks+1
+// launches per call. All control words (histograms, counts, look-back
+// granules, per-launch tickets) are zeroed by one memset per call.
 #include "../svx_launch.h"
 
 namespace svx {
 
-constexpr int kHistQuadsPerThread = 16;   // pass-1 slice = 256 x 16 quads
-constexpr int kQPT = 4;                   // pass-2 tile  = 256 x 4 quads = 4096 points
+constexpr int kQPT = 4;   // tile = 256 lanes x 4 quads = 4096 grid points (both passes)
 
 template <int STEP>
 struct QuadIn {
@@ -57,7 +58,7 @@ __device__ __forceinline__ int eval_point(const QuadIn<STEP>& in, int k, int gx,
     const uint32_t d = in.d[k];
     if (d == 0 || gx >= p.Wg) return 0;
     const int x = gx * STEP;
-    const float xc = (float)((double)x - p.cw);
+    const float xc = centred(x, p.cw_hi, p.cw_lo);
     const float r = __builtin_amdgcn_rcpf((float)d);
     const float K = p.B32 * r;
     const float X = xc * K, Y = yc * K, Z = p.fB32 * r;
@@ -68,85 +69,101 @@ __device__ __forceinline__ int eval_point(const QuadIn<STEP>& in, int k, int gx,
     return 1 + hue_bin(R, G, B);
 }
 
-int pipeline_slices_per_frame(const KParams& p) {
-    const int per = 256 * kHistQuadsPerThread;
-    return (p.frame_quads + per - 1) / per;
-}
-
 int pipeline_tiles_per_frame(const KParams& p) {
     const int per = 256 * kQPT;
     return (p.frame_quads + per - 1) / per;
 }
 
-// ---------------------------------------------------------------------------
-// pass 1: histogram + N_valid / N_kept. Also zeroes pass 2's look-back state.
-// ---------------------------------------------------------------------------
-template <int STEP>
-__global__ __launch_bounds__(256) void hist_kernel(PipeBuffers bf, int frame0, int slices,
-                                                   int status_words, KParams p) {
-    __shared__ uint32_t sh_hist[kBins];
-    __shared__ uint32_t sh_cnt[2];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < kBins; i += 256) sh_hist[i] = 0;
-    if (tid < 2) sh_cnt[tid] = 0;
-    // zero this chunk's look-back granules and ticket (pass 2 runs after us)
-    {
-        const int per = (status_words + gridDim.x - 1) / gridDim.x;
-        const int s0 = blockIdx.x * per;
-        for (int i = s0 + tid; i < s0 + per && i < status_words; i += 256) bf.status[i] = 0;
-        if (blockIdx.x == 0 && tid == 0) *bf.ticket = 0;
-    }
-    __syncthreads();
 
-    const int fl = blockIdx.x / slices;
-    const int slice = blockIdx.x - fl * slices;
-    const int frame = frame0 + fl;
+// Issue every load of the lane's kQPT quads before any use (memory-level
+// parallelism: 4 x 16 B per lane in flight).
+template <int STEP>
+__device__ __forceinline__ void load_tile(const uint8_t* disp, const uint8_t* bgr, int qbase, int tid,
+                                          const KParams& p, QuadIn<STEP> (&in)[kQPT], int (&gy)[kQPT],
+                                          int (&q)[kQPT]) {
+#pragma unroll
+    for (int i = 0; i < kQPT; ++i) {
+        // branch-free: out-of-range lanes re-load the last quad and are masked
+        // (keeps the arrays in registers and every load in flight together)
+        const int qi = qbase + i * 256 + tid;
+        const bool ok = qi < p.frame_quads;
+        const int qc = ok ? qi : p.frame_quads - 1;
+        const int g = qc / p.Q;
+        q[i] = qc - g * p.Q;
+        gy[i] = ok ? g : -1;
+        const int y = g * STEP;
+        load_quad<STEP>(disp + (int64_t)y * p.W, bgr + (int64_t)y * p.W * 3, q[i], in[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < kQPT; ++i) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) in[i].d[k] = gy[i] < 0 ? 0u : in[i].d[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// pass 1 tile: LDS histogram of the plane-kept points + N_valid / N_kept.
+// ---------------------------------------------------------------------------
+struct PipeShared {
+    uint32_t hist[kBins];         // pass 1
+    uint32_t okbits[kBins / 32];  // pass 2: hist[bin] > hist_thr
+    uint64_t wave[4];             // pass 2 block scan
+    uint32_t cnt[2];
+    uint32_t tile, excl;
+};
+
+template <int STEP>
+__device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int tile, const KParams& p,
+                                          PipeShared& sh) {
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kBins; i += 256) sh.hist[i] = 0;
+    if (tid < 2) sh.cnt[tid] = 0;
     const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
     const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
-    const int q0 = slice * 256 * kHistQuadsPerThread;
-    const int q1 = min(q0 + 256 * kHistQuadsPerThread, p.frame_quads);
+    QuadIn<STEP> in[kQPT];
+    int gy[kQPT], q[kQPT];
+    load_tile<STEP>(disp, bgr, tile * 256 * kQPT, tid, p, in, gy, q);
+    __syncthreads();
     uint32_t nv = 0, nk = 0;
-    for (int qi = q0 + tid; qi < q1; qi += 256) {
-        const int gy = qi / p.Q;
-        const int q = qi - gy * p.Q;
-        const int y = gy * STEP;
-        QuadIn<STEP> in;
-        load_quad<STEP>(disp + (int64_t)y * p.W, bgr + (int64_t)y * p.W * 3, q, in);
-        const float yc = (float)((double)y - p.ch);
+#pragma unroll
+    for (int i = 0; i < kQPT; ++i) {
+        if (gy[i] < 0) continue;
+        const int y = gy[i] * STEP;
+        const float yc = centred(y, p.ch_hi, p.ch_lo);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int gx = 4 * q + k;
-            nv += (in.d[k] != 0 && gx < p.Wg) ? 1u : 0u;
-            const int e = eval_point<STEP>(in, k, gx, y, yc, p);
+            const int gx = 4 * q[i] + k;
+            nv += (in[i].d[k] != 0 && gx < p.Wg) ? 1u : 0u;
+            const int e = eval_point<STEP>(in[i], k, gx, y, yc, p);
             if (e) {
                 ++nk;
-                atomicAdd(&sh_hist[e - 1], 1u);
+                atomicAdd(&sh.hist[e - 1], 1u);
             }
         }
     }
     nv = wave_sum(nv);
     nk = wave_sum(nk);
     if (lane_id() == 0) {
-        atomicAdd(&sh_cnt[0], nv);
-        atomicAdd(&sh_cnt[1], nk);
+        atomicAdd(&sh.cnt[0], nv);
+        atomicAdd(&sh.cnt[1], nk);
     }
     __syncthreads();
     if (tid == 0) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(bf.counts + 4 * frame + 0), (unsigned long long)sh_cnt[0]);
-        atomicAdd(reinterpret_cast<unsigned long long*>(bf.counts + 4 * frame + 1), (unsigned long long)sh_cnt[1]);
+        atomicAdd(reinterpret_cast<unsigned long long*>(bf.counts + 4 * frame + 0), (unsigned long long)sh.cnt[0]);
+        atomicAdd(reinterpret_cast<unsigned long long*>(bf.counts + 4 * frame + 1), (unsigned long long)sh.cnt[1]);
     }
     uint32_t* gh = bf.hist + (int64_t)frame * kBins;
     for (int i = tid; i < kBins; i += 256) {
-        const uint32_t v = sh_hist[i];
+        const uint32_t v = sh.hist[i];
         if (v) atomicAdd(gh + i, v);
     }
 }
 
 // ---------------------------------------------------------------------------
-// pass 2: keep2 filter, ordered compaction, fp32 XYZ + int32 (x, y).
+// pass 2 tile: keep2 filter, ordered compaction, fp32 XYZ + int32 (x, y).
 // Tile = 256 lanes x kQPT quads; quad (i, lane) = tile_base + i*256 + lane, so
-// each load/store wave-instruction is contiguous; the raster order inside the
-// tile is (i, lane), scanned with 4 x 16-bit fields packed in one u64.
+// each load wave-instruction is contiguous; the raster order inside the tile
+// is (i, lane), scanned with 4 x 16-bit fields packed in one u64.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
     const int lane = lane_id();
@@ -159,69 +176,55 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
 }
 
 template <int STEP>
-__global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0, int tiles, KParams p) {
-    __shared__ uint32_t sh_okbits[kBins / 32];
-    __shared__ uint64_t sh_wave[4];
-    __shared__ uint32_t sh_tile, sh_excl;
+__device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, int tile, int tiles,
+                                             const KParams& p, PipeShared& sh) {
     const int tid = threadIdx.x;
-    if (tid == 0) sh_tile = atomicAdd(bf.ticket, 1u);
-    __syncthreads();
-    const int g = (int)sh_tile;
-    const int fl = g / tiles;
-    const int tile = g - fl * tiles;
-    const int frame = frame0 + fl;
+    const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
+    const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
+    const int qbase = tile * 256 * kQPT;
+    QuadIn<STEP> in[kQPT];
+    int gyv[kQPT], qv[kQPT];
+    load_tile<STEP>(disp, bgr, qbase, tid, p, in, gyv, qv);
     {   // hist[bin] > hist_thr as a 1024-bit mask
         const uint32_t* gh = bf.hist + (int64_t)frame * kBins;
         const int wave = tid >> 6;
 #pragma unroll
         for (int r = 0; r < kBins / 256; ++r) {
-            const int bin = r * 256 + tid;
-            const uint64_t m = __ballot((int64_t)gh[bin] > (int64_t)p.hist_thr);
+            const uint64_t m = __ballot((int64_t)gh[r * 256 + tid] > (int64_t)p.hist_thr);
             if (lane_id() == 0) {
-                sh_okbits[(r * 256 + wave * 64) / 32] = (uint32_t)m;
-                sh_okbits[(r * 256 + wave * 64) / 32 + 1] = (uint32_t)(m >> 32);
+                sh.okbits[(r * 256 + wave * 64) / 32] = (uint32_t)m;
+                sh.okbits[(r * 256 + wave * 64) / 32 + 1] = (uint32_t)(m >> 32);
             }
         }
     }
     __syncthreads();
-
-    const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
-    const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
-    const int qbase = tile * 256 * kQPT;
     uint32_t dpack[kQPT];
     uint32_t keep = 0;  // bit 4*i + k
     uint64_t cnt = 0;
 #pragma unroll
     for (int i = 0; i < kQPT; ++i) {
-        const int qi = qbase + i * 256 + tid;
-        dpack[i] = 0;
-        if (qi < p.frame_quads) {
-            const int gy = qi / p.Q;
-            const int q = qi - gy * p.Q;
-            const int y = gy * STEP;
-            QuadIn<STEP> in;
-            load_quad<STEP>(disp + (int64_t)y * p.W, bgr + (int64_t)y * p.W * 3, q, in);
-            dpack[i] = in.d[0] | (in.d[1] << 8) | (in.d[2] << 16) | (in.d[3] << 24);
-            const float yc = (float)((double)y - p.ch);
+        dpack[i] = in[i].d[0] | (in[i].d[1] << 8) | (in[i].d[2] << 16) | (in[i].d[3] << 24);
+        if (gyv[i] < 0) continue;
+        const int y = gyv[i] * STEP;
+        const float yc = centred(y, p.ch_hi, p.ch_lo);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int e = eval_point<STEP>(in, k, 4 * q + k, y, yc, p);
-                if (e && ((sh_okbits[(e - 1) >> 5] >> ((e - 1) & 31)) & 1)) {
-                    keep |= 1u << (4 * i + k);
-                    cnt += 1ull << (16 * i);
-                }
+        for (int k = 0; k < 4; ++k) {
+            const int e = eval_point<STEP>(in[i], k, 4 * qv[i] + k, y, yc, p);
+            if (e && ((sh.okbits[(e - 1) >> 5] >> ((e - 1) & 31)) & 1)) {
+                keep |= 1u << (4 * i + k);
+                cnt += 1ull << (16 * i);
             }
         }
     }
     // block scan of the packed per-quad-row counts
     const uint64_t inc = wave_incl_scan64(cnt);
     const int wave = tid >> 6;
-    if (lane_id() == 63) sh_wave[wave] = inc;
+    if (lane_id() == 63) sh.wave[wave] = inc;
     __syncthreads();
     uint64_t wbase = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-        const uint64_t t = sh_wave[w];
+        const uint64_t t = sh.wave[w];
         wbase += (w < wave) ? t : 0ull;
         tot += t;
     }
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0
     for (int i = 0; i < kQPT; ++i) total += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
 
     if (wave == 0) {
-        uint64_t* st = bf.status + (int64_t)fl * tiles;
+        uint64_t* st = bf.status + (int64_t)frame * tiles;
         uint32_t excl = 0;
         if (tile == 0) {
             if (tid == 0) publish(st, kFlagInc, total);
@@ -241,14 +244,14 @@ __global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0
             if (tid == 0) publish(st + tile, kFlagInc, excl + total);
         }
         if (tid == 0) {
-            sh_excl = excl;
+            sh.excl = excl;
             if (tile == tiles - 1) bf.counts[4 * frame + 2] = excl + total;
         }
     }
     __syncthreads();
     if (!keep) return;
 
-    const int64_t fbase = (int64_t)frame * bf.cap + sh_excl;
+    const int64_t fbase = (int64_t)frame * bf.cap + sh.excl;
     float* oxyz = bf.xyz;
     int32_t* opts = bf.pts;
     uint32_t rowbase = 0;
@@ -258,18 +261,16 @@ __global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0
         rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
         const uint32_t km = (keep >> (4 * i)) & 0xF;
         if (!km) continue;
-        const int qi = qbase + i * 256 + tid;
-        const int gy = qi / p.Q;
-        const int q = qi - gy * p.Q;
-        const int y = gy * STEP;
-        const float yc = (float)((double)y - p.ch);
+        const int q = qv[i];
+        const int y = gyv[i] * STEP;
+        const float yc = centred(y, p.ch_hi, p.ch_lo);
         const int dyw = y >> 5, dyb = y & 31;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!(km & (1u << k))) continue;
             const uint32_t d = (dpack[i] >> (8 * k)) & 0xFF;
             const int x = (4 * q + k) * STEP;
-            const float xc = (float)((double)x - p.cw);
+            const float xc = centred(x, p.cw_hi, p.cw_lo);
             const float r = __builtin_amdgcn_rcpf((float)d);
             const float K = p.B32 * r;
             const int64_t at = fbase + o;
@@ -284,20 +285,44 @@ __global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0
     }
 }
 
-hipError_t launch_pipeline_chunk(const KParams& p, const PipeBuffers& b, int frame0, int frames,
-                                 hipStream_t s) {
-    const int slices = pipeline_slices_per_frame(p);
-    const int tiles = pipeline_tiles_per_frame(p);
-    const int status_words = frames * tiles;
-    const dim3 g1(frames * slices), g2(frames * tiles), blk(256);
-    if (p.step == 1) {
-        hipLaunchKernelGGL(hist_kernel<1>, g1, blk, 0, s, b, frame0, slices, status_words, p);
-        hipLaunchKernelGGL(compact_kernel<1>, g2, blk, 0, s, b, frame0, tiles, p);
-    } else if (p.step == 2) {
-        hipLaunchKernelGGL(hist_kernel<2>, g1, blk, 0, s, b, frame0, slices, status_words, p);
-        hipLaunchKernelGGL(compact_kernel<2>, g2, blk, 0, s, b, frame0, tiles, p);
+// ---------------------------------------------------------------------------
+// One launch = pass 2 of chunk c (tickets [0, n2)) + pass 1 of chunk c+1
+// (tickets [n2, n2+n1)). The ticket order puts every look-back predecessor in
+// front of its successor, and pass 1 tiles never wait on anything.
+// ---------------------------------------------------------------------------
+template <int STEP>
+__global__ __launch_bounds__(256) void pipeline_kernel(PipeBuffers bf, int p2_frame0, int p2_frames,
+                                                       int p1_frame0, int tiles, uint32_t* ticket,
+                                                       KParams p) {
+    __shared__ PipeShared sh;
+    if (threadIdx.x == 0) sh.tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int g = (int)sh.tile;
+    const int n2 = p2_frames * tiles;
+    if (g < n2) {
+        const int fl = g / tiles;
+        compact_tile<STEP>(bf, p2_frame0 + fl, g - fl * tiles, tiles, p, sh);
     } else {
-        return hipErrorInvalidValue;
+        const int h = g - n2;
+        const int fl = h / tiles;
+        hist_tile<STEP>(bf, p1_frame0 + fl, h - fl * tiles, p, sh);
+    }
+}
+
+hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk,
+                           uint32_t* tickets, hipStream_t s) {
+    const int tiles = pipeline_tiles_per_frame(p);
+    const int nchunks = (frames + chunk - 1) / chunk;
+    for (int c = 0; c <= nchunks; ++c) {
+        const int f2 = (c - 1) * chunk, n2 = c >= 1 ? min(chunk, frames - f2) : 0;
+        const int f1 = c * chunk, n1 = c < nchunks ? min(chunk, frames - f1) : 0;
+        const dim3 grid((n2 + n1) * tiles), blk(256);
+        if (p.step == 1)
+            hipLaunchKernelGGL(pipeline_kernel<1>, grid, blk, 0, s, b, f2, n2, f1, tiles, tickets + c, p);
+        else if (p.step == 2)
+            hipLaunchKernelGGL(pipeline_kernel<2>, grid, blk, 0, s, b, f2, n2, f1, tiles, tickets + c, p);
+        else
+            return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

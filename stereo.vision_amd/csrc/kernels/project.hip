@@ -125,12 +125,12 @@ __global__ __launch_bounds__(256) void project_dense_kernel(const uint8_t* __res
         const uint8_t* drow = disp + (int64_t)fl * p.frame_px + (int64_t)y * p.W;
         uint32_t d[4];
         load_disp_quad<STEP>(drow, q, d);
-        const float yc = (float)((double)y - p.ch);
+        const float yc = centred(y, p.ch_hi, p.ch_lo);
         float ox[4], oy[4], oz[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int gx = 4 * q + k;
-            const float xc = (float)((double)(gx * STEP) - p.cw);
+            const float xc = centred(gx * STEP, p.cw_hi, p.cw_lo);
             const float r = __builtin_amdgcn_rcpf((float)d[k]);
             const float K = p.B32 * r;
             const bool ok = (d[k] != 0) && (gx < p.Wg);

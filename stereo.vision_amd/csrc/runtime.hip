@@ -108,6 +108,10 @@ KParams make_params(int H, int W, int step, const sv_camera& cam) {
     p.fB = cam.f * cam.B;  // functions.py:191 evaluates f*B in fp64
     p.fB32 = (float)p.fB;
     p.B32 = (float)cam.B;
+    p.cw_hi = (float)cam.cw;
+    p.cw_lo = (float)(cam.cw - (double)p.cw_hi);
+    p.ch_hi = (float)cam.ch;
+    p.ch_lo = (float)(cam.ch - (double)p.ch_hi);
     p.dx_words = (W + 31) / 32;
     p.dy_words = (H + 31) / 32;
     return p;
@@ -183,7 +187,15 @@ struct sv_batch {
     int64_t Ng = 0;            // grid points per frame
     int64_t dense_per_frame = 0;
     hipStream_t stream = nullptr;
-    DevBuf disp, bgr, X, Y, Z, xyz, pts, hist, counts, status, ctrl;
+    DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl;
+    // pipeline control block (one memset per call): hist | counts | look-back
+    // granules | per-launch tickets | err
+    uint32_t* hist = nullptr;
+    int64_t* counts = nullptr;
+    uint64_t* status = nullptr;
+    uint32_t* tickets = nullptr;
+    uint32_t* err = nullptr;
+    size_t ctrl_bytes = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_ms[2] = {0, 0};
     bool have_ms[2] = {false, false};
@@ -337,8 +349,23 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
         e = b->xyz.ensure(sizeof(float) * 3 * (size_t)b->Ng * frames);
         if (e == hipSuccess) e = b->pts.ensure(sizeof(int32_t) * 2 * (size_t)b->Ng * frames);
     }
-    if (e == hipSuccess) e = b->hist.ensure(sizeof(uint32_t) * kBins * (size_t)frames);
-    if (e == hipSuccess) e = b->counts.ensure(sizeof(int64_t) * 4 * (size_t)frames);
+    if (e == hipSuccess) {
+        // worst case: chunk = 1 -> frames + 1 launches
+        const size_t tiles = (size_t)pipeline_tiles_per_frame(b->kp);
+        const size_t hist_b = sizeof(uint32_t) * kBins * frames, cnt_b = sizeof(int64_t) * 4 * frames;
+        const size_t st_b = sizeof(uint64_t) * tiles * frames, tk_b = sizeof(uint32_t) * (frames + 2 + 2);
+        e = b->ctrl.ensure(hist_b + cnt_b + st_b + tk_b);
+        if (e == hipSuccess) {
+            char* base = b->ctrl.as<char>();
+            b->hist = reinterpret_cast<uint32_t*>(base);
+            b->counts = reinterpret_cast<int64_t*>(base + hist_b);
+            b->status = reinterpret_cast<uint64_t*>(base + hist_b + cnt_b);
+            b->tickets = reinterpret_cast<uint32_t*>(base + hist_b + cnt_b + st_b);
+            b->err = b->tickets + frames + 2;
+            b->ctrl_bytes = hist_b + cnt_b + st_b + tk_b;
+            e = hipMemset(b->ctrl.p, 0, b->ctrl_bytes);
+        }
+    }
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
     if (e != hipSuccess) {
         sv_batch_destroy(b);
@@ -352,8 +379,7 @@ int sv_batch_destroy(sv_batch* b) {
     if (!b) return SV_OK;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
-    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->hist, &b->counts,
-                      &b->status, &b->ctrl})
+    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl})
         if (x->p) (void)hipFree(x->p);
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -368,7 +394,7 @@ int sv_batch_info(const sv_batch* b, int64_t* o) {
     o[1] = b->kp.Wg;
     o[2] = b->kp.pitch;
     o[3] = b->Ng;
-    o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->pts.bytes);
+    o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->pts.bytes + b->ctrl.bytes);
     o[5] = b->frames;
     o[6] = b->H;
     o[7] = b->W;
@@ -434,18 +460,14 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     const size_t cap = (size_t)b->Ng;
     HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames));
     HIP_TRY(b->pts.ensure(sizeof(int32_t) * 2 * cap * b->frames));
-    const int tiles = pipeline_tiles_per_frame(p);
-    HIP_TRY(b->status.ensure(sizeof(uint64_t) * (size_t)tiles * chunk));
-    HIP_TRY(b->ctrl.ensure(64));
     if (int rc = ensure_tables(*d, b->H, b->W, *cam, b->stream)) return rc;
     PipeBuffers bf;
     bf.disp = b->disp.as<uint8_t>();
     bf.bgr = b->bgr.as<uint8_t>();
-    bf.hist = b->hist.as<uint32_t>();
-    bf.counts = b->counts.as<int64_t>();
-    bf.status = b->status.as<uint64_t>();
-    bf.ticket = b->ctrl.as<uint32_t>();
-    bf.err = b->ctrl.as<uint32_t>() + 1;
+    bf.hist = b->hist;
+    bf.counts = b->counts;
+    bf.status = b->status;
+    bf.err = b->err;
     bf.xyz = b->xyz.as<float>();
     bf.pts = b->pts.as<int32_t>();
     bf.dxbits = d->tables.dx.as<uint32_t>();
@@ -454,13 +476,8 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     int t0, t1;
     HIP_TRY(hipEventRecord(b->ev[2], b->stream));
     HIP_TRY(b->timed_event(&t0));
-    HIP_TRY(hipMemsetAsync(b->hist.p, 0, sizeof(uint32_t) * kBins * (size_t)b->frames, b->stream));
-    HIP_TRY(hipMemsetAsync(b->counts.p, 0, sizeof(int64_t) * 4 * (size_t)b->frames, b->stream));
-    HIP_TRY(hipMemsetAsync(b->ctrl.p, 0, 64, b->stream));
-    for (int f0 = 0; f0 < b->frames; f0 += chunk) {
-        const int n = (b->frames - f0) < chunk ? (b->frames - f0) : chunk;
-        HIP_TRY(launch_pipeline_chunk(p, bf, f0, n, b->stream));
-    }
+    HIP_TRY(hipMemsetAsync(b->ctrl.p, 0, b->ctrl_bytes, b->stream));
+    HIP_TRY(launch_pipeline(p, bf, b->frames, chunk, b->tickets, b->stream));
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[3], b->stream));
     b->pending[1].push_back({t0, t1});
@@ -468,7 +485,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     if (sync) {
         HIP_TRY(hipStreamSynchronize(b->stream));
         uint32_t err = 0;
-        HIP_TRY(hipMemcpy(&err, bf.err, 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&err, b->err, 4, hipMemcpyDeviceToHost));
         if (err) return fail(SV_E_DEVICE, "pipeline look-back timed out");
     }
     return SV_OK;
@@ -486,9 +503,9 @@ int sv_batch_sync(sv_batch* b) {
     if (!b) return fail(SV_E_ARG, "null");
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
-    if (b->ctrl.p) {
+    if (b->err) {
         uint32_t err = 0;
-        HIP_TRY(hipMemcpy(&err, b->ctrl.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&err, b->err, 4, hipMemcpyDeviceToHost));
         if (err) return fail(SV_E_DEVICE, "pipeline look-back timed out");
     }
     return SV_OK;
@@ -544,7 +561,7 @@ int sv_batch_read_counts(sv_batch* b, int64_t* counts) {
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
     int64_t* tmp = new int64_t[4 * (size_t)b->frames];
-    hipError_t e = hipMemcpy(tmp, b->counts.p, sizeof(int64_t) * 4 * b->frames, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpy(tmp, b->counts, sizeof(int64_t) * 4 * b->frames, hipMemcpyDeviceToHost);
     if (e == hipSuccess)
         for (int f = 0; f < b->frames; ++f)
             for (int k = 0; k < 3; ++k) counts[3 * f + k] = tmp[4 * f + k];
@@ -557,7 +574,7 @@ int sv_batch_read_hist(sv_batch* b, int frame, uint32_t* hist) {
     if (!b || !hist || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "bad args");
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
-    HIP_TRY(hipMemcpy(hist, b->hist.as<uint32_t>() + (size_t)kBins * frame, 4 * kBins, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(hist, b->hist + (size_t)kBins * frame, 4 * kBins, hipMemcpyDeviceToHost));
     return SV_OK;
 }
 
@@ -566,7 +583,7 @@ int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
     int64_t c[4];
-    HIP_TRY(hipMemcpy(c, b->counts.as<int64_t>() + 4 * (size_t)frame, sizeof c, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(c, b->counts + 4 * (size_t)frame, sizeof c, hipMemcpyDeviceToHost));
     *n = c[2];
     if (c[2] > cap) return fail(SV_E_CAP, "capacity %lld < %lld", (long long)cap, (long long)c[2]);
     const size_t base = (size_t)b->Ng * frame;

@@ -26,6 +26,7 @@ struct KParams {
     // camera (functions.py:15-22)
     double f, B, cw, ch, fB;
     float fB32, B32;
+    float cw_hi, cw_lo, ch_hi, ch_lo;   // cw = cw_hi + cw_lo (fp32 split): x - cw in fp32 to 2^-23 rel
     // plane (a*X+b*Y+c*Z = 1) and thresholds
     double a, b, c, nrm, thr;
     float a32, b32, c32, thr32, inv_nrm32, guard32;   // guard32 = 2^-18 / nrm
@@ -38,7 +39,7 @@ struct KParams {
 // Hue bin: integer bin k <-> reference key str(round(colorsys hue, 3)).
 // exact rational t = 1000*n/(6*rng) (n in [0, 6 rng)); fp64 only on exact ties.
 // ---------------------------------------------------------------------------
-__device__ __noinline__ int hue_bin_tie_f64(int r, int g, int b, int mx, int mn) {
+__device__ __forceinline__ int hue_bin_tie_f64(int r, int g, int b, int mx, int mn) {
     // colorsys.rgb_to_hsv on numpy uint8 scalars, then numpy round(h, 3).
     const double rng = (double)(mx - mn);
     const double rc = (double)(mx - r) / rng;
@@ -80,11 +81,18 @@ __device__ __forceinline__ int hue_bin(int r, int g, int b) {
     return hue_bin_tie_f64(r, g, b, mx, mn);   // exact .5 tie: reference fp64 decides
 }
 
+// x - c in fp32 with relative error <= 2^-23 for any fp64 centre c: the first
+// subtraction is exact whenever x and c_hi are within 2x of each other
+// (Sterbenz), and otherwise |x - c| is large so one rounding costs 2^-24.
+__device__ __forceinline__ float centred(int x, float c_hi, float c_lo) {
+    return ((float)x - c_hi) - c_lo;
+}
+
 // ---------------------------------------------------------------------------
 // Plane keep test (functions.py:300-323) for grid pixel (x, y) with d > 0.
-// K = B/d (fp32), xc = x - cw, yc = y - ch (exact in fp32).
+// K = B/d (fp32), xc = x - cw, yc = y - ch (fp32, rel err <= 2^-23).
 // ---------------------------------------------------------------------------
-__device__ __noinline__ bool keep1_f64(int x, int y, uint32_t d, const KParams& p) {
+__device__ __forceinline__ bool keep1_f64(int x, int y, uint32_t d, const KParams& p) {
     const double Z = p.fB / (double)d;
     const double X = (((double)x - p.cw) * Z) / p.f;
     const double Y = (((double)y - p.ch) * Z) / p.f;

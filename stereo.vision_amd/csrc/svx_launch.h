@@ -34,8 +34,7 @@ struct PipeBuffers {
     const uint8_t* bgr;
     uint32_t* hist;      // frames x 1024
     int64_t* counts;     // frames x 4 (N_valid, N_kept, N_kept2, spare)
-    uint64_t* status;    // chunk x tiles look-back granules
-    uint32_t* ticket;
+    uint64_t* status;    // frames x tiles look-back granules
     uint32_t* err;
     float* xyz;          // frames x cap x 3
     int32_t* pts;        // frames x cap x 2
@@ -44,8 +43,9 @@ struct PipeBuffers {
     int64_t cap;         // points per frame (Ng)
 };
 int pipeline_tiles_per_frame(const KParams& p);
-int pipeline_slices_per_frame(const KParams& p);
-hipError_t launch_pipeline_chunk(const KParams& p, const PipeBuffers& b, int frame0, int frames,
-                                 hipStream_t s);
+// frames in chunks of `chunk`: chunks+1 launches; tickets[chunks+1] and the
+// look-back granules (frames x tiles) must be zero on entry.
+hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk,
+                           uint32_t* tickets, hipStream_t s);
 
 }  // namespace svx

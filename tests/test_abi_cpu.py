@@ -1,0 +1,97 @@
+"""CPU-only checks of the boundary: libsvx.so loads, exports every symbol that
+include/svx.h declares, the ctypes table matches, and the host-side drop-in
+logic behaves (no compute calls: there is no GPU here)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "svx.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sv_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from svx import _abi
+    lib = _abi.LIB_PATH
+    assert os.path.exists(lib), "run __graft_entry__.build() first"
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+
+
+def test_ctypes_table_covers_header():
+    from svx import _abi
+    assert set(declared_symbols()) == set(_abi.SIGNATURES)
+    lib = _abi.lib()
+    for name in _abi.SIGNATURES:
+        assert getattr(lib, name) is not None
+    assert _abi.lib().sv_version().decode().startswith("svx")
+
+
+def test_library_is_gfx950():
+    """The fat binary embeds gfx950 code objects (bundle id amdgcn-amd-amdhsa--gfx950)."""
+    from svx import _abi
+    blob = open(_abi.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_no_device_errors_are_raised_not_faked():
+    """Without a GPU every compute entry point must fail loudly (no CPU fallback)."""
+    import svx
+    from svx import SvxError, batch, dropin
+    if svx.device_count() > 0:
+        pytest.skip("GPU present")
+    with pytest.raises(SvxError):
+        dropin.projectDisparityTo3d(np.ones((8, 8), np.uint8), 128)
+    with pytest.raises(SvxError):
+        dropin.project3DPointsTo2DImagePoints([[1.0, 2.0, 3.0]])
+    with pytest.raises(SvxError):
+        batch.Batch(1)
+
+
+def test_dropin_argument_checks_before_device():
+    from svx import dropin
+    with pytest.raises(TypeError):
+        dropin.projectDisparityTo3d(np.zeros((4, 4), np.float64), 128)
+    with pytest.raises(ValueError):
+        dropin.projectDisparityTo3d(np.zeros((4, 4, 2), np.uint8), 128)
+    assert len(dropin.project3DPointsTo2DImagePoints([])) == 0
+    assert np.array(dropin.project3DPointsTo2DImagePoints([]), np.int32).reshape((-1, 1, 2)).shape == (0, 1, 2)
+
+
+def test_install_patches_module_attributes():
+    import types
+
+    from svx import dropin
+    m = types.SimpleNamespace(camera_focal_length_px=1.0, stereo_camera_baseline_m=2.0,
+                              image_centre_w=3.0, image_centre_h=4.0,
+                              projectDisparityTo3d=None, project3DPointsTo2DImagePoints=None)
+    dropin.install(m)
+    try:
+        assert m.projectDisparityTo3d is dropin.projectDisparityTo3d
+        assert m.project3DPointsTo2DImagePoints is dropin.project3DPointsTo2DImagePoints
+        assert m.project_disparity_to_3d is dropin.projectDisparityTo3d
+        assert m.project_3D_points_to_2D is dropin.project3DPointsTo2DImagePoints
+        cam = dropin._camera()
+        assert (cam.f, cam.B, cam.cw, cam.ch) == (1.0, 2.0, 3.0, 4.0)
+    finally:
+        dropin.uninstall()
+    cam = dropin._camera()
+    assert (cam.f, cam.B, cam.cw, cam.ch) == dropin.DEFAULT_CAMERA
+
+
+def test_header_cites_reference():
+    src = open(HEADER).read()
+    for cite in ("functions.py:178-198", "functions.py:201-209", "stereovision.py:84"):
+        assert cite in src

@@ -1,0 +1,87 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the sharded driver's host
+logic: frame sharding, max-over-ranks timing, the RCCL unique-id hand-off
+path (bytes broadcast) and the per-frame independence the sharding relies on
+(checked with the oracle standing in for the device)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_partitions_exactly():
+    from svx.dist import shard
+    for total in (1, 7, 4096, 32768, 32769):
+        for world in (1, 2, 3, 8):
+            spans = [shard(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0
+            for (f0, c0), (f1, _) in zip(spans, spans[1:]):
+                assert f0 + c0 == f1
+            assert sum(c for _, c in spans) == total
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import oracle
+    from svx import dist
+    ctrl = dist.Control()
+    try:
+        assert (ctrl.rank, ctrl.world) == (rank, world)
+        # unique-id style hand-off: 128 bytes from rank 0
+        payload = bytes(range(128)) if rank == 0 else bytes(128)
+        got = ctrl.broadcast_bytes(payload, src=0)
+        assert got == bytes(range(128))
+        mx = ctrl.max([float(rank + 1), -float(rank)])
+        sm = ctrl.sum([1.0, float(rank)])
+        # weak scaling: 2 frames per rank, global ids; per-frame results are independent
+        first, count = dist.shard(2 * world, world, rank)
+        counts = []
+        for f in range(first, first + count):
+            d, c = oracle.synth_frame(f)
+            crop = (np.ascontiguousarray(d[180:260]), np.ascontiguousarray(c[180:260]))
+            counts.append(oracle.pipeline_frame(*crop, 2, abc=oracle.synthetic_plane())["counts"])
+        tot = ctrl.sum(np.array(counts, np.float64).sum(axis=0))
+        ctrl.barrier()
+        q.put((rank, list(mx), list(sm), first, count, counts, list(tot)))
+    finally:
+        ctrl.close()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_control_plane_and_sharding():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    import oracle
+    ref = []
+    for f in range(2 * world):
+        d, c = oracle.synth_frame(f)
+        crop = (np.ascontiguousarray(d[180:260]), np.ascontiguousarray(c[180:260]))
+        ref.append(oracle.pipeline_frame(*crop, 2, abc=oracle.synthetic_plane())["counts"])
+    for rank, mx, sm, first, count, counts, tot in res:
+        assert mx == [2.0, 0.0] and sm == [2.0, 1.0]
+        assert (first, count) == (2 * rank, 2)
+        assert [tuple(c) for c in counts] == ref[first:first + count]
+        assert tot == list(np.array(ref, np.float64).sum(axis=0))

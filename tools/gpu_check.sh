@@ -13,9 +13,14 @@ rc=$?; echo "pytest rc=$rc"; tail -25 "$OUT/pytest_gpu.log"; stop_if_fatal $rc p
 [ "${SKIP_BENCH:-0}" = 1 ] && exit 0
 timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 5} > "$OUT/bench.log" 2>&1
 rc=$?; echo "bench rc=$rc"; tail -5 "$OUT/bench.log"; stop_if_fatal $rc bench
-[ "${SKIP_PROF:-0}" = 1 ] && exit 0
+if [ "${SKIP_PROF:-0}" != 1 ]; then
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
   python3 bench.py --steps 5 --warmup 1 --no-cpu > "$OUT/prof.log" 2>&1
-rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"
+rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"; stop_if_fatal $rc rocprof
 find "$OUT/prof" -name "*stats*" | head
+fi
+if [ -n "${SWEEP:-}" ]; then
+  timeout -k 10 600 python tools/sweep.py $SWEEP > "$OUT/sweep.log" 2>&1
+  rc=$?; echo "sweep rc=$rc"; cat "$OUT/sweep.log" | tail -20
+fi
