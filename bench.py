@@ -47,7 +47,9 @@ def parse():
     ap.add_argument("--step", type=int, default=1, help="grid step (reference hard-codes 2)")
     ap.add_argument("--chunk", type=int, default=0, help="pipeline frames per wave (0 = default)")
     ap.add_argument("--grid-cap", type=int, default=0)
-    ap.add_argument("--nt", type=int, default=0, help="non-temporal K1 stores")
+    ap.add_argument("--nt", type=int, default=1, help="non-temporal K1 stores (1 = measured faster)")
+    ap.add_argument("--ramp-ms", type=float, default=300.0,
+                    help="untimed K1 launches before the warmup steps, to let clocks settle")
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -112,6 +114,9 @@ def main():
     points_rank = ng * count
 
     # ---- headline: K1 dense projection --------------------------------------
+    t_ramp = time.perf_counter()
+    while (time.perf_counter() - t_ramp) * 1e3 < args.ramp_ms:
+        b.project(sync=True)
     for _ in range(args.warmup):
         b.project(sync=False)
     b.sync()

@@ -111,6 +111,7 @@ struct PipeShared {
     uint32_t cnt[2];
     uint32_t tile, excl;
 };
+static_assert(sizeof(PipeShared) < 8192, "LDS budget");
 
 template <int STEP>
 __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int tile, const KParams& p,
@@ -286,28 +287,36 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
 }
 
 // ---------------------------------------------------------------------------
-// One launch = pass 2 of chunk c (tickets [0, n2)) + pass 1 of chunk c+1
-// (tickets [n2, n2+n1)). The ticket order puts every look-back predecessor in
-// front of its successor, and pass 1 tiles never wait on anything.
+// One launch = pass 2 of chunk c-1 (blocks [0, n2*tiles)) + pass 1 of chunk c
+// (the rest). A pass-2 block is bound to a frame by blockIdx and takes its
+// tile id from that frame's ticket (one counter per frame, each on its own
+// 64-byte line: ~136 atomics per word instead of ~9K on one global word, which
+// saturates at ~88/us). A tile waits only on lower tiles of its own frame,
+// whose blocks took their tickets earlier and are therefore running: forward
+// progress does not depend on dispatch order. Pass-1 blocks wait on nothing.
 // ---------------------------------------------------------------------------
+constexpr int kTicketStride = 16;  // u32 words per frame ticket (64 B)
+
 template <int STEP>
 __global__ __launch_bounds__(256) void pipeline_kernel(PipeBuffers bf, int p2_frame0, int p2_frames,
-                                                       int p1_frame0, int tiles, uint32_t* ticket,
+                                                       int p1_frame0, int tiles, uint32_t* tickets,
                                                        KParams p) {
     __shared__ PipeShared sh;
-    if (threadIdx.x == 0) sh.tile = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int g = (int)sh.tile;
     const int n2 = p2_frames * tiles;
-    if (g < n2) {
-        const int fl = g / tiles;
-        compact_tile<STEP>(bf, p2_frame0 + fl, g - fl * tiles, tiles, p, sh);
+    const int bid = blockIdx.x;
+    if (bid < n2) {
+        const int frame = p2_frame0 + bid / tiles;
+        if (threadIdx.x == 0) sh.tile = atomicAdd(tickets + (int64_t)frame * kTicketStride, 1u);
+        __syncthreads();
+        compact_tile<STEP>(bf, frame, (int)sh.tile, tiles, p, sh);
     } else {
-        const int h = g - n2;
+        const int h = bid - n2;
         const int fl = h / tiles;
         hist_tile<STEP>(bf, p1_frame0 + fl, h - fl * tiles, p, sh);
     }
 }
+
+size_t pipeline_ticket_words(int frames) { return (size_t)frames * kTicketStride; }
 
 hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk,
                            uint32_t* tickets, hipStream_t s) {
@@ -318,9 +327,9 @@ hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, i
         const int f1 = c * chunk, n1 = c < nchunks ? min(chunk, frames - f1) : 0;
         const dim3 grid((n2 + n1) * tiles), blk(256);
         if (p.step == 1)
-            hipLaunchKernelGGL(pipeline_kernel<1>, grid, blk, 0, s, b, f2, n2, f1, tiles, tickets + c, p);
+            hipLaunchKernelGGL(pipeline_kernel<1>, grid, blk, 0, s, b, f2, n2, f1, tiles, tickets, p);
         else if (p.step == 2)
-            hipLaunchKernelGGL(pipeline_kernel<2>, grid, blk, 0, s, b, f2, n2, f1, tiles, tickets + c, p);
+            hipLaunchKernelGGL(pipeline_kernel<2>, grid, blk, 0, s, b, f2, n2, f1, tiles, tickets, p);
         else
             return hipErrorInvalidValue;
     }

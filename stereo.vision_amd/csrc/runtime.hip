@@ -200,7 +200,7 @@ struct sv_batch {
     float last_ms[2] = {0, 0};
     bool have_ms[2] = {false, false};
     int grid_cap = 0;          // K1 grid size cap (0 = one quad per lane)
-    int nontemporal = 0;       // K1 store flavour
+    int nontemporal = 1;       // K1 store flavour (non-temporal: measured faster)
     // per-launch timing accumulator: event pairs recorded on the batch stream
     std::vector<hipEvent_t> pool;
     std::vector<std::pair<int, int>> pending[2];  // (start idx, end idx) per op kind
@@ -353,7 +353,8 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
         // worst case: chunk = 1 -> frames + 1 launches
         const size_t tiles = (size_t)pipeline_tiles_per_frame(b->kp);
         const size_t hist_b = sizeof(uint32_t) * kBins * frames, cnt_b = sizeof(int64_t) * 4 * frames;
-        const size_t st_b = sizeof(uint64_t) * tiles * frames, tk_b = sizeof(uint32_t) * (frames + 2 + 2);
+        const size_t st_b = sizeof(uint64_t) * tiles * frames;
+        const size_t tk_b = sizeof(uint32_t) * (pipeline_ticket_words(frames) + 16);
         e = b->ctrl.ensure(hist_b + cnt_b + st_b + tk_b);
         if (e == hipSuccess) {
             char* base = b->ctrl.as<char>();
@@ -361,7 +362,7 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
             b->counts = reinterpret_cast<int64_t*>(base + hist_b);
             b->status = reinterpret_cast<uint64_t*>(base + hist_b + cnt_b);
             b->tickets = reinterpret_cast<uint32_t*>(base + hist_b + cnt_b + st_b);
-            b->err = b->tickets + frames + 2;
+            b->err = b->tickets + pipeline_ticket_words(frames);
             b->ctrl_bytes = hist_b + cnt_b + st_b + tk_b;
             e = hipMemset(b->ctrl.p, 0, b->ctrl_bytes);
         }

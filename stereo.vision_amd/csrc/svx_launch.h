@@ -43,8 +43,10 @@ struct PipeBuffers {
     int64_t cap;         // points per frame (Ng)
 };
 int pipeline_tiles_per_frame(const KParams& p);
-// frames in chunks of `chunk`: chunks+1 launches; tickets[chunks+1] and the
-// look-back granules (frames x tiles) must be zero on entry.
+// frames in chunks of `chunk`: chunks+1 launches; the per-frame tickets
+// (pipeline_ticket_words(frames) u32) and the look-back granules (frames x
+// tiles) must be zero on entry.
+size_t pipeline_ticket_words(int frames);
 hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk,
                            uint32_t* tickets, hipStream_t s);
 
