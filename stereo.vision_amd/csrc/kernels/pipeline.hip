@@ -7,22 +7,30 @@
 // (functions.py:201-209 + stereovision.py:112).
 //
 // The histogram must be complete before any point of a frame can be filtered,
-// so every frame is visited twice:
-//   pass 1  hist_tile     LDS histogram (4 KB) per 4096-point tile, flushed with
-//                         one global atomic per non-zero bin; N_valid, N_kept.
-//   pass 2  compact_tile  wave ballot/scan + LDS block scan inside the tile,
-//                         decoupled look-back across the tiles of a frame,
+// so every frame is visited twice, tile by tile (tile = 256 lanes x 4 quads =
+// 4096 grid points):
+//   pass 1  hist_tile     reads disparity + BGR (4 B/pt), evaluates keep1 and
+//                         the hue bin of every point; LDS histogram flushed
+//                         with one global atomic per non-zero bin; writes the
+//                         tile's keep1 bitmask (2 B per lane = 1 bit/pt) and
+//                         its bin-presence mask (1024 bits).
+//   pass 2  compact_tile  reads the keep1 bits + disparity (~1.1 B/pt); a tile
+//                         whose present bins are all above hist_thr ("clean",
+//                         nearly all of them) needs no hue at all; a "dirty"
+//                         tile re-reads its BGR and recomputes the bins of its
+//                         keep1 points. Wave scan + LDS block scan inside the
+//                         tile, decoupled look-back across the frame's tiles,
 //                         then fp32 XYZ + int32 (x,y) stores.
 // Frames go in chunks; launch c runs pass 2 of chunk c-1 together with pass 1
-// of chunk c (one ticketed grid), so a chunk's second read comes from the
-// 256 MB Infinity Cache shortly after its first, and there are chunks+1
-// launches per call. All control words (histograms, counts, look-back
-// granules, per-launch tickets) are zeroed by one memset per call.
+// of chunk c, so a chunk's second visit comes from the 256 MB Infinity Cache
+// shortly after its first; there are chunks+1 launches per call. All control
+// words (histograms, counts, look-back granules, tickets) are zeroed by one
+// memset per call; the keep/presence masks are fully rewritten by pass 1.
 #include "../svx_launch.h"
 
 namespace svx {
 
-constexpr int kQPT = 4;   // tile = 256 lanes x 4 quads = 4096 grid points (both passes)
+constexpr int kQPT = 4;   // quads per lane: tile = 256 x 4 quads = 4096 grid points
 
 template <int STEP>
 struct QuadIn {
@@ -31,15 +39,22 @@ struct QuadIn {
 };
 
 template <int STEP>
-__device__ __forceinline__ void load_quad(const uint8_t* drow, const uint8_t* crow, int q, QuadIn<STEP>& o) {
+__device__ __forceinline__ void load_disp(const uint8_t* drow, int q, uint32_t (&d)[4]) {
     if constexpr (STEP == 1) {
         const uint32_t w = *reinterpret_cast<const uint32_t*>(drow + 4 * q);
-        o.d[0] = w & 0xFF; o.d[1] = (w >> 8) & 0xFF; o.d[2] = (w >> 16) & 0xFF; o.d[3] = w >> 24;
+        d[0] = w & 0xFF; d[1] = (w >> 8) & 0xFF; d[2] = (w >> 16) & 0xFF; d[3] = w >> 24;
+    } else {
+        const uint2 w = *reinterpret_cast<const uint2*>(drow + 8 * q);
+        d[0] = w.x & 0xFF; d[1] = (w.x >> 16) & 0xFF; d[2] = w.y & 0xFF; d[3] = (w.y >> 16) & 0xFF;
+    }
+}
+
+template <int STEP>
+__device__ __forceinline__ void load_bgr(const uint8_t* crow, int q, QuadIn<STEP>& o) {
+    if constexpr (STEP == 1) {
         const uint32_t* cp = reinterpret_cast<const uint32_t*>(crow + 12 * q);
         o.c[0] = cp[0]; o.c[1] = cp[1]; o.c[2] = cp[2];
     } else {
-        const uint2 w = *reinterpret_cast<const uint2*>(drow + 8 * q);
-        o.d[0] = w.x & 0xFF; o.d[1] = (w.x >> 16) & 0xFF; o.d[2] = w.y & 0xFF; o.d[3] = (w.y >> 16) & 0xFF;
         const uint2* cp = reinterpret_cast<const uint2*>(crow + 24 * q);
         const uint2 a = cp[0], b = cp[1], c = cp[2];
         o.c[0] = a.x; o.c[1] = a.y; o.c[2] = b.x; o.c[3] = b.y; o.c[4] = c.x; o.c[5] = c.y;
@@ -47,26 +62,21 @@ __device__ __forceinline__ void load_quad(const uint8_t* drow, const uint8_t* cr
 }
 
 template <int STEP>
-__device__ __forceinline__ uint32_t quad_byte(const QuadIn<STEP>& o, int i) {
-    return (o.c[i >> 2] >> (8 * (i & 3))) & 0xFF;
+__device__ __forceinline__ int point_bin(const QuadIn<STEP>& in, int k) {
+    const int o = 3 * STEP * k;  // byte offset of pixel k inside the quad's BGR
+    const auto byte = [&](int i) { return (int)((in.c[i >> 2] >> (8 * (i & 3))) & 0xFF); };
+    return hue_bin(byte(o + 2), byte(o + 1), byte(o));   // (R, G, B) from BGR
 }
 
-// Evaluate point k of a quad: returns 0 = not kept, 1 + bin = plane-kept.
+// keep1 for one grid point (functions.py:300-323).
 template <int STEP>
-__device__ __forceinline__ int eval_point(const QuadIn<STEP>& in, int k, int gx, int y, float yc,
-                                          const KParams& p) {
-    const uint32_t d = in.d[k];
-    if (d == 0 || gx >= p.Wg) return 0;
+__device__ __forceinline__ bool point_keep1(uint32_t d, int gx, int y, float yc, const KParams& p) {
+    if (d == 0 || gx >= p.Wg) return false;
     const int x = gx * STEP;
     const float xc = centred(x, p.cw_hi, p.cw_lo);
     const float r = __builtin_amdgcn_rcpf((float)d);
     const float K = p.B32 * r;
-    const float X = xc * K, Y = yc * K, Z = p.fB32 * r;
-    if (!keep1(x, y, d, xc, yc, K, X, Y, Z, p)) return 0;
-    const int o = 3 * STEP * k;  // byte offset of the pixel inside the quad's BGR
-    const int B = (int)quad_byte<STEP>(in, o), G = (int)quad_byte<STEP>(in, o + 1),
-              R = (int)quad_byte<STEP>(in, o + 2);
-    return 1 + hue_bin(R, G, B);
+    return keep1(x, y, d, xc, yc, K, xc * K, yc * K, p.fB32 * r, p);
 }
 
 int pipeline_tiles_per_frame(const KParams& p) {
@@ -74,58 +84,58 @@ int pipeline_tiles_per_frame(const KParams& p) {
     return (p.frame_quads + per - 1) / per;
 }
 
-
-// Issue every load of the lane's kQPT quads before any use (memory-level
-// parallelism: 4 x 16 B per lane in flight).
-template <int STEP>
-__device__ __forceinline__ void load_tile(const uint8_t* disp, const uint8_t* bgr, int qbase, int tid,
-                                          const KParams& p, QuadIn<STEP> (&in)[kQPT], int (&gy)[kQPT],
-                                          int (&q)[kQPT]) {
+// Lane geometry of a tile: quad i of this lane = qbase + i*256 + lane (so each
+// wave-instruction touches contiguous memory). Out-of-range quads re-address
+// the last valid quad (branch-free loads) and are flagged gy = -1.
+__device__ __forceinline__ void tile_geometry(int qbase, int tid, const KParams& p, int (&gy)[kQPT],
+                                              int (&q)[kQPT]) {
 #pragma unroll
     for (int i = 0; i < kQPT; ++i) {
-        // branch-free: out-of-range lanes re-load the last quad and are masked
-        // (keeps the arrays in registers and every load in flight together)
         const int qi = qbase + i * 256 + tid;
         const bool ok = qi < p.frame_quads;
         const int qc = ok ? qi : p.frame_quads - 1;
         const int g = qc / p.Q;
         q[i] = qc - g * p.Q;
         gy[i] = ok ? g : -1;
-        const int y = g * STEP;
-        load_quad<STEP>(disp + (int64_t)y * p.W, bgr + (int64_t)y * p.W * 3, q[i], in[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < kQPT; ++i) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) in[i].d[k] = gy[i] < 0 ? 0u : in[i].d[k];
     }
 }
 
-// ---------------------------------------------------------------------------
-// pass 1 tile: LDS histogram of the plane-kept points + N_valid / N_kept.
-// ---------------------------------------------------------------------------
+template <int STEP>
+__device__ __forceinline__ const uint8_t* row_ptr(const uint8_t* base, int gy, int bpp, const KParams& p) {
+    const int g = gy < 0 ? 0 : gy;
+    return base + (int64_t)(g * STEP) * p.W * bpp;
+}
+
 struct PipeShared {
     uint32_t hist[kBins];         // pass 1
     uint32_t okbits[kBins / 32];  // pass 2: hist[bin] > hist_thr
     uint64_t wave[4];             // pass 2 block scan
     uint32_t cnt[2];
-    uint32_t tile, excl;
+    uint32_t tile, excl, dirty;
 };
 static_assert(sizeof(PipeShared) < 8192, "LDS budget");
 
+// ---------------------------------------------------------------------------
+// pass 1 tile
+// ---------------------------------------------------------------------------
 template <int STEP>
-__device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int tile, const KParams& p,
-                                          PipeShared& sh) {
+__device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int tile, int tiles,
+                                          const KParams& p, PipeShared& sh) {
     const int tid = threadIdx.x;
-    for (int i = tid; i < kBins; i += 256) sh.hist[i] = 0;
-    if (tid < 2) sh.cnt[tid] = 0;
     const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
     const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
-    QuadIn<STEP> in[kQPT];
     int gy[kQPT], q[kQPT];
-    load_tile<STEP>(disp, bgr, tile * 256 * kQPT, tid, p, in, gy, q);
+    tile_geometry(tile * 256 * kQPT, tid, p, gy, q);
+    QuadIn<STEP> in[kQPT];
+#pragma unroll
+    for (int i = 0; i < kQPT; ++i) {   // all loads in flight before any use
+        load_disp<STEP>(row_ptr<STEP>(disp, gy[i], 1, p), q[i], in[i].d);
+        load_bgr<STEP>(row_ptr<STEP>(bgr, gy[i], 3, p), q[i], in[i]);
+    }
+    for (int i = tid; i < kBins; i += 256) sh.hist[i] = 0;
+    if (tid < 2) sh.cnt[tid] = 0;
     __syncthreads();
-    uint32_t nv = 0, nk = 0;
+    uint32_t nv = 0, keep = 0;
 #pragma unroll
     for (int i = 0; i < kQPT; ++i) {
         if (gy[i] < 0) continue;
@@ -135,13 +145,15 @@ __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int 
         for (int k = 0; k < 4; ++k) {
             const int gx = 4 * q[i] + k;
             nv += (in[i].d[k] != 0 && gx < p.Wg) ? 1u : 0u;
-            const int e = eval_point<STEP>(in[i], k, gx, y, yc, p);
-            if (e) {
-                ++nk;
-                atomicAdd(&sh.hist[e - 1], 1u);
+            if (point_keep1<STEP>(in[i].d[k], gx, y, yc, p)) {
+                keep |= 1u << (4 * i + k);
+                atomicAdd(&sh.hist[point_bin<STEP>(in[i], k)], 1u);
             }
         }
     }
+    uint32_t nk = __builtin_popcount(keep);
+    const int64_t slot = (int64_t)frame * tiles + tile;
+    bf.kbits[slot * 256 + tid] = (uint16_t)keep;
     nv = wave_sum(nv);
     nk = wave_sum(nk);
     if (lane_id() == 0) {
@@ -154,17 +166,23 @@ __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int 
         atomicAdd(reinterpret_cast<unsigned long long*>(bf.counts + 4 * frame + 1), (unsigned long long)sh.cnt[1]);
     }
     uint32_t* gh = bf.hist + (int64_t)frame * kBins;
-    for (int i = tid; i < kBins; i += 256) {
-        const uint32_t v = sh.hist[i];
-        if (v) atomicAdd(gh + i, v);
+    uint32_t* pres = bf.pres + slot * (kBins / 32);
+    const int wave = tid >> 6;
+#pragma unroll
+    for (int r = 0; r < kBins / 256; ++r) {
+        const int b = r * 256 + tid;
+        const uint32_t v = sh.hist[b];
+        if (v) atomicAdd(gh + b, v);
+        const uint64_t m = __ballot(v != 0);
+        if (lane_id() == 0) {
+            pres[(r * 256 + wave * 64) / 32] = (uint32_t)m;
+            pres[(r * 256 + wave * 64) / 32 + 1] = (uint32_t)(m >> 32);
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
-// pass 2 tile: keep2 filter, ordered compaction, fp32 XYZ + int32 (x, y).
-// Tile = 256 lanes x kQPT quads; quad (i, lane) = tile_base + i*256 + lane, so
-// each load wave-instruction is contiguous; the raster order inside the tile
-// is (i, lane), scanned with 4 x 16-bit fields packed in one u64.
+// pass 2 tile
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
     const int lane = lane_id();
@@ -181,14 +199,17 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
                                              const KParams& p, PipeShared& sh) {
     const int tid = threadIdx.x;
     const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
-    const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
-    const int qbase = tile * 256 * kQPT;
-    QuadIn<STEP> in[kQPT];
     int gyv[kQPT], qv[kQPT];
-    load_tile<STEP>(disp, bgr, qbase, tid, p, in, gyv, qv);
-    {   // hist[bin] > hist_thr as a 1024-bit mask
+    tile_geometry(tile * 256 * kQPT, tid, p, gyv, qv);
+    const int64_t slot = (int64_t)frame * tiles + tile;
+    uint32_t keep = bf.kbits[slot * 256 + tid];
+    uint32_t dv[kQPT][4];
+#pragma unroll
+    for (int i = 0; i < kQPT; ++i) load_disp<STEP>(row_ptr<STEP>(disp, gyv[i], 1, p), qv[i], dv[i]);
+    {   // hist[bin] > hist_thr as a 1024-bit mask; the tile is dirty if a present bin fails it
         const uint32_t* gh = bf.hist + (int64_t)frame * kBins;
         const int wave = tid >> 6;
+        if (tid == 0) sh.dirty = 0;
 #pragma unroll
         for (int r = 0; r < kBins / 256; ++r) {
             const uint64_t m = __ballot((int64_t)gh[r * 256 + tid] > (int64_t)p.hist_thr);
@@ -197,26 +218,32 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
                 sh.okbits[(r * 256 + wave * 64) / 32 + 1] = (uint32_t)(m >> 32);
             }
         }
+        __syncthreads();
+        if (tid < kBins / 32) {
+            const uint32_t bad = bf.pres[slot * (kBins / 32) + tid] & ~sh.okbits[tid];
+            if (bad) atomicOr(&sh.dirty, 1u);
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    uint32_t dpack[kQPT];
-    uint32_t keep = 0;  // bit 4*i + k
-    uint64_t cnt = 0;
+    if (sh.dirty) {   // block-uniform and rare: recompute the bins of the keep1 points
+        const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
 #pragma unroll
-    for (int i = 0; i < kQPT; ++i) {
-        dpack[i] = in[i].d[0] | (in[i].d[1] << 8) | (in[i].d[2] << 16) | (in[i].d[3] << 24);
-        if (gyv[i] < 0) continue;
-        const int y = gyv[i] * STEP;
-        const float yc = centred(y, p.ch_hi, p.ch_lo);
+        for (int i = 0; i < kQPT; ++i) {
+            if (!((keep >> (4 * i)) & 0xF)) continue;
+            QuadIn<STEP> in;
+            load_bgr<STEP>(row_ptr<STEP>(bgr, gyv[i], 3, p), qv[i], in);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int e = eval_point<STEP>(in[i], k, 4 * qv[i] + k, y, yc, p);
-            if (e && ((sh.okbits[(e - 1) >> 5] >> ((e - 1) & 31)) & 1)) {
-                keep |= 1u << (4 * i + k);
-                cnt += 1ull << (16 * i);
+            for (int k = 0; k < 4; ++k) {
+                if (!(keep & (1u << (4 * i + k)))) continue;
+                const int bin = point_bin<STEP>(in, k);
+                if (!((sh.okbits[bin >> 5] >> (bin & 31)) & 1)) keep &= ~(1u << (4 * i + k));
             }
         }
     }
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kQPT; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
+
     // block scan of the packed per-quad-row counts
     const uint64_t inc = wave_incl_scan64(cnt);
     const int wave = tid >> 6;
@@ -269,7 +296,7 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!(km & (1u << k))) continue;
-            const uint32_t d = (dpack[i] >> (8 * k)) & 0xFF;
+            const uint32_t d = dv[i][k];
             const int x = (4 * q + k) * STEP;
             const float xc = centred(x, p.cw_hi, p.cw_lo);
             const float r = __builtin_amdgcn_rcpf((float)d);
@@ -312,7 +339,7 @@ __global__ __launch_bounds__(256) void pipeline_kernel(PipeBuffers bf, int p2_fr
     } else {
         const int h = bid - n2;
         const int fl = h / tiles;
-        hist_tile<STEP>(bf, p1_frame0 + fl, h - fl * tiles, p, sh);
+        hist_tile<STEP>(bf, p1_frame0 + fl, h - fl * tiles, tiles, p, sh);
     }
 }
 

@@ -187,7 +187,7 @@ struct sv_batch {
     int64_t Ng = 0;            // grid points per frame
     int64_t dense_per_frame = 0;
     hipStream_t stream = nullptr;
-    DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl;
+    DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks;
     // pipeline control block (one memset per call): hist | counts | look-back
     // granules | per-launch tickets | err
     uint32_t* hist = nullptr;
@@ -380,7 +380,7 @@ int sv_batch_destroy(sv_batch* b) {
     if (!b) return SV_OK;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
-    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl})
+    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks})
         if (x->p) (void)hipFree(x->p);
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -461,6 +461,9 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     const size_t cap = (size_t)b->Ng;
     HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames));
     HIP_TRY(b->pts.ensure(sizeof(int32_t) * 2 * cap * b->frames));
+    const size_t tiles = (size_t)pipeline_tiles_per_frame(p);
+    const size_t kb_bytes = sizeof(uint16_t) * 256 * tiles * b->frames;
+    HIP_TRY(b->masks.ensure(kb_bytes + sizeof(uint32_t) * (kBins / 32) * tiles * b->frames));
     if (int rc = ensure_tables(*d, b->H, b->W, *cam, b->stream)) return rc;
     PipeBuffers bf;
     bf.disp = b->disp.as<uint8_t>();
@@ -468,6 +471,8 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     bf.hist = b->hist;
     bf.counts = b->counts;
     bf.status = b->status;
+    bf.kbits = b->masks.as<uint16_t>();
+    bf.pres = reinterpret_cast<uint32_t*>(b->masks.as<char>() + kb_bytes);
     bf.err = b->err;
     bf.xyz = b->xyz.as<float>();
     bf.pts = b->pts.as<int32_t>();

@@ -63,22 +63,23 @@ __device__ __forceinline__ int hue_bin(int r, int g, int b) {
     const int mx = max(r, max(g, b));
     const int mn = min(r, min(g, b));
     const int rng = mx - mn;
-    if (rng == 0) return 0;
-    int n;
-    if (r == mx) n = g - b;
-    else if (g == mx) n = 2 * rng + b - r;
-    else n = 4 * rng + r - g;
-    if (n < 0) n += 6 * rng;
-    // t = 500 n / (3 rng); num < 2^20, den <= 765: fp32 quotient + exact fixup
+    int n = (r == mx) ? (g - b) : ((g == mx) ? (2 * rng + b - r) : (4 * rng + r - g));
+    n += (n < 0) ? 6 * rng : 0;
+    // t = 1000 n / (6 rng) = num / den exactly (num < 2^20, den <= 765).
+    // fp32: one rcp (<= 1 ulp) + one mul (0.5 ulp): |t - t_exact| < 1e-4.
+    // A non-tie rational is >= 1/(2 den) >= 6.5e-4 from a half-integer, so
+    // outside the +-2e-4 band around .5 the fp32 rounding is the exact one.
     const int num = 500 * n, den = 3 * rng;
-    int q = (int)((float)num * __builtin_amdgcn_rcpf((float)den));
-    int rem = num - q * den;
-    if (rem < 0) { q -= 1; rem += den; }
-    if (rem >= den) { q += 1; rem -= den; }
-    const int two_rem = 2 * rem;
-    if (two_rem > den) return q + 1;
-    if (two_rem < den) return q;
-    return hue_bin_tie_f64(r, g, b, mx, mn);   // exact .5 tie: reference fp64 decides
+    const float t = (float)num * __builtin_amdgcn_rcpf((float)den);
+    const float fl = __builtin_floorf(t);
+    const float fr = t - fl;
+    const int m = (int)fl;
+    int bin = m + (fr > 0.5f ? 1 : 0);
+    if (__builtin_fabsf(fr - 0.5f) < 2e-4f) {   // rare: decide in exact integers
+        const int two_rem = 2 * (num - m * den);
+        bin = two_rem > den ? m + 1 : (two_rem < den ? m : hue_bin_tie_f64(r, g, b, mx, mn));
+    }
+    return rng == 0 ? 0 : bin;   // grey: colorsys returns hue 0.0
 }
 
 // x - c in fp32 with relative error <= 2^-23 for any fp64 centre c: the first
@@ -107,8 +108,8 @@ __device__ __forceinline__ bool keep1(int x, int y, uint32_t d, float xc, float 
     const float S = __builtin_fmaf(p.abs_a32, __builtin_fabsf(xc),
                                    __builtin_fmaf(p.abs_b32, __builtin_fabsf(yc), p.abs_cf32)) * K;
     const float G = (S + 1.0f) * p.guard32;
-    if (dist < p.thr32 - G) return true;
-    if (dist > p.thr32 + G) return false;
+    const float e = dist - p.thr32;
+    if (__builtin_fabsf(e) > G) return e < 0.0f;
     return keep1_f64(x, y, d, p);
 }
 

@@ -35,6 +35,8 @@ struct PipeBuffers {
     uint32_t* hist;      // frames x 1024
     int64_t* counts;     // frames x 4 (N_valid, N_kept, N_kept2, spare)
     uint64_t* status;    // frames x tiles look-back granules
+    uint16_t* kbits;     // frames x tiles x 256: keep1 bit (4*i + k) of each lane's quads
+    uint32_t* pres;      // frames x tiles x 32: hue bins present among the tile's keep1 points
     uint32_t* err;
     float* xyz;          // frames x cap x 3
     int32_t* pts;        // frames x cap x 2

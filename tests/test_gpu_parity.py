@@ -220,6 +220,15 @@ def test_pipeline_planes_and_thresholds(svx_mod, plane, thr):
     _check_pipe(got, oracle.pipeline_frame(disp, bgr, 2, abc=np.array(plane), point_thr=thr, hist_thr=3))
 
 
+@pytest.mark.parametrize("hist_thr", [-1, 0, 40, 10 ** 9])
+def test_pipeline_hist_thresholds(svx_mod, hist_thr):
+    """Every tile clean (-1), most tiles dirty (40), everything filtered (1e9)."""
+    disp, bgr = oracle.synth_frame(23)
+    for step in (1, 2):
+        got = svx_mod.batch.pipeline_frame(disp, bgr, step, hist_thr=hist_thr)
+        _check_pipe(got, oracle.pipeline_frame(disp, bgr, step, hist_thr=hist_thr))
+
+
 def test_pipeline_edge_frames(svx_mod):
     z = np.zeros((544, 1024), np.uint8)
     bgr = np.zeros((544, 1024, 3), np.uint8)
