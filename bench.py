@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--ramp-ms", type=float, default=300.0,
                     help="untimed K1 launches before the warmup steps, to let clocks settle")
     ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the 1-frame latency probe (keeps K1's rocprof average = 4096-frame launches)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -94,6 +96,19 @@ def cpu_baseline(budget_s):
                       f"({pts} grid points, {dt:.1f} s): oracle/cpu_loop.py nested loop "
                       f"(functions.py:178-198 semantics)",
             "c_restatement_mpts": pts / dtc / 1e6, "cpu": model}
+
+
+def latency_1frame(sb, step, first, device):
+    """configs[1]: one 1024x544 frame, step 1: K1 kernel time (HIP events), us."""
+    with sb.Batch(1, H, W, step, with_bgr=False, device=device) as one:
+        one.synth(first)
+        for _ in range(5):
+            one.project(sync=False)
+        one.reset_timing()
+        for _ in range(50):
+            one.project(sync=False)
+        ms, n = one.timing("project")
+        return round(ms / n * 1e3, 2)
 
 
 def main():
@@ -165,15 +180,8 @@ def main():
     }
 
     # ---- config 2: single-frame latency ------------------------------------
-    with sb.Batch(1, H, W, args.step, with_bgr=False, device=local) as one:
-        one.synth(first)
-        for _ in range(5):
-            one.project(sync=False)
-        one.reset_timing()
-        for _ in range(50):
-            one.project(sync=False)
-        ms, n = one.timing("project")
-        out["latency_1frame_us"] = round(ms / n * 1e3, 2)
+    if not args.no_latency:
+        out["latency_1frame_us"] = latency_1frame(sb, args.step, first, local)
 
     # ---- config 4/5: pipeline ----------------------------------------------
     if want_pipe:

@@ -16,7 +16,7 @@ rc=$?; echo "bench rc=$rc"; tail -5 "$OUT/bench.log"; stop_if_fatal $rc bench
 if [ "${SKIP_PROF:-0}" != 1 ]; then
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-  python3 bench.py --steps 5 --warmup 1 --no-cpu > "$OUT/prof.log" 2>&1
+  python3 bench.py --steps 5 --warmup 1 --no-cpu --no-latency > "$OUT/prof.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"; stop_if_fatal $rc rocprof
 find "$OUT/prof" -name "*stats*" | head
 fi
