@@ -14,18 +14,18 @@
 //                         with one global atomic per non-zero bin; writes the
 //                         tile's keep1 bitmask (2 B per lane = 1 bit/pt) and
 //                         its bin-presence mask (1024 bits).
-//   pass 2  compact_tile  reads the keep1 bits + disparity (~1.1 B/pt); a tile
+//   pass 2  compact_frame reads the keep1 bits + disparity (~1.1 B/pt); a tile
 //                         whose present bins are all above hist_thr ("clean",
 //                         nearly all of them) needs no hue at all; a "dirty"
 //                         tile re-reads its BGR and recomputes the bins of its
-//                         keep1 points. Wave scan + LDS block scan inside the
-//                         tile, decoupled look-back across the frame's tiles,
-//                         then fp32 XYZ + int32 (x,y) stores.
-// Frames go in chunks; launch c runs pass 2 of chunk c-1 together with pass 1
-// of chunk c, so a chunk's second visit comes from the 256 MB Infinity Cache
-// shortly after its first; there are chunks+1 launches per call. All control
-// words (histograms, counts, look-back granules, tickets) are zeroed by one
-// memset per call; the keep/presence masks are fully rewritten by pass 1.
+//                         keep1 points. One workgroup per frame walks the tiles
+//                         in order (running offset in a register), compacting
+//                         through an LDS descriptor scatter so that all stores
+//                         are contiguous, non-temporal SoA writes.
+// Frames go in segments; pass 1 of segment s+1 (stream A) overlaps pass 2 of
+// segment s (stream B): pass 1 is VALU-heavy, pass 2 store-bound. The control
+// words (histograms, counts) are zeroed by one memset per call; the keep /
+// presence masks are fully rewritten by pass 1.
 #include "../svx_launch.h"
 
 namespace svx {
@@ -106,12 +106,9 @@ __device__ __forceinline__ const uint8_t* row_ptr(const uint8_t* base, int gy, i
     return base + (int64_t)(g * STEP) * p.W * bpp;
 }
 
-struct PipeShared {
-    uint32_t hist[kBins];         // pass 1
-    uint32_t okbits[kBins / 32];  // pass 2: hist[bin] > hist_thr
-    uint64_t wave[4];             // pass 2 block scan
+struct PipeShared {   // pass 1
+    uint32_t hist[kBins];
     uint32_t cnt[2];
-    uint32_t tile, excl, dirty;
 };
 static_assert(sizeof(PipeShared) < 8192, "LDS budget");
 
@@ -181,8 +178,25 @@ __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int 
     }
 }
 
+template <int STEP>
+__global__ __launch_bounds__(256) void hist_kernel(PipeBuffers bf, int frame0, int tiles, KParams p) {
+    __shared__ PipeShared sh;
+    const int fl = blockIdx.x / tiles;
+    hist_tile<STEP>(bf, frame0 + fl, blockIdx.x - fl * tiles, tiles, p, sh);
+}
+
 // ---------------------------------------------------------------------------
-// pass 2 tile
+// pass 2: one workgroup per frame, walking its tiles in raster order, so the
+// running output offset is a register (no inter-workgroup protocol at all).
+//   * the next tile's keep1 bits + disparity are loaded while the current one
+//     is compacted (register double-buffering);
+//   * which tiles are dirty (hold a keep1 point whose bin fails hist_thr) is
+//     decided once per frame from the presence masks;
+//   * compaction: a block scan gives each keep2 point its slot in the tile;
+//     lanes scatter a 4-byte descriptor (gx | gy | d) into LDS at that slot,
+//     then lane j of the block produces output j: every store instruction
+//     writes contiguous lanes into the SoA outputs (X, Y, Z, (x,y)) with
+//     non-temporal stores — no partial lines.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
     const int lane = lane_id();
@@ -194,172 +208,175 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
     return v;
 }
 
+constexpr int kMaxTiles = 2048;   // tiles per frame supported by the dirty bitmap
+
+struct CompactShared {
+    uint32_t okbits[kBins / 32];
+    uint32_t dirty[kMaxTiles / 32];
+    uint64_t wave[4];
+    uint32_t desc[2][256 * kQPT * 4];   // double-buffered output descriptors (2 x 16 KB)
+};
+
 template <int STEP>
-__device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, int tile, int tiles,
-                                             const KParams& p, PipeShared& sh) {
-    const int tid = threadIdx.x;
-    const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
-    int gyv[kQPT], qv[kQPT];
-    tile_geometry(tile * 256 * kQPT, tid, p, gyv, qv);
-    const int64_t slot = (int64_t)frame * tiles + tile;
-    uint32_t keep = bf.kbits[slot * 256 + tid];
-    uint32_t dv[kQPT][4];
+__device__ __forceinline__ void prefetch_tile(const PipeBuffers& bf, const uint8_t* disp, int64_t slot,
+                                              int qbase, int tid, const KParams& p, uint32_t& kb,
+                                              uint32_t (&dw)[kQPT][STEP]) {
+    kb = bf.kbits[slot * 256 + tid];
+    int gy[kQPT], q[kQPT];
+    tile_geometry(qbase, tid, p, gy, q);
 #pragma unroll
-    for (int i = 0; i < kQPT; ++i) load_disp<STEP>(row_ptr<STEP>(disp, gyv[i], 1, p), qv[i], dv[i]);
-    {   // hist[bin] > hist_thr as a 1024-bit mask; the tile is dirty if a present bin fails it
+    for (int i = 0; i < kQPT; ++i) {
+        const uint8_t* row = row_ptr<STEP>(disp, gy[i], 1, p);
+        if constexpr (STEP == 1) {
+            dw[i][0] = *reinterpret_cast<const uint32_t*>(row + 4 * q[i]);
+        } else {
+            const uint2 w = *reinterpret_cast<const uint2*>(row + 8 * q[i]);
+            dw[i][0] = w.x;
+            dw[i][1] = w.y;
+        }
+    }
+}
+
+template <int STEP>
+__global__ __launch_bounds__(256) void compact_frame_kernel(PipeBuffers bf, int frame0, int tiles, KParams p) {
+    __shared__ CompactShared sh;
+    constexpr int DW = STEP;   // disparity dwords kept per quad: 1 (step 1) / 2 (step 2)
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = tid >> 6;
+    const int frame = frame0 + blockIdx.x;
+    const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
+    const int64_t slot0 = (int64_t)frame * tiles;
+    {   // hist[bin] > hist_thr as a 1024-bit mask
         const uint32_t* gh = bf.hist + (int64_t)frame * kBins;
-        const int wave = tid >> 6;
-        if (tid == 0) sh.dirty = 0;
 #pragma unroll
         for (int r = 0; r < kBins / 256; ++r) {
             const uint64_t m = __ballot((int64_t)gh[r * 256 + tid] > (int64_t)p.hist_thr);
-            if (lane_id() == 0) {
+            if (lane == 0) {
                 sh.okbits[(r * 256 + wave * 64) / 32] = (uint32_t)m;
                 sh.okbits[(r * 256 + wave * 64) / 32 + 1] = (uint32_t)(m >> 32);
             }
         }
-        __syncthreads();
-        if (tid < kBins / 32) {
-            const uint32_t bad = bf.pres[slot * (kBins / 32) + tid] & ~sh.okbits[tid];
-            if (bad) atomicOr(&sh.dirty, 1u);
-        }
-        __syncthreads();
+        for (int w = tid; w < kMaxTiles / 32; w += 256) sh.dirty[w] = 0;
     }
-    if (sh.dirty) {   // block-uniform and rare: recompute the bins of the keep1 points
-        const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
+    __syncthreads();
+    // dirty tiles: any present bin that fails the histogram threshold
+    for (int i = tid; i < tiles * (kBins / 32); i += 256) {
+        const int t = i / (kBins / 32), w = i - t * (kBins / 32);
+        if (bf.pres[(slot0 + t) * (kBins / 32) + w] & ~sh.okbits[w]) atomicOr(&sh.dirty[t >> 5], 1u << (t & 31));
+    }
+    float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap;
+    float* oY = oX + bf.cap;
+    float* oZ = oY + bf.cap;
+    int2* oP = reinterpret_cast<int2*>(bf.pts) + (int64_t)frame * bf.cap;
+
+    uint32_t kb_n, dw_n[kQPT][DW];
+    prefetch_tile<STEP>(bf, disp, slot0, 0, tid, p, kb_n, dw_n);
+    uint32_t running = 0;
+    for (int t = 0; t < tiles; ++t) {
+        uint32_t keep = kb_n, dw[kQPT][DW];
+#pragma unroll
+        for (int i = 0; i < kQPT; ++i)
+#pragma unroll
+            for (int j = 0; j < DW; ++j) dw[i][j] = dw_n[i][j];
+        if (t + 1 < tiles) prefetch_tile<STEP>(bf, disp, slot0 + t + 1, (t + 1) * 256 * kQPT, tid, p, kb_n, dw_n);
+        const int qbase = t * 256 * kQPT;
+        int gy[kQPT], q[kQPT];
+        tile_geometry(qbase, tid, p, gy, q);
+        __syncthreads();   // dirty bitmap complete (first tile) / previous desc buffer drained
+        if ((sh.dirty[t >> 5] >> (t & 31)) & 1) {   // block-uniform, rare
+            const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
+#pragma unroll
+            for (int i = 0; i < kQPT; ++i) {
+                if (!((keep >> (4 * i)) & 0xF)) continue;
+                QuadIn<STEP> in;
+                load_bgr<STEP>(row_ptr<STEP>(bgr, gy[i], 3, p), q[i], in);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (!(keep & (1u << (4 * i + k)))) continue;
+                    const int bin = point_bin<STEP>(in, k);
+                    if (!((sh.okbits[bin >> 5] >> (bin & 31)) & 1)) keep &= ~(1u << (4 * i + k));
+                }
+            }
+        }
+        uint64_t cnt = 0;
+#pragma unroll
+        for (int i = 0; i < kQPT; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
+        const uint64_t inc = wave_incl_scan64(cnt);
+        if (lane == 63) sh.wave[wave] = inc;
+        __syncthreads();
+        uint64_t wbase = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint64_t v = sh.wave[w];
+            wbase += (w < wave) ? v : 0ull;
+            tot += v;
+        }
+        const uint64_t excl = wbase + inc - cnt;
+        uint32_t* desc = sh.desc[t & 1];
+        uint32_t rowbase = 0;
 #pragma unroll
         for (int i = 0; i < kQPT; ++i) {
-            if (!((keep >> (4 * i)) & 0xF)) continue;
-            QuadIn<STEP> in;
-            load_bgr<STEP>(row_ptr<STEP>(bgr, gyv[i], 3, p), qv[i], in);
+            uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
+            rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (!(keep & (1u << (4 * i + k)))) continue;
-                const int bin = point_bin<STEP>(in, k);
-                if (!((sh.okbits[bin >> 5] >> (bin & 31)) & 1)) keep &= ~(1u << (4 * i + k));
+                uint32_t d;
+                if constexpr (STEP == 1) d = (dw[i][0] >> (8 * k)) & 0xFF;
+                else d = (dw[i][k >> 1] >> (16 * (k & 1))) & 0xFF;
+                desc[o++] = (d << 24) | ((uint32_t)gy[i] << 12) | (uint32_t)(4 * q[i] + k);
             }
         }
-    }
-    uint64_t cnt = 0;
-#pragma unroll
-    for (int i = 0; i < kQPT; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
-
-    // block scan of the packed per-quad-row counts
-    const uint64_t inc = wave_incl_scan64(cnt);
-    const int wave = tid >> 6;
-    if (lane_id() == 63) sh.wave[wave] = inc;
-    __syncthreads();
-    uint64_t wbase = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const uint64_t t = sh.wave[w];
-        wbase += (w < wave) ? t : 0ull;
-        tot += t;
-    }
-    const uint64_t excl_packed = wbase + inc - cnt;
-    uint32_t total = 0;
-#pragma unroll
-    for (int i = 0; i < kQPT; ++i) total += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
-
-    if (wave == 0) {
-        uint64_t* st = bf.status + (int64_t)frame * tiles;
-        uint32_t excl = 0;
-        if (tile == 0) {
-            if (tid == 0) publish(st, kFlagInc, total);
-        } else {
-            if (tid == 0) publish(st + tile, kFlagAgg, total);
-            excl = lookback(st, tile, bf.err);
-            if (tid == 0) publish(st + tile, kFlagInc, excl + total);
-        }
-        if (tid == 0) {
-            sh.excl = excl;
-            if (tile == tiles - 1) bf.counts[4 * frame + 2] = excl + total;
-        }
-    }
-    __syncthreads();
-    if (!keep) return;
-
-    const int64_t fbase = (int64_t)frame * bf.cap + sh.excl;
-    float* oxyz = bf.xyz;
-    int32_t* opts = bf.pts;
-    uint32_t rowbase = 0;
-#pragma unroll
-    for (int i = 0; i < kQPT; ++i) {
-        uint32_t o = rowbase + (uint32_t)((excl_packed >> (16 * i)) & 0xFFFF);
-        rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
-        const uint32_t km = (keep >> (4 * i)) & 0xF;
-        if (!km) continue;
-        const int q = qv[i];
-        const int y = gyv[i] * STEP;
-        const float yc = centred(y, p.ch_hi, p.ch_lo);
-        const int dyw = y >> 5, dyb = y & 31;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (!(km & (1u << k))) continue;
-            const uint32_t d = dv[i][k];
-            const int x = (4 * q + k) * STEP;
+        const uint32_t total = rowbase;
+        __syncthreads();
+        for (uint32_t j = tid; j < total; j += 256) {
+            const uint32_t u = desc[j];
+            const uint32_t d = u >> 24;
+            const int y = (int)((u >> 12) & 0xFFF) * STEP;
+            const int x = (int)(u & 0xFFF) * STEP;
             const float xc = centred(x, p.cw_hi, p.cw_lo);
+            const float yc = centred(y, p.ch_hi, p.ch_lo);
             const float r = __builtin_amdgcn_rcpf((float)d);
             const float K = p.B32 * r;
-            const int64_t at = fbase + o;
-            oxyz[3 * at + 0] = xc * K;
-            oxyz[3 * at + 1] = yc * K;
-            oxyz[3 * at + 2] = p.fB32 * r;
             const int ddx = (bf.dxbits[d * p.dx_words + (x >> 5)] >> (x & 31)) & 1;
-            const int ddy = (bf.dybits[d * p.dy_words + dyw] >> dyb) & 1;
-            *reinterpret_cast<int2*>(opts + 2 * at) = make_int2(x - ddx, y - ddy);
-            ++o;
+            const int ddy = (bf.dybits[d * p.dy_words + (y >> 5)] >> (y & 31)) & 1;
+            const uint32_t at = running + j;
+            __builtin_nontemporal_store(xc * K, oX + at);
+            __builtin_nontemporal_store(yc * K, oY + at);
+            __builtin_nontemporal_store(p.fB32 * r, oZ + at);
+            const long long pk = ((long long)(uint32_t)(y - ddy) << 32) | (uint32_t)(x - ddx);
+            __builtin_nontemporal_store(pk, reinterpret_cast<long long*>(oP + at));
         }
+        running += total;
     }
+    if (tid == 0) bf.counts[4 * frame + 2] = running;
 }
 
-// ---------------------------------------------------------------------------
-// One launch = pass 2 of chunk c-1 (blocks [0, n2*tiles)) + pass 1 of chunk c
-// (the rest). A pass-2 block is bound to a frame by blockIdx and takes its
-// tile id from that frame's ticket (one counter per frame, each on its own
-// 64-byte line: ~136 atomics per word instead of ~9K on one global word, which
-// saturates at ~88/us). A tile waits only on lower tiles of its own frame,
-// whose blocks took their tickets earlier and are therefore running: forward
-// progress does not depend on dispatch order. Pass-1 blocks wait on nothing.
-// ---------------------------------------------------------------------------
-constexpr int kTicketStride = 16;  // u32 words per frame ticket (64 B)
-
-template <int STEP>
-__global__ __launch_bounds__(256) void pipeline_kernel(PipeBuffers bf, int p2_frame0, int p2_frames,
-                                                       int p1_frame0, int tiles, uint32_t* tickets,
-                                                       KParams p) {
-    __shared__ PipeShared sh;
-    const int n2 = p2_frames * tiles;
-    const int bid = blockIdx.x;
-    if (bid < n2) {
-        const int frame = p2_frame0 + bid / tiles;
-        if (threadIdx.x == 0) sh.tile = atomicAdd(tickets + (int64_t)frame * kTicketStride, 1u);
-        __syncthreads();
-        compact_tile<STEP>(bf, frame, (int)sh.tile, tiles, p, sh);
-    } else {
-        const int h = bid - n2;
-        const int fl = h / tiles;
-        hist_tile<STEP>(bf, p1_frame0 + fl, h - fl * tiles, tiles, p, sh);
-    }
-}
-
-size_t pipeline_ticket_words(int frames) { return (size_t)frames * kTicketStride; }
-
-hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk,
-                           uint32_t* tickets, hipStream_t s) {
+hipError_t launch_hist(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s) {
     const int tiles = pipeline_tiles_per_frame(p);
-    const int nchunks = (frames + chunk - 1) / chunk;
-    for (int c = 0; c <= nchunks; ++c) {
-        const int f2 = (c - 1) * chunk, n2 = c >= 1 ? min(chunk, frames - f2) : 0;
-        const int f1 = c * chunk, n1 = c < nchunks ? min(chunk, frames - f1) : 0;
-        const dim3 grid((n2 + n1) * tiles), blk(256);
-        if (p.step == 1)
-            hipLaunchKernelGGL(pipeline_kernel<1>, grid, blk, 0, s, b, f2, n2, f1, tiles, tickets, p);
-        else if (p.step == 2)
-            hipLaunchKernelGGL(pipeline_kernel<2>, grid, blk, 0, s, b, f2, n2, f1, tiles, tickets, p);
-        else
-            return hipErrorInvalidValue;
-    }
+    if (frames <= 0) return hipSuccess;
+    const dim3 grid(frames * tiles), blk(256);
+    if (p.step == 1)
+        hipLaunchKernelGGL(hist_kernel<1>, grid, blk, 0, s, b, frame0, tiles, p);
+    else if (p.step == 2)
+        hipLaunchKernelGGL(hist_kernel<2>, grid, blk, 0, s, b, frame0, tiles, p);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s) {
+    const int tiles = pipeline_tiles_per_frame(p);
+    if (frames <= 0) return hipSuccess;
+    if (tiles > kMaxTiles || p.Wg > 4096 || p.Hg > 4096) return hipErrorInvalidValue;
+    const dim3 grid(frames), blk(256);
+    if (p.step == 1)
+        hipLaunchKernelGGL(compact_frame_kernel<1>, grid, blk, 0, s, b, frame0, tiles, p);
+    else if (p.step == 2)
+        hipLaunchKernelGGL(compact_frame_kernel<2>, grid, blk, 0, s, b, frame0, tiles, p);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -186,14 +186,13 @@ struct sv_batch {
     KParams kp{};
     int64_t Ng = 0;            // grid points per frame
     int64_t dense_per_frame = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;    // K1, pass 1 (stream A)
+    hipStream_t stream2 = nullptr;   // pass 2 (stream B), overlaps the next segment's pass 1
+    std::vector<hipEvent_t> sync_ev; // segment hand-offs A -> B (timing disabled)
     DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks;
-    // pipeline control block (one memset per call): hist | counts | look-back
-    // granules | per-launch tickets | err
+    // pipeline control block (one memset per call): hist | counts | err
     uint32_t* hist = nullptr;
     int64_t* counts = nullptr;
-    uint64_t* status = nullptr;
-    uint32_t* tickets = nullptr;
     uint32_t* err = nullptr;
     size_t ctrl_bytes = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -350,23 +349,18 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
         if (e == hipSuccess) e = b->pts.ensure(sizeof(int32_t) * 2 * (size_t)b->Ng * frames);
     }
     if (e == hipSuccess) {
-        // worst case: chunk = 1 -> frames + 1 launches
-        const size_t tiles = (size_t)pipeline_tiles_per_frame(b->kp);
         const size_t hist_b = sizeof(uint32_t) * kBins * frames, cnt_b = sizeof(int64_t) * 4 * frames;
-        const size_t st_b = sizeof(uint64_t) * tiles * frames;
-        const size_t tk_b = sizeof(uint32_t) * (pipeline_ticket_words(frames) + 16);
-        e = b->ctrl.ensure(hist_b + cnt_b + st_b + tk_b);
+        e = b->ctrl.ensure(hist_b + cnt_b + 64);
         if (e == hipSuccess) {
             char* base = b->ctrl.as<char>();
             b->hist = reinterpret_cast<uint32_t*>(base);
             b->counts = reinterpret_cast<int64_t*>(base + hist_b);
-            b->status = reinterpret_cast<uint64_t*>(base + hist_b + cnt_b);
-            b->tickets = reinterpret_cast<uint32_t*>(base + hist_b + cnt_b + st_b);
-            b->err = b->tickets + pipeline_ticket_words(frames);
-            b->ctrl_bytes = hist_b + cnt_b + st_b + tk_b;
+            b->err = reinterpret_cast<uint32_t*>(base + hist_b + cnt_b);
+            b->ctrl_bytes = hist_b + cnt_b + 64;
             e = hipMemset(b->ctrl.p, 0, b->ctrl_bytes);
         }
     }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking);
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
     if (e != hipSuccess) {
         sv_batch_destroy(b);
@@ -385,6 +379,11 @@ int sv_batch_destroy(sv_batch* b) {
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : b->pool) (void)hipEventDestroy(ev);
+    for (auto& ev : b->sync_ev) (void)hipEventDestroy(ev);
+    if (b->stream2) {
+        (void)hipStreamSynchronize(b->stream2);
+        (void)hipStreamDestroy(b->stream2);
+    }
     delete b;
     return SV_OK;
 }
@@ -455,8 +454,9 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
                                int hist_thr, int chunk, int sync, Device* d) {
     if (!b->with_bgr) return fail(SV_E_ARG, "pipeline needs a batch created with bgr");
     KParams p = make_params(b->H, b->W, b->step, *cam);
+    if (p.Wg > 4096 || p.Hg > 4096) return fail(SV_E_ARG, "pipeline supports grids up to 4096 x 4096");
     set_plane(p, *plane, point_thr, hist_thr);
-    if (chunk <= 0) chunk = 16;
+    if (chunk <= 0) chunk = 256;
     if (chunk > b->frames) chunk = b->frames;
     const size_t cap = (size_t)b->Ng;
     HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames));
@@ -470,30 +470,37 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     bf.bgr = b->bgr.as<uint8_t>();
     bf.hist = b->hist;
     bf.counts = b->counts;
-    bf.status = b->status;
     bf.kbits = b->masks.as<uint16_t>();
     bf.pres = reinterpret_cast<uint32_t*>(b->masks.as<char>() + kb_bytes);
-    bf.err = b->err;
     bf.xyz = b->xyz.as<float>();
     bf.pts = b->pts.as<int32_t>();
     bf.dxbits = d->tables.dx.as<uint32_t>();
     bf.dybits = d->tables.dy.as<uint32_t>();
     bf.cap = (int64_t)cap;
+    const int nseg = (b->frames + chunk - 1) / chunk;
+    while ((int)b->sync_ev.size() < nseg + 2) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        b->sync_ev.push_back(e);
+    }
     int t0, t1;
     HIP_TRY(hipEventRecord(b->ev[2], b->stream));
     HIP_TRY(b->timed_event(&t0));
     HIP_TRY(hipMemsetAsync(b->ctrl.p, 0, b->ctrl_bytes, b->stream));
-    HIP_TRY(launch_pipeline(p, bf, b->frames, chunk, b->tickets, b->stream));
+    for (int s = 0; s < nseg; ++s) {
+        const int f0 = s * chunk, n = (b->frames - f0) < chunk ? (b->frames - f0) : chunk;
+        HIP_TRY(launch_hist(p, bf, f0, n, b->stream));
+        HIP_TRY(hipEventRecord(b->sync_ev[s], b->stream));
+        HIP_TRY(hipStreamWaitEvent(b->stream2, b->sync_ev[s], 0));
+        HIP_TRY(launch_compact(p, bf, f0, n, b->stream2));
+    }
+    HIP_TRY(hipEventRecord(b->sync_ev[nseg], b->stream2));
+    HIP_TRY(hipStreamWaitEvent(b->stream, b->sync_ev[nseg], 0));
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[3], b->stream));
     b->pending[1].push_back({t0, t1});
     b->have_ms[1] = true;
-    if (sync) {
-        HIP_TRY(hipStreamSynchronize(b->stream));
-        uint32_t err = 0;
-        HIP_TRY(hipMemcpy(&err, b->err, 4, hipMemcpyDeviceToHost));
-        if (err) return fail(SV_E_DEVICE, "pipeline look-back timed out");
-    }
+    if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }
 
@@ -592,9 +599,16 @@ int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64
     HIP_TRY(hipMemcpy(c, b->counts + 4 * (size_t)frame, sizeof c, hipMemcpyDeviceToHost));
     *n = c[2];
     if (c[2] > cap) return fail(SV_E_CAP, "capacity %lld < %lld", (long long)cap, (long long)c[2]);
-    const size_t base = (size_t)b->Ng * frame;
-    if (xyz && c[2]) HIP_TRY(hipMemcpy(xyz, b->xyz.as<float>() + 3 * base, 12 * c[2], hipMemcpyDeviceToHost));
-    if (pts && c[2]) HIP_TRY(hipMemcpy(pts, b->pts.as<int32_t>() + 2 * base, 8 * c[2], hipMemcpyDeviceToHost));
+    const size_t np = (size_t)c[2], cap_f = (size_t)b->Ng;
+    if (xyz && np) {   // device layout is SoA per frame: X[cap] Y[cap] Z[cap]
+        std::vector<float> soa(3 * np);
+        const float* src = b->xyz.as<float>() + 3 * cap_f * frame;
+        for (int k = 0; k < 3; ++k)
+            HIP_TRY(hipMemcpy(soa.data() + k * np, src + k * cap_f, 4 * np, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < np; ++i)
+            for (int k = 0; k < 3; ++k) xyz[3 * i + k] = soa[k * np + i];
+    }
+    if (pts && np) HIP_TRY(hipMemcpy(pts, b->pts.as<int32_t>() + 2 * cap_f * frame, 8 * np, hipMemcpyDeviceToHost));
     return SV_OK;
 }
 

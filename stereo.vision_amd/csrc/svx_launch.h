@@ -34,22 +34,18 @@ struct PipeBuffers {
     const uint8_t* bgr;
     uint32_t* hist;      // frames x 1024
     int64_t* counts;     // frames x 4 (N_valid, N_kept, N_kept2, spare)
-    uint64_t* status;    // frames x tiles look-back granules
     uint16_t* kbits;     // frames x tiles x 256: keep1 bit (4*i + k) of each lane's quads
     uint32_t* pres;      // frames x tiles x 32: hue bins present among the tile's keep1 points
-    uint32_t* err;
-    float* xyz;          // frames x cap x 3
-    int32_t* pts;        // frames x cap x 2
+    float* xyz;          // frames x {X[cap], Y[cap], Z[cap]} (SoA per frame)
+    int32_t* pts;        // frames x cap x (x, y) int32
     const uint32_t* dxbits;
     const uint32_t* dybits;
     int64_t cap;         // points per frame (Ng)
 };
 int pipeline_tiles_per_frame(const KParams& p);
-// frames in chunks of `chunk`: chunks+1 launches; the per-frame tickets
-// (pipeline_ticket_words(frames) u32) and the look-back granules (frames x
-// tiles) must be zero on entry.
-size_t pipeline_ticket_words(int frames);
-hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk,
-                           uint32_t* tickets, hipStream_t s);
+// pass 1 over frames [frame0, frame0+frames): grid = frames x tiles
+hipError_t launch_hist(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s);
+// pass 2 over the same frames (after their pass 1): one workgroup per frame
+hipError_t launch_compact(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s);
 
 }  // namespace svx
