@@ -14,14 +14,14 @@
 //                         with one global atomic per non-zero bin; writes the
 //                         tile's keep1 bitmask (2 B per lane = 1 bit/pt) and
 //                         its bin-presence mask (1024 bits).
-//   pass 2  compact_frame reads the keep1 bits + disparity (~1.1 B/pt); a tile
-//                         whose present bins are all above hist_thr ("clean",
-//                         nearly all of them) needs no hue at all; a "dirty"
-//                         tile re-reads its BGR and recomputes the bins of its
-//                         keep1 points. One workgroup per frame walks the tiles
-//                         in order (running offset in a register), compacting
-//                         through an LDS descriptor scatter so that all stores
-//                         are contiguous, non-temporal SoA writes.
+//   offsets               one small workgroup per frame: a tile whose present
+//                         bins all pass hist_thr ("clean", nearly all) keeps
+//                         its keep1 bits as keep2; a "dirty" tile re-reads its
+//                         BGR and rewrites its bits to keep2; the per-tile
+//                         counts are scanned into output offsets.
+//   pass 2  compact       one workgroup per tile: keep2 bits + disparity
+//                         (~1.1 B/pt) + offset in; block scan, LDS descriptor
+//                         scatter, then contiguous non-temporal SoA stores.
 // Frames go in segments; pass 1 of segment s+1 (stream A) overlaps pass 2 of
 // segment s (stream B): pass 1 is VALU-heavy, pass 2 store-bound. The control
 // words (histograms, counts) are zeroed by one memset per call; the keep /
@@ -159,6 +159,7 @@ __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int 
     }
     __syncthreads();
     if (tid == 0) {
+        bf.tcount[slot] = sh.cnt[1];
         atomicAdd(reinterpret_cast<unsigned long long*>(bf.counts + 4 * frame + 0), (unsigned long long)sh.cnt[0]);
         atomicAdd(reinterpret_cast<unsigned long long*>(bf.counts + 4 * frame + 1), (unsigned long long)sh.cnt[1]);
     }
@@ -186,17 +187,100 @@ __global__ __launch_bounds__(256) void hist_kernel(PipeBuffers bf, int frame0, i
 }
 
 // ---------------------------------------------------------------------------
-// pass 2: one workgroup per frame, walking its tiles in raster order, so the
-// running output offset is a register (no inter-workgroup protocol at all).
-//   * the next tile's keep1 bits + disparity are loaded while the current one
-//     is compacted (register double-buffering);
-//   * which tiles are dirty (hold a keep1 point whose bin fails hist_thr) is
-//     decided once per frame from the presence masks;
-//   * compaction: a block scan gives each keep2 point its slot in the tile;
-//     lanes scatter a 4-byte descriptor (gx | gy | d) into LDS at that slot,
-//     then lane j of the block produces output j: every store instruction
-//     writes contiguous lanes into the SoA outputs (X, Y, Z, (x,y)) with
-//     non-temporal stores — no partial lines.
+// offsets: one workgroup per frame (tiny). Decides which tiles are dirty (a
+// keep1 point whose bin fails hist_thr, from the presence masks), rewrites
+// those tiles' bits from keep1 to keep2 (re-reading their BGR), and scans the
+// per-tile keep2 counts into per-tile output offsets + N_kept2. After it, pass
+// 2 is embarrassingly parallel: no tickets, no look-back, no BGR.
+// ---------------------------------------------------------------------------
+constexpr int kMaxTiles = 2048;   // tiles per frame supported by one offsets workgroup
+
+struct OffsetsShared {
+    uint32_t okbits[kBins / 32];
+    uint32_t dirty[kMaxTiles / 32];
+    uint32_t cnt[kMaxTiles];
+    uint32_t wsum[4];
+};
+
+template <int STEP>
+__global__ __launch_bounds__(256) void offsets_kernel(PipeBuffers bf, int frame0, int tiles, KParams p) {
+    __shared__ OffsetsShared sh;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int frame = frame0 + blockIdx.x;
+    const int64_t slot0 = (int64_t)frame * tiles;
+    const uint32_t* gh = bf.hist + (int64_t)frame * kBins;
+#pragma unroll
+    for (int r = 0; r < kBins / 256; ++r) {   // hist[bin] > hist_thr as a 1024-bit mask
+        const uint64_t m = __ballot((int64_t)gh[r * 256 + tid] > (int64_t)p.hist_thr);
+        if (lane == 0) {
+            sh.okbits[(r * 256 + wave * 64) / 32] = (uint32_t)m;
+            sh.okbits[(r * 256 + wave * 64) / 32 + 1] = (uint32_t)(m >> 32);
+        }
+    }
+    for (int w = tid; w < kMaxTiles / 32; w += 256) sh.dirty[w] = 0;
+    for (int t = tid; t < tiles; t += 256) sh.cnt[t] = bf.tcount[slot0 + t];
+    __syncthreads();
+    for (int i = tid; i < tiles * (kBins / 32); i += 256) {
+        const int t = i / (kBins / 32), w = i - t * (kBins / 32);
+        if (bf.pres[(slot0 + t) * (kBins / 32) + w] & ~sh.okbits[w]) atomicOr(&sh.dirty[t >> 5], 1u << (t & 31));
+    }
+    __syncthreads();
+    const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
+    for (int t = 0; t < tiles; ++t) {   // uniform loop; work only on (rare) dirty tiles
+        if (!((sh.dirty[t >> 5] >> (t & 31)) & 1)) continue;
+        uint16_t* kbp = bf.kbits + (slot0 + t) * 256 + tid;
+        uint32_t keep = *kbp;
+        int gy[kQPT], q[kQPT];
+        tile_geometry(t * 256 * kQPT, tid, p, gy, q);
+#pragma unroll
+        for (int i = 0; i < kQPT; ++i) {
+            if (!((keep >> (4 * i)) & 0xF)) continue;
+            QuadIn<STEP> in;
+            load_bgr<STEP>(row_ptr<STEP>(bgr, gy[i], 3, p), q[i], in);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (!(keep & (1u << (4 * i + k)))) continue;
+                const int bin = point_bin<STEP>(in, k);
+                if (!((sh.okbits[bin >> 5] >> (bin & 31)) & 1)) keep &= ~(1u << (4 * i + k));
+            }
+        }
+        *kbp = (uint16_t)keep;
+        const uint32_t c = wave_sum(__builtin_popcount(keep));
+        if (lane == 0) sh.wsum[wave] = c;
+        __syncthreads();
+        if (tid == 0) sh.cnt[t] = sh.wsum[0] + sh.wsum[1] + sh.wsum[2] + sh.wsum[3];
+        __syncthreads();
+    }
+    // exclusive scan of the tile counts (<= 8 per lane, lane-major)
+    constexpr int PER = kMaxTiles / 256;
+    uint32_t v[PER], run = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int t = tid * PER + j;
+        v[j] = t < tiles ? sh.cnt[t] : 0u;
+        run += v[j];
+    }
+    const uint32_t inc = wave_incl_scan(run);
+    if (lane == 63) sh.wsum[wave] = inc;
+    __syncthreads();
+    uint32_t base = inc - run;
+    for (int w = 0; w < wave; ++w) base += sh.wsum[w];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int t = tid * PER + j;
+        if (t < tiles) bf.toff[slot0 + t] = base;
+        base += v[j];
+    }
+    if (tid == 255) bf.counts[4 * frame + 2] = base;
+}
+
+// ---------------------------------------------------------------------------
+// pass 2: one workgroup per tile. keep2 bits + disparity + the tile's output
+// offset in; a block scan gives each keep2 point its slot; lanes scatter a
+// 4-byte descriptor (d | gy | gx) into LDS at that slot, then lane j of the
+// block produces output j — every store instruction writes contiguous lanes of
+// the SoA outputs (X, Y, Z, (x,y)) with non-temporal stores, no partial lines.
+// The delta-table words of 8 outputs per lane are loaded before any is used.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
     const int lane = lane_id();
@@ -208,22 +292,25 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
     return v;
 }
 
-constexpr int kMaxTiles = 2048;   // tiles per frame supported by the dirty bitmap
-
 struct CompactShared {
-    uint32_t okbits[kBins / 32];
-    uint32_t dirty[kMaxTiles / 32];
     uint64_t wave[4];
-    uint32_t desc[2][256 * kQPT * 4];   // double-buffered output descriptors (2 x 16 KB)
+    uint32_t desc[256 * kQPT * 4];   // 16 KB: one descriptor per keep2 point of the tile
 };
 
 template <int STEP>
-__device__ __forceinline__ void prefetch_tile(const PipeBuffers& bf, const uint8_t* disp, int64_t slot,
-                                              int qbase, int tid, const KParams& p, uint32_t& kb,
-                                              uint32_t (&dw)[kQPT][STEP]) {
-    kb = bf.kbits[slot * 256 + tid];
+__global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0, int tiles, KParams p) {
+    __shared__ CompactShared sh;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int fl = blockIdx.x / tiles;
+    const int t = blockIdx.x - fl * tiles;
+    const int frame = frame0 + fl;
+    const int64_t slot = (int64_t)frame * tiles + t;
+    const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
+    const uint32_t keep = bf.kbits[slot * 256 + tid];
+    const uint32_t toff = bf.toff[slot];
     int gy[kQPT], q[kQPT];
-    tile_geometry(qbase, tid, p, gy, q);
+    tile_geometry(t * 256 * kQPT, tid, p, gy, q);
+    uint32_t dw[kQPT][STEP];
 #pragma unroll
     for (int i = 0; i < kQPT; ++i) {
         const uint8_t* row = row_ptr<STEP>(disp, gy[i], 1, p);
@@ -235,122 +322,74 @@ __device__ __forceinline__ void prefetch_tile(const PipeBuffers& bf, const uint8
             dw[i][1] = w.y;
         }
     }
-}
-
-template <int STEP>
-__global__ __launch_bounds__(256) void compact_frame_kernel(PipeBuffers bf, int frame0, int tiles, KParams p) {
-    __shared__ CompactShared sh;
-    constexpr int DW = STEP;   // disparity dwords kept per quad: 1 (step 1) / 2 (step 2)
-    const int tid = threadIdx.x;
-    const int lane = lane_id();
-    const int wave = tid >> 6;
-    const int frame = frame0 + blockIdx.x;
-    const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
-    const int64_t slot0 = (int64_t)frame * tiles;
-    {   // hist[bin] > hist_thr as a 1024-bit mask
-        const uint32_t* gh = bf.hist + (int64_t)frame * kBins;
+    uint64_t cnt = 0;
 #pragma unroll
-        for (int r = 0; r < kBins / 256; ++r) {
-            const uint64_t m = __ballot((int64_t)gh[r * 256 + tid] > (int64_t)p.hist_thr);
-            if (lane == 0) {
-                sh.okbits[(r * 256 + wave * 64) / 32] = (uint32_t)m;
-                sh.okbits[(r * 256 + wave * 64) / 32 + 1] = (uint32_t)(m >> 32);
-            }
-        }
-        for (int w = tid; w < kMaxTiles / 32; w += 256) sh.dirty[w] = 0;
-    }
+    for (int i = 0; i < kQPT; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
+    const uint64_t inc = wave_incl_scan64(cnt);
+    if (lane == 63) sh.wave[wave] = inc;
     __syncthreads();
-    // dirty tiles: any present bin that fails the histogram threshold
-    for (int i = tid; i < tiles * (kBins / 32); i += 256) {
-        const int t = i / (kBins / 32), w = i - t * (kBins / 32);
-        if (bf.pres[(slot0 + t) * (kBins / 32) + w] & ~sh.okbits[w]) atomicOr(&sh.dirty[t >> 5], 1u << (t & 31));
+    uint64_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint64_t v = sh.wave[w];
+        wbase += (w < wave) ? v : 0ull;
+        tot += v;
     }
-    float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap;
+    const uint64_t excl = wbase + inc - cnt;
+    uint32_t rowbase = 0;
+#pragma unroll
+    for (int i = 0; i < kQPT; ++i) {
+        uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
+        rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!(keep & (1u << (4 * i + k)))) continue;
+            uint32_t d;
+            if constexpr (STEP == 1) d = (dw[i][0] >> (8 * k)) & 0xFF;
+            else d = (dw[i][k >> 1] >> (16 * (k & 1))) & 0xFF;
+            sh.desc[o++] = (d << 24) | ((uint32_t)gy[i] << 12) | (uint32_t)(4 * q[i] + k);
+        }
+    }
+    const uint32_t total = rowbase;
+    __syncthreads();
+    const int64_t fbase = (int64_t)frame * bf.cap + toff;
+    float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap + toff;
     float* oY = oX + bf.cap;
     float* oZ = oY + bf.cap;
-    int2* oP = reinterpret_cast<int2*>(bf.pts) + (int64_t)frame * bf.cap;
-
-    uint32_t kb_n, dw_n[kQPT][DW];
-    prefetch_tile<STEP>(bf, disp, slot0, 0, tid, p, kb_n, dw_n);
-    uint32_t running = 0;
-    for (int t = 0; t < tiles; ++t) {
-        uint32_t keep = kb_n, dw[kQPT][DW];
+    long long* oP = reinterpret_cast<long long*>(bf.pts) + fbase;
+    constexpr int B = 8;   // outputs per lane per batch (table loads in flight together)
+    for (uint32_t j0 = 0; j0 < total; j0 += 256 * B) {
+        uint32_t u[B], wx[B], wy[B];
 #pragma unroll
-        for (int i = 0; i < kQPT; ++i)
-#pragma unroll
-            for (int j = 0; j < DW; ++j) dw[i][j] = dw_n[i][j];
-        if (t + 1 < tiles) prefetch_tile<STEP>(bf, disp, slot0 + t + 1, (t + 1) * 256 * kQPT, tid, p, kb_n, dw_n);
-        const int qbase = t * 256 * kQPT;
-        int gy[kQPT], q[kQPT];
-        tile_geometry(qbase, tid, p, gy, q);
-        __syncthreads();   // dirty bitmap complete (first tile) / previous desc buffer drained
-        if ((sh.dirty[t >> 5] >> (t & 31)) & 1) {   // block-uniform, rare
-            const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
-#pragma unroll
-            for (int i = 0; i < kQPT; ++i) {
-                if (!((keep >> (4 * i)) & 0xF)) continue;
-                QuadIn<STEP> in;
-                load_bgr<STEP>(row_ptr<STEP>(bgr, gy[i], 3, p), q[i], in);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (!(keep & (1u << (4 * i + k)))) continue;
-                    const int bin = point_bin<STEP>(in, k);
-                    if (!((sh.okbits[bin >> 5] >> (bin & 31)) & 1)) keep &= ~(1u << (4 * i + k));
-                }
-            }
+        for (int m = 0; m < B; ++m) {
+            const uint32_t j = j0 + m * 256 + tid;
+            u[m] = j < total ? sh.desc[j] : (1u << 24);
+            const uint32_t d = u[m] >> 24;
+            const int y = (int)((u[m] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(u[m] & 0xFFF) * STEP;
+            wx[m] = bf.dxbits[d * p.dx_words + (x >> 5)];
+            wy[m] = bf.dybits[d * p.dy_words + (y >> 5)];
         }
-        uint64_t cnt = 0;
 #pragma unroll
-        for (int i = 0; i < kQPT; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
-        const uint64_t inc = wave_incl_scan64(cnt);
-        if (lane == 63) sh.wave[wave] = inc;
-        __syncthreads();
-        uint64_t wbase = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const uint64_t v = sh.wave[w];
-            wbase += (w < wave) ? v : 0ull;
-            tot += v;
-        }
-        const uint64_t excl = wbase + inc - cnt;
-        uint32_t* desc = sh.desc[t & 1];
-        uint32_t rowbase = 0;
-#pragma unroll
-        for (int i = 0; i < kQPT; ++i) {
-            uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
-            rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (!(keep & (1u << (4 * i + k)))) continue;
-                uint32_t d;
-                if constexpr (STEP == 1) d = (dw[i][0] >> (8 * k)) & 0xFF;
-                else d = (dw[i][k >> 1] >> (16 * (k & 1))) & 0xFF;
-                desc[o++] = (d << 24) | ((uint32_t)gy[i] << 12) | (uint32_t)(4 * q[i] + k);
-            }
-        }
-        const uint32_t total = rowbase;
-        __syncthreads();
-        for (uint32_t j = tid; j < total; j += 256) {
-            const uint32_t u = desc[j];
-            const uint32_t d = u >> 24;
-            const int y = (int)((u >> 12) & 0xFFF) * STEP;
-            const int x = (int)(u & 0xFFF) * STEP;
+        for (int m = 0; m < B; ++m) {
+            const uint32_t j = j0 + m * 256 + tid;
+            if (j >= total) continue;
+            const uint32_t d = u[m] >> 24;
+            const int y = (int)((u[m] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(u[m] & 0xFFF) * STEP;
             const float xc = centred(x, p.cw_hi, p.cw_lo);
             const float yc = centred(y, p.ch_hi, p.ch_lo);
             const float r = __builtin_amdgcn_rcpf((float)d);
             const float K = p.B32 * r;
-            const int ddx = (bf.dxbits[d * p.dx_words + (x >> 5)] >> (x & 31)) & 1;
-            const int ddy = (bf.dybits[d * p.dy_words + (y >> 5)] >> (y & 31)) & 1;
-            const uint32_t at = running + j;
-            __builtin_nontemporal_store(xc * K, oX + at);
-            __builtin_nontemporal_store(yc * K, oY + at);
-            __builtin_nontemporal_store(p.fB32 * r, oZ + at);
+            const int ddx = (wx[m] >> (x & 31)) & 1;
+            const int ddy = (wy[m] >> (y & 31)) & 1;
+            __builtin_nontemporal_store(xc * K, oX + j);
+            __builtin_nontemporal_store(yc * K, oY + j);
+            __builtin_nontemporal_store(p.fB32 * r, oZ + j);
             const long long pk = ((long long)(uint32_t)(y - ddy) << 32) | (uint32_t)(x - ddx);
-            __builtin_nontemporal_store(pk, reinterpret_cast<long long*>(oP + at));
+            __builtin_nontemporal_store(pk, oP + j);
         }
-        running += total;
     }
-    if (tid == 0) bf.counts[4 * frame + 2] = running;
 }
 
 hipError_t launch_hist(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s) {
@@ -370,13 +409,16 @@ hipError_t launch_compact(const KParams& p, const PipeBuffers& b, int frame0, in
     const int tiles = pipeline_tiles_per_frame(p);
     if (frames <= 0) return hipSuccess;
     if (tiles > kMaxTiles || p.Wg > 4096 || p.Hg > 4096) return hipErrorInvalidValue;
-    const dim3 grid(frames), blk(256);
-    if (p.step == 1)
-        hipLaunchKernelGGL(compact_frame_kernel<1>, grid, blk, 0, s, b, frame0, tiles, p);
-    else if (p.step == 2)
-        hipLaunchKernelGGL(compact_frame_kernel<2>, grid, blk, 0, s, b, frame0, tiles, p);
-    else
+    const dim3 g_off(frames), g_tile(frames * tiles), blk(256);
+    if (p.step == 1) {
+        hipLaunchKernelGGL(offsets_kernel<1>, g_off, blk, 0, s, b, frame0, tiles, p);
+        hipLaunchKernelGGL(compact_kernel<1>, g_tile, blk, 0, s, b, frame0, tiles, p);
+    } else if (p.step == 2) {
+        hipLaunchKernelGGL(offsets_kernel<2>, g_off, blk, 0, s, b, frame0, tiles, p);
+        hipLaunchKernelGGL(compact_kernel<2>, g_tile, blk, 0, s, b, frame0, tiles, p);
+    } else {
         return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

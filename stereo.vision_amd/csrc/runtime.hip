@@ -463,7 +463,9 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     HIP_TRY(b->pts.ensure(sizeof(int32_t) * 2 * cap * b->frames));
     const size_t tiles = (size_t)pipeline_tiles_per_frame(p);
     const size_t kb_bytes = sizeof(uint16_t) * 256 * tiles * b->frames;
-    HIP_TRY(b->masks.ensure(kb_bytes + sizeof(uint32_t) * (kBins / 32) * tiles * b->frames));
+    const size_t pres_bytes = sizeof(uint32_t) * (kBins / 32) * tiles * b->frames;
+    const size_t tc_bytes = sizeof(uint32_t) * tiles * b->frames;
+    HIP_TRY(b->masks.ensure(kb_bytes + pres_bytes + 2 * tc_bytes));
     if (int rc = ensure_tables(*d, b->H, b->W, *cam, b->stream)) return rc;
     PipeBuffers bf;
     bf.disp = b->disp.as<uint8_t>();
@@ -472,6 +474,8 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     bf.counts = b->counts;
     bf.kbits = b->masks.as<uint16_t>();
     bf.pres = reinterpret_cast<uint32_t*>(b->masks.as<char>() + kb_bytes);
+    bf.tcount = reinterpret_cast<uint32_t*>(b->masks.as<char>() + kb_bytes + pres_bytes);
+    bf.toff = bf.tcount + tiles * b->frames;
     bf.xyz = b->xyz.as<float>();
     bf.pts = b->pts.as<int32_t>();
     bf.dxbits = d->tables.dx.as<uint32_t>();

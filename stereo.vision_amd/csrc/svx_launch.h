@@ -34,7 +34,9 @@ struct PipeBuffers {
     const uint8_t* bgr;
     uint32_t* hist;      // frames x 1024
     int64_t* counts;     // frames x 4 (N_valid, N_kept, N_kept2, spare)
-    uint16_t* kbits;     // frames x tiles x 256: keep1 bit (4*i + k) of each lane's quads
+    uint16_t* kbits;     // frames x tiles x 256: keep1 (pass 1) -> keep2 (offsets) bit 4*i+k of each lane's quads
+    uint32_t* tcount;    // frames x tiles: keep1 count per tile (pass 1)
+    uint32_t* toff;      // frames x tiles: output offset of each tile (offsets kernel)
     uint32_t* pres;      // frames x tiles x 32: hue bins present among the tile's keep1 points
     float* xyz;          // frames x {X[cap], Y[cap], Z[cap]} (SoA per frame)
     int32_t* pts;        // frames x cap x (x, y) int32
@@ -45,7 +47,8 @@ struct PipeBuffers {
 int pipeline_tiles_per_frame(const KParams& p);
 // pass 1 over frames [frame0, frame0+frames): grid = frames x tiles
 hipError_t launch_hist(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s);
-// pass 2 over the same frames (after their pass 1): one workgroup per frame
+// offsets (one workgroup per frame) + pass 2 (one workgroup per tile) over the
+// same frames, after their pass 1
 hipError_t launch_compact(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s);
 
 }  // namespace svx
