@@ -294,8 +294,11 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
 
 struct CompactShared {
     uint64_t wave[4];
-    uint32_t desc[256 * kQPT * 4];   // 16 KB: one descriptor per keep2 point of the tile
+    uint32_t desc[256 * kQPT * 4 + 4];   // one descriptor per keep2 point (+ alignment slack)
 };
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef int v4i __attribute__((ext_vector_type(4)));
 
 template <int STEP>
 __global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0, int tiles, KParams p) {
@@ -336,7 +339,10 @@ __global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0
         tot += v;
     }
     const uint64_t excl = wbase + inc - cnt;
-    uint32_t rowbase = 0;
+    // descriptors land at LDS slot (toff & 3) + o, so that LDS slot s <-> global
+    // element g0 + s with g0 = toff & ~3: output groups of 4 are 16-byte aligned
+    const uint32_t lead = toff & 3;
+    uint32_t rowbase = lead;
 #pragma unroll
     for (int i = 0; i < kQPT; ++i) {
         uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
@@ -350,44 +356,61 @@ __global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0
             sh.desc[o++] = (d << 24) | ((uint32_t)gy[i] << 12) | (uint32_t)(4 * q[i] + k);
         }
     }
-    const uint32_t total = rowbase;
+    const uint32_t end = rowbase;            // one past the last valid LDS slot
     __syncthreads();
-    const int64_t fbase = (int64_t)frame * bf.cap + toff;
-    float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap + toff;
+    const uint32_t g0 = toff - lead;
+    float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap + g0;
     float* oY = oX + bf.cap;
     float* oZ = oY + bf.cap;
-    long long* oP = reinterpret_cast<long long*>(bf.pts) + fbase;
-    constexpr int B = 8;   // outputs per lane per batch (table loads in flight together)
-    for (uint32_t j0 = 0; j0 < total; j0 += 256 * B) {
-        uint32_t u[B], wx[B], wy[B];
+    int32_t* oP = bf.pts + ((int64_t)frame * bf.cap + g0) * 2;
+    const uint32_t groups = (end + 3) >> 2;
+    for (uint32_t m = tid; m < groups; m += 256) {
+        const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.desc[4 * m]);
+        const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
+        uint32_t wx[4], wy[4];
+        bool ok[4];
 #pragma unroll
-        for (int m = 0; m < B; ++m) {
-            const uint32_t j = j0 + m * 256 + tid;
-            u[m] = j < total ? sh.desc[j] : (1u << 24);
-            const uint32_t d = u[m] >> 24;
-            const int y = (int)((u[m] >> 12) & 0xFFF) * STEP;
-            const int x = (int)(u[m] & 0xFFF) * STEP;
-            wx[m] = bf.dxbits[d * p.dx_words + (x >> 5)];
-            wy[m] = bf.dybits[d * p.dy_words + (y >> 5)];
+        for (int e = 0; e < 4; ++e) {   // all table loads of the group in flight together
+            const uint32_t s_ = 4 * m + e;
+            ok[e] = s_ >= lead && s_ < end;
+            const uint32_t uu = ok[e] ? u[e] : (1u << 24);
+            const uint32_t d = uu >> 24;
+            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
+            const int x = (int)(uu & 0xFFF) * STEP;
+            wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
+            wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
         }
+        float X[4], Y[4], Z[4];
+        int PX[4], PY[4];
 #pragma unroll
-        for (int m = 0; m < B; ++m) {
-            const uint32_t j = j0 + m * 256 + tid;
-            if (j >= total) continue;
-            const uint32_t d = u[m] >> 24;
-            const int y = (int)((u[m] >> 12) & 0xFFF) * STEP;
-            const int x = (int)(u[m] & 0xFFF) * STEP;
-            const float xc = centred(x, p.cw_hi, p.cw_lo);
-            const float yc = centred(y, p.ch_hi, p.ch_lo);
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t uu = ok[e] ? u[e] : (1u << 24);
+            const uint32_t d = uu >> 24;
+            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
+            const int x = (int)(uu & 0xFFF) * STEP;
             const float r = __builtin_amdgcn_rcpf((float)d);
             const float K = p.B32 * r;
-            const int ddx = (wx[m] >> (x & 31)) & 1;
-            const int ddy = (wy[m] >> (y & 31)) & 1;
-            __builtin_nontemporal_store(xc * K, oX + j);
-            __builtin_nontemporal_store(yc * K, oY + j);
-            __builtin_nontemporal_store(p.fB32 * r, oZ + j);
-            const long long pk = ((long long)(uint32_t)(y - ddy) << 32) | (uint32_t)(x - ddx);
-            __builtin_nontemporal_store(pk, oP + j);
+            X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
+            Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
+            Z[e] = p.fB32 * r;
+            PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
+            PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
+        }
+        if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
+            __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + 4 * m));
+            __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + 4 * m));
+            __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + 4 * m));
+            __builtin_nontemporal_store((v4i){PX[0], PY[0], PX[1], PY[1]}, reinterpret_cast<v4i*>(oP + 8 * m));
+            __builtin_nontemporal_store((v4i){PX[2], PY[2], PX[3], PY[3]}, reinterpret_cast<v4i*>(oP + 8 * m + 4));
+        } else {                // the tile's first / last group
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (!ok[e]) continue;
+                oX[4 * m + e] = X[e];
+                oY[4 * m + e] = Y[e];
+                oZ[4 * m + e] = Z[e];
+                *reinterpret_cast<int2*>(oP + 2 * (4 * m + e)) = make_int2(PX[e], PY[e]);
+            }
         }
     }
 }

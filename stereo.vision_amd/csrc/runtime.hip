@@ -185,6 +185,7 @@ struct sv_batch {
     bool with_bgr = false;
     KParams kp{};
     int64_t Ng = 0;            // grid points per frame
+    size_t cap = 0;            // per-frame point capacity of the pipeline outputs (Ng rounded up to 64)
     int64_t dense_per_frame = 0;
     hipStream_t stream = nullptr;    // K1, pass 1 (stream A)
     hipStream_t stream2 = nullptr;   // pass 2 (stream B), overlaps the next segment's pass 1
@@ -339,14 +340,15 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
     sv_camera cam0{1, 1, 0, 0};
     b->kp = make_params(H, W, step, cam0);
     b->Ng = (int64_t)b->kp.Hg * b->kp.Wg;
+    b->cap = ((size_t)b->Ng + 63) / 64 * 64;
     b->dense_per_frame = (int64_t)b->kp.Hg * b->kp.pitch;
     b->stream = d->stream;
     const size_t px = (size_t)frames * H * W;
     hipError_t e = b->disp.ensure(px);
     if (e == hipSuccess && b->with_bgr) e = b->bgr.ensure(px * 3);
     if (e == hipSuccess && with_points) {
-        e = b->xyz.ensure(sizeof(float) * 3 * (size_t)b->Ng * frames);
-        if (e == hipSuccess) e = b->pts.ensure(sizeof(int32_t) * 2 * (size_t)b->Ng * frames);
+        e = b->xyz.ensure(sizeof(float) * 3 * b->cap * frames);
+        if (e == hipSuccess) e = b->pts.ensure(sizeof(int32_t) * 2 * b->cap * frames);
     }
     if (e == hipSuccess) {
         const size_t hist_b = sizeof(uint32_t) * kBins * frames, cnt_b = sizeof(int64_t) * 4 * frames;
@@ -458,7 +460,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     set_plane(p, *plane, point_thr, hist_thr);
     if (chunk <= 0) chunk = 256;
     if (chunk > b->frames) chunk = b->frames;
-    const size_t cap = (size_t)b->Ng;
+    const size_t cap = b->cap;   // Ng rounded up to 64: 256-byte aligned SoA planes
     HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames));
     HIP_TRY(b->pts.ensure(sizeof(int32_t) * 2 * cap * b->frames));
     const size_t tiles = (size_t)pipeline_tiles_per_frame(p);
@@ -603,7 +605,7 @@ int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64
     HIP_TRY(hipMemcpy(c, b->counts + 4 * (size_t)frame, sizeof c, hipMemcpyDeviceToHost));
     *n = c[2];
     if (c[2] > cap) return fail(SV_E_CAP, "capacity %lld < %lld", (long long)cap, (long long)c[2]);
-    const size_t np = (size_t)c[2], cap_f = (size_t)b->Ng;
+    const size_t np = (size_t)c[2], cap_f = b->cap;
     if (xyz && np) {   // device layout is SoA per frame: X[cap] Y[cap] Z[cap]
         std::vector<float> soa(3 * np);
         const float* src = b->xyz.as<float>() + 3 * cap_f * frame;
