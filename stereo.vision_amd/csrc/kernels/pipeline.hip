@@ -22,9 +22,10 @@
 //   pass 2  compact       one workgroup per tile: keep2 bits + disparity
 //                         (~1.1 B/pt) + offset in; block scan, LDS descriptor
 //                         scatter, then contiguous non-temporal SoA stores.
-// Frames go in segments; pass 1 of segment s+1 (stream A) overlaps pass 2 of
-// segment s (stream B): pass 1 is VALU-heavy, pass 2 store-bound. The control
-// words (histograms, counts) are zeroed by one memset per call; the keep /
+// Frames go in chunks: launch c = pass 2 of chunk c-1 + pass 1 of chunk c in
+// one grid with interleaved roles (pass 1 is VALU-heavy, pass 2 store-bound,
+// so they share every CU well), then offsets(c). The control words
+// (histograms, counts) are zeroed by one memset per call; the keep /
 // presence masks are fully rewritten by pass 1.
 #include "../svx_launch.h"
 
@@ -179,12 +180,6 @@ __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int 
     }
 }
 
-template <int STEP>
-__global__ __launch_bounds__(256) void hist_kernel(PipeBuffers bf, int frame0, int tiles, KParams p) {
-    __shared__ PipeShared sh;
-    const int fl = blockIdx.x / tiles;
-    hist_tile<STEP>(bf, frame0 + fl, blockIdx.x - fl * tiles, tiles, p, sh);
-}
 
 // ---------------------------------------------------------------------------
 // offsets: one workgroup per frame (tiny). Decides which tiles are dirty (a
@@ -301,12 +296,9 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 template <int STEP>
-__global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0, int tiles, KParams p) {
-    __shared__ CompactShared sh;
+__device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, int t, int tiles,
+                                             const KParams& p, CompactShared& sh) {
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int fl = blockIdx.x / tiles;
-    const int t = blockIdx.x - fl * tiles;
-    const int frame = frame0 + fl;
     const int64_t slot = (int64_t)frame * tiles + t;
     const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
     const uint32_t keep = bf.kbits[slot * 256 + tid];
@@ -415,32 +407,60 @@ __global__ __launch_bounds__(256) void compact_kernel(PipeBuffers bf, int frame0
     }
 }
 
-hipError_t launch_hist(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s) {
-    const int tiles = pipeline_tiles_per_frame(p);
-    if (frames <= 0) return hipSuccess;
-    const dim3 grid(frames * tiles), blk(256);
-    if (p.step == 1)
-        hipLaunchKernelGGL(hist_kernel<1>, grid, blk, 0, s, b, frame0, tiles, p);
-    else if (p.step == 2)
-        hipLaunchKernelGGL(hist_kernel<2>, grid, blk, 0, s, b, frame0, tiles, p);
+// ---------------------------------------------------------------------------
+// One launch = pass 2 of chunk c-1 + pass 1 of chunk c. The two have no
+// dependency on each other, and the workgroup roles are interleaved (even
+// blockIdx: pass 2, odd: pass 1, while both last) so every CU runs VALU-heavy
+// pass-1 waves beside store-bound pass-2 waves. offsets(c) runs between
+// launches c and c+1 (stream order).
+// ---------------------------------------------------------------------------
+union StageShared {
+    PipeShared p1;
+    CompactShared p2;
+};
+
+template <int STEP>
+__global__ __launch_bounds__(256) void stage_kernel(PipeBuffers bf, int p2_frame0, int n2, int p1_frame0,
+                                                    int n1, int tiles, KParams p) {
+    __shared__ StageShared sh;
+    const int b = blockIdx.x;
+    const int both = 2 * min(n1, n2);
+    int role, idx;   // role 2 = pass 2, 1 = pass 1
+    if (b < both) {
+        role = (b & 1) ? 1 : 2;
+        idx = b >> 1;
+    } else {
+        role = n2 > n1 ? 2 : 1;
+        idx = (b - both) + both / 2;
+    }
+    const int fl = idx / tiles, t = idx - fl * tiles;
+    if (role == 2)
+        compact_tile<STEP>(bf, p2_frame0 + fl, t, tiles, p, sh.p2);
     else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
+        hist_tile<STEP>(bf, p1_frame0 + fl, t, tiles, p, sh.p1);
 }
 
-hipError_t launch_compact(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s) {
+hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk, hipStream_t s) {
     const int tiles = pipeline_tiles_per_frame(p);
     if (frames <= 0) return hipSuccess;
-    if (tiles > kMaxTiles || p.Wg > 4096 || p.Hg > 4096) return hipErrorInvalidValue;
-    const dim3 g_off(frames), g_tile(frames * tiles), blk(256);
-    if (p.step == 1) {
-        hipLaunchKernelGGL(offsets_kernel<1>, g_off, blk, 0, s, b, frame0, tiles, p);
-        hipLaunchKernelGGL(compact_kernel<1>, g_tile, blk, 0, s, b, frame0, tiles, p);
-    } else if (p.step == 2) {
-        hipLaunchKernelGGL(offsets_kernel<2>, g_off, blk, 0, s, b, frame0, tiles, p);
-        hipLaunchKernelGGL(compact_kernel<2>, g_tile, blk, 0, s, b, frame0, tiles, p);
-    } else {
+    if (tiles > kMaxTiles || p.Wg > 4096 || p.Hg > 4096 || (p.step != 1 && p.step != 2))
         return hipErrorInvalidValue;
+    const int nchunks = (frames + chunk - 1) / chunk;
+    const dim3 blk(256);
+    for (int c = 0; c <= nchunks; ++c) {
+        const int f2 = (c - 1) * chunk, n2 = c >= 1 ? min(chunk, frames - f2) : 0;
+        const int f1 = c * chunk, n1 = c < nchunks ? min(chunk, frames - f1) : 0;
+        const dim3 grid((n2 + n1) * tiles);
+        if (p.step == 1)
+            hipLaunchKernelGGL(stage_kernel<1>, grid, blk, 0, s, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
+        else
+            hipLaunchKernelGGL(stage_kernel<2>, grid, blk, 0, s, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
+        if (n1) {
+            if (p.step == 1)
+                hipLaunchKernelGGL(offsets_kernel<1>, dim3(n1), blk, 0, s, b, f1, tiles, p);
+            else
+                hipLaunchKernelGGL(offsets_kernel<2>, dim3(n1), blk, 0, s, b, f1, tiles, p);
+        }
     }
     return hipGetLastError();
 }

@@ -458,7 +458,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     KParams p = make_params(b->H, b->W, b->step, *cam);
     if (p.Wg > 4096 || p.Hg > 4096) return fail(SV_E_ARG, "pipeline supports grids up to 4096 x 4096");
     set_plane(p, *plane, point_thr, hist_thr);
-    if (chunk <= 0) chunk = 256;
+    if (chunk <= 0) chunk = 128;
     if (chunk > b->frames) chunk = b->frames;
     const size_t cap = b->cap;   // Ng rounded up to 64: 256-byte aligned SoA planes
     HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames));
@@ -483,25 +483,11 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     bf.dxbits = d->tables.dx.as<uint32_t>();
     bf.dybits = d->tables.dy.as<uint32_t>();
     bf.cap = (int64_t)cap;
-    const int nseg = (b->frames + chunk - 1) / chunk;
-    while ((int)b->sync_ev.size() < nseg + 2) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        b->sync_ev.push_back(e);
-    }
     int t0, t1;
     HIP_TRY(hipEventRecord(b->ev[2], b->stream));
     HIP_TRY(b->timed_event(&t0));
     HIP_TRY(hipMemsetAsync(b->ctrl.p, 0, b->ctrl_bytes, b->stream));
-    for (int s = 0; s < nseg; ++s) {
-        const int f0 = s * chunk, n = (b->frames - f0) < chunk ? (b->frames - f0) : chunk;
-        HIP_TRY(launch_hist(p, bf, f0, n, b->stream));
-        HIP_TRY(hipEventRecord(b->sync_ev[s], b->stream));
-        HIP_TRY(hipStreamWaitEvent(b->stream2, b->sync_ev[s], 0));
-        HIP_TRY(launch_compact(p, bf, f0, n, b->stream2));
-    }
-    HIP_TRY(hipEventRecord(b->sync_ev[nseg], b->stream2));
-    HIP_TRY(hipStreamWaitEvent(b->stream, b->sync_ev[nseg], 0));
+    HIP_TRY(launch_pipeline(p, bf, b->frames, chunk, b->stream));
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[3], b->stream));
     b->pending[1].push_back({t0, t1});

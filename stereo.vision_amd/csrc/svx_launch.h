@@ -45,10 +45,8 @@ struct PipeBuffers {
     int64_t cap;         // points per frame (Ng)
 };
 int pipeline_tiles_per_frame(const KParams& p);
-// pass 1 over frames [frame0, frame0+frames): grid = frames x tiles
-hipError_t launch_hist(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s);
-// offsets (one workgroup per frame) + pass 2 (one workgroup per tile) over the
-// same frames, after their pass 1
-hipError_t launch_compact(const KParams& p, const PipeBuffers& b, int frame0, int frames, hipStream_t s);
+// The whole chain for frames [0, frames) in chunks (chunks + 1 fused launches
+// + one offsets launch per chunk), all on stream s.
+hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk, hipStream_t s);
 
 }  // namespace svx
