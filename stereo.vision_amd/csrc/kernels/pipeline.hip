@@ -22,9 +22,9 @@
 //   pass 2  compact       one workgroup per tile: keep2 bits + disparity
 //                         (~1.1 B/pt) + offset in; block scan, LDS descriptor
 //                         scatter, then contiguous non-temporal SoA stores.
-// Frames go in chunks: launch c = pass 2 of chunk c-1 + pass 1 of chunk c in
+// Frames go in chunks: launch c = pass 2 of chunk c-2 + pass 1 of chunk c in
 // one grid with interleaved roles (pass 1 is VALU-heavy, pass 2 store-bound,
-// so they share every CU well), then offsets(c). The control words
+// so they share every CU); offsets(c-1) runs beside it on a second stream. The control words
 // (histograms, counts) are zeroed by one memset per call; the keep /
 // presence masks are fully rewritten by pass 1.
 #include "../svx_launch.h"
@@ -95,7 +95,7 @@ __device__ __forceinline__ void tile_geometry(int qbase, int tid, const KParams&
         const int qi = qbase + i * 256 + tid;
         const bool ok = qi < p.frame_quads;
         const int qc = ok ? qi : p.frame_quads - 1;
-        const int g = qc / p.Q;
+        const int g = fastdiv40(qc, p.Q_m40);
         q[i] = qc - g * p.Q;
         gy[i] = ok ? g : -1;
     }
@@ -408,11 +408,10 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
 }
 
 // ---------------------------------------------------------------------------
-// One launch = pass 2 of chunk c-1 + pass 1 of chunk c. The two have no
+// One launch = pass 2 of one chunk + pass 1 of a later chunk. The two have no
 // dependency on each other, and the workgroup roles are interleaved (even
 // blockIdx: pass 2, odd: pass 1, while both last) so every CU runs VALU-heavy
-// pass-1 waves beside store-bound pass-2 waves. offsets(c) runs between
-// launches c and c+1 (stream order).
+// pass-1 waves beside store-bound pass-2 waves.
 // ---------------------------------------------------------------------------
 union StageShared {
     PipeShared p1;
@@ -440,28 +439,43 @@ __global__ __launch_bounds__(256) void stage_kernel(PipeBuffers bf, int p2_frame
         hist_tile<STEP>(bf, p1_frame0 + fl, t, tiles, p, sh.p1);
 }
 
-hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk, hipStream_t s) {
+// Schedule (lag 2, two streams): stream A runs stage(c) = pass 2 of chunk
+// c-2 + pass 1 of chunk c; stream B runs offsets(c) as soon as stage(c) is
+// done, concurrently with stage(c+1); stage(c+2) waits for offsets(c). So the
+// small, latency-bound offsets kernel never sits on the critical path.
+// ev must hold 2 * chunks events: ev[2c] = pass 1 of c done, ev[2c+1] = offsets(c) done.
+hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk, hipStream_t sa,
+                           hipStream_t sb, hipEvent_t* ev) {
     const int tiles = pipeline_tiles_per_frame(p);
     if (frames <= 0) return hipSuccess;
     if (tiles > kMaxTiles || p.Wg > 4096 || p.Hg > 4096 || (p.step != 1 && p.step != 2))
         return hipErrorInvalidValue;
     const int nchunks = (frames + chunk - 1) / chunk;
     const dim3 blk(256);
-    for (int c = 0; c <= nchunks; ++c) {
-        const int f2 = (c - 1) * chunk, n2 = c >= 1 ? min(chunk, frames - f2) : 0;
-        const int f1 = c * chunk, n1 = c < nchunks ? min(chunk, frames - f1) : 0;
+    hipError_t e = hipSuccess;
+    for (int c = 0; c < nchunks + 2 && e == hipSuccess; ++c) {
+        const int c2 = c - 2;
+        const bool has2 = c2 >= 0 && c2 < nchunks, has1 = c < nchunks;
+        const int f2 = c2 * chunk, n2 = has2 ? min(chunk, frames - f2) : 0;
+        const int f1 = c * chunk, n1 = has1 ? min(chunk, frames - f1) : 0;
+        if (has2) e = hipStreamWaitEvent(sa, ev[2 * c2 + 1], 0);
+        if (e != hipSuccess) break;
         const dim3 grid((n2 + n1) * tiles);
         if (p.step == 1)
-            hipLaunchKernelGGL(stage_kernel<1>, grid, blk, 0, s, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
+            hipLaunchKernelGGL(stage_kernel<1>, grid, blk, 0, sa, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
         else
-            hipLaunchKernelGGL(stage_kernel<2>, grid, blk, 0, s, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
-        if (n1) {
-            if (p.step == 1)
-                hipLaunchKernelGGL(offsets_kernel<1>, dim3(n1), blk, 0, s, b, f1, tiles, p);
-            else
-                hipLaunchKernelGGL(offsets_kernel<2>, dim3(n1), blk, 0, s, b, f1, tiles, p);
-        }
+            hipLaunchKernelGGL(stage_kernel<2>, grid, blk, 0, sa, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
+        if (!has1) continue;
+        e = hipEventRecord(ev[2 * c], sa);
+        if (e == hipSuccess) e = hipStreamWaitEvent(sb, ev[2 * c], 0);
+        if (e != hipSuccess) break;
+        if (p.step == 1)
+            hipLaunchKernelGGL(offsets_kernel<1>, dim3(n1), blk, 0, sb, b, f1, tiles, p);
+        else
+            hipLaunchKernelGGL(offsets_kernel<2>, dim3(n1), blk, 0, sb, b, f1, tiles, p);
+        e = hipEventRecord(ev[2 * c + 1], sb);
     }
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 

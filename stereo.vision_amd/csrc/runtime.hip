@@ -100,6 +100,7 @@ KParams make_params(int H, int W, int step, const sv_camera& cam) {
     p.pitch = (p.Wg + 3) / 4 * 4;
     p.Q = p.pitch / 4;
     p.frame_quads = p.Hg * p.Q;
+    p.Q_m40 = p.Q > 0 ? (((uint64_t)1 << 40) + (uint64_t)p.Q - 1) / (uint64_t)p.Q : 0;
     p.frame_px = (int64_t)H * W;
     p.f = cam.f;
     p.B = cam.B;
@@ -188,8 +189,8 @@ struct sv_batch {
     size_t cap = 0;            // per-frame point capacity of the pipeline outputs (Ng rounded up to 64)
     int64_t dense_per_frame = 0;
     hipStream_t stream = nullptr;    // K1, pass 1 (stream A)
-    hipStream_t stream2 = nullptr;   // pass 2 (stream B), overlaps the next segment's pass 1
-    std::vector<hipEvent_t> sync_ev; // segment hand-offs A -> B (timing disabled)
+    hipStream_t stream2 = nullptr;   // pipeline offsets kernels (stream B), beside the stage launches
+    std::vector<hipEvent_t> sync_ev; // pipeline hand-offs between A and B (timing disabled)
     DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks;
     // pipeline control block (one memset per call): hist | counts | err
     uint32_t* hist = nullptr;
@@ -486,8 +487,14 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     int t0, t1;
     HIP_TRY(hipEventRecord(b->ev[2], b->stream));
     HIP_TRY(b->timed_event(&t0));
+    const int nchunks = (b->frames + chunk - 1) / chunk;
+    while ((int)b->sync_ev.size() < 2 * nchunks) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        b->sync_ev.push_back(e);
+    }
     HIP_TRY(hipMemsetAsync(b->ctrl.p, 0, b->ctrl_bytes, b->stream));
-    HIP_TRY(launch_pipeline(p, bf, b->frames, chunk, b->stream));
+    HIP_TRY(launch_pipeline(p, bf, b->frames, chunk, b->stream, b->stream2, b->sync_ev.data()));
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[3], b->stream));
     b->pending[1].push_back({t0, t1});

@@ -22,6 +22,7 @@ constexpr int kBins = 1024;   // hue bins 0..999 used; padded to 1024
 struct KParams {
     int H, W, step, Hg, Wg, pitch, Q;   // Q = quads per grid row = pitch/4
     int frame_quads;                    // Hg * Q
+    uint64_t Q_m40;                     // ceil(2^40 / Q): n / Q = (n * Q_m40) >> 40, exact for n < 2^28
     int64_t frame_px;                   // H * W
     // camera (functions.py:15-22)
     double f, B, cw, ch, fB;
@@ -80,6 +81,13 @@ __device__ __forceinline__ int hue_bin(int r, int g, int b) {
         bin = two_rem > den ? m + 1 : (two_rem < den ? m : hue_bin_tie_f64(r, g, b, mx, mn));
     }
     return rng == 0 ? 0 : bin;   // grey: colorsys returns hue 0.0
+}
+
+// n / d for 0 <= n < 2^28 with m40 = ceil(2^40 / d), d <= 2^12: with
+// m40 = (2^40 + e)/d, 0 <= e < d, the error term n*e/(d*2^40) < 1/d, so the
+// floor is exact. One 64-bit multiply instead of a ~20-instruction division.
+__device__ __forceinline__ int fastdiv40(int n, uint64_t m40) {
+    return (int)(((uint64_t)(uint32_t)n * m40) >> 40);
 }
 
 // x - c in fp32 with relative error <= 2^-23 for any fp64 centre c: the first

@@ -45,8 +45,10 @@ struct PipeBuffers {
     int64_t cap;         // points per frame (Ng)
 };
 int pipeline_tiles_per_frame(const KParams& p);
-// The whole chain for frames [0, frames) in chunks (chunks + 1 fused launches
-// + one offsets launch per chunk), all on stream s.
-hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk, hipStream_t s);
+// The whole chain for frames [0, frames) in chunks: chunks + 2 fused stage
+// launches on stream sa, one offsets launch per chunk on stream sb, ordered by
+// the 2 * chunks events in ev.
+hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk, hipStream_t sa,
+                           hipStream_t sb, hipEvent_t* ev);
 
 }  // namespace svx
