@@ -458,6 +458,7 @@ hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, i
         const bool has2 = c2 >= 0 && c2 < nchunks, has1 = c < nchunks;
         const int f2 = c2 * chunk, n2 = has2 ? min(chunk, frames - f2) : 0;
         const int f1 = c * chunk, n1 = has1 ? min(chunk, frames - f1) : 0;
+        if (!has1 && !has2) continue;   // the gap launch when there is a single chunk
         if (has2) e = hipStreamWaitEvent(sa, ev[2 * c2 + 1], 0);
         if (e != hipSuccess) break;
         const dim3 grid((n2 + n1) * tiles);
