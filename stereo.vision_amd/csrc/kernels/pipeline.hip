@@ -145,7 +145,8 @@ __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int 
             nv += (in[i].d[k] != 0 && gx < p.Wg) ? 1u : 0u;
             if (point_keep1<STEP>(in[i].d[k], gx, y, yc, p)) {
                 keep |= 1u << (4 * i + k);
-                atomicAdd(&sh.hist[point_bin<STEP>(in[i], k)], 1u);
+                const int bin = (p.ablate & 1) ? 0 : point_bin<STEP>(in[i], k);
+                if (!(p.ablate & 2)) atomicAdd(&sh.hist[bin], 1u);
             }
         }
     }
@@ -369,8 +370,8 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
             const uint32_t d = uu >> 24;
             const int y = (int)((uu >> 12) & 0xFFF) * STEP;
             const int x = (int)(uu & 0xFFF) * STEP;
-            wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
-            wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
+            wx[e] = (p.ablate & 8) ? 0u : bf.dxbits[d * p.dx_words + (x >> 5)];
+            wy[e] = (p.ablate & 8) ? 0u : bf.dybits[d * p.dy_words + (y >> 5)];
         }
         float X[4], Y[4], Z[4];
         int PX[4], PY[4];
@@ -387,6 +388,10 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
             Z[e] = p.fB32 * r;
             PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
             PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
+        }
+        if (p.ablate & 4) {
+            if (X[0] == 12345.f) oX[4 * m] = X[1] + Y[2] + Z[3] + (float)(PX[0] + PY[1]);   // keep the math live
+            continue;
         }
         if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
             __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + 4 * m));

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -135,6 +136,10 @@ void set_plane(KParams& p, const sv_plane& pl, double thr, int hist_thr) {
     p.abs_b32 = (float)std::fabs(pl.b);
     p.abs_cf32 = (float)(std::fabs(pl.c) * p.f);
     p.hist_thr = hist_thr;
+    // Diagnostic ablation for profiling only (documented in DESIGN.md): when set,
+    // kernels skip parts of their work and the results are NOT valid.
+    const char* ab = std::getenv("SVX_ABLATE");
+    p.ablate = ab ? std::atoi(ab) : 0;
 }
 
 int dev_get(int device, Device** out) {

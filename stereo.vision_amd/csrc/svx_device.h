@@ -34,6 +34,7 @@ struct KParams {
     float abs_a32, abs_b32, abs_cf32;      // |a|, |b|, |c|*f (bound of |aX|+|bY|+|cZ| per unit K)
     int hist_thr;
     int dx_words, dy_words;                // words per d-row of the delta bit tables
+    int ablate;                            // DIAGNOSTIC ONLY (env SVX_ABLATE): skip work, results invalid
 };
 
 // ---------------------------------------------------------------------------
