@@ -393,7 +393,13 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
             if (X[0] == 12345.f) oX[4 * m] = X[1] + Y[2] + Z[3] + (float)(PX[0] + PY[1]);   // keep the math live
             continue;
         }
-        if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
+        if (ok[0] && ok[3] && (p.ablate & 16)) {   // diagnostic: plain stores
+            *reinterpret_cast<v4f*>(oX + 4 * m) = (v4f){X[0], X[1], X[2], X[3]};
+            *reinterpret_cast<v4f*>(oY + 4 * m) = (v4f){Y[0], Y[1], Y[2], Y[3]};
+            *reinterpret_cast<v4f*>(oZ + 4 * m) = (v4f){Z[0], Z[1], Z[2], Z[3]};
+            *reinterpret_cast<v4i*>(oP + 8 * m) = (v4i){PX[0], PY[0], PX[1], PY[1]};
+            *reinterpret_cast<v4i*>(oP + 8 * m + 4) = (v4i){PX[2], PY[2], PX[3], PY[3]};
+        } else if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
             __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + 4 * m));
             __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + 4 * m));
             __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + 4 * m));
@@ -430,7 +436,10 @@ __global__ __launch_bounds__(256) void stage_kernel(PipeBuffers bf, int p2_frame
     const int b = blockIdx.x;
     const int both = 2 * min(n1, n2);
     int role, idx;   // role 2 = pass 2, 1 = pass 1
-    if (b < both) {
+    if (p.ablate & 64) {   // diagnostic: no interleave (all pass-2 blocks first)
+        role = b < n2 ? 2 : 1;
+        idx = b < n2 ? b : b - n2;
+    } else if (b < both) {
         role = (b & 1) ? 1 : 2;
         idx = b >> 1;
     } else {
