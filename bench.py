@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=4096, help="frames per GPU")
     ap.add_argument("--step", type=int, default=1, help="grid step (reference hard-codes 2)")
     ap.add_argument("--chunk", type=int, default=0, help="pipeline frames per wave (0 = default)")
-    ap.add_argument("--grid-cap", type=int, default=0)
+    ap.add_argument("--qpl", type=int, default=1, help="K1 quads (4 points) per lane: 1, 2, 4")
     ap.add_argument("--nt", type=int, default=1, help="non-temporal K1 stores (1 = measured faster)")
     ap.add_argument("--ramp-ms", type=float, default=300.0,
                     help="untimed K1 launches before the warmup steps, to let clocks settle")
@@ -123,7 +123,7 @@ def main():
     want_pipe = not args.no_pipeline
 
     b = sb.Batch(count, H, W, args.step, with_bgr=want_pipe, with_points=want_pipe, device=local)
-    b.tune(args.grid_cap, args.nt)
+    b.tune(args.qpl, args.nt)
     b.synth(first)
     ng = b.Ng
     points_rank = ng * count

@@ -86,9 +86,9 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
                     int with_points, sv_batch** out);
 int sv_batch_destroy(sv_batch* b);
 int sv_batch_info(const sv_batch* b, int64_t* out8); /* Hg, Wg, pitch, Ng, bytes, frames, H, W */
-/* K1 launch shape: grid_cap = max workgroups (0 = one quad per lane, no
- * grid-stride), nontemporal = 1 for non-temporal (streaming) stores. */
-int sv_batch_tune(sv_batch* b, int grid_cap, int nontemporal);
+/* K1 launch shape: qpl = quads (4 grid points) per lane, 1, 2 or 4 (0 = 1);
+ * nontemporal = 1 for non-temporal (streaming) stores. */
+int sv_batch_tune(sv_batch* b, int qpl, int nontemporal);
 
 /* Counter-based synthetic frames for global frame ids first..first+frames-1
  * (SURVEY §8d), generated on the device: inputs never cross PCIe. */

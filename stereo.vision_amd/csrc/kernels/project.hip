@@ -111,58 +111,79 @@ __device__ __forceinline__ void store4(float* p, float a, float b, float c, floa
 }
 
 template <int STEP, bool NT>
+__device__ __forceinline__ void project_quad(const uint32_t (&d)[4], int q, int y, float* __restrict__ X,
+                                             float* __restrict__ Y, float* __restrict__ Z, size_t o,
+                                             const KParams& p) {
+    const float yc = centred(y, p.ch_hi, p.ch_lo);
+    float ox[4], oy[4], oz[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int gx = 4 * q + k;
+        const float xc = centred(gx * STEP, p.cw_hi, p.cw_lo);
+        const float r = __builtin_amdgcn_rcpf((float)d[k]);
+        const float K = p.B32 * r;
+        const bool ok = (d[k] != 0) && (gx < p.Wg);
+        ox[k] = ok ? xc * K : 0.0f;
+        oy[k] = ok ? yc * K : 0.0f;
+        oz[k] = ok ? p.fB32 * r : 0.0f;
+    }
+    store4<NT>(X + o, ox[0], ox[1], ox[2], ox[3]);
+    store4<NT>(Y + o, oy[0], oy[1], oy[2], oy[3]);
+    store4<NT>(Z + o, oz[0], oz[1], oz[2], oz[3]);
+}
+
+// One block = QPL consecutive 256-quad slabs of the flattened (frame, row,
+// quad) space; every lane issues its QPL disparity loads before any store.
+template <int STEP, bool NT, int QPL>
 __global__ __launch_bounds__(256) void project_dense_kernel(const uint8_t* __restrict__ disp,
                                                             float* __restrict__ X, float* __restrict__ Y,
                                                             float* __restrict__ Z, uint32_t total_quads,
                                                             KParams p) {
-    const uint32_t stride = gridDim.x * 256u;
-    for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < total_quads; g += stride) {
+    const uint32_t base = blockIdx.x * (256u * QPL) + threadIdx.x;
+    uint32_t d[QPL][4];
+    int qv[QPL], yv[QPL];
+#pragma unroll
+    for (int j = 0; j < QPL; ++j) {
+        uint32_t g = base + 256u * j;
+        g = g < total_quads ? g : total_quads - 1;   // branch-free; stores are masked below
         const uint32_t row = g / (uint32_t)p.Q;
-        const int q = (int)(g - row * (uint32_t)p.Q);
+        qv[j] = (int)(g - row * (uint32_t)p.Q);
         const uint32_t fl = row / (uint32_t)p.Hg;
         const int gy = (int)(row - fl * (uint32_t)p.Hg);
-        const int y = gy * STEP;
-        const uint8_t* drow = disp + (int64_t)fl * p.frame_px + (int64_t)y * p.W;
-        uint32_t d[4];
-        load_disp_quad<STEP>(drow, q, d);
-        const float yc = centred(y, p.ch_hi, p.ch_lo);
-        float ox[4], oy[4], oz[4];
+        yv[j] = gy * STEP;
+        load_disp_quad<STEP>(disp + (int64_t)fl * p.frame_px + (int64_t)yv[j] * p.W, qv[j], d[j]);
+    }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int gx = 4 * q + k;
-            const float xc = centred(gx * STEP, p.cw_hi, p.cw_lo);
-            const float r = __builtin_amdgcn_rcpf((float)d[k]);
-            const float K = p.B32 * r;
-            const bool ok = (d[k] != 0) && (gx < p.Wg);
-            ox[k] = ok ? xc * K : 0.0f;
-            oy[k] = ok ? yc * K : 0.0f;
-            oz[k] = ok ? p.fB32 * r : 0.0f;
-        }
-        const size_t o = (size_t)g * 4;
-        store4<NT>(X + o, ox[0], ox[1], ox[2], ox[3]);
-        store4<NT>(Y + o, oy[0], oy[1], oy[2], oy[3]);
-        store4<NT>(Z + o, oz[0], oz[1], oz[2], oz[3]);
+    for (int j = 0; j < QPL; ++j) {
+        const uint32_t g = base + 256u * j;
+        if (g < total_quads) project_quad<STEP, NT>(d[j], qv[j], yv[j], X, Y, Z, (size_t)g * 4, p);
+    }
+}
+
+template <int STEP, bool NT>
+static void launch_dense_qpl(int qpl, dim3 block, const uint8_t* disp, float* X, float* Y, float* Z,
+                             uint32_t t, const KParams& p, hipStream_t s) {
+    const uint32_t per = 256u * (uint32_t)qpl;
+    const dim3 grid((t + per - 1) / per);
+    switch (qpl) {
+        case 2: hipLaunchKernelGGL((project_dense_kernel<STEP, NT, 2>), grid, block, 0, s, disp, X, Y, Z, t, p); break;
+        case 4: hipLaunchKernelGGL((project_dense_kernel<STEP, NT, 4>), grid, block, 0, s, disp, X, Y, Z, t, p); break;
+        default: hipLaunchKernelGGL((project_dense_kernel<STEP, NT, 1>), grid, block, 0, s, disp, X, Y, Z, t, p); break;
     }
 }
 
 hipError_t launch_project_dense(const KParams& p, const uint8_t* disp, float* X, float* Y, float* Z,
-                                int frames, int grid_cap, int nontemporal, hipStream_t s) {
+                                int frames, int qpl, int nontemporal, hipStream_t s) {
     const uint64_t total = (uint64_t)frames * (uint64_t)p.frame_quads;
     if (total >= (1ull << 32)) return hipErrorInvalidValue;
-    uint64_t blocks = (total + 255) / 256;
-    if (grid_cap > 0 && blocks > (uint64_t)grid_cap) blocks = grid_cap;
-    const dim3 grid((unsigned)blocks), block(256);
+    const dim3 block(256);
     const uint32_t t = (uint32_t)total;
     if (p.step == 1) {
-        if (nontemporal)
-            hipLaunchKernelGGL((project_dense_kernel<1, true>), grid, block, 0, s, disp, X, Y, Z, t, p);
-        else
-            hipLaunchKernelGGL((project_dense_kernel<1, false>), grid, block, 0, s, disp, X, Y, Z, t, p);
+        if (nontemporal) launch_dense_qpl<1, true>(qpl, block, disp, X, Y, Z, t, p, s);
+        else launch_dense_qpl<1, false>(qpl, block, disp, X, Y, Z, t, p, s);
     } else if (p.step == 2) {
-        if (nontemporal)
-            hipLaunchKernelGGL((project_dense_kernel<2, true>), grid, block, 0, s, disp, X, Y, Z, t, p);
-        else
-            hipLaunchKernelGGL((project_dense_kernel<2, false>), grid, block, 0, s, disp, X, Y, Z, t, p);
+        if (nontemporal) launch_dense_qpl<2, true>(qpl, block, disp, X, Y, Z, t, p, s);
+        else launch_dense_qpl<2, false>(qpl, block, disp, X, Y, Z, t, p, s);
     } else {
         return hipErrorInvalidValue;
     }

@@ -205,7 +205,7 @@ struct sv_batch {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_ms[2] = {0, 0};
     bool have_ms[2] = {false, false};
-    int grid_cap = 0;          // K1 grid size cap (0 = one quad per lane)
+    int qpl = 1;               // K1 quads per lane (1, 2 or 4)
     int nontemporal = 1;       // K1 store flavour (non-temporal: measured faster)
     // per-launch timing accumulator: event pairs recorded on the batch stream
     std::vector<hipEvent_t> pool;
@@ -409,9 +409,11 @@ int sv_batch_info(const sv_batch* b, int64_t* o) {
     return SV_OK;
 }
 
-int sv_batch_tune(sv_batch* b, int grid_cap, int nontemporal) {
+int sv_batch_tune(sv_batch* b, int qpl, int nontemporal) {
     if (!b) return fail(SV_E_ARG, "null batch");
-    b->grid_cap = grid_cap;
+    if (qpl == 0) qpl = 1;
+    if (qpl != 1 && qpl != 2 && qpl != 4) return fail(SV_E_ARG, "qpl must be 1, 2 or 4");
+    b->qpl = qpl;
     b->nontemporal = nontemporal;
     return SV_OK;
 }
@@ -449,7 +451,7 @@ int sv_batch_project(sv_batch* b, const sv_camera* cam, int sync) {
     HIP_TRY(hipEventRecord(b->ev[0], b->stream));
     HIP_TRY(b->timed_event(&t0));
     HIP_TRY(launch_project_dense(p, b->disp.as<uint8_t>(), b->X.as<float>(), b->Y.as<float>(), b->Z.as<float>(),
-                                 b->frames, b->grid_cap, b->nontemporal, b->stream));
+                                 b->frames, b->qpl, b->nontemporal, b->stream));
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[1], b->stream));
     b->pending[0].push_back({t0, t1});

@@ -10,9 +10,9 @@ namespace svx {
 // kernels/project.hip -------------------------------------------------------
 hipError_t launch_synth(const KParams& p, uint8_t* disp, uint8_t* bgr, int frames,
                         int64_t first_frame, hipStream_t s);
-// K1: dense fp32 projection. total_quads = frames * Hg * Q.
+// K1: dense fp32 projection over frames * Hg * Q quads; qpl = quads per lane (1, 2, 4).
 hipError_t launch_project_dense(const KParams& p, const uint8_t* disp, float* X, float* Y, float* Z,
-                                int frames, int grid_cap, int nontemporal, hipStream_t s);
+                                int frames, int qpl, int nontemporal, hipStream_t s);
 // Drop-in projection: fp64 XYZ, compacted in raster order (any H, W, step).
 hipError_t launch_project_compact_f64(const KParams& p, const uint8_t* disp, int64_t ld_disp,
                                       const uint8_t* bgr, int64_t ld_bgr, double* xyz, uint8_t* rgb,

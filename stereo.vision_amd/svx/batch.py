@@ -66,8 +66,9 @@ class Batch:
                 raise ValueError(f"bgr shape {bgr.shape} != {(self.H, self.W, 3)}")
         _abi.call("sv_batch_upload", self._h, frame, _abi.ptr(disp), _abi.ptr(bgr))
 
-    def tune(self, grid_cap=0, nontemporal=0):
-        _abi.call("sv_batch_tune", self._h, int(grid_cap), int(nontemporal))
+    def tune(self, qpl=1, nontemporal=1):
+        """K1 launch shape: quads per lane (1, 2, 4) and non-temporal stores."""
+        _abi.call("sv_batch_tune", self._h, int(qpl), int(nontemporal))
 
     # -- compute -------------------------------------------------------------------
     def project(self, camera=None, sync=True):

@@ -16,7 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--k1", default="0:0,0:1,2048:0,4096:0,8192:0,16384:0,8192:1")
+    ap.add_argument("--k1", default="1:1,2:1,4:1,1:0")
     ap.add_argument("--chunks", default="8,16,32,64")
     ap.add_argument("--step", type=int, default=1)
     a = ap.parse_args()
@@ -33,7 +33,7 @@ def main():
             b.project(sync=False)
         ms, n = b.timing("project")
         ms /= n
-        res.append({"k1_grid_cap": cap, "nt": nt, "ms": round(ms, 4),
+        res.append({"k1_qpl": cap, "nt": nt, "ms": round(ms, 4),
                     "GBps": round(13 * ng / ms / 1e6, 1), "Gpts": round(ng / ms / 1e6, 1)})
         print(json.dumps(res[-1]), flush=True)
     for c in a.chunks.split(","):
