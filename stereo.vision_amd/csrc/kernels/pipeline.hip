@@ -318,23 +318,6 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
             dw[i][1] = w.y;
         }
     }
-    // delta-table words of this lane's keep2 points, issued now so their
-    // latency hides under the block scan (functions.py:201-209 via the tables)
-    uint32_t dxw[kQPT][4], dyw[kQPT][4];
-#pragma unroll
-    for (int i = 0; i < kQPT; ++i) {
-        const int y = (gy[i] < 0 ? 0 : gy[i]) * STEP;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint32_t d;
-            if constexpr (STEP == 1) d = (dw[i][0] >> (8 * k)) & 0xFF;
-            else d = (dw[i][k >> 1] >> (16 * (k & 1))) & 0xFF;
-            const int x = (4 * q[i] + k) * STEP;
-            const bool kp = (keep >> (4 * i + k)) & 1;
-            dxw[i][k] = (kp && !(p.ablate & 8)) ? bf.dxbits[d * p.dx_words + (x >> 5)] : 0u;
-            dyw[i][k] = (kp && !(p.ablate & 8)) ? bf.dybits[d * p.dy_words + (y >> 5)] : 0u;
-        }
-    }
     uint64_t cnt = 0;
 #pragma unroll
     for (int i = 0; i < kQPT; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
@@ -350,25 +333,20 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
     }
     const uint64_t excl = wbase + inc - cnt;
     // descriptors land at LDS slot (toff & 3) + o, so that LDS slot s <-> global
-    // element g0 + s with g0 = toff & ~3: output groups of 4 are 16-byte aligned.
-    // descriptor = d:8 | ddx:1 | ddy:1 | gy:11 | gx:11
+    // element g0 + s with g0 = toff & ~3: output groups of 4 are 16-byte aligned
     const uint32_t lead = toff & 3;
     uint32_t rowbase = lead;
 #pragma unroll
     for (int i = 0; i < kQPT; ++i) {
         uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
         rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
-        const int y = (gy[i] < 0 ? 0 : gy[i]) * STEP;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!(keep & (1u << (4 * i + k)))) continue;
             uint32_t d;
             if constexpr (STEP == 1) d = (dw[i][0] >> (8 * k)) & 0xFF;
             else d = (dw[i][k >> 1] >> (16 * (k & 1))) & 0xFF;
-            const int gx = 4 * q[i] + k;
-            const uint32_t ddx = (dxw[i][k] >> ((gx * STEP) & 31)) & 1;
-            const uint32_t ddy = (dyw[i][k] >> (y & 31)) & 1;
-            sh.desc[o++] = (d << 24) | (ddx << 23) | (ddy << 22) | ((uint32_t)gy[i] << 11) | (uint32_t)gx;
+            sh.desc[o++] = (d << 24) | ((uint32_t)gy[i] << 12) | (uint32_t)(4 * q[i] + k);
         }
     }
     const uint32_t end = rowbase;            // one past the last valid LDS slot
@@ -382,30 +360,46 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
     for (uint32_t m = tid; m < groups; m += 256) {
         const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.desc[4 * m]);
         const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
-        float X[4], Y[4], Z[4];
-        int PX[4], PY[4];
+        uint32_t wx[4], wy[4];
         bool ok[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < 4; ++e) {   // all table loads of the group in flight together
             const uint32_t s_ = 4 * m + e;
             ok[e] = s_ >= lead && s_ < end;
             const uint32_t uu = ok[e] ? u[e] : (1u << 24);
             const uint32_t d = uu >> 24;
-            const int y = (int)((uu >> 11) & 0x7FF) * STEP;
-            const int x = (int)(uu & 0x7FF) * STEP;
+            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
+            const int x = (int)(uu & 0xFFF) * STEP;
+            wx[e] = (p.ablate & 8) ? 0u : bf.dxbits[d * p.dx_words + (x >> 5)];
+            wy[e] = (p.ablate & 8) ? 0u : bf.dybits[d * p.dy_words + (y >> 5)];
+        }
+        float X[4], Y[4], Z[4];
+        int PX[4], PY[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t uu = ok[e] ? u[e] : (1u << 24);
+            const uint32_t d = uu >> 24;
+            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
+            const int x = (int)(uu & 0xFFF) * STEP;
             const float r = __builtin_amdgcn_rcpf((float)d);
             const float K = p.B32 * r;
             X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
             Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
             Z[e] = p.fB32 * r;
-            PX[e] = x - (int)((uu >> 23) & 1);
-            PY[e] = y - (int)((uu >> 22) & 1);
+            PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
+            PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
         }
         if (p.ablate & 4) {
             if (X[0] == 12345.f) oX[4 * m] = X[1] + Y[2] + Z[3] + (float)(PX[0] + PY[1]);   // keep the math live
             continue;
         }
-        if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
+        if (ok[0] && ok[3] && (p.ablate & 16)) {   // diagnostic: plain stores
+            *reinterpret_cast<v4f*>(oX + 4 * m) = (v4f){X[0], X[1], X[2], X[3]};
+            *reinterpret_cast<v4f*>(oY + 4 * m) = (v4f){Y[0], Y[1], Y[2], Y[3]};
+            *reinterpret_cast<v4f*>(oZ + 4 * m) = (v4f){Z[0], Z[1], Z[2], Z[3]};
+            *reinterpret_cast<v4i*>(oP + 8 * m) = (v4i){PX[0], PY[0], PX[1], PY[1]};
+            *reinterpret_cast<v4i*>(oP + 8 * m + 4) = (v4i){PX[2], PY[2], PX[3], PY[3]};
+        } else if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
             __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + 4 * m));
             __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + 4 * m));
             __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + 4 * m));
@@ -468,7 +462,7 @@ hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, i
                            hipStream_t sb, hipEvent_t* ev) {
     const int tiles = pipeline_tiles_per_frame(p);
     if (frames <= 0) return hipSuccess;
-    if (tiles > kMaxTiles || p.Wg > 2048 || p.Hg > 2048 || (p.step != 1 && p.step != 2))
+    if (tiles > kMaxTiles || p.Wg > 4096 || p.Hg > 4096 || (p.step != 1 && p.step != 2))
         return hipErrorInvalidValue;
     const int nchunks = (frames + chunk - 1) / chunk;
     const dim3 blk(256);

@@ -464,7 +464,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
                                int hist_thr, int chunk, int sync, Device* d) {
     if (!b->with_bgr) return fail(SV_E_ARG, "pipeline needs a batch created with bgr");
     KParams p = make_params(b->H, b->W, b->step, *cam);
-    if (p.Wg > 2048 || p.Hg > 2048) return fail(SV_E_ARG, "pipeline supports grids up to 2048 x 2048");
+    if (p.Wg > 4096 || p.Hg > 4096) return fail(SV_E_ARG, "pipeline supports grids up to 4096 x 4096");
     set_plane(p, *plane, point_thr, hist_thr);
     if (chunk <= 0) chunk = 128;
     if (chunk > b->frames) chunk = b->frames;
