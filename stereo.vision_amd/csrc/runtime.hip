@@ -348,7 +348,6 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
     b->Ng = (int64_t)b->kp.Hg * b->kp.Wg;
     b->cap = ((size_t)b->Ng + 63) / 64 * 64;
     b->dense_per_frame = (int64_t)b->kp.Hg * b->kp.pitch;
-    b->stream = d->stream;
     const size_t px = (size_t)frames * H * W;
     hipError_t e = b->disp.ensure(px);
     if (e == hipSuccess && b->with_bgr) e = b->bgr.ensure(px * 3);
@@ -368,6 +367,7 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
             e = hipMemset(b->ctrl.p, 0, b->ctrl_bytes);
         }
     }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking);
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
     if (e != hipSuccess) {
@@ -392,6 +392,7 @@ int sv_batch_destroy(sv_batch* b) {
         (void)hipStreamSynchronize(b->stream2);
         (void)hipStreamDestroy(b->stream2);
     }
+    if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
     return SV_OK;
 }
@@ -466,7 +467,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     KParams p = make_params(b->H, b->W, b->step, *cam);
     if (p.Wg > 4096 || p.Hg > 4096) return fail(SV_E_ARG, "pipeline supports grids up to 4096 x 4096");
     set_plane(p, *plane, point_thr, hist_thr);
-    if (chunk <= 0) chunk = 128;
+    if (chunk <= 0) chunk = 1024;
     if (chunk > b->frames) chunk = b->frames;
     const size_t cap = b->cap;   // Ng rounded up to 64: 256-byte aligned SoA planes
     HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames));
