@@ -114,76 +114,38 @@ struct PipeShared {   // pass 1
 static_assert(sizeof(PipeShared) < 8192, "LDS budget");
 
 // ---------------------------------------------------------------------------
-// pass 1: kP1Tiles consecutive tiles of one frame per workgroup. The raw
-// inputs of tile j+1 (disparity + BGR, 16 dwords per lane at step 1) are
-// loaded into registers before tile j is computed, so a wave keeps a whole
-// tile of loads in flight while it works (MLP: these waves are otherwise
-// latency-bound once the pass-2 store stream loads the memory system).
-// LDS-only synchronisation uses a raw s_barrier after lgkmcnt(0): a
-// __syncthreads() would also wait vmcnt(0) behind the stores and drain the
-// prefetch.
+// pass 1 tile
 // ---------------------------------------------------------------------------
-constexpr int kP1Tiles = 4;
-
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) only
-    __builtin_amdgcn_s_barrier();
-}
-
 template <int STEP>
-struct RawTile {
-    uint32_t d[kQPT][STEP];       // raw disparity dwords of each quad
-    uint32_t c[kQPT][3 * STEP];   // raw BGR dwords of each quad
-    int gy[kQPT], q[kQPT];
-};
-
-template <int STEP>
-__device__ __forceinline__ void load_raw_tile(const uint8_t* disp, const uint8_t* bgr, int tile, int tid,
-                                              const KParams& p, RawTile<STEP>& r) {
-    tile_geometry(tile * 256 * kQPT, tid, p, r.gy, r.q);
-#pragma unroll
-    for (int i = 0; i < kQPT; ++i) {
-        const uint8_t* drow = row_ptr<STEP>(disp, r.gy[i], 1, p);
-        const uint8_t* crow = row_ptr<STEP>(bgr, r.gy[i], 3, p);
-        if constexpr (STEP == 1) {
-            r.d[i][0] = *reinterpret_cast<const uint32_t*>(drow + 4 * r.q[i]);
-            const uint32_t* cp = reinterpret_cast<const uint32_t*>(crow + 12 * r.q[i]);
-            r.c[i][0] = cp[0]; r.c[i][1] = cp[1]; r.c[i][2] = cp[2];
-        } else {
-            const uint2 w = *reinterpret_cast<const uint2*>(drow + 8 * r.q[i]);
-            r.d[i][0] = w.x; r.d[i][1] = w.y;
-            const uint2* cp = reinterpret_cast<const uint2*>(crow + 24 * r.q[i]);
-            const uint2 a = cp[0], b = cp[1], c = cp[2];
-            r.c[i][0] = a.x; r.c[i][1] = a.y; r.c[i][2] = b.x; r.c[i][3] = b.y; r.c[i][4] = c.x; r.c[i][5] = c.y;
-        }
-    }
-}
-
-template <int STEP>
-__device__ __forceinline__ void hist_one(const PipeBuffers& bf, int frame, int tile, int tiles,
-                                         const KParams& p, PipeShared& sh, const RawTile<STEP>& r) {
+__device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int tile, int tiles,
+                                          const KParams& p, PipeShared& sh) {
     const int tid = threadIdx.x;
+    const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
+    const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
+    int gy[kQPT], q[kQPT];
+    tile_geometry(tile * 256 * kQPT, tid, p, gy, q);
+    QuadIn<STEP> in[kQPT];
+#pragma unroll
+    for (int i = 0; i < kQPT; ++i) {   // all loads in flight before any use
+        load_disp<STEP>(row_ptr<STEP>(disp, gy[i], 1, p), q[i], in[i].d);
+        load_bgr<STEP>(row_ptr<STEP>(bgr, gy[i], 3, p), q[i], in[i]);
+    }
+    for (int i = tid; i < kBins; i += 256) sh.hist[i] = 0;
+    if (tid < 2) sh.cnt[tid] = 0;
+    __syncthreads();
     uint32_t nv = 0, keep = 0;
 #pragma unroll
     for (int i = 0; i < kQPT; ++i) {
-        if (r.gy[i] < 0) continue;
-        const int y = r.gy[i] * STEP;
+        if (gy[i] < 0) continue;
+        const int y = gy[i] * STEP;
         const float yc = centred(y, p.ch_hi, p.ch_lo);
-        QuadIn<STEP> in;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if constexpr (STEP == 1) in.d[k] = (r.d[i][0] >> (8 * k)) & 0xFF;
-            else in.d[k] = (r.d[i][k >> 1] >> (16 * (k & 1))) & 0xFF;
-        }
-#pragma unroll
-        for (int j = 0; j < 3 * STEP; ++j) in.c[j] = r.c[i][j];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int gx = 4 * r.q[i] + k;
-            nv += (in.d[k] != 0 && gx < p.Wg) ? 1u : 0u;
-            if (point_keep1<STEP>(in.d[k], gx, y, yc, p)) {
+            const int gx = 4 * q[i] + k;
+            nv += (in[i].d[k] != 0 && gx < p.Wg) ? 1u : 0u;
+            if (point_keep1<STEP>(in[i].d[k], gx, y, yc, p)) {
                 keep |= 1u << (4 * i + k);
-                const int bin = (p.ablate & 1) ? 0 : point_bin<STEP>(in, k);
+                const int bin = (p.ablate & 1) ? 0 : point_bin<STEP>(in[i], k);
                 if (!(p.ablate & 2)) atomicAdd(&sh.hist[bin], 1u);
             }
         }
@@ -197,7 +159,7 @@ __device__ __forceinline__ void hist_one(const PipeBuffers& bf, int frame, int t
         atomicAdd(&sh.cnt[0], nv);
         atomicAdd(&sh.cnt[1], nk);
     }
-    lds_barrier();
+    __syncthreads();
     if (tid == 0) {
         bf.tcount[slot] = sh.cnt[1];
         atomicAdd(reinterpret_cast<unsigned long long*>(bf.counts + 4 * frame + 0), (unsigned long long)sh.cnt[0]);
@@ -207,36 +169,18 @@ __device__ __forceinline__ void hist_one(const PipeBuffers& bf, int frame, int t
     uint32_t* pres = bf.pres + slot * (kBins / 32);
     const int wave = tid >> 6;
 #pragma unroll
-    for (int rr = 0; rr < kBins / 256; ++rr) {
-        const int b = rr * 256 + tid;
+    for (int r = 0; r < kBins / 256; ++r) {
+        const int b = r * 256 + tid;
         const uint32_t v = sh.hist[b];
         if (v) atomicAdd(gh + b, v);
         const uint64_t m = __ballot(v != 0);
         if (lane_id() == 0) {
-            pres[(rr * 256 + wave * 64) / 32] = (uint32_t)m;
-            pres[(rr * 256 + wave * 64) / 32 + 1] = (uint32_t)(m >> 32);
+            pres[(r * 256 + wave * 64) / 32] = (uint32_t)m;
+            pres[(r * 256 + wave * 64) / 32 + 1] = (uint32_t)(m >> 32);
         }
     }
 }
 
-template <int STEP>
-__device__ __forceinline__ void hist_tiles(const PipeBuffers& bf, int frame, int tile0, int ntiles, int tiles,
-                                           const KParams& p, PipeShared& sh) {
-    const int tid = threadIdx.x;
-    const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
-    const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
-    RawTile<STEP> cur, nxt;
-    load_raw_tile<STEP>(disp, bgr, tile0, tid, p, cur);
-    for (int j = 0; j < ntiles; ++j) {
-        if (j + 1 < ntiles) load_raw_tile<STEP>(disp, bgr, tile0 + j + 1, tid, p, nxt);
-        for (int i = tid; i < kBins; i += 256) sh.hist[i] = 0;
-        if (tid < 2) sh.cnt[tid] = 0;
-        lds_barrier();   // zeroed (and the previous tile's flush reads are done)
-        hist_one<STEP>(bf, frame, tile0 + j, tiles, p, sh, cur);
-        lds_barrier();   // flush reads of sh.hist done before the next zeroing
-        cur = nxt;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // offsets: one workgroup per frame (tiny). Decides which tiles are dirty (a
@@ -502,15 +446,11 @@ __global__ __launch_bounds__(256) void stage_kernel(PipeBuffers bf, int p2_frame
         role = n2 > n1 ? 2 : 1;
         idx = (b - both) + both / 2;
     }
-    if (role == 2) {
-        const int fl = idx / tiles, t = idx - fl * tiles;
+    const int fl = idx / tiles, t = idx - fl * tiles;
+    if (role == 2)
         compact_tile<STEP>(bf, p2_frame0 + fl, t, tiles, p, sh.p2);
-    } else {
-        const int per = (tiles + kP1Tiles - 1) / kP1Tiles;   // pass-1 blocks per frame
-        const int fl = idx / per, g = idx - fl * per;
-        const int t0 = g * kP1Tiles;
-        hist_tiles<STEP>(bf, p1_frame0 + fl, t0, min(kP1Tiles, tiles - t0), tiles, p, sh.p1);
-    }
+    else
+        hist_tile<STEP>(bf, p1_frame0 + fl, t, tiles, p, sh.p1);
 }
 
 // Schedule (lag 2, two streams): stream A runs stage(c) = pass 2 of chunk
@@ -535,12 +475,11 @@ hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, i
         if (!has1 && !has2) continue;   // the gap launch when there is a single chunk
         if (has2) e = hipStreamWaitEvent(sa, ev[2 * c2 + 1], 0);
         if (e != hipSuccess) break;
-        const int p1per = (tiles + kP1Tiles - 1) / kP1Tiles;
-        const dim3 grid(n2 * tiles + n1 * p1per);
+        const dim3 grid((n2 + n1) * tiles);
         if (p.step == 1)
-            hipLaunchKernelGGL(stage_kernel<1>, grid, blk, 0, sa, b, f2, n2 * tiles, f1, n1 * p1per, tiles, p);
+            hipLaunchKernelGGL(stage_kernel<1>, grid, blk, 0, sa, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
         else
-            hipLaunchKernelGGL(stage_kernel<2>, grid, blk, 0, sa, b, f2, n2 * tiles, f1, n1 * p1per, tiles, p);
+            hipLaunchKernelGGL(stage_kernel<2>, grid, blk, 0, sa, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
         if (!has1) continue;
         e = hipEventRecord(ev[2 * c], sa);
         if (e == hipSuccess) e = hipStreamWaitEvent(sb, ev[2 * c], 0);
