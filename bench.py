@@ -118,7 +118,9 @@ def main():
 
     rank, world, local = dist.env_topology()
     ctrl = dist.Control()
-    comm = dist.RcclComm(ctrl, local) if world > 1 else None
+    # RCCL whenever launched by torchrun (also at world size 1, so the device
+    # collective path is the one that runs), never for a plain `python bench.py`
+    comm = dist.RcclComm(ctrl, local) if "WORLD_SIZE" in os.environ else None
     first, count = dist.shard(args.frames * world, world, rank)
     want_pipe = not args.no_pipeline
 
@@ -215,7 +217,7 @@ def main():
             "frac": round(pbytes / p_avg_s / 1e9 / PEAK_HBM_GBS, 4),
             "algorithmic_bytes_per_call": pbytes,
             "counts_total": {"valid": int(counts[0]), "kept": int(counts[1]), "kept2": n_kept2},
-            "plane_broadcast": "RCCL ncclBroadcast over xGMI" if comm else "n/a (1 GPU)",
+            "plane_broadcast": "RCCL ncclBroadcast over xGMI, every step" if comm else "n/a (single process)",
         }
 
     if rank == 0 and world == 1 and not args.no_cpu:
