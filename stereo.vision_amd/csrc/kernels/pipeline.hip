@@ -447,10 +447,11 @@ __global__ __launch_bounds__(256) void stage_kernel(PipeBuffers bf, int p2_frame
         idx = (b - both) + both / 2;
     }
     const int fl = idx / tiles, t = idx - fl * tiles;
-    if (role == 2)
-        compact_tile<STEP>(bf, p2_frame0 + fl, t, tiles, p, sh.p2);
-    else
-        hist_tile<STEP>(bf, p1_frame0 + fl, t, tiles, p, sh.p1);
+    if (role == 2) {
+        if (!(p.ablate & 256)) compact_tile<STEP>(bf, p2_frame0 + fl, t, tiles, p, sh.p2);
+    } else {
+        if (!(p.ablate & 128)) hist_tile<STEP>(bf, p1_frame0 + fl, t, tiles, p, sh.p1);
+    }
 }
 
 // Schedule (lag 2, two streams): stream A runs stage(c) = pass 2 of chunk
