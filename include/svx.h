@@ -106,6 +106,13 @@ int sv_batch_project(sv_batch* b, const sv_camera* cam, int sync);
 int sv_batch_pipeline(sv_batch* b, const sv_camera* cam, const sv_plane* plane,
                       double point_thr, int hist_thr, int chunk, int sync);
 
+/* Pipeline kernel family: 0 = auto (frame-resident for >= 512 frames when the
+ * frame fits, else tiled), 1 = tiled (tiles of 4096 points across workgroups,
+ * offsets kernel between the passes), 2 = frame-resident (one workgroup per
+ * frame, LDS histogram; frames of <= 1M grid points at step 1). Results are
+ * identical; only the speed differs. */
+int sv_batch_pipeline_mode(sv_batch* b, int mode);
+
 int sv_batch_sync(sv_batch* b);
 /* ms of the last sv_batch_project / sv_batch_pipeline, from HIP events
  * recorded on the batch stream around the kernels. which: 0 = project,

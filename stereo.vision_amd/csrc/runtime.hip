@@ -81,6 +81,8 @@ struct Device {
 };
 
 constexpr int kMaxDev = 64;
+// auto mode: one workgroup per frame needs enough frames to fill 256 CUs
+constexpr int kResidentMinFrames = 512;
 Device g_dev[kMaxDev];
 std::mutex g_init_mu;
 
@@ -135,6 +137,26 @@ void set_plane(KParams& p, const sv_plane& pl, double thr, int hist_thr) {
     p.abs_a32 = (float)std::fabs(pl.a);
     p.abs_b32 = (float)std::fabs(pl.b);
     p.abs_cf32 = (float)(std::fabs(pl.c) * p.f);
+    // keep1_lean constants. u = B*(a*(x-cw) + b*(y-ch) + c*f) = al*x + bb*y + b0.
+    // fp32 error of e = |u - d| - t*d is <= 2^-21 * M with
+    // M = 2*U + 255*(1+t) + 255, U = |al|*W + |bb|*H + |b0| (derivation in
+    // DESIGN.md §2.3); the reference's own fp64 error is <= 2^-48 * M. The guard
+    // 2^-16 * M leaves a 32x margin; non-finite constants force the exact path.
+    {
+        const double al = p.B * pl.a, bb = p.B * pl.b;
+        const double b0 = p.B * pl.c * p.f - bb * p.ch - al * p.cw;
+        const double t = thr * p.nrm;
+        const double U = std::fabs(al) * p.W + std::fabs(bb) * p.H + std::fabs(b0);
+        const double M = 2.0 * U + 255.0 * (1.0 + std::fabs(t)) + 255.0;
+        p.al32 = (float)al;
+        p.bb32 = (float)bb;
+        p.b032 = (float)b0;
+        p.tn32 = (float)t;
+        const double g = std::ldexp(M, -16);
+        const bool finite = std::isfinite(g) && std::isfinite((double)p.al32) && std::isfinite((double)p.bb32) &&
+                            std::isfinite((double)p.b032) && std::isfinite((double)p.tn32);
+        p.g32 = finite ? (float)g : INFINITY;
+    }
     p.hist_thr = hist_thr;
     // Diagnostic ablation for profiling only (documented in DESIGN.md): when set,
     // kernels skip parts of their work and the results are NOT valid.
@@ -207,6 +229,7 @@ struct sv_batch {
     bool have_ms[2] = {false, false};
     int qpl = 1;               // K1 quads per lane (1, 2 or 4)
     int nontemporal = 1;       // K1 store flavour (non-temporal: measured faster)
+    int pipe_mode = 0;         // 0 auto, 1 tiled (pipeline.hip), 2 frame-resident (resident.hip)
     // per-launch timing accumulator: event pairs recorded on the batch stream
     std::vector<hipEvent_t> pool;
     std::vector<std::pair<int, int>> pending[2];  // (start idx, end idx) per op kind
@@ -492,7 +515,22 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     bf.dxbits = d->tables.dx.as<uint32_t>();
     bf.dybits = d->tables.dy.as<uint32_t>();
     bf.cap = (int64_t)cap;
+    int mode = b->pipe_mode;
+    if (mode == 0) mode = (b->frames >= kResidentMinFrames && resident_supported(p)) ? 2 : 1;
+    if (mode == 2 && !resident_supported(p))
+        return fail(SV_E_ARG, "frame-resident pipeline: frame too large (grid %d x %d)", p.Hg, p.Wg);
     int t0, t1;
+    if (mode == 2) {   // every output word (hist, counts, points) is rewritten: no memset
+        HIP_TRY(hipEventRecord(b->ev[2], b->stream));
+        HIP_TRY(b->timed_event(&t0));
+        HIP_TRY(launch_pipeline_resident(p, bf, b->frames, b->stream));
+        HIP_TRY(b->timed_event(&t1));
+        HIP_TRY(hipEventRecord(b->ev[3], b->stream));
+        b->pending[1].push_back({t0, t1});
+        b->have_ms[1] = true;
+        if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
+        return SV_OK;
+    }
     HIP_TRY(hipEventRecord(b->ev[2], b->stream));
     HIP_TRY(b->timed_event(&t0));
     const int nchunks = (b->frames + chunk - 1) / chunk;
@@ -517,6 +555,13 @@ int sv_batch_pipeline(sv_batch* b, const sv_camera* cam, const sv_plane* plane, 
     Device* d;
     if (int rc = dev_get(b->device, &d)) return rc;
     return batch_pipeline_impl(b, cam, plane, point_thr, hist_thr, chunk, sync, d);
+}
+
+int sv_batch_pipeline_mode(sv_batch* b, int mode) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    if (mode < 0 || mode > 2) return fail(SV_E_ARG, "pipeline mode must be 0 (auto), 1 (tiled) or 2 (resident)");
+    b->pipe_mode = mode;
+    return SV_OK;
 }
 
 int sv_batch_sync(sv_batch* b) {

@@ -32,6 +32,10 @@ struct KParams {
     double a, b, c, nrm, thr;
     float a32, b32, c32, thr32, inv_nrm32, guard32;   // guard32 = 2^-18 / nrm
     float abs_a32, abs_b32, abs_cf32;      // |a|, |b|, |c|*f (bound of |aX|+|bY|+|cZ| per unit K)
+    // keep1 in the division-free form |u - d| < t*d with u = B*(a*xc + b*yc + c*f)
+    // (real-equivalent to dist < thr after multiplying by d/B > 0):
+    // u = fma(al32, x, fma(bb32, y, b032)); decided in fp32 unless |e| <= g32.
+    float al32, bb32, b032, tn32, g32;
     int hist_thr;
     int dx_words, dy_words;                // words per d-row of the delta bit tables
     int ablate;                            // DIAGNOSTIC ONLY (env SVX_ABLATE): skip work, results invalid
@@ -120,6 +124,34 @@ __device__ __forceinline__ bool keep1(int x, int y, uint32_t d, float xc, float 
     const float e = dist - p.thr32;
     if (__builtin_fabsf(e) > G) return e < 0.0f;
     return keep1_f64(x, y, d, p);
+}
+
+// Division-free keep1 for one grid point (see KParams): returns the fp32
+// decision and flags *unc when the exact fp64 reference arithmetic must decide
+// (|e| within the rigorous error guard g32, or e not finite). d == 0 never
+// keeps and is never uncertain.
+__device__ __forceinline__ bool keep1_lean(float xf, float beta, float df, const KParams& p, bool& unc) {
+    const float u = __builtin_fmaf(p.al32, xf, beta);
+    const float s = u - df;
+    const float e = __builtin_fmaf(-p.tn32, df, __builtin_fabsf(s));
+    unc = !(__builtin_fabsf(e) > p.g32) && df != 0.0f;
+    return e < 0.0f && df != 0.0f;
+}
+
+// Hue bin in fp32 with one rcp: |t - t_exact| <= 2.5 * 2^-23 * |t| < 3e-4,
+// while a non-tie t is >= 1/(2*3*rng) >= 6.5e-4 from a half-integer. *near
+// flags the +-4e-4 band around .5 where the caller must use hue_bin().
+// col = B | G << 8 | R << 16 (bits 24..31 ignored).
+__device__ __forceinline__ int hue_bin_fast(uint32_t col, bool& near) {
+    const int b = (int)(col & 0xFF), g = (int)((col >> 8) & 0xFF), r = (int)((col >> 16) & 0xFF);
+    const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
+    const int rng = mx - mn;
+    const int n = (r == mx) ? (g - b) : ((g == mx) ? (2 * rng + b - r) : (4 * rng + r - g));
+    const float t = ((float)n * __builtin_amdgcn_rcpf((float)rng)) * (500.0f / 3.0f);
+    const float rt = __builtin_rintf(t);
+    near = __builtin_fabsf(t - rt) > 0.5f - 4e-4f;   // NaN (grey) -> false
+    const int bin = (int)rt + (n < 0 ? 1000 : 0);    // (h mod 1): rint(t + 1000) = rint(t) + 1000
+    return rng == 0 ? 0 : bin;
 }
 
 // ---------------------------------------------------------------------------

@@ -51,4 +51,9 @@ int pipeline_tiles_per_frame(const KParams& p);
 hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, int chunk, hipStream_t sa,
                            hipStream_t sb, hipEvent_t* ev);
 
+// kernels/resident.hip -----------------------------------------------------
+// One workgroup per frame (both passes, LDS histogram, running output offset).
+bool resident_supported(const KParams& p);
+hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, int frames, hipStream_t s);
+
 }  // namespace svx

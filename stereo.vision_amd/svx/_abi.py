@@ -51,6 +51,7 @@ SIGNATURES = {
     "sv_batch_upload": [P, I, P, P],
     "sv_batch_project": [P, ctypes.POINTER(Camera), I],
     "sv_batch_pipeline": [P, ctypes.POINTER(Camera), ctypes.POINTER(Plane), D, I, I, I],
+    "sv_batch_pipeline_mode": [P, I],
     "sv_batch_sync": [P],
     "sv_batch_last_ms": [P, I, PF],
     "sv_batch_timing": [P, I, ctypes.POINTER(D), PI64],

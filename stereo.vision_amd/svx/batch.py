@@ -70,6 +70,13 @@ class Batch:
         """K1 launch shape: quads per lane (1, 2, 4) and non-temporal stores."""
         _abi.call("sv_batch_tune", self._h, int(qpl), int(nontemporal))
 
+    PIPE_MODES = {"auto": 0, "tiled": 1, "resident": 2}
+
+    def pipeline_mode(self, mode="auto"):
+        """Pipeline kernel family: "auto", "tiled" (tiles across workgroups) or
+        "resident" (one workgroup per frame). Results are identical."""
+        _abi.call("sv_batch_pipeline_mode", self._h, self.PIPE_MODES[mode])
+
     # -- compute -------------------------------------------------------------------
     def project(self, camera=None, sync=True):
         cam = camera or CAMERA

@@ -205,45 +205,81 @@ def test_pipeline_full_frames_step2(svx_mod, golden, fid):
     assert oracle.digest(got["pts"].reshape(-1, 1, 2)) == m["plane_points"]
 
 
+def _pipe(svx_mod, kind, disp, bgr, step, **kw):
+    """One host frame through the fused chain: "frame" = sv_pipeline_frame (tiled
+    kernels), "resident" = a 1-frame batch forced onto the frame-resident kernel."""
+    if kind == "frame":
+        return svx_mod.batch.pipeline_frame(disp, bgr, step, **kw)
+    H, W = disp.shape
+    with svx_mod.batch.Batch(1, H=H, W=W, step=step, with_bgr=True, with_points=True) as b:
+        b.pipeline_mode("resident")
+        b.upload(0, disp, bgr)
+        b.pipeline(**kw)
+        xyz, pts = b.read_points(0)
+        return dict(counts=tuple(int(v) for v in b.read_counts()[0]), hist=b.read_hist(0), pts=pts, xyz2=xyz)
+
+
+KINDS = ["frame", "resident"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("fid", [0, 1, 4095])
-def test_pipeline_full_frames_step1(svx_mod, fid):
+def test_pipeline_full_frames_step1(svx_mod, fid, kind):
     disp, bgr = oracle.synth_frame(fid)
-    got = svx_mod.batch.pipeline_frame(disp, bgr, 1)
+    got = _pipe(svx_mod, kind, disp, bgr, 1)
     _check_pipe(got, oracle.pipeline_frame(disp, bgr, 1))
 
 
+@pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("plane", [(-0.007, 2.79, 0.457), (0.01, 2.5, 0.6), (0.0, 1e-3, 1e-3)])
 @pytest.mark.parametrize("thr", [0.05, 0.01, 0.2])
-def test_pipeline_planes_and_thresholds(svx_mod, plane, thr):
+def test_pipeline_planes_and_thresholds(svx_mod, plane, thr, kind):
     disp, bgr = oracle.synth_frame(17)
-    got = svx_mod.batch.pipeline_frame(disp, bgr, 2, plane=plane, point_thr=thr, hist_thr=3)
+    got = _pipe(svx_mod, kind, disp, bgr, 2, plane=plane, point_thr=thr, hist_thr=3)
     _check_pipe(got, oracle.pipeline_frame(disp, bgr, 2, abc=np.array(plane), point_thr=thr, hist_thr=3))
 
 
+@pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("hist_thr", [-1, 0, 40, 10 ** 9])
-def test_pipeline_hist_thresholds(svx_mod, hist_thr):
+def test_pipeline_hist_thresholds(svx_mod, hist_thr, kind):
     """Every tile clean (-1), most tiles dirty (40), everything filtered (1e9)."""
     disp, bgr = oracle.synth_frame(23)
     for step in (1, 2):
-        got = svx_mod.batch.pipeline_frame(disp, bgr, step, hist_thr=hist_thr)
+        got = _pipe(svx_mod, kind, disp, bgr, step, hist_thr=hist_thr)
         _check_pipe(got, oracle.pipeline_frame(disp, bgr, step, hist_thr=hist_thr))
 
 
-def test_pipeline_edge_frames(svx_mod):
+@pytest.mark.parametrize("kind", KINDS)
+def test_pipeline_edge_frames(svx_mod, kind):
     z = np.zeros((544, 1024), np.uint8)
     bgr = np.zeros((544, 1024, 3), np.uint8)
-    got = svx_mod.batch.pipeline_frame(z, bgr, 2)
+    got = _pipe(svx_mod, kind, z, bgr, 2)
     assert got["counts"] == (0, 0, 0) and got["pts"].shape == (0, 2)
     full = np.full((544, 1024), 255, np.uint8)
-    _check_pipe(svx_mod.batch.pipeline_frame(full, bgr, 1), oracle.pipeline_frame(full, bgr, 1))
+    _check_pipe(_pipe(svx_mod, kind, full, bgr, 1), oracle.pipeline_frame(full, bgr, 1))
     rng = np.random.default_rng(3)
     for H, W in ((2, 8), (9, 16), (33, 64)):
         d = rng.integers(0, 256, (H, W)).astype(np.uint8)
         c = rng.integers(0, 4, (H, W, 3)).astype(np.uint8)
         for step in (1, 2):
-            got = svx_mod.batch.pipeline_frame(d, c, step, plane=(0.0, 0.0, 0.01), point_thr=1e9, hist_thr=0)
+            got = _pipe(svx_mod, kind, d, c, step, plane=(0.0, 0.0, 0.01), point_thr=1e9, hist_thr=0)
             _check_pipe(got, oracle.pipeline_frame(d, c, step, abc=np.array([0.0, 0.0, 0.01]),
                                                     point_thr=1e9, hist_thr=0))
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_pipeline_random_colours_and_planes(svx_mod, kind):
+    """Uniformly random BGR (every hue bin, exact ties included) and random
+    disparity, under planes that put many points near the keep1 boundary."""
+    rng = np.random.default_rng(11)
+    for trial in range(3):
+        d = rng.integers(0, 256, (544, 1024)).astype(np.uint8)
+        c = rng.integers(0, 256, (544, 1024, 3)).astype(np.uint8)
+        plane = (float(rng.normal(0, 0.01)), float(rng.uniform(1, 3)), float(rng.uniform(0.2, 0.6)))
+        for step in (1, 2):
+            got = _pipe(svx_mod, kind, d, c, step, plane=plane, point_thr=0.3, hist_thr=50)
+            _check_pipe(got, oracle.pipeline_frame(d, c, step, abc=np.array(plane), point_thr=0.3,
+                                                    hist_thr=50))
 
 
 # ---------------------------------------------------------------------------
@@ -266,10 +302,12 @@ def test_batch_dense_projection(svx_mod, step, tune):
                 np.testing.assert_allclose(a, r, rtol=RTOL, atol=0)
 
 
-@pytest.mark.parametrize("step,chunk", [(1, 16), (1, 3), (2, 1), (2, 5)])
-def test_batch_pipeline(svx_mod, step, chunk):
+@pytest.mark.parametrize("step,chunk,mode", [(1, 16, "tiled"), (1, 3, "tiled"), (2, 1, "tiled"),
+                                             (2, 5, "tiled"), (1, 0, "resident"), (2, 0, "resident")])
+def test_batch_pipeline(svx_mod, step, chunk, mode):
     frames, first = 7, 1000
     with svx_mod.batch.Batch(frames, step=step, with_bgr=True, with_points=True) as b:
+        b.pipeline_mode(mode)
         b.synth(first)
         b.pipeline(chunk=chunk)
         counts = b.read_counts()
@@ -284,7 +322,8 @@ def test_batch_pipeline(svx_mod, step, chunk):
 def test_batch_baseline_size_properties(svx_mod):
     """BASELINE configs 3/4 at full size (4096 frames, step 1): sampled frames equal
     the oracle; every frame's counts are consistent; results do not depend on the
-    chunking (the property multi-GPU sharding relies on)."""
+    chunking (the property multi-GPU sharding relies on) nor on the kernel
+    family: the tiled and the frame-resident pipelines agree on all 4096 frames."""
     frames = 4096
     with svx_mod.batch.Batch(frames, step=1, with_bgr=True, with_points=True) as b:
         b.synth(0)
@@ -295,6 +334,7 @@ def test_batch_baseline_size_properties(svx_mod):
             RX, RY, RZ = oracle.project_dense(disp, 1)
             assert np.array_equal(Z == 0, RZ == 0)
             np.testing.assert_allclose(Z, RZ, rtol=RTOL, atol=0)
+        b.pipeline_mode("tiled")
         b.pipeline(chunk=16)
         c16 = b.read_counts()
         h16 = b.read_hist(4095)
@@ -312,6 +352,18 @@ def test_batch_baseline_size_properties(svx_mod):
         assert np.array_equal(b.read_hist(4095), h16)
         x29, p29 = b.read_points(4095)
         assert np.array_equal(p29, p16) and np.array_equal(x29, x16)
+        b.pipeline_mode("resident")
+        b.pipeline()
+        assert np.array_equal(b.read_counts(), c16)
+        for f in (0, 777, 4095):
+            xr, pr = b.read_points(f)
+            if f == 4095:
+                assert np.array_equal(b.read_hist(f), h16)
+                assert np.array_equal(pr, p16) and np.array_equal(xr, x16)
+            else:
+                disp, bgr = oracle.synth_frame(f)
+                ref = oracle.pipeline_frame(disp, bgr, 1)
+                assert np.array_equal(pr, ref["pts"])
 
 
 def test_errors_are_raised(svx_mod):

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--k1", default="1:1,2:1,4:1,1:0")
     ap.add_argument("--chunks", default="8,16,32,64")
     ap.add_argument("--step", type=int, default=1)
+    ap.add_argument("--modes", default="tiled,resident")
     a = ap.parse_args()
     b = sb.Batch(a.frames, step=a.step, with_bgr=True, with_points=True)
     b.synth(0)
@@ -36,16 +37,18 @@ def main():
         res.append({"k1_qpl": cap, "nt": nt, "ms": round(ms, 4),
                     "GBps": round(13 * ng / ms / 1e6, 1), "Gpts": round(ng / ms / 1e6, 1)})
         print(json.dumps(res[-1]), flush=True)
-    for c in a.chunks.split(","):
-        c = int(c)
-        b.pipeline(chunk=c, sync=True)
-        b.reset_timing()
-        for _ in range(a.reps):
-            b.pipeline(chunk=c, sync=False)
-        ms, n = b.timing("pipeline")
-        ms /= n
-        res.append({"chunk": c, "pipeline_ms": round(ms, 4), "Gpts": round(ng / ms / 1e6, 1)})
-        print(json.dumps(res[-1]), flush=True)
+    for mode in a.modes.split(","):
+        b.pipeline_mode(mode)
+        for c in (a.chunks.split(",") if mode == "tiled" else ["0"]):
+            c = int(c)
+            b.pipeline(chunk=c, sync=True)
+            b.reset_timing()
+            for _ in range(a.reps):
+                b.pipeline(chunk=c, sync=False)
+            ms, n = b.timing("pipeline")
+            ms /= n
+            res.append({"mode": mode, "chunk": c, "pipeline_ms": round(ms, 4), "Gpts": round(ng / ms / 1e6, 1)})
+            print(json.dumps(res[-1]), flush=True)
     b.close()
 
 
