@@ -6,27 +6,32 @@
 // (functions.py:228-230); the keep2 points in raster order as fp32 X, Y, Z +
 // int32 (x, y) back-projection (functions.py:201-209, stereovision.py:112).
 //
+// keep1 comes from a per-call interval table (keep_table_kernel): for grid
+// point (gy, gx) the reference keeps exactly the disparities d in [lo, hi].
+// The table is built once per call (plane, threshold, camera) by evaluating the
+// reference predicate for every d = 1..255 — fp32 with a rigorous guard, the
+// reference's fp64 arithmetic inside the guard — and checking that the kept
+// set is one interval (the exact predicate |B*L/d - 1| < t is quasi-convex in
+// d); if it is not, the call falls back to the tiled kernels. The streaming
+// loops then test keep1 with two byte compares and no floating point.
+//
 // Because one workgroup walks its frame chunk by chunk (chunk = 256 lanes x
 // QPL quads x 4 grid points, raster order), nothing crosses workgroups: the
 // histogram lives in LDS, the output offset is a running register, and there
 // are no tickets, look-back, global atomics or hand-off buffers.
 //
-//   pass 1  per chunk: disparity + BGR in (4 B/pt); division-free keep1
-//           (|u - d| < t*d, fp32 with a rigorous guard, fp64 reference
-//           arithmetic inside it); the colours of kept points are packed
-//           densely into the wave's LDS region and binned there (fp32 hue,
-//           exact integer/fp64 path in the tie band) with LDS atomics whose
-//           return value marks "candidate" chunks: a point whose bin had fewer
-//           than hist_thr points before it. A bin that ends <= hist_thr has
-//           ALL its points candidates, so only candidate ("dirty") chunks can
-//           lose keep1 points in pass 2.
-//   pass 2  per chunk: disparity in (1 B/pt), keep1 again (same code, same
-//           bits); dirty chunks re-read BGR and drop points whose bin ends
-//           <= hist_thr; block scan; 4-byte descriptors (d | gy | gx) scattered
-//           into LDS; lane j then produces outputs 4j..4j+3 with 16-byte
-//           non-temporal stores to the SoA planes, so stores are contiguous.
-// Frames <= kRMaxChunks chunks; the launcher falls back to the tiled pipeline
-// otherwise (and for batches too small to fill the chip).
+//   pass 1  per chunk: disparity + BGR + table in; the colours of keep1 points
+//           are packed densely into the wave's LDS region and binned there
+//           (fp32 hue, exact integer/fp64 path in the tie band) with LDS
+//           atomics whose return value marks "candidate" chunks: a point whose
+//           bin had fewer than hist_thr points before it. A bin that ends
+//           <= hist_thr has ALL its points candidates, so only candidate
+//           ("dirty") chunks can lose keep1 points in pass 2.
+//   pass 2  per chunk: disparity + table in; dirty chunks re-read BGR and drop
+//           points whose bin ends <= hist_thr (dense, same LDS staging); block
+//           scan; 4-byte descriptors (d | gy | gx) scattered into LDS; lane j
+//           then produces outputs 4j..4j+3 with 16-byte non-temporal stores to
+//           the SoA planes, so every store instruction is contiguous.
 #include "../svx_launch.h"
 
 namespace svx {
@@ -35,26 +40,68 @@ constexpr int kRMaxChunks = 256;
 constexpr int kRStage = 4096;   // LDS staging slots; a power of two (wrap-around below)
 constexpr int kRBins = 1000;    // bins 0..999: t < 1000 - 1000/(6*255) so rint(t) <= 999
 
-struct ResidentShared {
-    uint32_t hist[kRBins];
-    uint32_t dirty[kRMaxChunks / 32];
-    uint64_t wtot[4];
-    uint32_t red[8];
-    uint32_t stage[kRStage];
-};
-static_assert(sizeof(ResidentShared) <= 20480, "8 workgroups per CU (160 KiB LDS)");
 
 template <int STEP>
 struct RCfg {
     static constexpr int QPL = STEP == 1 ? 4 : 2;   // quads per lane per chunk
     static constexpr int CW = 3 * STEP;            // BGR dwords per quad
-    static constexpr int PTS = 256 * QPL * 4;      // grid points per chunk
 };
 
-int resident_chunks_per_frame(const KParams& p, int step) {
-    const int per = 256 * (step == 1 ? 4 : 2);
+int resident_chunks_per_frame(const KParams& p) {
+    const int per = 256 * (p.step == 1 ? 4 : 2);
     return (p.frame_quads + per - 1) / per;
 }
+
+// ---------------------------------------------------------------------------
+// keep1 interval table: one uint16 (lo | hi << 8) per grid point of a
+// Hg x pitch grid; lo = 255, hi = 0 for "never" (and for the pad columns).
+// One lane per grid point, brute force over d = 1..255.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void keep_table_kernel(uint16_t* __restrict__ tab, uint32_t* __restrict__ err,
+                                                         KParams p) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= p.Hg * p.pitch) return;
+    const int gy = i / p.pitch, gx = i - gy * p.pitch;
+    uint32_t entry = 0x00FF;
+    if (gx < p.Wg) {
+        const int x = gx * p.step, y = gy * p.step;
+        const float xf = (float)x;
+        const float beta = __builtin_fmaf(p.bb32, (float)y, p.b032);
+        int lo = 256, hi = 0, cnt = 0;
+        for (int d = 1; d < 256; ++d) {
+            bool unc;
+            bool k = keep1_lean(xf, beta, (float)d, p, unc);
+            if (__builtin_expect(unc, 0)) k = keep1_f64(x, y, (uint32_t)d, p);
+            if (k) {
+                lo = min(lo, d);
+                hi = d;
+                ++cnt;
+            }
+        }
+        if (cnt) {
+            if (cnt == hi - lo + 1) entry = (uint32_t)lo | ((uint32_t)hi << 8);
+            else atomicOr(err, 1u);   // not an interval: the caller uses the tiled kernels
+        }
+    }
+    tab[i] = (uint16_t)entry;
+}
+
+hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, hipStream_t s) {
+    const int n = p.Hg * p.pitch;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(keep_table_kernel, dim3((n + 255) / 256), dim3(256), 0, s, tab, err, p);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Streaming loops
+// ---------------------------------------------------------------------------
+struct RParams {      // what the streaming kernel needs (kept small: SGPR budget)
+    int W, Wg, Q, pitch, frame_quads, nchunks, hist_thr, dx_words, dy_words, ablate;
+    uint64_t Q_m40;
+    int64_t frame_px;
+    float B32, fB32, cw_hi, cw_lo, ch_hi, ch_lo;
+};
 
 template <int STEP>
 struct RQuads {   // this lane's quads of one chunk
@@ -63,7 +110,7 @@ struct RQuads {   // this lane's quads of one chunk
 };
 
 template <int STEP>
-__device__ __forceinline__ void r_geometry(int c, int tid, const KParams& p, RQuads<STEP>& g) {
+__device__ __forceinline__ void r_geometry(int c, int tid, const RParams& p, RQuads<STEP>& g) {
     constexpr int QPL = RCfg<STEP>::QPL;
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
@@ -76,21 +123,22 @@ __device__ __forceinline__ void r_geometry(int c, int tid, const KParams& p, RQu
     }
 }
 
+// byte offset of quad (gy, q) in a frame plane with `bpp` bytes per pixel
 template <int STEP>
-__device__ __forceinline__ const uint8_t* r_row(const uint8_t* frame_base, int gy, int bpp, const KParams& p) {
-    return frame_base + (int64_t)((gy < 0 ? 0 : gy) * STEP) * p.W * bpp;
+__device__ __forceinline__ uint32_t r_off(int gy, int q, int bpp, const RParams& p) {
+    return (uint32_t)(((gy < 0 ? 0 : gy) * STEP) * p.W + 4 * STEP * q) * (uint32_t)bpp;
 }
 
 template <int STEP>
-__device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<STEP>& g, const KParams& p,
+__device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<STEP>& g, const RParams& p,
                                             uint32_t (&dw)[RCfg<STEP>::QPL][STEP]) {
 #pragma unroll
     for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
-        const uint8_t* row = r_row<STEP>(fdisp, g.gy[i], 1, p);
+        const uint8_t* a = fdisp + r_off<STEP>(g.gy[i], g.q[i], 1, p);
         if constexpr (STEP == 1) {
-            dw[i][0] = *reinterpret_cast<const uint32_t*>(row + 4 * g.q[i]);
+            dw[i][0] = *reinterpret_cast<const uint32_t*>(a);
         } else {
-            const uint2 w = *reinterpret_cast<const uint2*>(row + 8 * g.q[i]);
+            const uint2 w = *reinterpret_cast<const uint2*>(a);
             dw[i][0] = w.x;
             dw[i][1] = w.y;
         }
@@ -98,20 +146,30 @@ __device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<S
 }
 
 template <int STEP>
-__device__ __forceinline__ void r_load_bgr(const uint8_t* fbgr, const RQuads<STEP>& g, const KParams& p,
+__device__ __forceinline__ void r_load_tab(const uint16_t* tab, const RQuads<STEP>& g, const RParams& p,
+                                           uint2 (&tw)[RCfg<STEP>::QPL]) {
+#pragma unroll
+    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
+        const int gy = g.gy[i] < 0 ? 0 : g.gy[i];
+        tw[i] = *reinterpret_cast<const uint2*>(tab + (uint32_t)(gy * p.pitch + 4 * g.q[i]));
+    }
+}
+
+template <int STEP>
+__device__ __forceinline__ void r_load_bgr(const uint8_t* fbgr, const RQuads<STEP>& g, const RParams& p,
                                            uint32_t (&cw)[RCfg<STEP>::QPL][RCfg<STEP>::CW]) {
 #pragma unroll
     for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
-        const uint8_t* row = r_row<STEP>(fbgr, g.gy[i], 3, p);
+        const uint8_t* a = fbgr + r_off<STEP>(g.gy[i], g.q[i], 3, p);
         if constexpr (STEP == 1) {
-            const uint32_t* cp = reinterpret_cast<const uint32_t*>(row + 12 * g.q[i]);
+            const uint32_t* cp = reinterpret_cast<const uint32_t*>(a);
             cw[i][0] = cp[0];
             cw[i][1] = cp[1];
             cw[i][2] = cp[2];
         } else {
-            const uint2* cp = reinterpret_cast<const uint2*>(row + 24 * g.q[i]);
-            const uint2 a = cp[0], b = cp[1], c = cp[2];
-            cw[i][0] = a.x; cw[i][1] = a.y; cw[i][2] = b.x; cw[i][3] = b.y; cw[i][4] = c.x; cw[i][5] = c.y;
+            const uint2* cp = reinterpret_cast<const uint2*>(a);
+            const uint2 x = cp[0], y = cp[1], z = cp[2];
+            cw[i][0] = x.x; cw[i][1] = x.y; cw[i][2] = y.x; cw[i][3] = y.y; cw[i][4] = z.x; cw[i][5] = z.y;
         }
     }
 }
@@ -139,247 +197,342 @@ __device__ __forceinline__ int r_bin(uint32_t col) {
     return bin;
 }
 
-// keep1 bits of this lane's chunk (bit 4i+k = point k of quad i) + valid count.
+// keep1 bits of this lane's chunk (bit 4i+k = point k of quad i): lo <= d <= hi.
 template <int STEP>
-__device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP>::QPL][STEP], const RQuads<STEP>& g,
-                                            const KParams& p, uint32_t* nvalid) {
-    constexpr int QPL = RCfg<STEP>::QPL;
-    uint32_t keep = 0, unc = 0, nv = 0;
+__device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP>::QPL][STEP],
+                                            const uint2 (&tw)[RCfg<STEP>::QPL], const RQuads<STEP>& g) {
+    uint32_t keep = 0;
 #pragma unroll
-    for (int i = 0; i < QPL; ++i) {
-        const int y = g.gy[i] * STEP;
-        const float beta = __builtin_fmaf(p.bb32, (float)y, p.b032);
-        const bool rowok = g.gy[i] >= 0;
+    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
+        uint32_t k4 = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int gx = 4 * g.q[i] + k;
-            const bool in = rowok && gx < p.Wg;
+            const uint32_t t = (k < 2 ? tw[i].x : tw[i].y) >> (16 * (k & 1));
             const uint32_t d = r_d<STEP>(dw[i], k);
-            bool u;
-            const bool kp = keep1_lean((float)(gx * STEP), beta, (float)d, p, u);
-            keep |= (uint32_t)(kp && in) << (4 * i + k);
-            unc |= (uint32_t)(u && in) << (4 * i + k);
-            nv += (d != 0 && in) ? 1u : 0u;
+            k4 |= (uint32_t)(d >= (t & 0xFF) && d <= ((t >> 8) & 0xFF)) << k;
         }
+        keep |= (g.gy[i] >= 0 ? k4 : 0u) << (4 * i);
     }
-    if (__builtin_expect(unc != 0, 0)) {   // rare: the guard band -> exact fp64 reference arithmetic
-#pragma unroll
-        for (int i = 0; i < QPL; ++i) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t bit = 1u << (4 * i + k);
-                if (unc & bit) {
-                    const bool kk = keep1_f64((4 * g.q[i] + k) * STEP, g.gy[i] * STEP, r_d<STEP>(dw[i], k), p);
-                    keep = kk ? (keep | bit) : (keep & ~bit);
-                }
-            }
-        }
-    }
-    if (nvalid) *nvalid += nv;
     return keep;
+}
+
+// grid points with d != 0 in this lane's chunk (pad columns and rows past the end excluded)
+template <int STEP>
+__device__ __forceinline__ uint32_t r_nvalid(const uint32_t (&dw)[RCfg<STEP>::QPL][STEP], const RQuads<STEP>& g,
+                                             const RParams& p) {
+    uint32_t n = 0;
+#pragma unroll
+    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
+        const int nin = g.gy[i] < 0 ? 0 : min(4, p.Wg - 4 * g.q[i]);
+        uint32_t v;   // the quad's 4 disparity bytes, point k at byte k
+        if constexpr (STEP == 1) v = dw[i][0];
+        else v = __builtin_amdgcn_perm(dw[i][1], dw[i][0], 0x06040200u);
+        v &= nin >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nin)) - 1u);
+        const uint32_t nz = (((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+        n += __builtin_popcount(nz);
+    }
+    return n;
+}
+
+// Pack the colours of the keep bits into this wave's LDS region, in (lane, bit)
+// order; returns the wave's total and this lane's first slot.
+template <int STEP>
+__device__ __forceinline__ uint32_t r_stage_colours(uint32_t keep,
+                                                    const uint32_t (&cw)[RCfg<STEP>::QPL][RCfg<STEP>::CW],
+                                                    uint32_t* wstage, uint32_t& pos0) {
+    const uint32_t cnt = __builtin_popcount(keep);
+    const uint32_t inc = wave_incl_scan(cnt);
+    pos0 = inc - cnt;
+    uint32_t pos = pos0;
+#pragma unroll
+    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (keep & (1u << (4 * i + k))) wstage[pos++] = r_col<STEP>(cw[i], k);
+        }
+    }
+    return __shfl(inc, 63, kWave);
 }
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 template <int STEP>
-__global__ __launch_bounds__(256) void resident_kernel(PipeBuffers bf, int frame0, int nchunks, KParams p) {
+struct P1Regs {
+    RQuads<STEP> g;
+    uint32_t dw[RCfg<STEP>::QPL][STEP];
+    uint32_t cw[RCfg<STEP>::QPL][RCfg<STEP>::CW];
+    uint2 tw[RCfg<STEP>::QPL];
+};
+
+template <int STEP>
+struct P2Regs {
+    RQuads<STEP> g;
+    uint32_t dw[RCfg<STEP>::QPL][STEP];
+    uint2 tw[RCfg<STEP>::QPL];
+};
+
+template <int STEP>
+__device__ __forceinline__ void p1_load(P1Regs<STEP>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
+                                        const uint16_t* tab, const RParams& p) {
+    r_geometry<STEP>(c, tid, p, r.g);
+    r_load_disp<STEP>(fdisp, r.g, p, r.dw);
+    r_load_tab<STEP>(tab, r.g, p, r.tw);
+    r_load_bgr<STEP>(fbgr, r.g, p, r.cw);
+}
+
+template <int STEP>
+__device__ __forceinline__ void p2_load(P2Regs<STEP>& r, int c, int tid, const uint8_t* fdisp, const uint16_t* tab,
+                                        const RParams& p) {
+    r_geometry<STEP>(c, tid, p, r.g);
+    r_load_disp<STEP>(fdisp, r.g, p, r.dw);
+    r_load_tab<STEP>(tab, r.g, p, r.tw);
+}
+
+// pass 1 of one chunk: keep1, valid/kept counts, dense hue binning into hist,
+// candidate mark into dirty. Wave-local (no barrier).
+template <int STEP>
+__device__ __forceinline__ void p1_chunk(const P1Regs<STEP>& r, int c, uint32_t* hist, uint32_t* dirty,
+                                         uint32_t* wstage, const RParams& p, uint32_t& nvalid, uint32_t& nkept) {
+    const int lane = lane_id();
+    const uint32_t keep = r_keep1<STEP>(r.dw, r.tw, r.g);
+    nvalid += r_nvalid<STEP>(r.dw, r.g, p);
+    nkept += __builtin_popcount(keep);
+    uint32_t pos0;
+    const uint32_t wtotal = r_stage_colours<STEP>(keep, r.cw, wstage, pos0);
+    bool cand = false;
+    for (uint32_t j = lane; j < ((p.ablate & 512) ? 0u : wtotal); j += kWave) {   // ablate: DIAGNOSTIC ONLY
+        const int bin = r_bin(wstage[j]);
+        const uint32_t old = atomicAdd(&hist[bin], 1u);
+        cand |= (int64_t)old < (int64_t)p.hist_thr;
+    }
+    if (__ballot(cand) && lane == 0) atomicOr(&dirty[c >> 5], 1u << (c & 31));
+}
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// pass 2 of one chunk: keep2, block scan, descriptor scatter, contiguous
+// output stores. Two barriers. Loads chunk c + 1 into r before the stores.
+template <int STEP, bool PF, class SH>
+__device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, const uint32_t* hist,
+                                         const uint32_t* dirty, SH& sh, uint32_t* wstage,
+                                         const uint8_t* fdisp, const uint8_t* fbgr, const uint16_t* tab,
+                                         const PipeBuffers& bf, float* oX, int32_t* oP, uint32_t& running,
+                                         const RParams& p) {
     constexpr int QPL = RCfg<STEP>::QPL;
-    constexpr int WREGION = 64 * QPL * 4;   // staging slots per wave in pass 1
-    __shared__ ResidentShared sh;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = frame0 + blockIdx.x;
+    uint32_t keep = r_keep1<STEP>(r.dw, r.tw, r.g);
+    if ((dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: candidate chunk (rare); wave-local staging
+        uint32_t cw[QPL][RCfg<STEP>::CW];
+        r_load_bgr<STEP>(fbgr, r.g, p, cw);
+        uint32_t pos0;
+        const uint32_t wtotal = r_stage_colours<STEP>(keep, cw, wstage, pos0);
+        for (uint32_t j = lane; j < wtotal; j += kWave) {
+            const int bin = r_bin(wstage[j]);
+            wstage[j] = (int64_t)hist[bin] > (int64_t)p.hist_thr ? 1u : 0u;
+        }
+        uint32_t pos = pos0;
+#pragma unroll
+        for (int b = 0; b < 4 * QPL; ++b) {
+            if (keep & (1u << b)) {
+                if (!wstage[pos]) keep &= ~(1u << b);
+                ++pos;
+            }
+        }
+    }
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < QPL; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
+    uint64_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint64_t t = __shfl_up(inc, o, kWave);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) sh.wtot[wave] = inc;
+    __syncthreads();
+    uint64_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint64_t v = sh.wtot[w];
+        wbase += (w < wave) ? v : 0ull;
+        tot += v;
+    }
+    const uint64_t excl = wbase + inc - cnt;
+    // LDS slot s <-> output running - lead + s, so groups of 4 are 16-byte aligned
+    const uint32_t lead = running & 3;
+    uint32_t rowbase = lead;
+#pragma unroll
+    for (int i = 0; i < QPL; ++i) {
+        uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
+        rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (keep & (1u << (4 * i + k))) {
+                const uint32_t d = r_d<STEP>(r.dw[i], k);
+                sh.stage[(o++) & (kRStage - 1)] = (d << 24) | ((uint32_t)r.g.gy[i] << 12) | (uint32_t)(4 * r.g.q[i] + k);
+            }
+        }
+    }
+    const uint32_t end = rowbase;   // one past the last valid slot
+    if (PF && more) p2_load<STEP>(r, c + 1, tid, fdisp, tab, p);   // next chunk in flight before the stores
+    __syncthreads();
+    float* oY = oX + bf.cap;
+    float* oZ = oY + bf.cap;
+    const uint32_t g0 = running - lead;
+    const uint32_t groups = (end + 3) >> 2;
+    for (uint32_t m = tid; m < groups; m += 256) {
+        const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.stage[(4 * m) & (kRStage - 1)]);
+        const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
+        float X[4], Y[4], Z[4];
+        int PX[4], PY[4];
+        bool ok[4];
+        uint32_t wx[4], wy[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t s_ = 4 * m + e;
+            ok[e] = s_ >= lead && s_ < end;
+            const uint32_t uu = ok[e] ? u[e] : (1u << 24);
+            const uint32_t d = uu >> 24;
+            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
+            const int x = (int)(uu & 0xFFF) * STEP;
+            wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
+            wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t uu = ok[e] ? u[e] : (1u << 24);
+            const uint32_t d = uu >> 24;
+            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
+            const int x = (int)(uu & 0xFFF) * STEP;
+            const float rr = __builtin_amdgcn_rcpf((float)d);
+            const float K = p.B32 * rr;
+            X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
+            Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
+            Z[e] = p.fB32 * rr;
+            PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
+            PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
+        }
+        const int64_t go = (int64_t)g0 + 4 * m;
+        if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
+            __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + go));
+            __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + go));
+            __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + go));
+            __builtin_nontemporal_store((v4i){PX[0], PY[0], PX[1], PY[1]}, reinterpret_cast<v4i*>(oP + 2 * go));
+            __builtin_nontemporal_store((v4i){PX[2], PY[2], PX[3], PY[3]}, reinterpret_cast<v4i*>(oP + 2 * go + 4));
+        } else {                // the chunk's first / last group
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (!ok[e]) continue;
+                oX[go + e] = X[e];
+                oY[go + e] = Y[e];
+                oZ[go + e] = Z[e];
+                *reinterpret_cast<int2*>(oP + 2 * (go + e)) = make_int2(PX[e], PY[e]);
+            }
+        }
+    }
+    running += end - lead;
+}
+
+// ---------------------------------------------------------------------------
+// One workgroup = one frame: pass 1 over all chunks, then pass 2 (grid = frames).
+// ---------------------------------------------------------------------------
+struct FusedShared {
+    uint32_t hist[kRBins];
+    uint32_t dirty[kRMaxChunks / 32];
+    uint64_t wtot[4];
+    uint32_t red[8];
+    uint32_t stage[kRStage];
+};
+static_assert(sizeof(FusedShared) <= 20480, "8 workgroups per CU (160 KiB LDS)");
+
+template <int STEP, bool PF>
+__global__ __launch_bounds__(256) void resident_fused_kernel(PipeBuffers bf, const uint16_t* __restrict__ tab,
+                                                             RParams p) {
+    constexpr int QPL = RCfg<STEP>::QPL;
+    constexpr int WREGION = 64 * QPL * 4;
+    __shared__ FusedShared sh;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int frame = blockIdx.x;
+    const int nch = p.nchunks;
     const uint8_t* fdisp = bf.disp + (int64_t)frame * p.frame_px;
     const uint8_t* fbgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
+    uint32_t* wstage = sh.stage + wave * WREGION;
     for (int i = tid; i < kRBins; i += 256) sh.hist[i] = 0;
     if (tid < kRMaxChunks / 32) sh.dirty[tid] = 0;
     __syncthreads();
-
-    // ---------------- pass 1: histogram + candidate chunks ----------------
     uint32_t nvalid = 0, nkept = 0;
-    uint32_t* wstage = sh.stage + wave * WREGION;
-    for (int c = 0; c < ((p.ablate & 128) ? 0 : nchunks); ++c) {   // ablate: DIAGNOSTIC ONLY
-        RQuads<STEP> g;
-        r_geometry<STEP>(c, tid, p, g);
-        uint32_t dw[QPL][STEP], cw[QPL][RCfg<STEP>::CW];
-        r_load_disp<STEP>(fdisp, g, p, dw);
-        r_load_bgr<STEP>(fbgr, g, p, cw);
-        uint32_t keep = r_keep1<STEP>(dw, g, p, &nvalid);
-        if (p.ablate & 1024) keep = (cw[0][0] == 12345u) ? keep : 0u;
-        const uint32_t cnt = __builtin_popcount(keep);
-        nkept += cnt;
-        const uint32_t inc = wave_incl_scan(cnt);
-        const uint32_t wtotal = __shfl(inc, 63, kWave);
-        uint32_t pos = inc - cnt;
-#pragma unroll
-        for (int i = 0; i < QPL; ++i) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (keep & (1u << (4 * i + k))) wstage[pos++] = r_col<STEP>(cw[i], k);
-            }
-        }
-        bool cand = false;
-        for (uint32_t j = lane; j < ((p.ablate & 512) ? 0u : wtotal); j += kWave) {   // dense: kept colours only
-            const int bin = r_bin(wstage[j]);
-            const uint32_t old = atomicAdd(&sh.hist[bin], 1u);
-            cand |= (int64_t)old < (int64_t)p.hist_thr;
-        }
-        if (__ballot(cand) && lane == 0) atomicOr(&sh.dirty[c >> 5], 1u << (c & 31));
+    for (int c = 0; c < ((p.ablate & 128) ? 0 : nch); ++c) {   // ablate: DIAGNOSTIC ONLY
+        P1Regs<STEP> r1;
+        p1_load<STEP>(r1, c, tid, fdisp, fbgr, tab, p);
+        p1_chunk<STEP>(r1, c, sh.hist, sh.dirty, wstage, p, nvalid, nkept);
     }
-    __syncthreads();   // histogram complete
-
-    {   // the frame's histogram (read back by the API; bins >= 1000 are never produced)
-        uint32_t* gh = bf.hist + (int64_t)frame * kBins;
-        for (int b = tid; b < kBins; b += 256) gh[b] = b < kRBins ? sh.hist[b] : 0u;
-    }
-
-    // ---------------- pass 2: keep2 + ordered compaction + outputs ----------
-    float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap;
-    float* oY = oX + bf.cap;
-    float* oZ = oY + bf.cap;
-    int32_t* oP = bf.pts + (int64_t)frame * bf.cap * 2;
-    uint32_t running = 0;
-    for (int c = 0; c < ((p.ablate & 256) ? 0 : nchunks); ++c) {
-        RQuads<STEP> g;
-        r_geometry<STEP>(c, tid, p, g);
-        uint32_t dw[QPL][STEP];
-        r_load_disp<STEP>(fdisp, g, p, dw);
-        uint32_t keep = r_keep1<STEP>(dw, g, p, nullptr);
-        if ((sh.dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: rare candidate chunk
-            uint32_t cw[QPL][RCfg<STEP>::CW];
-            r_load_bgr<STEP>(fbgr, g, p, cw);
-#pragma unroll
-            for (int i = 0; i < QPL; ++i) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t bit = 1u << (4 * i + k);
-                    if (keep & bit) {
-                        const int bin = r_bin(r_col<STEP>(cw[i], k));
-                        if (!((int64_t)sh.hist[bin] > (int64_t)p.hist_thr)) keep &= ~bit;
-                    }
-                }
-            }
-        }
-        uint64_t cnt = 0;
-#pragma unroll
-        for (int i = 0; i < QPL; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
-        uint64_t inc = cnt;
-#pragma unroll
-        for (int o = 1; o < kWave; o <<= 1) {
-            const uint64_t t = __shfl_up(inc, o, kWave);
-            if (lane >= o) inc += t;
-        }
-        if (lane == 63) sh.wtot[wave] = inc;
-        __syncthreads();
-        uint64_t wbase = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const uint64_t v = sh.wtot[w];
-            wbase += (w < wave) ? v : 0ull;
-            tot += v;
-        }
-        const uint64_t excl = wbase + inc - cnt;
-        // LDS slot s <-> output running - lead + s, so groups of 4 are 16-byte aligned
-        const uint32_t lead = running & 3;
-        uint32_t rowbase = lead;
-#pragma unroll
-        for (int i = 0; i < QPL; ++i) {
-            uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
-            rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (keep & (1u << (4 * i + k))) {
-                    const uint32_t d = r_d<STEP>(dw[i], k);
-                    sh.stage[(o++) & (kRStage - 1)] = (d << 24) | ((uint32_t)g.gy[i] << 12) | (uint32_t)(4 * g.q[i] + k);
-                }
-            }
-        }
-        const uint32_t end = rowbase;   // one past the last valid slot
-        __syncthreads();
-        const uint32_t g0 = running - lead;
-        const uint32_t groups = (end + 3) >> 2;
-        for (uint32_t m = tid; m < groups; m += 256) {
-            const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.stage[(4 * m) & (kRStage - 1)]);
-            const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
-            float X[4], Y[4], Z[4];
-            int PX[4], PY[4];
-            bool ok[4];
-            uint32_t wx[4], wy[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t s_ = 4 * m + e;
-                ok[e] = s_ >= lead && s_ < end;
-                const uint32_t uu = ok[e] ? u[e] : (1u << 24);
-                const uint32_t d = uu >> 24;
-                const int y = (int)((uu >> 12) & 0xFFF) * STEP;
-                const int x = (int)(uu & 0xFFF) * STEP;
-                wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
-                wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t uu = ok[e] ? u[e] : (1u << 24);
-                const uint32_t d = uu >> 24;
-                const int y = (int)((uu >> 12) & 0xFFF) * STEP;
-                const int x = (int)(uu & 0xFFF) * STEP;
-                const float r = __builtin_amdgcn_rcpf((float)d);
-                const float K = p.B32 * r;
-                X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
-                Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
-                Z[e] = p.fB32 * r;
-                PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
-                PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
-            }
-            const int64_t go = (int64_t)g0 + 4 * m;
-            if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
-                __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + go));
-                __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + go));
-                __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + go));
-                __builtin_nontemporal_store((v4i){PX[0], PY[0], PX[1], PY[1]}, reinterpret_cast<v4i*>(oP + 2 * go));
-                __builtin_nontemporal_store((v4i){PX[2], PY[2], PX[3], PY[3]}, reinterpret_cast<v4i*>(oP + 2 * go + 4));
-            } else {                // the chunk's first / last group
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (!ok[e]) continue;
-                    oX[go + e] = X[e];
-                    oY[go + e] = Y[e];
-                    oZ[go + e] = Z[e];
-                    *reinterpret_cast<int2*>(oP + 2 * (go + e)) = make_int2(PX[e], PY[e]);
-                }
-            }
-        }
-        running += end - lead;
-    }
-
-    // ---------------- frame counts ----------------
     nvalid = wave_sum(nvalid);
     nkept = wave_sum(nkept);
     if (lane == 0) {
         sh.red[wave] = nvalid;
         sh.red[4 + wave] = nkept;
     }
-    __syncthreads();
-    if (tid == 0) {
-        int64_t* cn = bf.counts + 4 * (int64_t)frame;
-        cn[0] = (int64_t)sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
-        cn[1] = (int64_t)sh.red[4] + sh.red[5] + sh.red[6] + sh.red[7];
-        cn[2] = running;
+    __syncthreads();   // histogram, dirty bits, counts complete
+    {
+        uint32_t* gh = bf.hist + (int64_t)frame * kBins;
+        for (int b = tid; b < kBins; b += 256) gh[b] = b < kRBins ? sh.hist[b] : 0u;
+        if (tid == 0) {
+            int64_t* cn = bf.counts + 4 * (int64_t)frame;
+            cn[0] = (int64_t)sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
+            cn[1] = (int64_t)sh.red[4] + sh.red[5] + sh.red[6] + sh.red[7];
+        }
     }
+    float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap;
+    int32_t* oP = bf.pts + (int64_t)frame * bf.cap * 2;
+    uint32_t running = 0;
+    const int n2 = (p.ablate & 256) ? 0 : nch;
+    P2Regs<STEP> r2;
+    if (PF && n2 > 0) p2_load<STEP>(r2, 0, tid, fdisp, tab, p);
+    for (int c = 0; c < n2; ++c) {
+        if (!PF) p2_load<STEP>(r2, c, tid, fdisp, tab, p);
+        p2_chunk<STEP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
+                           running, p);
+    }
+    if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;
 }
 
 bool resident_supported(const KParams& p) {
     return (p.step == 1 || p.step == 2) && p.Wg <= 4096 && p.Hg <= 4096 &&
-           resident_chunks_per_frame(p, p.step) <= kRMaxChunks;
+           resident_chunks_per_frame(p) <= kRMaxChunks && p.frame_px * 3 < (1ll << 31);
 }
 
-hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, int frames, hipStream_t s) {
+hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, const uint16_t* tab, int frames,
+                                    bool prefetch, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
-    if (!resident_supported(p)) return hipErrorInvalidValue;
-    const int nch = resident_chunks_per_frame(p, p.step);
-    if (p.step == 1)
-        hipLaunchKernelGGL(resident_kernel<1>, dim3(frames), dim3(256), 0, s, b, 0, nch, p);
-    else
-        hipLaunchKernelGGL(resident_kernel<2>, dim3(frames), dim3(256), 0, s, b, 0, nch, p);
+    if (!resident_supported(kp)) return hipErrorInvalidValue;
+    RParams p;
+    p.W = kp.W;
+    p.Wg = kp.Wg;
+    p.Q = kp.Q;
+    p.pitch = kp.pitch;
+    p.frame_quads = kp.frame_quads;
+    p.nchunks = resident_chunks_per_frame(kp);
+    p.hist_thr = kp.hist_thr;
+    p.dx_words = kp.dx_words;
+    p.dy_words = kp.dy_words;
+    p.ablate = kp.ablate;
+    p.Q_m40 = kp.Q_m40;
+    p.frame_px = kp.frame_px;
+    p.B32 = kp.B32;
+    p.fB32 = kp.fB32;
+    p.cw_hi = kp.cw_hi;
+    p.cw_lo = kp.cw_lo;
+    p.ch_hi = kp.ch_hi;
+    p.ch_lo = kp.ch_lo;
+    if (kp.step == 1) {
+        if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, true>), dim3(frames), dim3(256), 0, s, b, tab, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<1, false>), dim3(frames), dim3(256), 0, s, b, tab, p);
+    } else {
+        if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<2, true>), dim3(frames), dim3(256), 0, s, b, tab, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<2, false>), dim3(frames), dim3(256), 0, s, b, tab, p);
+    }
     return hipGetLastError();
 }
 

@@ -218,7 +218,8 @@ struct sv_batch {
     hipStream_t stream = nullptr;    // K1, pass 1 (stream A)
     hipStream_t stream2 = nullptr;   // pipeline offsets kernels (stream B), beside the stage launches
     std::vector<hipEvent_t> sync_ev; // pipeline hand-offs between A and B (timing disabled)
-    DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks;
+    DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks, ktab;
+    uint32_t* ktab_err_host = nullptr;   // pinned: keep-table "not an interval" flag
     // pipeline control block (one memset per call): hist | counts | err
     uint32_t* hist = nullptr;
     int64_t* counts = nullptr;
@@ -405,8 +406,9 @@ int sv_batch_destroy(sv_batch* b) {
     if (!b) return SV_OK;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
-    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks})
+    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks, &b->ktab})
         if (x->p) (void)hipFree(x->p);
+    if (b->ktab_err_host) (void)hipHostFree(b->ktab_err_host);
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : b->pool) (void)hipEventDestroy(ev);
@@ -517,13 +519,23 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     bf.cap = (int64_t)cap;
     int mode = b->pipe_mode;
     if (mode == 0) mode = (b->frames >= kResidentMinFrames && resident_supported(p)) ? 2 : 1;
-    if (mode == 2 && !resident_supported(p))
+    if (mode >= 2 && !resident_supported(p))
         return fail(SV_E_ARG, "frame-resident pipeline: frame too large (grid %d x %d)", p.Hg, p.Wg);
     int t0, t1;
-    if (mode == 2) {   // every output word (hist, counts, points) is rewritten: no memset
+    if (mode >= 2) {   // every output word (hist, counts, points) is rewritten: no memset
+        const size_t tab_bytes = sizeof(uint16_t) * (size_t)p.Hg * p.pitch;
+        HIP_TRY(b->ktab.ensure(tab_bytes + 64));
+        if (!b->ktab_err_host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&b->ktab_err_host), 64));
+        uint16_t* tab = b->ktab.as<uint16_t>();
+        uint32_t* terr = reinterpret_cast<uint32_t*>(b->ktab.as<char>() + (tab_bytes + 15) / 16 * 16);
         HIP_TRY(hipEventRecord(b->ev[2], b->stream));
         HIP_TRY(b->timed_event(&t0));
-        HIP_TRY(launch_pipeline_resident(p, bf, b->frames, b->stream));
+        HIP_TRY(hipMemsetAsync(terr, 0, 4, b->stream));
+        HIP_TRY(launch_keep_table(p, tab, terr, b->stream));
+        HIP_TRY(hipMemcpyAsync(b->ktab_err_host, terr, 4, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
+        if (*b->ktab_err_host) goto tiled;   // a keep set that is not one interval: exact tiled kernels
+        HIP_TRY(launch_pipeline_resident(p, bf, tab, b->frames, mode == 2, b->stream));
         HIP_TRY(b->timed_event(&t1));
         HIP_TRY(hipEventRecord(b->ev[3], b->stream));
         b->pending[1].push_back({t0, t1});
@@ -533,6 +545,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     }
     HIP_TRY(hipEventRecord(b->ev[2], b->stream));
     HIP_TRY(b->timed_event(&t0));
+tiled:
     const int nchunks = (b->frames + chunk - 1) / chunk;
     while ((int)b->sync_ev.size() < 2 * nchunks) {
         hipEvent_t e;
@@ -559,7 +572,8 @@ int sv_batch_pipeline(sv_batch* b, const sv_camera* cam, const sv_plane* plane, 
 
 int sv_batch_pipeline_mode(sv_batch* b, int mode) {
     if (!b) return fail(SV_E_ARG, "null batch");
-    if (mode < 0 || mode > 2) return fail(SV_E_ARG, "pipeline mode must be 0 (auto), 1 (tiled) or 2 (resident)");
+    if (mode < 0 || mode > 3)
+        return fail(SV_E_ARG, "pipeline mode must be 0 (auto), 1 (tiled), 2 (resident) or 3 (resident, no prefetch)");
     b->pipe_mode = mode;
     return SV_OK;
 }

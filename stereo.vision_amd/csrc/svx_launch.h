@@ -53,7 +53,13 @@ hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, i
 
 // kernels/resident.hip -----------------------------------------------------
 // One workgroup per frame (both passes, LDS histogram, running output offset).
+// keep1 from a per-call interval table (uint16 lo | hi << 8 per grid point of
+// Hg x pitch); *err is set when some grid point's keep set is not an interval.
 bool resident_supported(const KParams& p);
-hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, int frames, hipStream_t s);
+hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, hipStream_t s);
+// One workgroup per frame (pass 1 then pass 2); prefetch = pass 2 loads the
+// next chunk before issuing this chunk's stores (costs registers).
+hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, const uint16_t* tab, int frames,
+                                    bool prefetch, hipStream_t s);
 
 }  // namespace svx

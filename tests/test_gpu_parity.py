@@ -212,14 +212,14 @@ def _pipe(svx_mod, kind, disp, bgr, step, **kw):
         return svx_mod.batch.pipeline_frame(disp, bgr, step, **kw)
     H, W = disp.shape
     with svx_mod.batch.Batch(1, H=H, W=W, step=step, with_bgr=True, with_points=True) as b:
-        b.pipeline_mode("resident")
+        b.pipeline_mode(kind)
         b.upload(0, disp, bgr)
         b.pipeline(**kw)
         xyz, pts = b.read_points(0)
         return dict(counts=tuple(int(v) for v in b.read_counts()[0]), hist=b.read_hist(0), pts=pts, xyz2=xyz)
 
 
-KINDS = ["frame", "resident"]
+KINDS = ["frame", "resident", "resident_nopf"]
 
 
 @pytest.mark.parametrize("kind", KINDS)
@@ -303,7 +303,8 @@ def test_batch_dense_projection(svx_mod, step, tune):
 
 
 @pytest.mark.parametrize("step,chunk,mode", [(1, 16, "tiled"), (1, 3, "tiled"), (2, 1, "tiled"),
-                                             (2, 5, "tiled"), (1, 0, "resident"), (2, 0, "resident")])
+                                             (2, 5, "tiled"), (1, 0, "resident"), (2, 0, "resident"),
+                                             (1, 0, "resident_nopf"), (1, 3, "resident_nopf"), (2, 2, "resident_nopf")])
 def test_batch_pipeline(svx_mod, step, chunk, mode):
     frames, first = 7, 1000
     with svx_mod.batch.Batch(frames, step=step, with_bgr=True, with_points=True) as b:
@@ -352,18 +353,19 @@ def test_batch_baseline_size_properties(svx_mod):
         assert np.array_equal(b.read_hist(4095), h16)
         x29, p29 = b.read_points(4095)
         assert np.array_equal(p29, p16) and np.array_equal(x29, x16)
-        b.pipeline_mode("resident")
-        b.pipeline()
-        assert np.array_equal(b.read_counts(), c16)
-        for f in (0, 777, 4095):
-            xr, pr = b.read_points(f)
-            if f == 4095:
-                assert np.array_equal(b.read_hist(f), h16)
-                assert np.array_equal(pr, p16) and np.array_equal(xr, x16)
-            else:
-                disp, bgr = oracle.synth_frame(f)
-                ref = oracle.pipeline_frame(disp, bgr, 1)
-                assert np.array_equal(pr, ref["pts"])
+        for mode in ("resident", "resident_nopf"):
+            b.pipeline_mode(mode)
+            b.pipeline()
+            assert np.array_equal(b.read_counts(), c16)
+            for f in (0, 777, 4095):
+                xr, pr = b.read_points(f)
+                if f == 4095:
+                    assert np.array_equal(b.read_hist(f), h16)
+                    assert np.array_equal(pr, p16) and np.array_equal(xr, x16)
+                else:
+                    disp, bgr = oracle.synth_frame(f)
+                    ref = oracle.pipeline_frame(disp, bgr, 1)
+                    assert np.array_equal(pr, ref["pts"])
 
 
 def test_errors_are_raised(svx_mod):

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--chunks", default="8,16,32,64")
     ap.add_argument("--step", type=int, default=1)
     ap.add_argument("--modes", default="tiled,resident")
+    ap.add_argument("--rchunks", default="0", help="resident: frames per launch (0 = default)")
     a = ap.parse_args()
     b = sb.Batch(a.frames, step=a.step, with_bgr=True, with_points=True)
     b.synth(0)
@@ -39,7 +40,7 @@ def main():
         print(json.dumps(res[-1]), flush=True)
     for mode in a.modes.split(","):
         b.pipeline_mode(mode)
-        for c in (a.chunks.split(",") if mode == "tiled" else ["0"]):
+        for c in (a.chunks if mode == "tiled" else a.rchunks).split(","):
             c = int(c)
             b.pipeline(chunk=c, sync=True)
             b.reset_timing()

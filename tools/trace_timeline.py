@@ -8,7 +8,7 @@ last_end = {}
 for r in rows:
     name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("svx::", "")[:28]
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    if "stage" not in name and "offsets" not in name and "fill" not in name:
+    if not any(k in name for k in ("stage", "offsets", "fill", "resident", "keep_table")):
         continue
     if t0 is None:
         t0 = s
