@@ -218,6 +218,8 @@ def main():
             "algorithmic_bytes_per_call": pbytes,
             "counts_total": {"valid": int(counts[0]), "kept": int(counts[1]), "kept2": n_kept2},
             "plane_broadcast": "RCCL ncclBroadcast over xGMI, every step" if comm else "n/a (single process)",
+            "kernels": "keep_table_kernel (per call) + resident_fused_kernel (one workgroup per frame)"
+                       if args.frames >= 512 else "tiled: stage_kernel + offsets_kernel",
         }
 
     if rank == 0 and world == 1 and not args.no_cpu:

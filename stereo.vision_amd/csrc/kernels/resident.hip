@@ -381,31 +381,35 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, cons
     float* oY = oX + bf.cap;
     float* oZ = oY + bf.cap;
     const uint32_t g0 = running - lead;
-    const uint32_t groups = (end + 3) >> 2;
-    for (uint32_t m = tid; m < groups; m += 256) {
-        const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.stage[(4 * m) & (kRStage - 1)]);
-        const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
+    const uint32_t groups = (p.ablate & 16384) ? 0u : (end + 3) >> 2;   // ablate: DIAGNOSTIC ONLY
+    // Group m = output slots 4m..4m+3. The next group's descriptors and delta
+    // words are fetched before this group's stores: vmcnt counts loads and
+    // stores in issue order, so a load issued after a store would wait for it.
+    uint32_t m = tid;
+    uint32_t u[4], wx[4], wy[4];
+    auto fetch = [&](uint32_t mm) {
+        const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.stage[(4 * mm) & (kRStage - 1)]);
+        u[0] = u4.x; u[1] = u4.y; u[2] = u4.z; u[3] = u4.w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t s_ = 4 * mm + e;
+            if (!(s_ >= lead && s_ < end)) u[e] = 1u << 24;   // d = 1 at (0, 0): harmless filler
+            const uint32_t d = u[e] >> 24;
+            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(u[e] & 0xFFF) * STEP;
+            wx[e] = (p.ablate & 8192) ? 0u : bf.dxbits[d * p.dx_words + (x >> 5)];
+            wy[e] = (p.ablate & 8192) ? 0u : bf.dybits[d * p.dy_words + (y >> 5)];
+        }
+    };
+    if (m < groups) fetch(m);
+    while (m < groups) {
         float X[4], Y[4], Z[4];
         int PX[4], PY[4];
-        bool ok[4];
-        uint32_t wx[4], wy[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const uint32_t s_ = 4 * m + e;
-            ok[e] = s_ >= lead && s_ < end;
-            const uint32_t uu = ok[e] ? u[e] : (1u << 24);
-            const uint32_t d = uu >> 24;
-            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
-            const int x = (int)(uu & 0xFFF) * STEP;
-            wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
-            wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint32_t uu = ok[e] ? u[e] : (1u << 24);
-            const uint32_t d = uu >> 24;
-            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
-            const int x = (int)(uu & 0xFFF) * STEP;
+            const uint32_t d = u[e] >> 24;
+            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(u[e] & 0xFFF) * STEP;
             const float rr = __builtin_amdgcn_rcpf((float)d);
             const float K = p.B32 * rr;
             X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
@@ -414,8 +418,14 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, cons
             PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
             PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
         }
-        const int64_t go = (int64_t)g0 + 4 * m;
-        if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
+        const uint32_t s0 = 4 * m;
+        const bool full = s0 >= lead && s0 + 3 < end;
+        const int64_t go = (int64_t)g0 + s0;
+        const uint32_t mn = m + 256;
+        if (mn < groups) fetch(mn);   // before the stores below
+        if (p.ablate & 4096) {   // diagnostic: keep the math live, no stores
+            if (X[0] == 12345.f) oX[go] = X[1] + Y[2] + Z[3] + (float)(PX[0] + PY[1] + PX[2] + PY[3]);
+        } else if (full) {   // 16-byte non-temporal stores
             __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + go));
             __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + go));
             __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + go));
@@ -424,13 +434,15 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, cons
         } else {                // the chunk's first / last group
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                if (!ok[e]) continue;
+                const uint32_t s_ = s0 + e;
+                if (!(s_ >= lead && s_ < end)) continue;
                 oX[go + e] = X[e];
                 oY[go + e] = Y[e];
                 oZ[go + e] = Z[e];
                 *reinterpret_cast<int2*>(oP + 2 * (go + e)) = make_int2(PX[e], PY[e]);
             }
         }
+        m = mn;
     }
     running += end - lead;
 }
