@@ -39,12 +39,14 @@ def main():
             out["k1_fetch_bytes_per_launch"] = fetch
             out["k1_write_bytes_per_launch"] = write
             out["k1_hbm_bytes_per_launch"] = fetch + write
-        if "pipeline_kernel" in k:
-            n = len(cs["FETCH_SIZE"])
-            out["pipeline_kernel"] = k
-            out["pipeline_launches_profiled"] = n
-            out["pipeline_fetch_bytes_total"] = 2 * 1024 * sum(cs["FETCH_SIZE"])
-            out["pipeline_write_bytes_total"] = 1024 * sum(cs["WRITE_SIZE"])
+        if any(t in k for t in ("resident_fused_kernel", "keep_table_kernel", "stage_kernel", "offsets_kernel")):
+            pk = out.setdefault("pipeline_kernels", {})
+            pk[k] = {"launches": len(cs["FETCH_SIZE"]),
+                     "fetch_bytes_total": 2 * 1024 * sum(cs["FETCH_SIZE"]),
+                     "write_bytes_total": 1024 * sum(cs["WRITE_SIZE"])}
+    if "pipeline_kernels" in out:   # per call (prof_workload runs one pipeline call)
+        out["pipeline_hbm_bytes_per_call"] = sum(v["fetch_bytes_total"] + v["write_bytes_total"]
+                                                 for v in out["pipeline_kernels"].values())
     print(json.dumps(out, indent=1))
 
 
