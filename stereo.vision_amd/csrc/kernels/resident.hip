@@ -312,20 +312,91 @@ __device__ __forceinline__ void p1_chunk(const P1Regs<STEP>& r, int c, uint32_t*
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 
-// pass 2 of one chunk: keep2, block scan, descriptor scatter, contiguous
-// output stores. Two barriers. Loads chunk c + 1 into r before the stores.
+// Write outputs [a, b) of the frame from their LDS descriptors (slot = g mod
+// kRStage). Group = 4 outputs at a 16-byte-aligned position; lane j takes
+// groups j, j + 256, ... The next group's descriptors and delta-table words are
+// fetched before this group's stores: vmcnt counts loads and stores in issue
+// order, so a load issued after a store would wait for it.
+template <int STEP>
+__device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint32_t b, const PipeBuffers& bf,
+                                         float* oX, float* oY, float* oZ, int32_t* oP, const RParams& p) {
+    const uint32_t first = a & ~3u;
+    const uint32_t groups = (p.ablate & 16384) ? 0u : (b - first + 3) >> 2;   // ablate: DIAGNOSTIC ONLY
+    uint32_t m = threadIdx.x;
+    uint32_t u[4], wx[4], wy[4];
+    auto fetch = [&](uint32_t mm) {
+        const uint32_t g = first + 4 * mm;
+        const uint4 u4 = *reinterpret_cast<const uint4*>(&stage[g & (kRStage - 1)]);
+        u[0] = u4.x; u[1] = u4.y; u[2] = u4.z; u[3] = u4.w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (!(g + e >= a && g + e < b)) u[e] = 1u << 24;   // d = 1 at (0, 0): harmless filler
+            const uint32_t d = u[e] >> 24;
+            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(u[e] & 0xFFF) * STEP;
+            wx[e] = (p.ablate & 8192) ? 0u : bf.dxbits[d * p.dx_words + (x >> 5)];
+            wy[e] = (p.ablate & 8192) ? 0u : bf.dybits[d * p.dy_words + (y >> 5)];
+        }
+    };
+    if (m < groups) fetch(m);
+    while (m < groups) {
+        float X[4], Y[4], Z[4];
+        int PX[4], PY[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t d = u[e] >> 24;
+            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(u[e] & 0xFFF) * STEP;
+            const float rr = __builtin_amdgcn_rcpf((float)d);
+            const float K = p.B32 * rr;
+            X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
+            Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
+            Z[e] = p.fB32 * rr;
+            PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
+            PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
+        }
+        const uint32_t g = first + 4 * m;
+        const bool full = g >= a && g + 3 < b;
+        const uint32_t mn = m + 256;
+        if (mn < groups) fetch(mn);   // before the stores below
+        if (p.ablate & 4096) {   // diagnostic: keep the math live, no stores
+            if (X[0] == 12345.f) oX[g] = X[1] + Y[2] + Z[3] + (float)(PX[0] + PY[1] + PX[2] + PY[3]);
+        } else if (full) {   // 16-byte non-temporal stores: whole groups, lines filled in order
+            __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + g));
+            __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + g));
+            __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + g));
+            __builtin_nontemporal_store((v4i){PX[0], PY[0], PX[1], PY[1]}, reinterpret_cast<v4i*>(oP + 2 * (size_t)g));
+            __builtin_nontemporal_store((v4i){PX[2], PY[2], PX[3], PY[3]}, reinterpret_cast<v4i*>(oP + 2 * (size_t)g + 4));
+        } else {                // a frame's last group, or a rare early tail
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (!(g + e >= a && g + e < b)) continue;
+                oX[g + e] = X[e];
+                oY[g + e] = Y[e];
+                oZ[g + e] = Z[e];
+                *reinterpret_cast<int2*>(oP + 2 * (size_t)(g + e)) = make_int2(PX[e], PY[e]);
+            }
+        }
+        m = mn;
+    }
+}
+
+// pass 2 of one chunk: keep2, block scan, descriptor scatter, then the
+// chunk's whole output groups. Two barriers. Loads chunk c + 1 into r before
+// the stores (PF).
 template <int STEP, bool PF, class SH>
 __device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, const uint32_t* hist,
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
                                          const uint8_t* fdisp, const uint8_t* fbgr, const uint16_t* tab,
                                          const PipeBuffers& bf, float* oX, int32_t* oP, uint32_t& running,
-                                         const RParams& p) {
+                                         uint32_t& flushed, const RParams& p) {
     constexpr int QPL = RCfg<STEP>::QPL;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     uint32_t keep = r_keep1<STEP>(r.dw, r.tw, r.g);
-    if ((dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: candidate chunk (rare); wave-local staging
+    if ((dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: candidate chunk (rare)
         uint32_t cw[QPL][RCfg<STEP>::CW];
         r_load_bgr<STEP>(fbgr, r.g, p, cw);
+        __syncthreads();   // every wave is done writing the previous chunk: sh.stage is free
         uint32_t pos0;
         const uint32_t wtotal = r_stage_colours<STEP>(keep, cw, wstage, pos0);
         for (uint32_t j = lane; j < wtotal; j += kWave) {
@@ -360,9 +431,21 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, cons
         tot += v;
     }
     const uint64_t excl = wbase + inc - cnt;
-    // LDS slot s <-> output running - lead + s, so groups of 4 are 16-byte aligned
-    const uint32_t lead = running & 3;
-    uint32_t rowbase = lead;
+    // LDS slot of output g = g mod kRStage. Outputs [flushed, running) are the
+    // previous chunk's unwritten tail (< 4, restored from sh.red), so every
+    // group of 4 written below is whole and 16-byte aligned. If this chunk's
+    // points would wrap onto that tail (almost every point kept), the tail is
+    // written first as a partial group (uniform, rare).
+    const uint32_t T = (uint32_t)((tot >> 0) & 0xFFFF) + (uint32_t)((tot >> 16) & 0xFFFF) +
+                       (uint32_t)((tot >> 32) & 0xFFFF) + (uint32_t)((tot >> 48) & 0xFFFF);
+    float* oY = oX + bf.cap;
+    float* oZ = oY + bf.cap;
+    if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (kRStage - 1)] = sh.red[tid];   // the tail
+    if (T > (uint32_t)kRStage - (running - flushed)) {
+        p2_write<STEP>(sh.stage, flushed, running, bf, oX, oY, oZ, oP, p);
+        flushed = running;
+    }
+    uint32_t rowbase = running;
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
         uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
@@ -375,76 +458,17 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, cons
             }
         }
     }
-    const uint32_t end = rowbase;   // one past the last valid slot
     if (PF && more) p2_load<STEP>(r, c + 1, tid, fdisp, tab, p);   // next chunk in flight before the stores
     __syncthreads();
-    float* oY = oX + bf.cap;
-    float* oZ = oY + bf.cap;
-    const uint32_t g0 = running - lead;
-    const uint32_t groups = (p.ablate & 16384) ? 0u : (end + 3) >> 2;   // ablate: DIAGNOSTIC ONLY
-    // Group m = output slots 4m..4m+3. The next group's descriptors and delta
-    // words are fetched before this group's stores: vmcnt counts loads and
-    // stores in issue order, so a load issued after a store would wait for it.
-    uint32_t m = tid;
-    uint32_t u[4], wx[4], wy[4];
-    auto fetch = [&](uint32_t mm) {
-        const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.stage[(4 * mm) & (kRStage - 1)]);
-        u[0] = u4.x; u[1] = u4.y; u[2] = u4.z; u[3] = u4.w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint32_t s_ = 4 * mm + e;
-            if (!(s_ >= lead && s_ < end)) u[e] = 1u << 24;   // d = 1 at (0, 0): harmless filler
-            const uint32_t d = u[e] >> 24;
-            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
-            const int x = (int)(u[e] & 0xFFF) * STEP;
-            wx[e] = (p.ablate & 8192) ? 0u : bf.dxbits[d * p.dx_words + (x >> 5)];
-            wy[e] = (p.ablate & 8192) ? 0u : bf.dybits[d * p.dy_words + (y >> 5)];
-        }
-    };
-    if (m < groups) fetch(m);
-    while (m < groups) {
-        float X[4], Y[4], Z[4];
-        int PX[4], PY[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint32_t d = u[e] >> 24;
-            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
-            const int x = (int)(u[e] & 0xFFF) * STEP;
-            const float rr = __builtin_amdgcn_rcpf((float)d);
-            const float K = p.B32 * rr;
-            X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
-            Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
-            Z[e] = p.fB32 * rr;
-            PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
-            PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
-        }
-        const uint32_t s0 = 4 * m;
-        const bool full = s0 >= lead && s0 + 3 < end;
-        const int64_t go = (int64_t)g0 + s0;
-        const uint32_t mn = m + 256;
-        if (mn < groups) fetch(mn);   // before the stores below
-        if (p.ablate & 4096) {   // diagnostic: keep the math live, no stores
-            if (X[0] == 12345.f) oX[go] = X[1] + Y[2] + Z[3] + (float)(PX[0] + PY[1] + PX[2] + PY[3]);
-        } else if (full) {   // 16-byte non-temporal stores
-            __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + go));
-            __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + go));
-            __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + go));
-            __builtin_nontemporal_store((v4i){PX[0], PY[0], PX[1], PY[1]}, reinterpret_cast<v4i*>(oP + 2 * go));
-            __builtin_nontemporal_store((v4i){PX[2], PY[2], PX[3], PY[3]}, reinterpret_cast<v4i*>(oP + 2 * go + 4));
-        } else {                // the chunk's first / last group
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t s_ = s0 + e;
-                if (!(s_ >= lead && s_ < end)) continue;
-                oX[go + e] = X[e];
-                oY[go + e] = Y[e];
-                oZ[go + e] = Z[e];
-                *reinterpret_cast<int2*>(oP + 2 * (go + e)) = make_int2(PX[e], PY[e]);
-            }
-        }
-        m = mn;
+    running += T;
+    const uint32_t upto = more ? (running & ~3u) : running;   // the last chunk flushes its tail
+    // keep the new tail (< 4 descriptors) out of sh.stage's way: the next
+    // chunk's dirty path may reuse sh.stage before its scatter restores them
+    if (tid < (int)(running - upto)) sh.red[tid] = sh.stage[(upto + tid) & (kRStage - 1)];
+    if (upto > flushed) {
+        p2_write<STEP>(sh.stage, flushed, upto, bf, oX, oY, oZ, oP, p);
+        flushed = upto;
     }
-    running += end - lead;
 }
 
 // ---------------------------------------------------------------------------
@@ -498,14 +522,14 @@ __global__ __launch_bounds__(256) void resident_fused_kernel(PipeBuffers bf, con
     }
     float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap;
     int32_t* oP = bf.pts + (int64_t)frame * bf.cap * 2;
-    uint32_t running = 0;
+    uint32_t running = 0, flushed = 0;
     const int n2 = (p.ablate & 256) ? 0 : nch;
     P2Regs<STEP> r2;
     if (PF && n2 > 0) p2_load<STEP>(r2, 0, tid, fdisp, tab, p);
     for (int c = 0; c < n2; ++c) {
         if (!PF) p2_load<STEP>(r2, c, tid, fdisp, tab, p);
         p2_chunk<STEP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
-                           running, p);
+                           running, flushed, p);
     }
     if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;
 }
