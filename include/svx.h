@@ -76,6 +76,30 @@ int sv_pipeline_frame(const uint8_t* disp, const uint8_t* bgr, int H, int W, int
                       int64_t* out_counts, uint32_t* out_hist, float* out_xyz, int32_t* out_pts,
                       int64_t cap);
 
+/* ---- disparity pre-pass, host frames, synchronous ---- */
+
+/* Replaces functions.py:141-148 fillDisparity(disparity, previousDisparity):
+ * out = d > 2 ? d : min(255, d + prev) per pixel (cv2.threshold BINARY at 2,
+ * bitwise_not, masked copy of prev, saturating cv2.add); prev NULL -> copy. */
+int sv_fill_previous(const uint8_t* disp, const uint8_t* prev, int H, int W, uint8_t* out);
+/* Replaces functions.py:150-162 fillAltDisparity(disparity), IN PLACE like the
+ * reference: pixels < 2 of each row <- trunc(mean of the row's non-zero values). */
+int sv_fill_mean(uint8_t* disp, int H, int W);
+/* Replaces functions.py:169-172 maskDisparity(disparity) with the caller's
+ * carmask (functions.py:35): out = mask != 0 ? d : 0. */
+int sv_mask_disparity(const uint8_t* disp, const uint8_t* mask, int H, int W, uint8_t* out);
+
+/* ---- road raster + non-zero walk, host, synchronous -- */
+
+/* Replaces functions.py:339-344 generatePointsAsImage(points): an H x W grey
+ * image, 0 except 255 at every [x, y] of pts (n x 2 int32, the planePoints of
+ * stereovision.py:112-113). Negative indices wrap like numpy's; a point past
+ * [-W, W) x [-H, H) fails with SV_E_ARG (numpy raises IndexError). */
+int sv_road_raster(const int32_t* pts, int64_t n, int H, int W, uint8_t* out_img);
+/* The pixel walk at the end of functions.py:355-366 (sanitiseRoadImage):
+ * out = [j, i] (int32) of every non-zero pixel, raster order. W <= 4096. */
+int sv_nonzero_points(const uint8_t* img, int H, int W, int32_t* out, int64_t cap, int64_t* out_n);
+
 /* ---- batched, device-resident API ------------- */
 typedef struct sv_batch sv_batch;
 
@@ -112,6 +136,24 @@ int sv_batch_pipeline(sv_batch* b, const sv_camera* cam, const sv_plane* plane,
  * frame, LDS histogram; frames of <= 1M grid points at step 1). Results are
  * identical; only the speed differs. */
 int sv_batch_pipeline_mode(sv_batch* b, int mode);
+
+/* Pre-pass over the batch's frames in order (stereovision.py:53-76): option
+ * 1 = fillDisparity with the previous CLEANED frame (frame 0 uses prev0, or is
+ * left as is when prev0 is NULL), 2 = fillAltDisparity, 0 = none. The cleaned
+ * disparity replaces the batch's; with a mask set (sv_batch_set_mask, the grey
+ * carmask, NULL clears it) the masked disparity of functions.py:169-172 is
+ * also written (sv_batch_read_disp). capDisparity (functions.py:164-167)
+ * returns its input unchanged, so it has no kernel. */
+int sv_batch_set_mask(sv_batch* b, const uint8_t* mask);
+int sv_batch_prepass(sv_batch* b, int option, const uint8_t* prev0, int sync);
+int sv_batch_read_disp(sv_batch* b, int frame, uint8_t* disp, uint8_t* masked);
+
+/* Road images of the pipeline's int32 points (generatePointsAsImage per
+ * frame), their raster-order non-zero walks, and read-back (img and/or the
+ * walk; n receives the walk's length). */
+int sv_batch_road_raster(sv_batch* b, int sync);
+int sv_batch_nonzero(sv_batch* b, int sync);
+int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int64_t cap, int64_t* n);
 
 int sv_batch_sync(sv_batch* b);
 /* ms of the last sv_batch_project / sv_batch_pipeline, from HIP events

@@ -1,0 +1,154 @@
+// Disparity pre-pass kernels (gfx950): the per-pixel uint8 stages that feed
+// the projection, all HBM-bound byte streams.
+//
+//  * fill_prev_kernel  — fillDisparity (functions.py:141-148) applied frame
+//                        after frame as performStereoVision does with
+//                        prev_disp (stereovision.py:56-60, functions.py:131-135):
+//                        cleaned_f = raw_f > 2 ? raw_f : sat8(raw_f + cleaned_{f-1})
+//                        (cv2.threshold(..., 2, 255, BINARY) -> NOT -> masked
+//                        copy of prev -> cv2.add, saturating). The frame
+//                        recurrence runs in registers: one lane owns 4 pixels
+//                        and walks the batch's frames in order, 8 frames of
+//                        loads in flight.
+//  * fill_mean_kernel  — fillAltDisparity (functions.py:150-162): per row, the
+//                        mean of the non-zero values (0 if none), assigned with
+//                        numpy's float->uint8 truncation to every pixel < 2.
+//                        The mean of uint8 values is exact in fp64 until the
+//                        final division, and a non-integer S/C is >= 1/C away
+//                        from an integer, so trunc(S/C) == S div C.
+//                        One wave per row.
+//  * mask_kernel       — maskDisparity (functions.py:169-172):
+//                        bitwise_and(d, d, mask=carmask) = carmask != 0 ? d : 0,
+//                        with the mask pre-expanded to 0x00 / 0xFF bytes.
+#include "../svx_launch.h"
+
+namespace svx {
+
+__device__ __forceinline__ uint32_t fill4(uint32_t raw, uint32_t prev) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t r = (raw >> (8 * k)) & 0xFF, q = (prev >> (8 * k)) & 0xFF;
+        const uint32_t s = r + q;
+        out |= (r > 2 ? r : (s > 255 ? 255 : s)) << (8 * k);
+    }
+    return out;
+}
+
+constexpr int kFillUnroll = 8;
+
+// words = pixels / 4 per frame; disp may equal out (in place).
+__global__ __launch_bounds__(256) void fill_prev_kernel(const uint32_t* raw, uint32_t* out, uint32_t* masked,
+                                                        const uint32_t* __restrict__ mask, const uint32_t* prev0,
+                                                        int frames, int64_t words) {
+    const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+    if (i >= words) return;
+    uint32_t c = prev0 ? prev0[i] : 0u;
+    bool have = prev0 != nullptr;
+    const uint32_t m = mask ? mask[i] : 0u;
+    for (int f0 = 0; f0 < frames; f0 += kFillUnroll) {
+        uint32_t r[kFillUnroll];
+#pragma unroll
+        for (int u = 0; u < kFillUnroll; ++u)
+            r[u] = f0 + u < frames ? raw[(int64_t)(f0 + u) * words + i] : 0u;
+#pragma unroll
+        for (int u = 0; u < kFillUnroll; ++u) {
+            if (f0 + u >= frames) break;
+            c = have ? fill4(r[u], c) : r[u];
+            have = true;
+            out[(int64_t)(f0 + u) * words + i] = c;
+            if (masked) masked[(int64_t)(f0 + u) * words + i] = c & m;
+        }
+    }
+}
+
+// One wave per row of W bytes (W % 4 == 0); rows = frames * H.
+__global__ __launch_bounds__(256) void fill_mean_kernel(uint8_t* disp, uint8_t* masked, const uint8_t* __restrict__ mask,
+                                                        int64_t rows, int H, int W) {
+    const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int lane = lane_id();
+    uint32_t* rp = reinterpret_cast<uint32_t*>(disp + row * W);
+    const int words = W / 4;
+    uint32_t sum = 0, cnt = 0;
+    for (int w = lane; w < words; w += kWave) {
+        const uint32_t v = rp[w];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t b = (v >> (8 * k)) & 0xFF;
+            sum += b;
+            cnt += b != 0;
+        }
+    }
+    sum = wave_sum(sum);
+    cnt = wave_sum(cnt);
+    const uint32_t mean = cnt ? sum / cnt : 0u;   // numpy: nan mean -> 0.0; uint8 <- trunc(mean)
+    const int64_t mrow = (row % H) * (int64_t)W;
+    uint32_t* mp = masked ? reinterpret_cast<uint32_t*>(masked + row * W) : nullptr;
+    const uint32_t* kp = mask ? reinterpret_cast<const uint32_t*>(mask + mrow) : nullptr;
+    for (int w = lane; w < words; w += kWave) {
+        const uint32_t v = rp[w];
+        uint32_t o = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t b = (v >> (8 * k)) & 0xFF;
+            o |= (b < 2 ? mean : b) << (8 * k);
+        }
+        rp[w] = o;
+        if (mp) mp[w] = o & kp[w];
+    }
+}
+
+__global__ __launch_bounds__(256) void mask_kernel(const uint32_t* disp, uint32_t* out, const uint32_t* __restrict__ mask,
+                                                   int64_t words_per_frame, int64_t total_words) {
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total_words; i += (int64_t)gridDim.x * 256)
+        out[i] = disp[i] & mask[i % words_per_frame];
+}
+
+// Expand a grey mask to 0x00 / 0xFF bytes: bitwise_and(..., mask=m) keeps a pixel iff m != 0.
+__global__ __launch_bounds__(256) void mask_bytes_kernel(const uint8_t* m, uint8_t* out, int64_t n) {
+    const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+    if (i < n) out[i] = m[i] ? 0xFF : 0x00;
+}
+
+hipError_t launch_mask_bytes(const uint8_t* m, uint8_t* out, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mask_bytes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, m, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_prev(const uint8_t* raw, uint8_t* out, uint8_t* masked, const uint8_t* mask_ff,
+                            const uint8_t* prev0, int frames, int64_t frame_px, hipStream_t s) {
+    if (frames <= 0 || frame_px <= 0) return hipSuccess;
+    if (frame_px % 4) return hipErrorInvalidValue;
+    const int64_t words = frame_px / 4;
+    hipLaunchKernelGGL(fill_prev_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const uint32_t*>(raw), reinterpret_cast<uint32_t*>(out),
+                       reinterpret_cast<uint32_t*>(masked), reinterpret_cast<const uint32_t*>(mask_ff),
+                       reinterpret_cast<const uint32_t*>(prev0), frames, words);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_mean(uint8_t* disp, uint8_t* masked, const uint8_t* mask_ff, int frames, int H, int W,
+                            hipStream_t s) {
+    const int64_t rows = (int64_t)frames * H;
+    if (rows <= 0) return hipSuccess;
+    if (W % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fill_mean_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, disp, masked, mask_ff,
+                       rows, H, W);
+    return hipGetLastError();
+}
+
+hipError_t launch_mask(const uint8_t* disp, uint8_t* out, const uint8_t* mask_ff, int frames, int64_t frame_px,
+                       hipStream_t s) {
+    if (frames <= 0 || frame_px <= 0) return hipSuccess;
+    if (frame_px % 4) return hipErrorInvalidValue;
+    const int64_t wpf = frame_px / 4, total = wpf * frames;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(mask_kernel, dim3((unsigned)blocks), dim3(256), 0, s, reinterpret_cast<const uint32_t*>(disp),
+                       reinterpret_cast<uint32_t*>(out), reinterpret_cast<const uint32_t*>(mask_ff), wpf, total);
+    return hipGetLastError();
+}
+
+}  // namespace svx

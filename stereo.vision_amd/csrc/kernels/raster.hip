@@ -1,0 +1,108 @@
+// Road raster + non-zero walk (gfx950), SURVEY §8f rank 2.
+//
+//  * raster_kernel   — generatePointsAsImage (functions.py:339-344): a black
+//                      grey image with 255 at every [x, y] of the int32
+//                      planePoints (stereovision.py:112-113, :136). Python's
+//                      negative indices wrap (img[-1] is the last row); the
+//                      host checks the range first, as numpy would raise.
+//  * nonzero_kernel  — the pixel walk that ends sanitiseRoadImage
+//                      (functions.py:359-365): [j, i] of every non-zero pixel
+//                      in raster order. One workgroup per image; chunks of
+//                      256 lanes x 16 pixels; a block scan orders the lanes and
+//                      a running offset orders the chunks, so the list is
+//                      written once, in order, with no cross-workgroup sync.
+#include "../svx_launch.h"
+
+namespace svx {
+
+// points: frames x cap x 2 int32 (x, y); counts[frame * cstride + cidx] = points of the frame
+__global__ __launch_bounds__(256) void raster_kernel(const int32_t* __restrict__ pts, const int64_t* __restrict__ counts,
+                                                     int cstride, int cidx, int64_t cap, uint8_t* __restrict__ img,
+                                                     int H, int W) {
+    const int frame = blockIdx.y;
+    const int64_t n = counts ? counts[(int64_t)frame * cstride + cidx] : cap;
+    const int2* fp = reinterpret_cast<const int2*>(pts) + (int64_t)frame * cap;
+    uint8_t* fi = img + (int64_t)frame * H * W;
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int2 p = fp[i];
+        const int x = p.x < 0 ? p.x + W : p.x, y = p.y < 0 ? p.y + H : p.y;
+        fi[(int64_t)y * W + x] = 255;
+    }
+}
+
+hipError_t launch_raster(const int32_t* pts, const int64_t* counts, int cstride, int cidx, int64_t cap, uint8_t* img,
+                         int frames, int H, int W, hipStream_t s) {
+    if (frames <= 0 || (int64_t)H * W <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(img, 0, (size_t)frames * H * W, s);
+    if (e != hipSuccess) return e;
+    if (cap <= 0) return hipSuccess;
+    int64_t bx = (cap + 256 * 8 - 1) / (256 * 8);
+    if (bx > 1024) bx = 1024;
+    hipLaunchKernelGGL(raster_kernel, dim3((unsigned)bx, (unsigned)frames), dim3(256), 0, s, pts, counts, cstride, cidx,
+                       cap, img, H, W);
+    return hipGetLastError();
+}
+
+struct NonzeroShared {
+    uint32_t wtot[4];
+};
+
+// img: frames x frame_px u8 (frame_px % 4 == 0); out: frames x cap x 2 int32 ([j, i]); counts[frame]
+__global__ __launch_bounds__(256) void nonzero_kernel(const uint8_t* __restrict__ img, int64_t frame_px, int W,
+                                                      uint64_t W_m40, int32_t* __restrict__ out, int64_t cap,
+                                                      int64_t* __restrict__ counts) {
+    __shared__ NonzeroShared sh;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int frame = blockIdx.x;
+    const uint32_t* fi = reinterpret_cast<const uint32_t*>(img + (int64_t)frame * frame_px);
+    int2* fo = reinterpret_cast<int2*>(out) + (int64_t)frame * cap;
+    const int64_t words = frame_px / 4, vecs = (words + 3) / 4;   // lane = 4 words = 16 pixels
+    uint32_t running = 0;
+    for (int64_t base = 0; base < vecs; base += 256) {
+        const int64_t v = base + tid;
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = 4 * v + k < words ? fi[4 * v + k] : 0u;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t nz = (((w[k] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w[k]) & 0x80808080u;   // bit 7 of each non-zero byte
+            bits |= ((nz >> 7) & 1u) << (4 * k) | ((nz >> 15) & 1u) << (4 * k + 1) |
+                    ((nz >> 23) & 1u) << (4 * k + 2) | ((nz >> 31) & 1u) << (4 * k + 3);
+        }
+        const uint32_t cnt = __builtin_popcount(bits);
+        const uint32_t inc = wave_incl_scan(cnt);
+        if (lane == 63) sh.wtot[wave] = inc;
+        __syncthreads();
+        uint32_t wbase = 0, tot = 0;
+#pragma unroll
+        for (int w4 = 0; w4 < 4; ++w4) {
+            const uint32_t t = sh.wtot[w4];
+            wbase += w4 < wave ? t : 0u;
+            tot += t;
+        }
+        __syncthreads();   // sh.wtot is rewritten next chunk
+        uint32_t o = running + wbase + inc - cnt;
+        const int64_t p0 = v * 16;
+        while (bits) {
+            const int b = __builtin_ctz(bits);
+            bits &= bits - 1;
+            const int64_t p = p0 + b;
+            const int y = fastdiv40((int)p, W_m40);
+            fo[o++] = make_int2((int)(p - (int64_t)y * W), y);
+        }
+        running += tot;
+    }
+    if (tid == 0) counts[frame] = running;
+}
+
+hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
+                          hipStream_t s) {
+    if (frames <= 0) return hipSuccess;
+    if (px % 4 || px >= (1ll << 28) || W <= 0 || W > 4096) return hipErrorInvalidValue;
+    const uint64_t m40 = (((uint64_t)1 << 40) + (uint64_t)W - 1) / (uint64_t)W;
+    hipLaunchKernelGGL(nonzero_kernel, dim3(frames), dim3(256), 0, s, img, px, W, m40, out, cap, counts);
+    return hipGetLastError();
+}
+
+}  // namespace svx

@@ -75,7 +75,7 @@ struct Device {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // drop-in scratch
-    DevBuf disp, bgr, xyz, rgb, ctrl, xy;
+    DevBuf disp, bgr, xyz, rgb, ctrl, xy, aux, aux2;
     Tables tables;
     sv_batch* frame_batch = nullptr;  // cached 1-frame batch for sv_pipeline_frame
 };
@@ -219,6 +219,9 @@ struct sv_batch {
     hipStream_t stream2 = nullptr;   // pipeline offsets kernels (stream B), beside the stage launches
     std::vector<hipEvent_t> sync_ev; // pipeline hand-offs between A and B (timing disabled)
     DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks, ktab;
+    DevBuf mdisp, carmask;      // pre-pass: masked disparity (frames x H x W), 0x00/0xFF mask (H x W)
+    DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
+    bool have_mask = false;
     uint32_t* ktab_err_host = nullptr;   // pinned: keep-table "not an interval" flag
     // pipeline control block (one memset per call): hist | counts | err
     uint32_t* hist = nullptr;
@@ -406,7 +409,8 @@ int sv_batch_destroy(sv_batch* b) {
     if (!b) return SV_OK;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
-    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks, &b->ktab})
+    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks, &b->ktab,
+                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount})
         if (x->p) (void)hipFree(x->p);
     if (b->ktab_err_host) (void)hipHostFree(b->ktab_err_host);
     for (auto& ev : b->ev)
@@ -706,6 +710,235 @@ int sv_pipeline_frame(const uint8_t* disp, const uint8_t* bgr, int H, int W, int
     if (out_pts || out_xyz) {
         int64_t n = 0;
         if (int rc = sv_batch_read_points(b, 0, out_xyz, out_pts, cap, &n)) return rc;
+    }
+    return SV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// disparity pre-pass (functions.py:131-172): host frames, synchronous
+// ---------------------------------------------------------------------------
+namespace {
+// upload an H x W u8 host image into a pitch = round_up(W, 4) device buffer (zero pad)
+int upload_u8(DevBuf& buf, const uint8_t* src, int H, int W, int pitch, hipStream_t s) {
+    HIP_TRY(buf.ensure((size_t)H * pitch));
+    if (pitch != W) HIP_TRY(hipMemsetAsync(buf.p, 0, (size_t)H * pitch, s));
+    HIP_TRY(hipMemcpy2DAsync(buf.p, pitch, src, W, W, H, hipMemcpyHostToDevice, s));
+    return SV_OK;
+}
+int download_u8(uint8_t* dst, const DevBuf& buf, int H, int W, int pitch, hipStream_t s) {
+    HIP_TRY(hipMemcpy2DAsync(dst, W, buf.p, pitch, W, H, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SV_OK;
+}
+}  // namespace
+
+int sv_fill_previous(const uint8_t* disp, const uint8_t* prev, int H, int W, uint8_t* out) {
+    if (!disp || !out || H < 0 || W < 0) return fail(SV_E_ARG, "sv_fill_previous: bad arguments");
+    if ((int64_t)H * W == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    const int pitch = (W + 3) / 4 * 4;
+    if (int rc = upload_u8(d->disp, disp, H, W, pitch, d->stream)) return rc;
+    if (prev)
+        if (int rc = upload_u8(d->aux, prev, H, W, pitch, d->stream)) return rc;
+    HIP_TRY(launch_fill_prev(d->disp.as<uint8_t>(), d->disp.as<uint8_t>(), nullptr, nullptr,
+                             prev ? d->aux.as<uint8_t>() : nullptr, 1, (int64_t)H * pitch, d->stream));
+    return download_u8(out, d->disp, H, W, pitch, d->stream);
+}
+
+int sv_fill_mean(uint8_t* disp, int H, int W) {
+    if (!disp || H < 0 || W < 0) return fail(SV_E_ARG, "sv_fill_mean: bad arguments");
+    if ((int64_t)H * W == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    const int pitch = (W + 3) / 4 * 4;
+    if (int rc = upload_u8(d->disp, disp, H, W, pitch, d->stream)) return rc;
+    HIP_TRY(launch_fill_mean(d->disp.as<uint8_t>(), nullptr, nullptr, 1, H, pitch, d->stream));
+    return download_u8(disp, d->disp, H, W, pitch, d->stream);
+}
+
+int sv_mask_disparity(const uint8_t* disp, const uint8_t* mask, int H, int W, uint8_t* out) {
+    if (!disp || !mask || !out || H < 0 || W < 0) return fail(SV_E_ARG, "sv_mask_disparity: bad arguments");
+    if ((int64_t)H * W == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    const int pitch = (W + 3) / 4 * 4;
+    const int64_t px = (int64_t)H * pitch;
+    if (int rc = upload_u8(d->disp, disp, H, W, pitch, d->stream)) return rc;
+    if (int rc = upload_u8(d->aux, mask, H, W, pitch, d->stream)) return rc;
+    HIP_TRY(d->aux2.ensure((size_t)px));
+    HIP_TRY(launch_mask_bytes(d->aux.as<uint8_t>(), d->aux2.as<uint8_t>(), px, d->stream));
+    HIP_TRY(launch_mask(d->disp.as<uint8_t>(), d->disp.as<uint8_t>(), d->aux2.as<uint8_t>(), 1, px, d->stream));
+    return download_u8(out, d->disp, H, W, pitch, d->stream);
+}
+
+int sv_batch_set_mask(sv_batch* b, const uint8_t* mask) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    HIP_TRY(hipSetDevice(b->device));
+    if (!mask) {
+        b->have_mask = false;
+        return SV_OK;
+    }
+    const int64_t px = (int64_t)b->H * b->W;
+    HIP_TRY(b->carmask.ensure((size_t)px * 2));
+    uint8_t* grey = b->carmask.as<uint8_t>() + px;
+    HIP_TRY(hipMemcpyAsync(grey, mask, (size_t)px, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(launch_mask_bytes(grey, b->carmask.as<uint8_t>(), px, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    b->have_mask = true;
+    return SV_OK;
+}
+
+int sv_batch_prepass(sv_batch* b, int option, const uint8_t* prev0, int sync) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    if (option < 0 || option > 2) return fail(SV_E_ARG, "prepass option must be 0 (none), 1 (previous) or 2 (mean)");
+    HIP_TRY(hipSetDevice(b->device));
+    const int64_t px = (int64_t)b->H * b->W;
+    uint8_t* masked = nullptr;
+    const uint8_t* mff = b->have_mask ? b->carmask.as<uint8_t>() : nullptr;
+    if (b->have_mask) {
+        HIP_TRY(b->mdisp.ensure((size_t)px * b->frames));
+        masked = b->mdisp.as<uint8_t>();
+    }
+    uint8_t* disp = b->disp.as<uint8_t>();
+    if (option == 1) {
+        const uint8_t* p0 = nullptr;
+        if (prev0) {
+            Device* d;
+            if (int rc = dev_get(b->device, &d)) return rc;
+            HIP_TRY(d->aux.ensure((size_t)px));
+            HIP_TRY(hipMemcpyAsync(d->aux.p, prev0, (size_t)px, hipMemcpyHostToDevice, b->stream));
+            p0 = d->aux.as<uint8_t>();
+        }
+        HIP_TRY(launch_fill_prev(disp, disp, masked, mff, p0, b->frames, px, b->stream));
+    } else if (option == 2) {
+        HIP_TRY(launch_fill_mean(disp, masked, mff, b->frames, b->H, b->W, b->stream));
+    } else if (masked) {
+        HIP_TRY(launch_mask(disp, masked, mff, b->frames, px, b->stream));
+    }
+    if (sync || prev0) HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_read_disp(sv_batch* b, int frame, uint8_t* disp, uint8_t* masked) {
+    if (!b || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "bad args");
+    if (masked && !b->mdisp.p) return fail(SV_E_STATE, "no masked disparity (set a mask and run the pre-pass)");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    const size_t px = (size_t)b->H * b->W;
+    if (disp) HIP_TRY(hipMemcpy(disp, b->disp.as<uint8_t>() + px * frame, px, hipMemcpyDeviceToHost));
+    if (masked) HIP_TRY(hipMemcpy(masked, b->mdisp.as<uint8_t>() + px * frame, px, hipMemcpyDeviceToHost));
+    return SV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// road raster + non-zero walk (functions.py:339-344, :359-365)
+// ---------------------------------------------------------------------------
+int sv_road_raster(const int32_t* pts, int64_t n, int H, int W, uint8_t* out_img) {
+    if (n < 0 || H < 0 || W < 0 || !out_img || (n > 0 && !pts)) return fail(SV_E_ARG, "sv_road_raster: bad arguments");
+    for (int64_t i = 0; i < n; ++i) {   // numpy raises IndexError past these; negatives wrap
+        const int32_t x = pts[2 * i], y = pts[2 * i + 1];
+        if (x < -W || x >= W || y < -H || y >= H)
+            return fail(SV_E_ARG, "index out of range: point %lld is [%d, %d] for a %d x %d image", (long long)i, x, y, H, W);
+    }
+    if ((int64_t)H * W == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    HIP_TRY(d->aux.ensure((size_t)H * W));
+    HIP_TRY(d->xy.ensure(sizeof(int32_t) * 2 * (size_t)(n > 0 ? n : 1)));
+    if (n) HIP_TRY(hipMemcpyAsync(d->xy.p, pts, sizeof(int32_t) * 2 * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_raster(d->xy.as<int32_t>(), nullptr, 0, 0, n, d->aux.as<uint8_t>(), 1, H, W, s));
+    HIP_TRY(hipMemcpyAsync(out_img, d->aux.p, (size_t)H * W, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SV_OK;
+}
+
+int sv_nonzero_points(const uint8_t* img, int H, int W, int32_t* out, int64_t cap, int64_t* out_n) {
+    if (!img || !out_n || H < 0 || W < 0 || W > 4096 || (int64_t)H * W >= (1ll << 28))
+        return fail(SV_E_ARG, "sv_nonzero_points: bad arguments (W <= 4096, H*W < 2^28)");
+    *out_n = 0;
+    const int64_t px = (int64_t)H * W;
+    if (px == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    const int64_t padded = (px + 3) / 4 * 4;   // zero tail: no extra non-zero pixels
+    HIP_TRY(d->aux.ensure((size_t)padded));
+    if (padded != px) HIP_TRY(hipMemsetAsync(d->aux.as<uint8_t>() + px, 0, (size_t)(padded - px), s));
+    HIP_TRY(hipMemcpyAsync(d->aux.p, img, (size_t)px, hipMemcpyHostToDevice, s));
+    HIP_TRY(d->xy.ensure(sizeof(int32_t) * 2 * (size_t)px + 64));
+    int64_t* cnt = reinterpret_cast<int64_t*>(d->xy.as<char>() + sizeof(int32_t) * 2 * (size_t)px);
+    HIP_TRY(launch_nonzero(d->aux.as<uint8_t>(), 1, padded, W, d->xy.as<int32_t>(), px, cnt, s));
+    int64_t n = 0;
+    HIP_TRY(hipMemcpyAsync(&n, cnt, sizeof n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (n > cap) return fail(SV_E_CAP, "capacity %lld < %lld non-zero pixels", (long long)cap, (long long)n);
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(out, d->xy.p, sizeof(int32_t) * 2 * n, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    *out_n = n;
+    return SV_OK;
+}
+
+int sv_batch_road_raster(sv_batch* b, int sync) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    if (!b->pts.p) return fail(SV_E_STATE, "no pipeline points (create the batch with points and run the pipeline)");
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t px = (size_t)b->H * b->W;
+    HIP_TRY(b->road.ensure(px * b->frames));
+    HIP_TRY(launch_raster(b->pts.as<int32_t>(), b->counts, 4, 2, (int64_t)b->cap, b->road.as<uint8_t>(), b->frames, b->H,
+                          b->W, b->stream));
+    if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_nonzero(sv_batch* b, int sync) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    if (!b->road.p) return fail(SV_E_STATE, "no road images (sv_batch_road_raster first)");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(b->nz.ensure(sizeof(int32_t) * 2 * b->cap * b->frames));
+    HIP_TRY(b->nzcount.ensure(sizeof(int64_t) * b->frames));
+    HIP_TRY(launch_nonzero(b->road.as<uint8_t>(), b->frames, (int64_t)b->H * b->W, b->W, b->nz.as<int32_t>(),
+                           (int64_t)b->cap, b->nzcount.as<int64_t>(), b->stream));
+    if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int64_t cap, int64_t* n) {
+    if (!b || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "bad args");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    const size_t px = (size_t)b->H * b->W;
+    if (img) {
+        if (!b->road.p) return fail(SV_E_STATE, "no road images");
+        HIP_TRY(hipMemcpy(img, b->road.as<uint8_t>() + px * frame, px, hipMemcpyDeviceToHost));
+    }
+    if (n) {
+        if (!b->nz.p) return fail(SV_E_STATE, "no non-zero walk (sv_batch_nonzero first)");
+        int64_t k = 0;
+        HIP_TRY(hipMemcpy(&k, b->nzcount.as<int64_t>() + frame, sizeof k, hipMemcpyDeviceToHost));
+        *n = k;
+        if (k > cap) return fail(SV_E_CAP, "capacity %lld < %lld", (long long)cap, (long long)k);
+        if (k && nzpts)
+            HIP_TRY(hipMemcpy(nzpts, b->nz.as<int32_t>() + 2 * b->cap * frame, sizeof(int32_t) * 2 * k,
+                              hipMemcpyDeviceToHost));
     }
     return SV_OK;
 }

@@ -43,6 +43,17 @@ SIGNATURES = {
     "sv_backproject": [P, I64, I64, ctypes.POINTER(Camera), P],
     "sv_pipeline_frame": [P, P, I, I, I, ctypes.POINTER(Camera), ctypes.POINTER(Plane), D, I,
                           P, P, P, P, I64],
+    "sv_fill_previous": [P, P, I, I, P],
+    "sv_fill_mean": [P, I, I],
+    "sv_mask_disparity": [P, P, I, I, P],
+    "sv_batch_set_mask": [P, P],
+    "sv_batch_prepass": [P, I, P, I],
+    "sv_batch_read_disp": [P, I, P, P],
+    "sv_road_raster": [P, I64, I, I, P],
+    "sv_nonzero_points": [P, I, I, P, I64, PI64],
+    "sv_batch_road_raster": [P, I],
+    "sv_batch_nonzero": [P, I],
+    "sv_batch_read_road": [P, I, P, P, I64, PI64],
     "sv_batch_create": [I, I, I, I, I, I, I, ctypes.POINTER(P)],
     "sv_batch_destroy": [P],
     "sv_batch_info": [P, P],

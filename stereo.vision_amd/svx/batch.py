@@ -77,6 +77,26 @@ class Batch:
         "resident" (one workgroup per frame). Results are identical."""
         _abi.call("sv_batch_pipeline_mode", self._h, self.PIPE_MODES[mode])
 
+    PREPASS = {"none": 0, "previous": 1, "mean": 2}
+
+    def set_mask(self, mask):
+        """Grey carmask (H x W uint8) for the pre-pass's masked disparity; None clears it."""
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        if m is not None and m.shape != (self.H, self.W):
+            raise ValueError(f"mask shape {m.shape} != {(self.H, self.W)}")
+        _abi.call("sv_batch_set_mask", self._h, _abi.ptr(m))
+
+    def prepass(self, option="previous", prev0=None, sync=True):
+        """stereovision.py:53-76 over the batch's frames in order (see sv_batch_prepass)."""
+        p0 = None if prev0 is None else np.ascontiguousarray(prev0, np.uint8)
+        _abi.call("sv_batch_prepass", self._h, self.PREPASS[option], _abi.ptr(p0), int(sync))
+
+    def read_disp(self, frame, masked=False):
+        d = np.empty((self.H, self.W), np.uint8)
+        m = np.empty((self.H, self.W), np.uint8) if masked else None
+        _abi.call("sv_batch_read_disp", self._h, frame, _abi.ptr(d), _abi.ptr(m))
+        return (d, m) if masked else d
+
     # -- compute -------------------------------------------------------------------
     def project(self, camera=None, sync=True):
         cam = camera or CAMERA
@@ -106,6 +126,24 @@ class Batch:
 
     def reset_timing(self):
         _abi.call("sv_batch_timing_reset", self._h)
+
+    def road_raster(self, sync=True):
+        """generatePointsAsImage of every frame's pipeline points (device)."""
+        _abi.call("sv_batch_road_raster", self._h, int(sync))
+
+    def nonzero(self, sync=True):
+        """Raster-order non-zero walk of every road image (device)."""
+        _abi.call("sv_batch_nonzero", self._h, int(sync))
+
+    def read_road(self, frame, walk=False):
+        img = np.empty((self.H, self.W), np.uint8)
+        if not walk:
+            _abi.call("sv_batch_read_road", self._h, frame, _abi.ptr(img), None, 0, None)
+            return img
+        n = ctypes.c_int64(0)
+        pts = np.empty((self.Ng, 2), np.int32)
+        _abi.call("sv_batch_read_road", self._h, frame, _abi.ptr(img), _abi.ptr(pts), self.Ng, ctypes.byref(n))
+        return img, pts[: n.value]
 
     # -- outputs -------------------------------------------------------------------
     def read_dense(self, frame):

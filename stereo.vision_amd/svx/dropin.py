@@ -21,6 +21,13 @@ reference:
 * ``project3DPointsTo2DImagePoints(points)`` (functions.py:201-209): returns
   an (N, 2) float64 array that ``np.array(.., np.int32).reshape((-1,1,2))``
   (stereovision.py:112-113) accepts, (0, 2) for no points.
+* ``generatePointsAsImage(points)`` (functions.py:339-344): grey road image;
+  ``nonzero_points(img)`` gives sanitiseRoadImage's final pixel walk.
+* disparity pre-pass (functions.py:141-172): ``fillDisparity`` (new array, or
+  the input itself when there is no previous frame), ``fillAltDisparity`` (in
+  place, returns its argument), ``maskDisparity`` (new array; the mask is the
+  installed module's ``carmask``, functions.py:35) and ``capDisparity`` (returns
+  its argument: the reference discards the masked result, functions.py:164-167).
 
 Failures raise ``RuntimeError`` (``SvxError``), which the reference's own
 ``try/except`` at stereovision.py:92-126 handles like any reference error.
@@ -109,11 +116,109 @@ def project3DPointsTo2DImagePoints(points):  # noqa: N802
     return out
 
 
+# ---------------------------------------------------------------------------
+# disparity pre-pass (functions.py:141-172)
+# ---------------------------------------------------------------------------
+def fill_previous(disparity, previous):
+    """Array form of fillDisparity: d > 2 ? d : min(255, d + prev)."""
+    disp = _as_u8(disparity, 2, "disparity")
+    prev = _as_u8(previous, 2, "previousDisparity")
+    if prev.shape != disp.shape:
+        raise ValueError(f"previousDisparity shape {prev.shape} != disparity shape {disp.shape}")
+    out = np.empty_like(disp)
+    _abi.call("sv_fill_previous", _abi.ptr(disp), _abi.ptr(prev), disp.shape[0], disp.shape[1], _abi.ptr(out))
+    return out
+
+
+def fillDisparity(disparity, previousDisparity):  # noqa: N802
+    """functions.py:141-148 on the GPU."""
+    if previousDisparity is None:
+        return disparity
+    return fill_previous(disparity, previousDisparity)
+
+
+def fillAltDisparity(disparity):  # noqa: N802
+    """functions.py:150-162 on the GPU: in place (like the reference), returns its argument."""
+    if not isinstance(disparity, np.ndarray) or disparity.dtype != np.uint8 or disparity.ndim != 2:
+        raise TypeError("fillAltDisparity expects a 2-D uint8 numpy array")
+    work = np.ascontiguousarray(disparity).copy() if not disparity.flags.c_contiguous else disparity
+    _abi.call("sv_fill_mean", _abi.ptr(work), work.shape[0], work.shape[1])
+    if work is not disparity:
+        disparity[...] = work
+    return disparity
+
+
+def mask_disparity(disparity, mask):
+    """Array form of maskDisparity with an explicit grey mask: mask != 0 ? d : 0."""
+    disp = _as_u8(disparity, 2, "disparity")
+    m = _as_u8(mask, 2, "mask")
+    if m.shape != disp.shape:
+        raise ValueError(f"mask shape {m.shape} != disparity shape {disp.shape}")
+    out = np.empty_like(disp)
+    _abi.call("sv_mask_disparity", _abi.ptr(disp), _abi.ptr(m), disp.shape[0], disp.shape[1], _abi.ptr(out))
+    return out
+
+
+def maskDisparity(disparity):  # noqa: N802
+    """functions.py:169-172 on the GPU, with the installed module's carmask."""
+    if _module is None or getattr(_module, "carmask", None) is None:
+        raise RuntimeError("maskDisparity needs the reference's carmask: install(functions) first "
+                           "(or call mask_disparity(disparity, mask))")
+    return mask_disparity(disparity, _module.carmask)
+
+
+def capDisparity(disparity):  # noqa: N802
+    """functions.py:164-167: the reference computes a masked copy and discards it,
+    returning its argument; so does this (no device work)."""
+    return disparity
+
+
+# ---------------------------------------------------------------------------
+# road raster (functions.py:339-344) and the non-zero walk (functions.py:359-365)
+# ---------------------------------------------------------------------------
+def road_raster(points, shape=(544, 1024)):
+    """Array form of generatePointsAsImage: (H, W) uint8, 255 at each [x, y]."""
+    p = np.ascontiguousarray(np.asarray(points).reshape(-1, 2), dtype=np.int32)
+    H, W = shape
+    img = np.empty((H, W), np.uint8)
+    try:
+        _abi.call("sv_road_raster", _abi.ptr(p), len(p), H, W, _abi.ptr(img))
+    except _abi.SvxError as e:
+        if "index out of range" in str(e):
+            raise IndexError(str(e)) from None
+        raise
+    return img
+
+
+def generatePointsAsImage(points):  # noqa: N802
+    """functions.py:339-344 on the GPU: the installed module's blackImg shape (the
+    reference copies that black image), 544 x 1024 otherwise."""
+    black = getattr(_module, "blackImg", None) if _module is not None else None
+    shape = black.shape[:2] if black is not None else (544, 1024)
+    return road_raster(points, shape)
+
+
+def nonzero_points(img):
+    """The pixel walk that ends sanitiseRoadImage (functions.py:359-365):
+    (K, 2) int32 [j, i] of the non-zero pixels in raster order."""
+    im = _as_u8(img, 2, "image")
+    H, W = im.shape
+    out = np.empty((max(H * W, 1), 2), np.int32)
+    n = ctypes.c_int64(0)
+    _abi.call("sv_nonzero_points", _abi.ptr(im), H, W, _abi.ptr(out), H * W, ctypes.byref(n))
+    return out[: n.value]
+
+
 # snake_case names used by BASELINE.json
 project_disparity_to_3d = projectDisparityTo3d
 project_3D_points_to_2D = project3DPointsTo2DImagePoints
 
-PATCHED = ("projectDisparityTo3d", "project3DPointsTo2DImagePoints")
+PATCHED = ("projectDisparityTo3d", "project3DPointsTo2DImagePoints", "fillDisparity", "fillAltDisparity",
+           "maskDisparity", "capDisparity", "generatePointsAsImage")
+ALIASES = {"project_disparity_to_3d": "projectDisparityTo3d",
+           "project_3D_points_to_2D": "project3DPointsTo2DImagePoints"}
+_saved = {}
+_ABSENT = object()
 
 
 def install(functions_module):
@@ -122,13 +227,22 @@ def install(functions_module):
     global _module
     _abi.lib()  # fail loudly now if libsvx is missing
     _module = functions_module
-    for name in PATCHED:
-        setattr(functions_module, name, globals()[name])
-    functions_module.project_disparity_to_3d = projectDisparityTo3d
-    functions_module.project_3D_points_to_2D = project3DPointsTo2DImagePoints
+    for name in PATCHED + tuple(ALIASES):
+        if name not in _saved:
+            _saved[name] = getattr(functions_module, name, _ABSENT)
+        setattr(functions_module, name, globals()[ALIASES.get(name, name)])
     return functions_module
 
 
 def uninstall():
+    """Restore the attributes install() replaced."""
     global _module
+    if _module is not None:
+        for name, fn in _saved.items():
+            if fn is _ABSENT:
+                if hasattr(_module, name):
+                    delattr(_module, name)
+            else:
+                setattr(_module, name, fn)
+    _saved.clear()
     _module = None

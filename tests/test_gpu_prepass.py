@@ -1,0 +1,133 @@
+"""Pre-pass (functions.py:131-172) and road raster / non-zero walk
+(functions.py:339-365) on the GPU against the oracle restatements and the
+reference-run fixtures (tests/golden/prepass.json)."""
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN
+
+sys.path.insert(0, GOLDEN)
+import prepass_inputs  # noqa: E402
+from test_prepass_cpu import carmask  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+META = json.load(open(os.path.join(GOLDEN, "prepass.json")))
+
+
+@pytest.fixture(scope="module")
+def svx_mod():
+    import svx
+    from svx import batch, dropin
+    assert svx.device_count() >= 1
+    return types.SimpleNamespace(svx=svx, batch=batch, dropin=dropin)
+
+
+def test_fill_mean_reference_fixture(svx_mod):
+    for d, ref in zip(prepass_inputs.fill_mean_inputs(oracle.synth_frame), META["fill_mean"]):
+        work = d.copy()
+        out = svx_mod.dropin.fillAltDisparity(work)
+        assert out is work                                   # in place, like the reference
+        assert oracle.digest(out) == ref["out"]
+    strided = prepass_inputs.fill_mean_inputs(oracle.synth_frame)[0][:, ::2].copy()[:, :500]
+    view = np.zeros((544, 1000), np.uint8)[:, ::2]
+    view[...] = strided
+    svx_mod.dropin.fillAltDisparity(view)
+    assert np.array_equal(view, oracle.fill_mean(strided))
+
+
+def test_fill_previous(svx_mod):
+    for d, p in prepass_inputs.fill_prev_inputs():
+        assert np.array_equal(svx_mod.dropin.fillDisparity(d, p), oracle.fill_previous(d, p))
+        assert svx_mod.dropin.fillDisparity(d, None) is d
+
+
+def test_mask_and_cap(svx_mod):
+    m = carmask()
+    d, _ = oracle.synth_frame(9)
+    f = types.SimpleNamespace(carmask=m)
+    svx_mod.dropin.install(f)
+    try:
+        assert np.array_equal(f.maskDisparity(d), oracle.mask_disparity(d, m))
+        assert f.capDisparity(d) is d
+    finally:
+        svx_mod.dropin.uninstall()
+    odd = np.arange(7 * 13, dtype=np.uint8).reshape(7, 13)
+    mo = (np.arange(7 * 13).reshape(7, 13) % 3).astype(np.uint8)
+    assert np.array_equal(svx_mod.dropin.mask_disparity(odd, mo), oracle.mask_disparity(odd, mo))
+
+
+@pytest.mark.parametrize("option", ["previous", "mean", "none"])
+def test_batch_prepass(svx_mod, option):
+    frames, first = 6, 200
+    m = carmask()
+    rng = np.random.default_rng(5)
+    raw = []
+    for f in range(frames):
+        d, _ = oracle.synth_frame(first + f)
+        d = d.copy()
+        d[rng.random(d.shape) < 0.2] = rng.integers(0, 3)
+        raw.append(d)
+    prev0 = rng.integers(0, 256, (544, 1024)).astype(np.uint8)
+    with svx_mod.batch.Batch(frames, with_bgr=False) as b:
+        for f, d in enumerate(raw):
+            b.upload(f, d)
+        b.set_mask(m)
+        b.prepass(option, prev0=prev0 if option == "previous" else None)
+        if option == "previous":
+            ref = oracle.fill_previous_chain(raw, prev0)
+        elif option == "mean":
+            ref = [oracle.fill_mean(d) for d in raw]
+        else:
+            ref = raw
+        for f in range(frames):
+            dc, dm = b.read_disp(f, masked=True)
+            assert np.array_equal(dc, ref[f]), f
+            assert np.array_equal(dm, oracle.mask_disparity(ref[f], m)), f
+    with svx_mod.batch.Batch(3, with_bgr=False) as b:   # no prev0: frame 0 is left as is
+        for f in range(3):
+            b.upload(f, raw[f])
+        b.prepass("previous")
+        ref = oracle.fill_previous_chain(raw[:3])
+        for f in range(3):
+            assert np.array_equal(b.read_disp(f), ref[f])
+
+
+def test_road_raster_reference_fixture(svx_mod, golden):
+    for fid, ref in META["road_raster_step2"].items():
+        m = golden.meta["full_frames_step2"][fid]
+        disp, bgr = oracle.synth_frame(0 if fid == "0r" else int(fid))
+        pp = oracle.pipeline_frame(disp, bgr, 2, abc=np.array(m["abc"]))["pts"].reshape(-1, 1, 2)
+        img = svx_mod.dropin.generatePointsAsImage(pp)
+        assert oracle.digest(img) == ref["image"]
+        nzp = svx_mod.dropin.nonzero_points(img)
+        assert np.array_equal(nzp, oracle.nonzero_points(img))
+    assert svx_mod.dropin.road_raster(np.zeros((0, 1, 2), np.int32)).sum() == 0
+    img = svx_mod.dropin.road_raster(np.array([[[-1, -1]], [[3, 0]]], np.int32), (4, 8))   # numpy wraps negatives
+    assert img[3, 7] == 255 and img[0, 3] == 255 and int((img != 0).sum()) == 2
+    with pytest.raises(IndexError):
+        svx_mod.dropin.road_raster(np.array([[8, 0]], np.int32), (4, 8))
+    odd = (np.random.default_rng(1).random((9, 13)) < 0.3).astype(np.uint8) * 7
+    assert np.array_equal(svx_mod.dropin.nonzero_points(odd), oracle.nonzero_points(odd))
+
+
+@pytest.mark.parametrize("step", [1, 2])
+def test_batch_road_raster_and_walk(svx_mod, step):
+    frames, first = 5, 321
+    with svx_mod.batch.Batch(frames, step=step, with_bgr=True, with_points=True) as b:
+        b.synth(first)
+        b.pipeline()
+        b.road_raster()
+        b.nonzero()
+        for f in range(frames):
+            disp, bgr = oracle.synth_frame(first + f)
+            ref = oracle.pipeline_frame(disp, bgr, step)
+            rimg = oracle.road_raster(ref["pts"])
+            img, walk = b.read_road(f, walk=True)
+            assert np.array_equal(img, rimg)
+            assert np.array_equal(walk, oracle.nonzero_points(rimg))
