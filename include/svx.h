@@ -100,6 +100,26 @@ int sv_road_raster(const int32_t* pts, int64_t n, int H, int W, uint8_t* out_img
  * out = [j, i] (int32) of every non-zero pixel, raster order. W <= 4096. */
 int sv_nonzero_points(const uint8_t* img, int H, int W, int32_t* out, int64_t cap, int64_t* out_n);
 
+/* ---- RANSAC plane fit --------------------------------- */
+
+/* The draws of functions.py:278-298 RANSAC(points, trials), replayed exactly
+ * as CPython's `random` makes them (MT19937, _randbelow, random.sample's pool
+ * and set branches; per trial sample(points, k) then the non-collinear
+ * triple of functions.py:240-260), starting from mt_state = random.getstate()'s
+ * 624 words + index (advanced in place, for random.setstate). pts: n rows of
+ * stride ld >= 3 doubles (X, Y, Z first). Outputs per trial: sidx (k indices),
+ * tri (3 indices). *out_trials = trials, or 0 when n < k (sample raises before
+ * drawing, so no trial runs and the state is untouched). Host only. */
+int sv_ransac_draw(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
+                   int32_t* tri, int* out_trials);
+/* sv_ransac_draw, then every trial on the GPU: out_abc (trials x 3) =
+ * inv([P1;P2;P3]) 1 (functions.py:267), out_err = mean |P.abc - 1| / |abc| over
+ * the trial's sample (functions.py:269-275, :289), out_flag = 0 ok, 1 singular,
+ * 2 ill-conditioned (the caller re-decides flagged trials and the near-best
+ * ones with the reference's own numpy calls). */
+int sv_ransac(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
+              int32_t* tri, double* out_abc, double* out_err, uint8_t* out_flag, int* out_trials);
+
 /* ---- batched, device-resident API ------------- */
 typedef struct sv_batch sv_batch;
 

@@ -1,0 +1,187 @@
+// RANSAC plane fit (functions.py:240-298), SURVEY §8f rank 1.
+//
+// The reference draws from Python's global `random` (unseeded). To be a
+// drop-in whose effect on the program is identical, the draws are replayed
+// exactly: CPython's MT19937 (genrand_uint32), getrandbits(k) = word >> (32-k)
+// for k <= 32, _randbelow_with_getrandbits (rejection on k = n.bit_length()
+// bits) and random.sample's two branches (pool swap for n <= setsize, set
+// rejection otherwise), starting from the caller's random.getstate() and
+// handing the advanced state back. The draw order per trial is the
+// reference's: sample(points, 600) (functions.py:286), then
+// randomNonCollinearPoints' three sample(points, 1) until numpy's cross(P1-P2,
+// P2-P3) is not all zero (functions.py:240-260, products rounded before the
+// subtraction as numpy.cross does). That sequential bookkeeping runs on the
+// host (it needs nothing but integer draws and the 3 points of each attempt).
+//
+// The numeric work — per trial abc = inv([P1;P2;P3]) 1 (functions.py:267),
+// d = |abc| (:269) and the mean distance of the 600 sampled points
+// (:274-275, :289) — is one workgroup per trial on the GPU, in fp64. Trials
+// whose 3x3 system is singular or ill-conditioned are flagged so the caller
+// re-decides them with the reference's own numpy calls (it also re-derives the
+// winner's plane that way, so the plane it returns is bit-identical).
+#include <cmath>
+#include <unordered_set>
+#include <vector>
+
+#include "../svx_launch.h"
+
+namespace svx {
+
+// ---------------------------------------------------------------------------
+// CPython Random (Modules/_randommodule.c + Lib/random.py, 3.10)
+// ---------------------------------------------------------------------------
+struct PyMT {
+    uint32_t mt[624];
+    int index;
+
+    uint32_t genrand() {
+        constexpr uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, A = 0x9908b0dfu;
+        if (index >= 624) {
+            int kk;
+            uint32_t y;
+            for (kk = 0; kk < 624 - 397; kk++) {
+                y = (mt[kk] & UPPER) | (mt[kk + 1] & LOWER);
+                mt[kk] = mt[kk + 397] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+            }
+            for (; kk < 623; kk++) {
+                y = (mt[kk] & UPPER) | (mt[kk + 1] & LOWER);
+                mt[kk] = mt[kk + (397 - 624)] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+            }
+            y = (mt[623] & UPPER) | (mt[0] & LOWER);
+            mt[623] = mt[396] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+            index = 0;
+        }
+        uint32_t y = mt[index++];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        return y;
+    }
+    uint32_t getrandbits(int k) { return k == 0 ? 0u : genrand() >> (32 - k); }   // k <= 32
+    uint32_t randbelow(uint32_t n) {
+        if (!n) return 0;
+        const int k = 32 - __builtin_clz(n);   // n.bit_length()
+        uint32_t r = getrandbits(k);
+        while (r >= n) r = getrandbits(k);
+        return r;
+    }
+};
+
+// random.sample(range(n), k) -> out[0..k). Caller guarantees 0 <= k <= n.
+static void py_sample(PyMT& rng, uint32_t n, int k, int32_t* out, std::vector<uint32_t>& pool,
+                      std::unordered_set<uint32_t>& selected) {
+    int64_t setsize = 21;
+    if (k > 5) setsize += (int64_t)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
+    if ((int64_t)n <= setsize) {
+        pool.resize(n);
+        for (uint32_t i = 0; i < n; ++i) pool[i] = i;
+        for (int i = 0; i < k; ++i) {
+            const uint32_t j = rng.randbelow(n - i);
+            out[i] = (int32_t)pool[j];
+            pool[j] = pool[n - i - 1];
+        }
+    } else {
+        selected.clear();
+        for (int i = 0; i < k; ++i) {
+            uint32_t j = rng.randbelow(n);
+            while (selected.count(j)) j = rng.randbelow(n);
+            selected.insert(j);
+            out[i] = (int32_t)j;
+        }
+    }
+}
+
+// numpy.cross(P1 - P2, P2 - P3) == 0 in every component (functions.py:255-258)
+static bool collinear(const double* p1, const double* p2, const double* p3) {
+    volatile double a0 = p1[0] - p2[0], a1 = p1[1] - p2[1], a2 = p1[2] - p2[2];
+    volatile double b0 = p2[0] - p3[0], b1 = p2[1] - p3[1], b2 = p2[2] - p3[2];
+    volatile double t0 = a1 * b2, u0 = a2 * b1, t1 = a2 * b0, u1 = a0 * b2, t2 = a0 * b1, u2 = a1 * b0;
+    const double c0 = t0 - u0, c1 = t1 - u1, c2 = t2 - u2;
+    return c0 == 0.0 && c1 == 0.0 && c2 == 0.0;
+}
+
+int ransac_draw(uint32_t* state625, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
+                int32_t* tri) {
+    if (n < k || n < 1 || n >= (1ll << 31)) return 0;   // random.sample raises before drawing: no trial runs
+    PyMT rng;
+    for (int i = 0; i < 624; ++i) rng.mt[i] = state625[i];
+    rng.index = (int)state625[624];
+    std::vector<uint32_t> pool;
+    std::unordered_set<uint32_t> selected;
+    selected.reserve(2 * (size_t)k + 16);
+    for (int t = 0; t < trials; ++t) {
+        py_sample(rng, (uint32_t)n, k, sidx + (int64_t)t * k, pool, selected);
+        uint32_t i1, i2, i3;
+        do {   // randomNonCollinearPoints: three sample(points, 1) per attempt
+            i1 = rng.randbelow((uint32_t)n);
+            i2 = rng.randbelow((uint32_t)n);
+            i3 = rng.randbelow((uint32_t)n);
+        } while (collinear(pts + i1 * ld, pts + i2 * ld, pts + i3 * ld));
+        tri[3 * t + 0] = (int32_t)i1;
+        tri[3 * t + 1] = (int32_t)i2;
+        tri[3 * t + 2] = (int32_t)i3;
+    }
+    for (int i = 0; i < 624; ++i) state625[i] = rng.mt[i];
+    state625[624] = (uint32_t)rng.index;
+    return trials;
+}
+
+// ---------------------------------------------------------------------------
+// Trial evaluation: one workgroup per trial.
+// flag: 0 ok, 1 singular (det == 0), 2 ill-conditioned (|det| < 1e-6 |r1||r2||r3|)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ransac_eval_kernel(const double* __restrict__ pts, int64_t ld,
+                                                          const int32_t* __restrict__ sidx,
+                                                          const int32_t* __restrict__ tri, int k,
+                                                          double* __restrict__ abc_out, double* __restrict__ err_out,
+                                                          uint8_t* __restrict__ flag_out) {
+    __shared__ double part[4];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const double* r1 = pts + (int64_t)tri[3 * t + 0] * ld;
+    const double* r2 = pts + (int64_t)tri[3 * t + 1] * ld;
+    const double* r3 = pts + (int64_t)tri[3 * t + 2] * ld;
+    // inv(P) 1 = (r2 x r3 + r3 x r1 + r1 x r2) / det, det = r1 . (r2 x r3)
+    const double c23[3] = {r2[1] * r3[2] - r2[2] * r3[1], r2[2] * r3[0] - r2[0] * r3[2], r2[0] * r3[1] - r2[1] * r3[0]};
+    const double c31[3] = {r3[1] * r1[2] - r3[2] * r1[1], r3[2] * r1[0] - r3[0] * r1[2], r3[0] * r1[1] - r3[1] * r1[0]};
+    const double c12[3] = {r1[1] * r2[2] - r1[2] * r2[1], r1[2] * r2[0] - r1[0] * r2[2], r1[0] * r2[1] - r1[1] * r2[0]};
+    const double det = r1[0] * c23[0] + r1[1] * c23[1] + r1[2] * c23[2];
+    const double a = (c23[0] + c31[0] + c12[0]) / det;
+    const double b = (c23[1] + c31[1] + c12[1]) / det;
+    const double c = (c23[2] + c31[2] + c12[2]) / det;
+    const double nrm = sqrt(a * a + b * b + c * c);
+    const double* sp = nullptr;
+    double s = 0.0;
+    const int32_t* ti = sidx + (int64_t)t * k;
+    for (int j = tid; j < k; j += 256) {
+        sp = pts + (int64_t)ti[j] * ld;
+        s += fabs((sp[0] * a + sp[1] * b + sp[2] * c - 1.0) / nrm);
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+    if (lane_id() == 0) part[tid >> 6] = s;
+    __syncthreads();
+    if (tid == 0) {
+        const double e = (part[0] + part[1] + part[2] + part[3]) / k;
+        const double n1 = sqrt(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
+        const double n2 = sqrt(r2[0] * r2[0] + r2[1] * r2[1] + r2[2] * r2[2]);
+        const double n3 = sqrt(r3[0] * r3[0] + r3[1] * r3[1] + r3[2] * r3[2]);
+        uint8_t fl = 0;
+        if (det == 0.0) fl = 1;
+        else if (!(fabs(det) >= 1e-6 * n1 * n2 * n3) || !isfinite(e)) fl = 2;
+        err_out[t] = e;
+        abc_out[3 * t + 0] = a;
+        abc_out[3 * t + 1] = b;
+        abc_out[3 * t + 2] = c;
+        flag_out[t] = fl;
+    }
+}
+
+hipError_t launch_ransac_eval(const double* pts, int64_t ld, const int32_t* sidx, const int32_t* tri, int trials,
+                              int k, double* abc, double* err, uint8_t* flag, hipStream_t s) {
+    if (trials <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ransac_eval_kernel, dim3(trials), dim3(256), 0, s, pts, ld, sidx, tri, k, abc, err, flag);
+    return hipGetLastError();
+}
+
+}  // namespace svx

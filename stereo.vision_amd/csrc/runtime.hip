@@ -944,6 +944,53 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 }
 
 // ---------------------------------------------------------------------------
+// RANSAC (functions.py:240-298): exact draw replay on the host, trials on the GPU
+// ---------------------------------------------------------------------------
+int sv_ransac_draw(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
+                   int32_t* tri, int* out_trials) {
+    if (!mt_state || !out_trials || trials < 0 || k < 0 || ld < 3 || n < 0 || (n > 0 && !pts) ||
+        (trials > 0 && (!sidx || !tri)))
+        return fail(SV_E_ARG, "sv_ransac_draw: bad arguments");
+    if (mt_state[624] > 624) return fail(SV_E_ARG, "sv_ransac_draw: MT index %u > 624", mt_state[624]);
+    *out_trials = ransac_draw(mt_state, pts, n, ld, trials, k, sidx, tri);
+    return SV_OK;
+}
+
+int sv_ransac(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
+              int32_t* tri, double* out_abc, double* out_err, uint8_t* out_flag, int* out_trials) {
+    if (int rc = sv_ransac_draw(mt_state, pts, n, ld, trials, k, sidx, tri, out_trials)) return rc;
+    const int ran = *out_trials;
+    if (ran == 0) return SV_OK;
+    if (!out_abc || !out_err || !out_flag) return fail(SV_E_ARG, "sv_ransac: null outputs");
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    const size_t pbytes = sizeof(double) * (size_t)n * ld;
+    const size_t ibytes = sizeof(int32_t) * ((size_t)ran * k + 3 * (size_t)ran);
+    const size_t obytes = sizeof(double) * 4 * (size_t)ran + (size_t)ran;
+    HIP_TRY(d->xyz.ensure(pbytes));
+    HIP_TRY(d->aux.ensure(ibytes));
+    HIP_TRY(d->aux2.ensure(obytes));
+    int32_t* dsidx = d->aux.as<int32_t>();
+    int32_t* dtri = dsidx + (size_t)ran * k;
+    double* dabc = d->aux2.as<double>();
+    double* derr = dabc + 3 * (size_t)ran;
+    uint8_t* dflag = reinterpret_cast<uint8_t*>(derr + ran);
+    HIP_TRY(hipMemcpyAsync(d->xyz.p, pts, pbytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dsidx, sidx, sizeof(int32_t) * (size_t)ran * k, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dtri, tri, sizeof(int32_t) * 3 * (size_t)ran, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_ransac_eval(d->xyz.as<double>(), ld, dsidx, dtri, ran, k, dabc, derr, dflag, s));
+    HIP_TRY(hipMemcpyAsync(out_abc, dabc, sizeof(double) * 3 * ran, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_err, derr, sizeof(double) * ran, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_flag, dflag, (size_t)ran, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SV_OK;
+}
+
+// ---------------------------------------------------------------------------
 // verification helpers
 // ---------------------------------------------------------------------------
 int sv_hue_lut(int device, int16_t* out_lut) {

@@ -82,4 +82,14 @@ hipError_t launch_raster(const int32_t* pts, const int64_t* counts, int cstride,
 hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
                           hipStream_t s);
 
+// kernels/ransac.hip -------------------------------------------------------
+// Host: replay CPython's random draws of RANSAC (functions.py:240-298) from a
+// random.getstate() word vector (624 MT words + index; updated in place);
+// returns the number of trials drawn (0 when n < k: sample raises first).
+int ransac_draw(uint32_t* state625, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
+                int32_t* tri);
+// Device: abc, mean distance and a 0/1/2 (ok/singular/ill-conditioned) flag per trial.
+hipError_t launch_ransac_eval(const double* pts, int64_t ld, const int32_t* sidx, const int32_t* tri, int trials,
+                              int k, double* abc, double* err, uint8_t* flag, hipStream_t s);
+
 }  // namespace svx

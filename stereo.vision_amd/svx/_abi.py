@@ -54,6 +54,8 @@ SIGNATURES = {
     "sv_batch_road_raster": [P, I],
     "sv_batch_nonzero": [P, I],
     "sv_batch_read_road": [P, I, P, P, I64, PI64],
+    "sv_ransac_draw": [P, P, I64, I64, I, I, P, P, ctypes.POINTER(I)],
+    "sv_ransac": [P, P, I64, I64, I, I, P, P, P, P, P, ctypes.POINTER(I)],
     "sv_batch_create": [I, I, I, I, I, I, I, ctypes.POINTER(P)],
     "sv_batch_destroy": [P],
     "sv_batch_info": [P, P],

@@ -23,6 +23,8 @@ reference:
   (stereovision.py:112-113) accepts, (0, 2) for no points.
 * ``generatePointsAsImage(points)`` (functions.py:339-344): grey road image;
   ``nonzero_points(img)`` gives sanitiseRoadImage's final pixel walk.
+* ``RANSAC(points, trials)`` (functions.py:278-298): see svx/ransac.py — same
+  draws from the global ``random`` stream, trials on the GPU, same plane bits.
 * disparity pre-pass (functions.py:141-172): ``fillDisparity`` (new array, or
   the input itself when there is no previous frame), ``fillAltDisparity`` (in
   place, returns its argument), ``maskDisparity`` (new array; the mask is the
@@ -213,8 +215,10 @@ def nonzero_points(img):
 project_disparity_to_3d = projectDisparityTo3d
 project_3D_points_to_2D = project3DPointsTo2DImagePoints
 
+from .ransac import RANSAC  # noqa: E402  (functions.py:278-298)
+
 PATCHED = ("projectDisparityTo3d", "project3DPointsTo2DImagePoints", "fillDisparity", "fillAltDisparity",
-           "maskDisparity", "capDisparity", "generatePointsAsImage")
+           "maskDisparity", "capDisparity", "generatePointsAsImage", "RANSAC")
 ALIASES = {"project_disparity_to_3d": "projectDisparityTo3d",
            "project_3D_points_to_2D": "project3DPointsTo2DImagePoints"}
 _saved = {}

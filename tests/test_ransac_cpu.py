@@ -1,0 +1,90 @@
+"""RANSAC (functions.py:240-298): the oracle restatement against the
+reference-run fixtures, and libsvx's host replay of CPython's random draws
+against CPython itself. CPU only (sv_ransac_draw never touches the GPU)."""
+import ctypes
+import hashlib
+import json
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN
+from oracle import ransac as oransac
+from test_prepass_cpu import carmask
+
+sys.path.insert(0, GOLDEN)
+import ransac_inputs  # noqa: E402
+
+FIX = json.load(open(os.path.join(GOLDEN, "ransac.json")))
+
+
+def state_digest():
+    return hashlib.sha256(repr(random.getstate()).encode()).hexdigest()[:16]
+
+
+def bits(abc):
+    return [format(int(v), "016x") for v in np.asarray(abc, np.float64).reshape(3).view(np.uint64)]
+
+
+@pytest.fixture(scope="module")
+def cases():
+    m = carmask()
+    return {name: ransac_inputs.case_points(name, oracle, m) for name in ransac_inputs.CASES}
+
+
+def test_oracle_matches_reference(cases):
+    saved = random.getstate()
+    try:
+        for key, ref in FIX.items():
+            name, seed = key.split("/")
+            random.seed(int(seed))
+            abc, _ = oransac.ransac(cases[name], ref["trials"])
+            assert (None if abc is None else bits(abc)) == ref["abc_bits"], key
+            assert state_digest() == ref["state_after"], key
+    finally:
+        random.setstate(saved)
+
+
+def _draw(state, pts, trials, k):
+    from svx import _abi
+    words = np.array(state[1], dtype=np.uint32)
+    pts = np.ascontiguousarray(pts, np.float64)
+    sidx = np.empty((max(trials, 1), k), np.int32)
+    tri = np.empty((max(trials, 1), 3), np.int32)
+    ran = ctypes.c_int(0)
+    _abi.call("sv_ransac_draw", _abi.ptr(words), _abi.ptr(pts), len(pts), pts.shape[1], trials, k,
+              _abi.ptr(sidx), _abi.ptr(tri), ctypes.byref(ran))
+    return ran.value, sidx[: ran.value], tri[: ran.value], (state[0], tuple(int(v) for v in words), state[2])
+
+
+@pytest.mark.parametrize("n,k,trials,seed", [(26287, 600, 40, 0), (2000, 600, 30, 1), (4117, 600, 5, 2),
+                                             (4118, 600, 5, 3), (700, 600, 10, 4), (64, 5, 50, 5),
+                                             (22, 1, 20, 6), (599, 600, 3, 7), (1 << 20, 600, 3, 8)])
+def test_host_draw_replay_matches_cpython(cases, n, k, trials, seed):
+    """Both random.sample branches (n <= setsize: pool; else set), n a power of
+    two (rejection at half rate), n < k (no draws), and the collinear retries."""
+    rng = np.random.default_rng(seed)
+    pts = rng.normal(0, 10, (n, 3))
+    if n == 700:
+        pts = cases["collinear"]
+    r = random.Random(seed)
+    st0 = r.getstate()
+    ran, sidx, tri, st1 = _draw(st0, pts, trials, k)
+    _, recs = oransac.ransac(pts, trials, k, rng=r)
+    assert ran == len(recs)
+    for t, rec in enumerate(recs):
+        assert list(sidx[t]) == rec["idx"]
+        assert tuple(tri[t]) == rec["tri"]
+    assert st1 == r.getstate()
+
+
+def test_host_draw_rejects_bad_state():
+    from svx import _abi
+    st = list(random.Random(1).getstate()[1])
+    st[624] = 700
+    with pytest.raises(_abi.SvxError):
+        _draw((3, tuple(st), None), np.zeros((10, 3)), 1, 1)
