@@ -75,7 +75,7 @@ def RANSAC(points, trials):  # noqa: N802 (reference signature)
             abc = np.dot(np.linalg.inv(arr[g["tri"][t], :3]), np.ones([3, 1]))
         except Exception:                  # functions.py:294-296 swallows per-trial errors
             continue
-        d = math.sqrt(abc[0] * abc[0] + abc[1] * abc[1] + abc[2] * abc[2])
+        d = math.sqrt((abc[0] * abc[0] + abc[1] * abc[1] + abc[2] * abc[2]).item())
         e = np.mean(abs((np.dot(arr[g["sidx"][t], :3], abc) - 1) / d))
         if e < best_err:
             best, best_err = abc, e

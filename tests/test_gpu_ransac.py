@@ -53,7 +53,8 @@ def test_per_trial_errors_match_oracle(svx_mod, cases):   # noqa: F811
             assert g["flag"][t] != 0
         elif g["flag"][t] == 0:
             assert abs(g["err"][t] - rec["err"]) <= 1e-9 * rec["err"]
-            np.testing.assert_allclose(g["abc"][t], rec["abc"].reshape(3), rtol=1e-9)
+            ref = rec["abc"].reshape(3)
+            np.testing.assert_allclose(g["abc"][t], ref, rtol=0, atol=1e-9 * np.linalg.norm(ref))
 
 
 def test_ransac_installed_and_degenerate(svx_mod, cases):   # noqa: F811
