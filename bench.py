@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the 1-frame latency probe (keeps K1's rocprof average = 4096-frame launches)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the SURVEY §8f component timings")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args()
@@ -96,6 +97,63 @@ def cpu_baseline(budget_s):
                       f"({pts} grid points, {dt:.1f} s): oracle/cpu_loop.py nested loop "
                       f"(functions.py:178-198 semantics)",
             "c_restatement_mpts": pts / dtc / 1e6, "cpu": model}
+
+
+def _timed(b, fn, reps):
+    """mean ms of fn() over reps, HIP-synchronised around the loop (device work on the batch stream)."""
+    fn()
+    b.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    b.sync()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def extras(b, sb, args, device, with_cpu):
+    """SURVEY §8f components on the same resident batch (after the headline runs):
+    road raster + non-zero walk of the pipeline's points, the disparity pre-pass
+    (fillDisparity recurrence + carmask) over the batch, and the RANSAC drop-in
+    on one frame's masked points (600 trials) next to the CPU restatement."""
+    import random
+
+    from svx import ransac
+
+    import oracle
+    from oracle import ransac as oransac
+    ex = {}
+    px = b.frames * H * W
+    n2 = int(b.read_counts()[:, 2].sum())
+    ms = _timed(b, lambda: (b.road_raster(sync=False), b.nonzero(sync=False)), 3)
+    byts = px + 8 * n2 + px + 8 * n2          # raster: zero + point reads (+1 B each); walk: image + [j,i]
+    ex["road_raster_nonzero"] = {"ms_per_batch": round(ms, 3), "approx_GBps": round(byts / ms / 1e6, 1),
+                                 "points": n2, "kernels": "raster_kernel + nonzero_kernel"}
+    mask = np.zeros((H, W), np.uint8)
+    mask[H // 3:, 64:W - 64] = 255            # a carmask-like region (timing only)
+    b.set_mask(mask)
+    ms = _timed(b, lambda: b.prepass("previous", sync=False), 3)
+    ex["prepass_fill_previous_masked"] = {"ms_per_batch": round(ms, 3), "GBps": round(3 * px / ms / 1e6, 1),
+                                          "bytes_per_pixel": 3, "kernel": "fill_prev_kernel"}
+    disp, _ = oracle.synth_frame(0)
+    pts = list(oracle.project(oracle.mask_disparity(disp, mask), None, 2)[0])
+    st = random.getstate()
+    random.seed(0)
+    ransac.RANSAC(pts, 600)
+    t0 = time.perf_counter()
+    for s in range(5):
+        random.seed(s)
+        ransac.RANSAC(pts, 600)
+    gpu_ms = (time.perf_counter() - t0) / 5 * 1e3
+    r = {"points": len(pts), "trials": 600, "ms_per_call": round(gpu_ms, 2),
+         "path": "host CPython-random replay + ransac_eval_kernel + numpy re-decision of the winner"}
+    if with_cpu:
+        t0 = time.perf_counter()
+        random.seed(0)
+        oransac.ransac(np.asarray(pts), 600)
+        r["cpu_restatement_ms_per_call"] = round((time.perf_counter() - t0) * 1e3, 1)
+    random.setstate(st)
+    ex["ransac_dropin"] = r
+    return ex
 
 
 def latency_1frame(sb, step, first, device):
@@ -221,6 +279,9 @@ def main():
             "kernels": "keep_table_kernel (per call) + resident_fused_kernel (one workgroup per frame)"
                        if args.frames >= 512 else "tiled: stage_kernel + offsets_kernel",
         }
+
+    if want_pipe and not args.no_extras:
+        out["extras"] = extras(b, sb, args, local, rank == 0 and world == 1 and not args.no_cpu)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
