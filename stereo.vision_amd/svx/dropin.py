@@ -91,6 +91,45 @@ def project_frame(disparity, rgb=None, step=REFERENCE_STEP, camera=None):
     return xyz[:k], (out_rgb[:k] if out_rgb is not None else None)
 
 
+class PointList(list):
+    """The list of row views projectDisparityTo3d returns, remembering the (N, 3|6)
+    array behind it while the list is unmodified, so later GPU stages (RANSAC,
+    back-projection) skip re-stacking N Python rows. Any list mutation drops it;
+    writes through a row view write the array itself, so they stay consistent."""
+
+    __slots__ = ("_array",)
+
+    def __init__(self, array):
+        super().__init__(array)
+        self._array = array
+
+    def array(self):
+        a = self._array
+        return a if a is not None and len(a) == len(self) else None
+
+    def _drop(name):  # noqa: N805
+        base = getattr(list, name)
+
+        def f(self, *a, **k):
+            self._array = None
+            return base(self, *a, **k)
+        f.__name__ = name
+        return f
+
+    for _n in ("append", "extend", "insert", "remove", "pop", "clear", "sort", "reverse", "__setitem__",
+               "__delitem__", "__iadd__", "__imul__"):
+        locals()[_n] = _drop(_n)
+    del _n, _drop
+
+
+def as_points_array(points):
+    """(N, >=3) float64 C-contiguous array of a point sequence (zero-copy for a PointList)."""
+    if isinstance(points, PointList) and points.array() is not None:
+        return points.array()
+    arr = points if isinstance(points, np.ndarray) else np.asarray(points)
+    return np.ascontiguousarray(arr, dtype=np.float64)
+
+
 def projectDisparityTo3d(disparity, max_disparity, rgb=[]):  # noqa: N802,B006 (reference signature)
     """functions.py:178-198 on the GPU. Returns a list of rows (see module doc)."""
     xyz, rgbs = project_frame(disparity, rgb)
@@ -100,7 +139,7 @@ def projectDisparityTo3d(disparity, max_disparity, rgb=[]):  # noqa: N802,B006 (
         rows = np.empty((len(xyz), 6), np.float64)
         rows[:, :3] = xyz
         rows[:, 3:] = rgbs
-    return list(rows)
+    return PointList(rows)
 
 
 def project3DPointsTo2DImagePoints(points):  # noqa: N802
@@ -108,8 +147,7 @@ def project3DPointsTo2DImagePoints(points):  # noqa: N802
     n = len(points)
     if n == 0:
         return np.zeros((0, 2), np.float64)
-    arr = points if isinstance(points, np.ndarray) else np.asarray(points)
-    arr = np.ascontiguousarray(arr, dtype=np.float64)
+    arr = as_points_array(points)
     if arr.ndim != 2 or arr.shape[1] < 3:
         raise ValueError(f"points must be rows of at least [X, Y, Z], got shape {arr.shape}")
     out = np.empty((n, 2), np.float64)

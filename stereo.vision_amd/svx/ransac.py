@@ -28,11 +28,8 @@ BAND = 1e-6           # GPU error vs numpy: |dE|/E < 1e-7 for |det| >= 1e-6 |r1|
 
 
 def _points_array(points):
-    if isinstance(points, np.ndarray):
-        arr = points
-    else:
-        arr = np.asarray(points)
-    arr = np.ascontiguousarray(arr, dtype=np.float64)
+    from .dropin import as_points_array
+    arr = as_points_array(points)
     if arr.ndim != 2 or arr.shape[1] < 3:
         raise ValueError(f"points must be rows of at least [X, Y, Z], got shape {arr.shape}")
     return arr

@@ -95,3 +95,19 @@ def test_header_cites_reference():
     src = open(HEADER).read()
     for cite in ("functions.py:178-198", "functions.py:201-209", "stereovision.py:84"):
         assert cite in src
+
+
+def test_point_list_tracks_its_array():
+    from svx.dropin import PointList, as_points_array
+    a = np.arange(12, dtype=np.float64).reshape(4, 3)
+    pl = PointList(a)
+    assert isinstance(pl, list) and len(pl) == 4 and as_points_array(pl) is a
+    pl[1][0] = 99.0                       # a write through a row view is a write to the array
+    assert a[1, 0] == 99.0 and as_points_array(pl) is a
+    pl.append(np.zeros(3))
+    assert pl.array() is None and as_points_array(pl).shape == (5, 3)
+    pl2 = PointList(a)
+    del pl2[0]
+    assert pl2.array() is None and np.array_equal(as_points_array(pl2), a[1:])
+    import random
+    assert len(random.Random(0).sample(PointList(a), 2)) == 2
