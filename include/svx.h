@@ -175,6 +175,31 @@ int sv_batch_road_raster(sv_batch* b, int sync);
 int sv_batch_nonzero(sv_batch* b, int sync);
 int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int64_t cap, int64_t* n);
 
+/* Batched RANSAC (stereovision.py:84-94 for every frame):
+ * maskpoints = the fp64 step-2 projection of the batch's disparity under the
+ * mask set by sv_batch_set_mask (functions.py:169-172, :178-198), then
+ * RANSAC(maskpoints, trials) (functions.py:278-298) with the draws CPython
+ * makes after random.seed(seed_base + first_frame + frame) — replayed on the
+ * device, one workgroup per frame. Per frame: abc (the plane), err (its mean
+ * distance), trial (the winning trial, -1 when fewer than k points: the
+ * reference returns (None, None)), flags (1: a trial was singular and
+ * skipped; 2: the winner's 3x3 system is ill-conditioned; 4: the runner-up's
+ * error is within 1e-9 relative — only these frames can differ from numpy's
+ * LAPACK-based choice; 8: every triple drawn in 65,536 attempts was collinear
+ * — the reference never returns there — trial = -1; 16: more than 2^28
+ * draws in one frame, trial = -1). Step-2 grids of
+ * <= 163,840 points; 1 <= k <= 1024. */
+int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame, int trials, int k,
+                    int sync);
+int sv_batch_read_ransac(sv_batch* b, int frame, double* abc, double* err, int32_t* trial, uint32_t* flags);
+int sv_batch_read_maskpoints(sv_batch* b, int frame, double* xyz, int64_t cap, int64_t* n);
+/* Draw-level verification: record the first `trials` trials' drawn indices of
+ * every frame in later sv_batch_ransac calls (0 = off); read one frame's as
+ * trials x (k + 3) int32 (the sample, then P1..P3 of the accepted triple;
+ * -1 where a trial did not run). */
+int sv_batch_ransac_trace(sv_batch* b, int trials);
+int sv_batch_read_ransac_trace(sv_batch* b, int frame, int32_t* out);
+
 int sv_batch_sync(sv_batch* b);
 /* ms of the last sv_batch_project / sv_batch_pipeline, from HIP events
  * recorded on the batch stream around the kernels. which: 0 = project,

@@ -1,0 +1,483 @@
+// Batched RANSAC on the device ("batched-friendly").
+//
+//  * maskpoints_kernel — stereovision.py:85 for every frame of a batch:
+//      projectDisparityTo3d(maskDisparity(disparity), 128) = the fp64 X, Y, Z of
+//      every d > 0 grid point of the masked disparity on the reference's step-2
+//      grid (functions.py:185-193), in raster order, same arithmetic as the
+//      drop-in (bit-identical). One workgroup per frame, running offset.
+//  * ransac_batch_kernel — functions.py:278-298 for every frame, with the
+//      batch RNG contract: frame F draws CPython's stream after
+//      random.seed(seed_base + F). One workgroup per frame:
+//        wave 0 replays the stream: init_by_array seeding (one lane), the
+//          MT19937 twist in ascending 64-word steps (reads before writes, so
+//          the in-place recurrence holds), tempering, and _randbelow /
+//          random.sample consumed 64 draws at a time: a ballot finds the
+//          accepted draws, an LDS bitmap the already-selected indices, and
+//          draws repeated inside one batch are resolved in lane (= stream)
+//          order; then the three sample(points, 1) draws and numpy's
+//          cross-product test (functions.py:240-260), redrawn while collinear;
+//        waves 1-3 evaluate the previous trial meanwhile (abc from the
+//          adjugate in fp64, mean |P.abc - 1| / |abc| over the sample) and
+//          keep the first strict minimum (functions.py:289-293).
+//      The plane is the GPU's fp64 solve of the winning 3x3 system (within
+//      ~1e-15 relative of numpy's LAPACK solve, not bit-identical); frames
+//      whose decision could hinge on that (a singular system, an
+//      ill-conditioned winner, a near-tie) are flagged.
+#include "../svx_launch.h"
+
+namespace svx {
+
+// ---------------------------------------------------------------------------
+// maskpoints: step-2 grid of the (optionally masked) disparity -> fp64 XYZ
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void maskpoints_kernel(const uint8_t* __restrict__ disp,
+                                                         const uint8_t* __restrict__ mask_ff, int64_t frame_px,
+                                                         int H, int W, KParams p, double* __restrict__ out,
+                                                         int64_t cap, int64_t* __restrict__ counts) {
+    __shared__ uint32_t wtot[4];
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int frame = blockIdx.x;
+    const uint8_t* fd = disp + (int64_t)frame * frame_px;
+    double* fo = out + (int64_t)frame * cap * 3;
+    const int Hg = (H - 1 + 1) / 2, Wg = (W - 1 + 1) / 2;   // range(0, H-1, 2) x range(0, W-1, 2)
+    const int64_t ng = (int64_t)Hg * Wg;
+    uint32_t running = 0;
+    for (int64_t base = 0; base < ng; base += 256 * 4) {
+        uint32_t dv[4];
+        int gyv[4], gxv[4];
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = base + 4 * tid + k;
+            dv[k] = 0;
+            gyv[k] = gxv[k] = 0;
+            if (i < ng) {
+                const int gy = (int)(i / Wg), gx = (int)(i - (int64_t)gy * Wg);
+                const int64_t px = (int64_t)(2 * gy) * W + 2 * gx;
+                uint32_t d = fd[px];
+                if (mask_ff) d &= mask_ff[px];
+                dv[k] = d;
+                gyv[k] = gy;
+                gxv[k] = gx;
+                m |= (d != 0) << k;
+            }
+        }
+        const uint32_t cnt = __builtin_popcount(m);
+        const uint32_t inc = wave_incl_scan(cnt);
+        if (lane == 63) wtot[wave] = inc;
+        __syncthreads();
+        uint32_t wbase = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            wbase += w < wave ? wtot[w] : 0u;
+            tot += wtot[w];
+        }
+        __syncthreads();
+        uint32_t o = running + wbase + inc - cnt;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!(m & (1u << k))) continue;
+            const int y = 2 * gyv[k], x = 2 * gxv[k];
+            const double Z = p.fB / (double)dv[k];           // functions.py:191
+            const double X = (((double)x - p.cw) * Z) / p.f;  // :192
+            const double Y = (((double)y - p.ch) * Z) / p.f;  // :193
+            fo[3 * (int64_t)o + 0] = X;
+            fo[3 * (int64_t)o + 1] = Y;
+            fo[3 * (int64_t)o + 2] = Z;
+            ++o;
+        }
+        running += tot;
+    }
+    if (tid == 0) counts[frame] = running;
+}
+
+hipError_t launch_maskpoints(const uint8_t* disp, const uint8_t* mask_ff, int frames, int H, int W, const KParams& p,
+                             double* out, int64_t cap, int64_t* counts, hipStream_t s) {
+    if (frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(maskpoints_kernel, dim3(frames), dim3(256), 0, s, disp, mask_ff, (int64_t)H * W, H, W, p, out,
+                       cap, counts);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// RANSAC, one workgroup per frame
+// ---------------------------------------------------------------------------
+constexpr int kRBMaxK = 1024;          // sample size limit
+constexpr int kRBBitmapWords = 5120;   // 20 KB: the set branch for n <= 163,840 points
+// randomNonCollinearPoints loops for ever on degenerate input (every triple
+// collinear); the kernel gives up after this many attempts in one trial and
+// flags the frame (8) instead of hanging the device
+constexpr int kRBMaxAttempts = 1 << 16;
+// every loop of the replay advances the stream; past this many draws in one
+// frame (240k trials of 600) the frame stops with flag 16, so no input can keep
+// a wave spinning
+constexpr uint32_t kRBMaxDraws = 1u << 28;
+// the pool branch's list shares the bitmap: n <= setsize(k <= 1024) = 21 + 4096 = 4117 < 5120 words
+
+struct RansacShared {
+    uint32_t mt[624];
+    uint32_t tout[2][624];                    // tempered outputs of twists t (slot t & 1)
+    union {
+        uint32_t bitmap[kRBBitmapWords];      // set branch: selected indices of the current sample
+        int32_t pool[kRBBitmapWords];         // pool branch: the shrinking list
+    };
+    int32_t idx[2][kRBMaxK];                  // per trial (double-buffered): the sample
+    double tri[2][12];                        // abc[3], d, flag, then P1..P3 unused (padding)
+    double red[4];
+    uint32_t misc[8];
+};
+static_assert(sizeof(RansacShared) <= 40960, "4 workgroups per CU");
+
+// CPython's init_genrand + init_by_array (Modules/_randommodule.c) for a
+// non-negative seed < 2^64: key = its 32-bit words, little-endian, at least one.
+__device__ void rb_seed(uint32_t* mt, uint64_t seed) {
+    mt[0] = 19650218u;
+    for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    const int klen = (seed >> 32) ? 2 : 1;
+    int i = 1, j = 0;
+    for (int k = 624; k; --k) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+        ++i;
+        ++j;
+        if (i >= 624) {
+            mt[0] = mt[623];
+            i = 1;
+        }
+        if (j >= klen) j = 0;
+    }
+    for (int k = 623; k; --k) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+        ++i;
+        if (i >= 624) {
+            mt[0] = mt[623];
+            i = 1;
+        }
+    }
+    mt[0] = 0x80000000u;
+}
+
+// Wave 0's lanes hand data to each other through LDS with no workgroup
+// barrier. The hardware keeps one wave's LDS operations in order, but the
+// compiler reasons per lane (lane i's store to mt[j] never aliases lane i's
+// load of mt[j - 35]) and may move loads above earlier stores: every hand-off
+// between lanes goes through this point (a compiler memory barrier + LDS wait).
+__device__ __forceinline__ void rb_wave_lds_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t rb_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+// One MT19937 twist of mt (in place, one wave, ascending 64-word steps: every
+// step reads its inputs before writing, which is what the sequential in-place
+// recurrence needs) and its tempered outputs into out.
+__device__ void rb_twist(uint32_t* mt, uint32_t* out) {
+    constexpr uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, A = 0x9908b0dfu;
+    const int lane = lane_id();
+    for (int b = 0; b < 623; b += 64) {
+        const int kk = b + lane;
+        uint32_t nv = 0;
+        if (kk < 623) {
+            const uint32_t y = (mt[kk] & UPPER) | (mt[kk + 1] & LOWER);
+            const uint32_t src = kk < 227 ? mt[kk + 397] : mt[kk - 227];
+            nv = src ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+        }
+        rb_wave_lds_sync();   // every read of this step before any write of it
+        if (kk < 623) mt[kk] = nv;
+        rb_wave_lds_sync();   // later steps read kk - 227 and kk + 1 written here
+    }
+    if (lane == 0) {
+        const uint32_t y = (mt[623] & UPPER) | (mt[0] & LOWER);
+        mt[623] = mt[396] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    }
+    rb_wave_lds_sync();
+    for (int b = 0; b < 624; b += 64) {
+        const int kk = b + lane;
+        if (kk < 624) out[kk] = rb_temper(mt[kk]);
+    }
+    rb_wave_lds_sync();
+}
+
+struct RbStream {   // wave 0's view of the frame's output stream
+    uint32_t pos;     // next unconsumed output
+    uint32_t twists;  // twists generated (outputs [0, 624 * twists) exist)
+};
+
+// make outputs [pos, pos + 64) available (at most one new twist per call)
+__device__ __forceinline__ void rb_ensure(RansacShared& sh, RbStream& st) {
+    while (st.pos + 64 > 624 * st.twists) {
+        rb_twist(sh.mt, sh.tout[st.twists & 1]);
+        ++st.twists;
+    }
+}
+
+__device__ __forceinline__ uint32_t rb_word(const RansacShared& sh, uint32_t q) {
+    return sh.tout[(q / 624) & 1][q % 624];
+}
+
+// numpy.cross(P1 - P2, P2 - P3) all zero (functions.py:255-258); products rounded first
+__device__ __forceinline__ bool rb_collinear(const double* p1, const double* p2, const double* p3) {
+    const double a0 = p1[0] - p2[0], a1 = p1[1] - p2[1], a2 = p1[2] - p2[2];
+    const double b0 = p2[0] - p3[0], b1 = p2[1] - p3[1], b2 = p2[2] - p3[2];
+    const double c0 = a1 * b2 - a2 * b1, c1 = a2 * b0 - a0 * b2, c2 = a0 * b1 - a1 * b0;
+    return c0 == 0.0 && c1 == 0.0 && c2 == 0.0;
+}
+
+// wave 0: k accepted draws of randbelow(n) in stream order -> out[0..m) (m <= 3)
+__device__ void rb_draw_below(RansacShared& sh, RbStream& st, uint32_t n, int kb, int m, uint32_t* out) {
+    const int lane = lane_id();
+    int got = 0;
+    while (got < m && st.pos < kRBMaxDraws) {
+        rb_ensure(sh, st);
+        const uint32_t r = rb_word(sh, st.pos + lane) >> (32 - kb);
+        uint64_t acc = __ballot(r < n);
+        int last = 63;
+        while (acc && got < m) {
+            const int l = __builtin_ctzll(acc);
+            acc &= acc - 1;
+            out[got++] = __shfl(r, l, kWave);
+            last = l;
+        }
+        st.pos += (got == m) ? (uint32_t)(last + 1) : 64u;
+    }
+}
+
+// wave 0: random.sample(range(n), k) into idx (set branch), then clear the bits.
+__device__ void rb_sample_set(RansacShared& sh, RbStream& st, uint32_t n, int kb, int k, int32_t* idx) {
+    const int lane = lane_id();
+    int have = 0;
+    while (have < k && st.pos < kRBMaxDraws) {
+        rb_ensure(sh, st);
+        const uint32_t r = rb_word(sh, st.pos + lane) >> (32 - kb);
+        const bool acc = r < n;
+        const uint32_t bit = 1u << (r & 31);
+        const uint32_t word = acc ? sh.bitmap[r >> 5] : 0u;
+        const bool cand = acc && !(word & bit);
+        // claim the candidates' bits; a candidate whose bit was already set by
+        // this same batch repeats an earlier or later lane's draw
+        const uint32_t old = cand ? atomicOr(&sh.bitmap[r >> 5], bit) : 0u;
+        uint64_t col = __ballot(cand && (old & bit));
+        uint64_t dups = 0;
+        while (col) {   // rare: resolve each repeated value in lane (= stream) order
+            const int l = __builtin_ctzll(col);
+            const uint32_t v = __shfl(r, l, kWave);
+            const uint64_t eq = __ballot(cand && r == v);
+            dups |= eq & (eq - 1);   // all but the lowest lane
+            col &= ~eq;
+        }
+        const bool sel = cand && !((dups >> lane) & 1ull);
+        const uint64_t sm = __ballot(sel);
+        const int need = k - have;
+        int cut = 63;   // the last lane this sample consumes
+        if (__builtin_popcountll(sm) >= need) {
+            uint64_t t = sm;
+            for (int q = 1; q < need; ++q) t &= t - 1;
+            cut = __builtin_ctzll(t);
+        }
+        if (sel) {
+            if (lane <= cut) idx[have + __builtin_popcountll(sm & ((1ull << lane) - 1))] = (int32_t)r;
+            else atomicAnd(&sh.bitmap[r >> 5], ~bit);   // drawn by the next consumer, not this sample
+        }
+        have += __builtin_popcountll(cut == 63 ? sm : sm & ((2ull << cut) - 1));
+        st.pos += (uint32_t)(cut + 1);
+        rb_wave_lds_sync();   // the next batch reads bits set/cleared by other lanes
+    }
+    for (int q = lane; q < have; q += kWave) {
+        const uint32_t r = (uint32_t)idx[q];
+        atomicAnd(&sh.bitmap[r >> 5], ~(1u << (r & 31)));
+    }
+    rb_wave_lds_sync();
+}
+
+// wave 0, lane 0 drives: random.sample(range(n), k), pool branch (n <= setsize)
+__device__ void rb_sample_pool(RansacShared& sh, RbStream& st, uint32_t n, int k, int32_t* idx) {
+    const int lane = lane_id();
+    for (uint32_t q = lane; q < n; q += kWave) sh.pool[q] = (int32_t)q;
+    rb_wave_lds_sync();
+    for (int i = 0; i < k && st.pos < kRBMaxDraws; ++i) {
+        const uint32_t bound = n - (uint32_t)i;
+        const int kb = 32 - __builtin_clz(bound);
+        uint32_t j = 0;
+        rb_draw_below(sh, st, bound, kb, 1, &j);
+        if (lane == 0) {
+            idx[i] = sh.pool[j];
+            sh.pool[j] = sh.pool[n - i - 1];
+        }
+    }
+    rb_wave_lds_sync();   // idx (and the trace) read by every lane next
+}
+
+__global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restrict__ pts, int64_t cap,
+                                                           const int64_t* __restrict__ counts, uint64_t seed_base,
+                                                           int64_t first_frame, int trials, int k,
+                                                           double* __restrict__ out_abc, double* __restrict__ out_err,
+                                                           int32_t* __restrict__ out_trial,
+                                                           uint32_t* __restrict__ out_flags,
+                                                           int32_t* __restrict__ trace, int trace_trials) {
+    __shared__ RansacShared sh;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int frame = blockIdx.x;
+    const int64_t n64 = counts[frame];
+    const double* fp = pts + (int64_t)frame * cap * 3;
+    if (n64 < k || trials <= 0) {   // every trial's random.sample raises: (None, None)
+        if (tid == 0) {
+            out_trial[frame] = -1;
+            out_flags[frame] = 0;
+            out_err[frame] = 0.0;
+            out_abc[3 * frame] = out_abc[3 * frame + 1] = out_abc[3 * frame + 2] = 0.0;
+        }
+        return;
+    }
+    const uint32_t n = (uint32_t)n64;
+    const int kb = 32 - __builtin_clz(n);
+    int64_t setsize = 21;
+    if (k > 5) {
+        int64_t pw = 1;
+        while (pw < 3ll * k) pw *= 4;   // 4 ** ceil(log4(3k)); 3k is never a power of 4
+        setsize += pw;
+    }
+    const bool pool = (int64_t)n <= setsize;
+    for (int q = tid; q < kRBBitmapWords; q += 256) sh.bitmap[q] = 0;
+    if (tid == 0) {
+        sh.misc[0] = 0;
+        rb_seed(sh.mt, seed_base + (uint64_t)(first_frame + frame));
+    }
+    __syncthreads();
+    RbStream st{0, 0};
+    double best = __builtin_huge_val(), second = __builtin_huge_val();
+    int best_t = -1;
+    uint32_t flags = 0;
+    double babc[3] = {0, 0, 0};
+    // step s: wave 0 draws trial s (s < trials), waves 1-3 evaluate trial s - 1
+    for (int s = 0; s <= trials; ++s) {
+        const int buf = s & 1;
+        if (wave == 0 && s < trials) {
+            int32_t* idx = sh.idx[buf];
+            if (pool) rb_sample_pool(sh, st, n, k, idx);
+            else rb_sample_set(sh, st, n, kb, k, idx);
+            uint32_t t3[3] = {0, 0, 0};
+            const double *p1, *p2, *p3;
+            int attempts = 0;
+            bool degenerate = false;
+            do {   // randomNonCollinearPoints
+                if (++attempts > kRBMaxAttempts) {
+                    degenerate = true;
+                    break;
+                }
+                rb_draw_below(sh, st, n, kb, 3, t3);
+                p1 = fp + 3 * (int64_t)t3[0];
+                p2 = fp + 3 * (int64_t)t3[1];
+                p3 = fp + 3 * (int64_t)t3[2];
+            } while (st.pos < kRBMaxDraws && rb_collinear(p1, p2, p3));
+            if (st.pos >= kRBMaxDraws) {
+                if (lane == 0) {
+                    sh.misc[0] = 2;
+                    sh.tri[buf][4] = 1.0;
+                }
+            } else if (degenerate) {
+                if (lane == 0) {
+                    sh.misc[0] = 1;
+                    sh.tri[buf][4] = 1.0;   // nothing to evaluate
+                }
+            } else if (s < trace_trials) {   // the draws themselves, for draw-level parity tests
+                int32_t* tr = trace + ((int64_t)frame * trace_trials + s) * (k + 3);
+                for (int q = lane; q < k; q += kWave) tr[q] = idx[q];
+                if (lane < 3) tr[k + lane] = (int32_t)(lane == 0 ? t3[0] : lane == 1 ? t3[1] : t3[2]);
+            }
+            if (!degenerate && st.pos < kRBMaxDraws && lane == 0) {
+                // inv([P1;P2;P3]) 1 = (r2 x r3 + r3 x r1 + r1 x r2) / det
+                const double* r1 = p1;
+                const double* r2 = p2;
+                const double* r3 = p3;
+                const double c23[3] = {r2[1] * r3[2] - r2[2] * r3[1], r2[2] * r3[0] - r2[0] * r3[2],
+                                       r2[0] * r3[1] - r2[1] * r3[0]};
+                const double c31[3] = {r3[1] * r1[2] - r3[2] * r1[1], r3[2] * r1[0] - r3[0] * r1[2],
+                                       r3[0] * r1[1] - r3[1] * r1[0]};
+                const double c12[3] = {r1[1] * r2[2] - r1[2] * r2[1], r1[2] * r2[0] - r1[0] * r2[2],
+                                       r1[0] * r2[1] - r1[1] * r2[0]};
+                const double det = r1[0] * c23[0] + r1[1] * c23[1] + r1[2] * c23[2];
+                const double a = (c23[0] + c31[0] + c12[0]) / det;
+                const double b = (c23[1] + c31[1] + c12[1]) / det;
+                const double c = (c23[2] + c31[2] + c12[2]) / det;
+                const double n1 = sqrt(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
+                const double n2 = sqrt(r2[0] * r2[0] + r2[1] * r2[1] + r2[2] * r2[2]);
+                const double n3 = sqrt(r3[0] * r3[0] + r3[1] * r3[1] + r3[2] * r3[2]);
+                double fl = 0.0;
+                if (det == 0.0) fl = 1.0;                                 // numpy: LinAlgError, trial skipped
+                else if (!(fabs(det) >= 1e-6 * n1 * n2 * n3)) fl = 2.0;   // ill-conditioned
+                sh.tri[buf][0] = a;
+                sh.tri[buf][1] = b;
+                sh.tri[buf][2] = c;
+                sh.tri[buf][3] = sqrt(a * a + b * b + c * c);
+                sh.tri[buf][4] = fl;
+            }
+        }
+        if (wave != 0 && s > 0) {
+            const int pb = buf ^ 1;
+            const double a = sh.tri[pb][0], b = sh.tri[pb][1], c = sh.tri[pb][2], d = sh.tri[pb][3];
+            const double fl = sh.tri[pb][4];
+            double sum = 0.0;
+            if (fl != 1.0) {
+                for (int j = tid - 64; j < k; j += 192) {
+                    const double* q = fp + 3 * (int64_t)sh.idx[pb][j];
+                    sum += fabs((q[0] * a + q[1] * b + q[2] * c - 1.0) / d);
+                }
+            }
+#pragma unroll
+            for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
+            if (lane == 0) sh.red[wave] = sum;
+        }
+        __syncthreads();
+        if (tid == 64 && s > 0) {   // one lane of wave 1 keeps the decision (trial order, strict <)
+            const int pb = buf ^ 1;
+            const double fl = sh.tri[pb][4];
+            if (fl == 1.0) {
+                flags |= 1u;
+            } else {
+                const double e = (sh.red[1] + sh.red[2] + sh.red[3]) / k;
+                if (e < best) {
+                    second = best;
+                    best = e;
+                    best_t = s - 1;
+                    babc[0] = sh.tri[pb][0];
+                    babc[1] = sh.tri[pb][1];
+                    babc[2] = sh.tri[pb][2];
+                    flags = (flags & ~2u) | (fl == 2.0 ? 2u : 0u);
+                } else if (e < second) {
+                    second = e;
+                }
+            }
+        }
+        __syncthreads();   // sh.idx / sh.tri of this step are reused two steps later
+        if (sh.misc[0]) break;   // uniform: read after the barrier
+    }
+    if (tid == 64) {
+        if (sh.misc[0]) {   // 1: the reference would never return; 2: draw budget
+            best_t = -1;
+            flags |= sh.misc[0] == 1 ? 8u : 16u;
+        }
+        if (best_t >= 0 && second <= best * (1.0 + 1e-9)) flags |= 4u;   // near-tie
+        out_trial[frame] = best_t;
+        out_err[frame] = best;
+        out_flags[frame] = flags;
+        out_abc[3 * frame + 0] = babc[0];
+        out_abc[3 * frame + 1] = babc[1];
+        out_abc[3 * frame + 2] = babc[2];
+    }
+}
+
+hipError_t launch_ransac_batch(const double* pts, int64_t cap, const int64_t* counts, uint64_t seed_base,
+                               int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
+                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, hipStream_t s) {
+    if (frames <= 0) return hipSuccess;
+    if (k < 1 || k > kRBMaxK || cap > (int64_t)kRBBitmapWords * 32) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ransac_batch_kernel, dim3(frames), dim3(256), 0, s, pts, cap, counts, seed_base, first_frame,
+                       trials, k, abc, err, trial, flags, trace, trace ? trace_trials : 0);
+    return hipGetLastError();
+}
+
+}  // namespace svx

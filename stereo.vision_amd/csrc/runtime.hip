@@ -221,6 +221,10 @@ struct sv_batch {
     DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks, ktab;
     DevBuf mdisp, carmask;      // pre-pass: masked disparity (frames x H x W), 0x00/0xFF mask (H x W)
     DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
+    DevBuf mpts, rres;          // maskpoints (frames x mcap x 3 fp64) + counts; batched RANSAC results
+    DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
+    int64_t mcap = 0;
+    int trace_trials = 0, trace_k = 0;
     bool have_mask = false;
     uint32_t* ktab_err_host = nullptr;   // pinned: keep-table "not an interval" flag
     // pipeline control block (one memset per call): hist | counts | err
@@ -410,7 +414,7 @@ int sv_batch_destroy(sv_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks, &b->ktab,
-                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount})
+                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->rres, &b->rtrace})
         if (x->p) (void)hipFree(x->p);
     if (b->ktab_err_host) (void)hipHostFree(b->ktab_err_host);
     for (auto& ev : b->ev)
@@ -940,6 +944,106 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
             HIP_TRY(hipMemcpy(nzpts, b->nz.as<int32_t>() + 2 * b->cap * frame, sizeof(int32_t) * 2 * k,
                               hipMemcpyDeviceToHost));
     }
+    return SV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// batched RANSAC (stereovision.py:85-94 per frame, seeded per frame)
+// ---------------------------------------------------------------------------
+namespace {
+struct RansacRes {   // layout of b->rres
+    double* abc;
+    double* err;
+    int32_t* trial;
+    uint32_t* flags;
+    int64_t* mcount;
+};
+RansacRes ransac_res(sv_batch* b) {
+    RansacRes r;
+    const size_t F = (size_t)b->frames;
+    r.abc = b->rres.as<double>();
+    r.err = r.abc + 3 * F;
+    r.mcount = reinterpret_cast<int64_t*>(r.err + F);
+    r.trial = reinterpret_cast<int32_t*>(r.mcount + F);
+    r.flags = reinterpret_cast<uint32_t*>(r.trial + F);
+    return r;
+}
+}  // namespace
+
+int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame, int trials, int k,
+                    int sync) {
+    if (!b || !cam || trials < 0 || k < 1 || k > 1024 || first_frame < 0)
+        return fail(SV_E_ARG, "sv_batch_ransac: bad arguments (1 <= k <= 1024, trials >= 0)");
+    const int Hg = grid_len(b->H, 2), Wg = grid_len(b->W, 2);
+    const int64_t mcap = (int64_t)Hg * Wg;
+    if (mcap > 163840)
+        return fail(SV_E_ARG, "sv_batch_ransac: %lld step-2 grid points per frame > 163,840 (LDS sample bitmap)",
+                    (long long)mcap);
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t F = (size_t)b->frames;
+    HIP_TRY(b->mpts.ensure(sizeof(double) * 3 * (size_t)(mcap > 0 ? mcap : 1) * F));
+    HIP_TRY(b->rres.ensure(F * (sizeof(double) * 4 + sizeof(int64_t) + sizeof(int32_t) + sizeof(uint32_t))));
+    b->mcap = mcap;
+    const RansacRes r = ransac_res(b);
+    const KParams p = make_params(b->H, b->W, 2, *cam);
+    const uint8_t* mff = b->have_mask ? b->carmask.as<uint8_t>() : nullptr;
+    HIP_TRY(launch_maskpoints(b->disp.as<uint8_t>(), mff, b->frames, b->H, b->W, p, b->mpts.as<double>(), mcap,
+                              r.mcount, b->stream));
+    int32_t* trace = nullptr;
+    if (b->trace_trials > 0) {
+        HIP_TRY(b->rtrace.ensure(sizeof(int32_t) * F * b->trace_trials * (size_t)(k + 3)));
+        HIP_TRY(hipMemsetAsync(b->rtrace.p, 0xff, sizeof(int32_t) * F * b->trace_trials * (size_t)(k + 3), b->stream));
+        trace = b->rtrace.as<int32_t>();
+    }
+    b->trace_k = k;
+    HIP_TRY(launch_ransac_batch(b->mpts.as<double>(), mcap, r.mcount, seed_base, first_frame, b->frames, trials, k,
+                                r.abc, r.err, r.trial, r.flags, trace, b->trace_trials, b->stream));
+    if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_read_ransac(sv_batch* b, int frame, double* abc, double* err, int32_t* trial, uint32_t* flags) {
+    if (!b || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "bad args");
+    if (!b->rres.p) return fail(SV_E_STATE, "no RANSAC results (sv_batch_ransac first)");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    const RansacRes r = ransac_res(b);
+    if (abc) HIP_TRY(hipMemcpy(abc, r.abc + 3 * frame, 3 * sizeof(double), hipMemcpyDeviceToHost));
+    if (err) HIP_TRY(hipMemcpy(err, r.err + frame, sizeof(double), hipMemcpyDeviceToHost));
+    if (trial) HIP_TRY(hipMemcpy(trial, r.trial + frame, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (flags) HIP_TRY(hipMemcpy(flags, r.flags + frame, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return SV_OK;
+}
+
+int sv_batch_ransac_trace(sv_batch* b, int trials) {
+    if (!b || trials < 0) return fail(SV_E_ARG, "bad args");
+    b->trace_trials = trials;
+    return SV_OK;
+}
+
+int sv_batch_read_ransac_trace(sv_batch* b, int frame, int32_t* out) {
+    if (!b || frame < 0 || frame >= b->frames || !out) return fail(SV_E_ARG, "bad args");
+    if (!b->trace_trials || !b->rtrace.p) return fail(SV_E_STATE, "no trace (sv_batch_ransac_trace, then sv_batch_ransac)");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    const size_t per = (size_t)b->trace_trials * (b->trace_k + 3);
+    HIP_TRY(hipMemcpy(out, b->rtrace.as<int32_t>() + per * frame, sizeof(int32_t) * per, hipMemcpyDeviceToHost));
+    return SV_OK;
+}
+
+int sv_batch_read_maskpoints(sv_batch* b, int frame, double* xyz, int64_t cap, int64_t* n) {
+    if (!b || frame < 0 || frame >= b->frames || !n) return fail(SV_E_ARG, "bad args");
+    if (!b->rres.p) return fail(SV_E_STATE, "no maskpoints (sv_batch_ransac first)");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    const RansacRes r = ransac_res(b);
+    int64_t k = 0;
+    HIP_TRY(hipMemcpy(&k, r.mcount + frame, sizeof k, hipMemcpyDeviceToHost));
+    *n = k;
+    if (k > cap) return fail(SV_E_CAP, "capacity %lld < %lld", (long long)cap, (long long)k);
+    if (k && xyz)
+        HIP_TRY(hipMemcpy(xyz, b->mpts.as<double>() + 3 * (size_t)b->mcap * frame, sizeof(double) * 3 * k,
+                          hipMemcpyDeviceToHost));
     return SV_OK;
 }
 

@@ -56,6 +56,11 @@ SIGNATURES = {
     "sv_batch_read_road": [P, I, P, P, I64, PI64],
     "sv_ransac_draw": [P, P, I64, I64, I, I, P, P, ctypes.POINTER(I)],
     "sv_ransac": [P, P, I64, I64, I, I, P, P, P, P, P, ctypes.POINTER(I)],
+    "sv_batch_ransac": [P, ctypes.POINTER(Camera), ctypes.c_uint64, I64, I, I, I],
+    "sv_batch_read_ransac": [P, I, P, P, P, P],
+    "sv_batch_read_maskpoints": [P, I, P, I64, PI64],
+    "sv_batch_ransac_trace": [P, I],
+    "sv_batch_read_ransac_trace": [P, I, P],
     "sv_batch_create": [I, I, I, I, I, I, I, ctypes.POINTER(P)],
     "sv_batch_destroy": [P],
     "sv_batch_info": [P, P],

@@ -145,6 +145,42 @@ class Batch:
         _abi.call("sv_batch_read_road", self._h, frame, _abi.ptr(img), _abi.ptr(pts), self.Ng, ctypes.byref(n))
         return img, pts[: n.value]
 
+    def ransac(self, seed_base, trials, k=600, first_frame=0, camera=None, sync=True):
+        """RANSAC(maskpoints, trials) of every frame on the device (stereovision.py:84-94), frame F
+        drawing what CPython draws after random.seed(seed_base + first_frame + F)."""
+        cam = camera or CAMERA
+        _abi.call("sv_batch_ransac", self._h, ctypes.byref(cam), int(seed_base), int(first_frame), int(trials),
+                  int(k), int(sync))
+
+    def read_ransac(self, frame):
+        """dict(abc (3,) float64, err, trial (-1: none ran), flags) of one frame."""
+        abc = np.empty(3, np.float64)
+        err = ctypes.c_double(0)
+        trial = ctypes.c_int32(0)
+        flags = ctypes.c_uint32(0)
+        _abi.call("sv_batch_read_ransac", self._h, frame, _abi.ptr(abc), ctypes.byref(err), ctypes.byref(trial),
+                  ctypes.byref(flags))
+        return dict(abc=abc, err=float(err.value), trial=int(trial.value), flags=int(flags.value))
+
+    def ransac_trace(self, trials):
+        """Record the first `trials` trials' drawn indices per frame in later ransac() calls."""
+        self._trace = int(trials)
+        _abi.call("sv_batch_ransac_trace", self._h, int(trials))
+
+    def read_ransac_trace(self, frame, k=600):
+        """(trials, k + 3) int32: each traced trial's sample indices, then P1..P3."""
+        out = np.empty((self._trace, k + 3), np.int32)
+        _abi.call("sv_batch_read_ransac_trace", self._h, frame, _abi.ptr(out))
+        return out
+
+    def read_maskpoints(self, frame):
+        """The frame's maskpoints (n x 3 float64, raster order) as the batched RANSAC saw them."""
+        cap = (self.H // 2) * (self.W // 2)
+        xyz = np.empty((max(cap, 1), 3), np.float64)
+        n = ctypes.c_int64(0)
+        _abi.call("sv_batch_read_maskpoints", self._h, frame, _abi.ptr(xyz), cap, ctypes.byref(n))
+        return xyz[: n.value]
+
     # -- outputs -------------------------------------------------------------------
     def read_dense(self, frame):
         shape = (self.Hg, self.pitch)

@@ -1,0 +1,178 @@
+"""Batched on-device RANSAC (sv_batch_ransac): per frame, maskpoints =
+projectDisparityTo3d(maskDisparity(d), 128) (stereovision.py:85) and
+RANSAC(maskpoints, trials) (functions.py:278-298) with the draws CPython makes
+after random.seed(seed_base + frame). Checked against the reference-run
+fixtures (tests/golden/ransac.json: the reference's RANSAC on synthetic frame
+0/1's maskpoints under seeds 0, 1, 12345, 7) and against the oracle
+restatement driven by random.Random(seed) for many frames, both branches of
+random.sample, two-word seeds, k != 600 and n < k.
+
+Tolerance: the plane is the GPU's fp64 adjugate solve, numpy's is LAPACK's LU:
+abc within 1e-12 relative of the reference's (far below the 1e-5 contract);
+the winning trial index identical unless the frame is flagged (ill-conditioned
+winner or a near-tie, flags 2 | 4), where the winner's error must be within
+1e-9 relative of the reference's best."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import ransac as oransac
+from test_prepass_cpu import carmask
+from test_ransac_cpu import FIX
+
+pytestmark = pytest.mark.gpu
+
+H, W = 544, 1024
+
+
+@pytest.fixture(scope="module")
+def svb():
+    import svx
+    from svx import batch
+    assert svx.device_count() >= 1
+    return batch
+
+
+def _abc_from_bits(b):
+    return np.array([int(x, 16) for x in b], np.uint64).view(np.float64)
+
+
+def _oracle_frame(pts, trials, seed, k=600):
+    r = random.Random(seed)
+    best, recs = oransac.ransac(pts, trials, k=k, rng=r)
+    errs = [rec.get("err") for rec in recs]
+    if best is None:
+        return None, -1, None
+    cand = [(e, t) for t, e in enumerate(errs) if e is not None]
+    e, t = min(cand)   # first strict minimum == min over (err, index)
+    return best.reshape(3), t, e
+
+
+def _check(res, ref_abc, ref_t, ref_e, what):
+    if ref_abc is None:
+        assert res["trial"] == -1, what
+        return
+    if res["flags"] & 6:   # ill-conditioned winner / near-tie: any trial within the band is a valid winner
+        assert res["err"] <= ref_e * (1 + 1e-9) + 1e-300, (what, res, ref_e)
+        return
+    assert res["trial"] == ref_t, what
+    assert abs(res["err"] - ref_e) <= 1e-9 * ref_e, what
+    np.testing.assert_allclose(res["abc"], ref_abc, rtol=0, atol=1e-12 * np.linalg.norm(ref_abc), err_msg=what)
+
+
+def _check_draws(b, frame, pts, seed, trials, k=600):
+    tr = b.read_ransac_trace(frame, k)
+    _, recs = oransac.ransac(pts, trials, k=k, rng=random.Random(seed))
+    for t, rec in enumerate(recs[: len(tr)]):
+        got = list(tr[t, :k])
+        if got != rec["idx"]:
+            j = next(i for i in range(k) if got[i] != rec["idx"][i])
+            raise AssertionError(f"frame {frame} trial {t}: sample differs first at {j}: "
+                                 f"{got[max(0, j - 2):j + 3]} vs {rec['idx'][max(0, j - 2):j + 3]}")
+        assert tuple(tr[t, k:]) == rec["tri"], (frame, t, tuple(tr[t, k:]), rec["tri"])
+
+
+def test_batch_draws_match_cpython(svb):
+    """The drawn indices themselves (trial samples and triples) equal CPython's."""
+    m = carmask()
+    with svb.Batch(2, H=H, W=W, step=2, with_bgr=False) as b:
+        b.synth(0)
+        b.set_mask(m)
+        b.ransac_trace(4)
+        b.ransac(seed_base=0, trials=4)
+        for f in range(2):
+            _check_draws(b, f, b.read_maskpoints(f), f, 4)
+
+
+def test_batch_matches_reference_fixtures(svb):
+    m = carmask()
+    with svb.Batch(2, H=H, W=W, step=2, with_bgr=False) as b:
+        b.synth(0)
+        b.set_mask(m)
+        for key, ref in FIX.items():
+            name, seed = key.split("/")
+            if name not in ("frame0", "frame1"):
+                continue
+            frame = int(name[-1])
+            b.ransac(seed_base=int(seed) - frame, trials=ref["trials"])
+            res = b.read_ransac(frame)
+            assert res["trial"] >= 0 and not (res["flags"] & 6), (key, res)
+            ref_abc = _abc_from_bits(ref["abc_bits"])
+            np.testing.assert_allclose(res["abc"], ref_abc, rtol=0, atol=1e-12 * np.linalg.norm(ref_abc),
+                                       err_msg=key)
+
+
+def test_batch_maskpoints_bit_exact(svb):
+    m = carmask()
+    with svb.Batch(3, H=H, W=W, step=1, with_bgr=False) as b:
+        b.synth(5)
+        b.set_mask(m)
+        b.ransac(seed_base=0, trials=1)
+        for f in range(3):
+            d, _ = oracle.synth_frame(5 + f)
+            ref, _ = oracle.project(oracle.mask_disparity(d, m), None, 2)
+            got = b.read_maskpoints(f)
+            assert got.shape == ref.shape and np.array_equal(got.view(np.uint64), ref.view(np.uint64)), f
+
+
+def test_batch_many_frames_vs_oracle(svb):
+    m = carmask()
+    frames, trials, base = 6, 40, 1000
+    with svb.Batch(frames, H=H, W=W, step=2, with_bgr=False) as b:
+        b.synth(20)
+        b.set_mask(m)
+        b.ransac(seed_base=base, trials=trials, first_frame=20)
+        for f in range(frames):
+            pts = b.read_maskpoints(f)
+            ref = _oracle_frame(pts, trials, base + 20 + f)
+            _check(b.read_ransac(f), *ref, what=f"frame {f}")
+
+
+def _sparse_frame(n, seed):
+    """A disparity whose step-2 grid holds exactly n non-zero points at random places."""
+    rng = np.random.default_rng(seed)
+    hg, wg = H // 2, W // 2
+    cells = rng.choice(hg * wg, n, replace=False)
+    d = np.zeros((H, W), np.uint8)
+    d[2 * (cells // wg), 2 * (cells % wg)] = rng.integers(1, 256, n)
+    return d
+
+
+@pytest.mark.parametrize("ns,k,seed_base", [
+    ((3000, 4117, 4118, 4500), 600, 7),      # pool branch (n <= 4117), set branch with many repeats
+    ((599, 600, 601, 20000), 600, 2**32 + 3),   # n < k (no trial), n == k, two-word seeds
+    ((20, 21, 22, 300), 5, 11),             # k <= 5: setsize 21
+    ((50, 3, 4, 9), 1, 2**40),              # k = 1 (n = 3: collinear redraws of repeated points)
+])
+def test_batch_sample_branches(svb, ns, k, seed_base):
+    trials = 25
+    with svb.Batch(len(ns), H=H, W=W, step=2, with_bgr=False) as b:
+        for f, n in enumerate(ns):
+            b.upload(f, _sparse_frame(n, 100 + n + f))
+        b.set_mask(None)
+        b.ransac(seed_base=seed_base, trials=trials, k=k)
+        for f, n in enumerate(ns):
+            pts = b.read_maskpoints(f)
+            assert len(pts) == n
+            ref = _oracle_frame(pts, trials, seed_base + f, k=k)
+            _check(b.read_ransac(f), *ref, what=f"n={n} k={k}")
+
+
+def test_batch_degenerate_frame_gives_up(svb):
+    """All maskpoints on one line: the reference loops for ever in
+    randomNonCollinearPoints; the kernel stops, flags the frame (8) and the
+    other frames of the batch are unaffected."""
+    line = np.zeros((H, W), np.uint8)
+    line[100, 0:1000:2] = 50                 # one grid row, one disparity: collinear
+    good = _sparse_frame(5000, 3)
+    with svb.Batch(2, H=H, W=W, step=2, with_bgr=False) as b:
+        b.upload(0, line)
+        b.upload(1, good)
+        b.set_mask(None)
+        b.ransac(seed_base=0, trials=3, k=100)
+        r0 = b.read_ransac(0)
+        assert r0["trial"] == -1 and r0["flags"] & 8
+        ref = _oracle_frame(b.read_maskpoints(1), 3, 1, k=100)
+        _check(b.read_ransac(1), *ref, what="good frame")
