@@ -150,6 +150,16 @@ int sv_batch_project(sv_batch* b, const sv_camera* cam, int sync);
 int sv_batch_pipeline(sv_batch* b, const sv_camera* cam, const sv_plane* plane,
                       double point_thr, int hist_thr, int chunk, int sync);
 
+/* The pipeline with every frame's own plane: the plane the last
+ * sv_batch_ransac found for it (stereovision.py:94-113 per frame). A frame
+ * without a plane (trial -1: the reference's plane step raises) keeps no
+ * points. Tiled kernels (the frame-resident family takes one plane per call).
+ * sv_batch_read_frame_plane: a, b, c and |abc| (-1 without a plane) as the
+ * kernels use them. */
+int sv_batch_pipeline_planes(sv_batch* b, const sv_camera* cam, double point_thr, int hist_thr, int chunk,
+                             int sync);
+int sv_batch_read_frame_plane(sv_batch* b, int frame, double* out4);
+
 /* Pipeline kernel family: 0 = auto (frame-resident for >= 512 frames when the
  * frame fits, else tiled), 1 = tiled (tiles of 4096 points across workgroups,
  * offsets kernel between the passes), 2 = frame-resident (one workgroup per

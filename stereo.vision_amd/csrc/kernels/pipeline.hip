@@ -116,10 +116,17 @@ static_assert(sizeof(PipeShared) < 8192, "LDS budget");
 // ---------------------------------------------------------------------------
 // pass 1 tile
 // ---------------------------------------------------------------------------
-template <int STEP>
+template <int STEP, bool PF>
 __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int tile, int tiles,
-                                          const KParams& p, PipeShared& sh) {
+                                          const KParams& p0, PipeShared& sh) {
     const int tid = threadIdx.x;
+    KParams p = p0;
+    bool live = true;
+    if constexpr (PF) {   // this frame's plane (uniform: scalar loads)
+        const FramePlane fpl = bf.planes[frame];
+        apply_plane(p, fpl);
+        live = fpl.valid != 0;
+    }
     const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
     const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
     int gy[kQPT], q[kQPT];
@@ -143,7 +150,7 @@ __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int 
         for (int k = 0; k < 4; ++k) {
             const int gx = 4 * q[i] + k;
             nv += (in[i].d[k] != 0 && gx < p.Wg) ? 1u : 0u;
-            if (point_keep1<STEP>(in[i].d[k], gx, y, yc, p)) {
+            if (live && point_keep1<STEP>(in[i].d[k], gx, y, yc, p)) {
                 keep |= 1u << (4 * i + k);
                 const int bin = (p.ablate & 1) ? 0 : point_bin<STEP>(in[i], k);
                 if (!(p.ablate & 2)) atomicAdd(&sh.hist[bin], 1u);
@@ -429,7 +436,7 @@ union StageShared {
     CompactShared p2;
 };
 
-template <int STEP>
+template <int STEP, bool PF>
 __global__ __launch_bounds__(256) void stage_kernel(PipeBuffers bf, int p2_frame0, int n2, int p1_frame0,
                                                     int n1, int tiles, KParams p) {
     __shared__ StageShared sh;
@@ -450,7 +457,7 @@ __global__ __launch_bounds__(256) void stage_kernel(PipeBuffers bf, int p2_frame
     if (role == 2) {
         if (!(p.ablate & 256)) compact_tile<STEP>(bf, p2_frame0 + fl, t, tiles, p, sh.p2);
     } else {
-        if (!(p.ablate & 128)) hist_tile<STEP>(bf, p1_frame0 + fl, t, tiles, p, sh.p1);
+        if (!(p.ablate & 128)) hist_tile<STEP, PF>(bf, p1_frame0 + fl, t, tiles, p, sh.p1);
     }
 }
 
@@ -477,10 +484,9 @@ hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, i
         if (has2) e = hipStreamWaitEvent(sa, ev[2 * c2 + 1], 0);
         if (e != hipSuccess) break;
         const dim3 grid((n2 + n1) * tiles);
-        if (p.step == 1)
-            hipLaunchKernelGGL(stage_kernel<1>, grid, blk, 0, sa, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
-        else
-            hipLaunchKernelGGL(stage_kernel<2>, grid, blk, 0, sa, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
+        const auto kern = b.planes ? (p.step == 1 ? stage_kernel<1, true> : stage_kernel<2, true>)
+                                   : (p.step == 1 ? stage_kernel<1, false> : stage_kernel<2, false>);
+        hipLaunchKernelGGL(kern, grid, blk, 0, sa, b, f2, n2 * tiles, f1, n1 * tiles, tiles, p);
         if (!has1) continue;
         e = hipEventRecord(ev[2 * c], sa);
         if (e == hipSuccess) e = hipStreamWaitEvent(sb, ev[2 * c], 0);

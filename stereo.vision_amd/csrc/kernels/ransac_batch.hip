@@ -480,4 +480,26 @@ hipError_t launch_ransac_batch(const double* pts, int64_t cap, const int64_t* co
     return hipGetLastError();
 }
 
+// keep1 plane fields of every frame (plane_fields, as the host's set_plane)
+__global__ void frame_planes_kernel(const double* __restrict__ abc, const int32_t* __restrict__ trial, int frames,
+                                    double f, FramePlane* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= frames) return;
+    FramePlane o;
+    if (trial[i] >= 0) {
+        plane_fields(o, abc[3 * i], abc[3 * i + 1], abc[3 * i + 2], f);
+    } else {
+        plane_fields(o, 0.0, 0.0, 0.0, f);
+        o.valid = 0;
+    }
+    out[i] = o;
+}
+
+hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, double f, FramePlane* out,
+                               hipStream_t s) {
+    if (frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(frame_planes_kernel, dim3((frames + 255) / 256), dim3(256), 0, s, abc, trial, frames, f, out);
+    return hipGetLastError();
+}
+
 }  // namespace svx

@@ -122,21 +122,11 @@ KParams make_params(int H, int W, int step, const sv_camera& cam) {
 }
 
 void set_plane(KParams& p, const sv_plane& pl, double thr, int hist_thr) {
-    p.a = pl.a;
-    p.b = pl.b;
-    p.c = pl.c;
-    p.nrm = std::sqrt(pl.a * pl.a + pl.b * pl.b + pl.c * pl.c);  // functions.py:307
+    FramePlane fp;
+    plane_fields(fp, pl.a, pl.b, pl.c, p.f);
+    apply_plane(p, fp);
     p.thr = thr;
-    p.a32 = (float)pl.a;
-    p.b32 = (float)pl.b;
-    p.c32 = (float)pl.c;
     p.thr32 = (float)thr;
-    p.inv_nrm32 = (float)(1.0 / p.nrm);
-    p.guard32 = (float)(std::ldexp(1.0, -18) / p.nrm);
-    if (!std::isfinite(p.guard32)) p.guard32 = INFINITY;  // degenerate plane: always exact path
-    p.abs_a32 = (float)std::fabs(pl.a);
-    p.abs_b32 = (float)std::fabs(pl.b);
-    p.abs_cf32 = (float)(std::fabs(pl.c) * p.f);
     // keep1_lean constants. u = B*(a*(x-cw) + b*(y-ch) + c*f) = al*x + bb*y + b0.
     // fp32 error of e = |u - d| - t*d is <= 2^-21 * M with
     // M = 2*U + 255*(1+t) + 255, U = |al|*W + |bb|*H + |b0| (derivation in
@@ -223,6 +213,7 @@ struct sv_batch {
     DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
     DevBuf mpts, rres;          // maskpoints (frames x mcap x 3 fp64) + counts; batched RANSAC results
     DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
+    DevBuf fplanes;             // per-frame keep1 plane fields (FramePlane) for sv_batch_pipeline_planes
     int64_t mcap = 0;
     int trace_trials = 0, trace_k = 0;
     bool have_mask = false;
@@ -414,7 +405,7 @@ int sv_batch_destroy(sv_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks, &b->ktab,
-                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->rres, &b->rtrace})
+                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->rres, &b->rtrace, &b->fplanes})
         if (x->p) (void)hipFree(x->p);
     if (b->ktab_err_host) (void)hipHostFree(b->ktab_err_host);
     for (auto& ev : b->ev)
@@ -494,8 +485,28 @@ int sv_batch_project(sv_batch* b, const sv_camera* cam, int sync) {
     return SV_OK;
 }
 
+namespace {
+struct RansacRes {   // layout of b->rres
+    double* abc;
+    double* err;
+    int32_t* trial;
+    uint32_t* flags;
+    int64_t* mcount;
+};
+RansacRes ransac_res(sv_batch* b) {
+    RansacRes r;
+    const size_t F = (size_t)b->frames;
+    r.abc = b->rres.as<double>();
+    r.err = r.abc + 3 * F;
+    r.mcount = reinterpret_cast<int64_t*>(r.err + F);
+    r.trial = reinterpret_cast<int32_t*>(r.mcount + F);
+    r.flags = reinterpret_cast<uint32_t*>(r.trial + F);
+    return r;
+}
+}  // namespace
+
 static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane* plane, double point_thr,
-                               int hist_thr, int chunk, int sync, Device* d) {
+                               int hist_thr, int chunk, int sync, Device* d, const FramePlane* planes = nullptr) {
     if (!b->with_bgr) return fail(SV_E_ARG, "pipeline needs a batch created with bgr");
     KParams p = make_params(b->H, b->W, b->step, *cam);
     if (p.Wg > 4096 || p.Hg > 4096) return fail(SV_E_ARG, "pipeline supports grids up to 4096 x 4096");
@@ -525,7 +536,8 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     bf.dxbits = d->tables.dx.as<uint32_t>();
     bf.dybits = d->tables.dy.as<uint32_t>();
     bf.cap = (int64_t)cap;
-    int mode = b->pipe_mode;
+    bf.planes = planes;
+    int mode = planes ? 1 : b->pipe_mode;   // the resident kernels take one plane (its keep table) per call
     if (mode == 0) mode = (b->frames >= kResidentMinFrames && resident_supported(p)) ? 2 : 1;
     if (mode >= 2 && !resident_supported(p))
         return fail(SV_E_ARG, "frame-resident pipeline: frame too large (grid %d x %d)", p.Hg, p.Wg);
@@ -576,6 +588,34 @@ int sv_batch_pipeline(sv_batch* b, const sv_camera* cam, const sv_plane* plane, 
     Device* d;
     if (int rc = dev_get(b->device, &d)) return rc;
     return batch_pipeline_impl(b, cam, plane, point_thr, hist_thr, chunk, sync, d);
+}
+
+int sv_batch_pipeline_planes(sv_batch* b, const sv_camera* cam, double point_thr, int hist_thr, int chunk,
+                             int sync) {
+    if (!b || !cam) return fail(SV_E_ARG, "null");
+    if (!b->rres.p) return fail(SV_E_STATE, "no per-frame planes (sv_batch_ransac first)");
+    Device* d;
+    if (int rc = dev_get(b->device, &d)) return rc;
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(b->fplanes.ensure(sizeof(FramePlane) * (size_t)b->frames));
+    const RansacRes r = ransac_res(b);
+    HIP_TRY(launch_frame_planes(r.abc, r.trial, b->frames, cam->f, b->fplanes.as<FramePlane>(), b->stream));
+    const sv_plane none{0.0, 0.0, 0.0};   // per-frame planes replace it
+    return batch_pipeline_impl(b, cam, &none, point_thr, hist_thr, chunk, sync, d, b->fplanes.as<FramePlane>());
+}
+
+int sv_batch_read_frame_plane(sv_batch* b, int frame, double* out4) {
+    if (!b || frame < 0 || frame >= b->frames || !out4) return fail(SV_E_ARG, "bad args");
+    if (!b->fplanes.p) return fail(SV_E_STATE, "no per-frame planes (sv_batch_pipeline_planes first)");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    FramePlane fp;
+    HIP_TRY(hipMemcpy(&fp, b->fplanes.as<FramePlane>() + frame, sizeof fp, hipMemcpyDeviceToHost));
+    out4[0] = fp.a;
+    out4[1] = fp.b;
+    out4[2] = fp.c;
+    out4[3] = fp.valid ? fp.nrm : -1.0;
+    return SV_OK;
 }
 
 int sv_batch_pipeline_mode(sv_batch* b, int mode) {
@@ -950,25 +990,6 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 // ---------------------------------------------------------------------------
 // batched RANSAC (stereovision.py:85-94 per frame, seeded per frame)
 // ---------------------------------------------------------------------------
-namespace {
-struct RansacRes {   // layout of b->rres
-    double* abc;
-    double* err;
-    int32_t* trial;
-    uint32_t* flags;
-    int64_t* mcount;
-};
-RansacRes ransac_res(sv_batch* b) {
-    RansacRes r;
-    const size_t F = (size_t)b->frames;
-    r.abc = b->rres.as<double>();
-    r.err = r.abc + 3 * F;
-    r.mcount = reinterpret_cast<int64_t*>(r.err + F);
-    r.trial = reinterpret_cast<int32_t*>(r.mcount + F);
-    r.flags = reinterpret_cast<uint32_t*>(r.trial + F);
-    return r;
-}
-}  // namespace
 
 int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame, int trials, int k,
                     int sync) {

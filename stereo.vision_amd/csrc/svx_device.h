@@ -41,6 +41,48 @@ struct KParams {
     int ablate;                            // DIAGNOSTIC ONLY (env SVX_ABLATE): skip work, results invalid
 };
 
+// The plane-dependent fields of KParams used by keep1 (tiled pipeline), for
+// one frame of the per-frame-plane pipeline (planes from the batched RANSAC).
+// plane_fields is the single definition, shared by the host's set_plane and
+// the device's per-frame kernel, so both give the same bits.
+struct FramePlane {
+    double a, b, c, nrm;
+    float a32, b32, c32, inv_nrm32, guard32, abs_a32, abs_b32, abs_cf32;
+    uint32_t valid;   // 0: RANSAC found no plane (the reference's plane step raises: no points)
+};
+
+__host__ __device__ inline void plane_fields(FramePlane& o, double a, double b, double c, double f) {
+    o.a = a;
+    o.b = b;
+    o.c = c;
+    o.nrm = __builtin_sqrt(a * a + b * b + c * c);   // functions.py:307 (correctly rounded, host and device)
+    o.a32 = (float)a;
+    o.b32 = (float)b;
+    o.c32 = (float)c;
+    o.inv_nrm32 = (float)(1.0 / o.nrm);
+    o.guard32 = (float)(0x1p-18 / o.nrm);
+    if (!__builtin_isfinite(o.guard32)) o.guard32 = __builtin_inff();   // degenerate plane: always the exact path
+    o.abs_a32 = (float)__builtin_fabs(a);
+    o.abs_b32 = (float)__builtin_fabs(b);
+    o.abs_cf32 = (float)(__builtin_fabs(c) * f);
+    o.valid = 1;
+}
+
+__host__ __device__ inline void apply_plane(KParams& p, const FramePlane& o) {
+    p.a = o.a;
+    p.b = o.b;
+    p.c = o.c;
+    p.nrm = o.nrm;
+    p.a32 = o.a32;
+    p.b32 = o.b32;
+    p.c32 = o.c32;
+    p.inv_nrm32 = o.inv_nrm32;
+    p.guard32 = o.guard32;
+    p.abs_a32 = o.abs_a32;
+    p.abs_b32 = o.abs_b32;
+    p.abs_cf32 = o.abs_cf32;
+}
+
 // ---------------------------------------------------------------------------
 // Hue bin: integer bin k <-> reference key str(round(colorsys hue, 3)).
 // exact rational t = 1000*n/(6*rng) (n in [0, 6 rng)); fp64 only on exact ties.

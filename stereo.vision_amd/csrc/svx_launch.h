@@ -43,6 +43,7 @@ struct PipeBuffers {
     const uint32_t* dxbits;
     const uint32_t* dybits;
     int64_t cap;         // points per frame (Ng)
+    const FramePlane* planes = nullptr;   // per-frame planes (tiled kernels), or the KParams plane
 };
 int pipeline_tiles_per_frame(const KParams& p);
 // The whole chain for frames [0, frames) in chunks: chunks + 2 fused stage
@@ -101,8 +102,11 @@ hipError_t launch_maskpoints(const uint8_t* disp, const uint8_t* mask_ff, int fr
 // abc (frames x 3), err, winning trial (-1: none ran), flags (1 a singular
 // trial, 2 ill-conditioned winner, 4 near-tie). cap <= 163,840, k <= 1024.
 // trace (optional): frames x trace_trials x (k + 3) drawn indices (sample, then P1..P3).
+// frame_planes: the keep1 plane fields of every frame from its RANSAC result.
 hipError_t launch_ransac_batch(const double* pts, int64_t cap, const int64_t* counts, uint64_t seed_base,
                                int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
                                int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, hipStream_t s);
+hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, double f, FramePlane* out,
+                               hipStream_t s);
 
 }  // namespace svx

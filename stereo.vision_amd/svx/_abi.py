@@ -70,6 +70,8 @@ SIGNATURES = {
     "sv_batch_project": [P, ctypes.POINTER(Camera), I],
     "sv_batch_pipeline": [P, ctypes.POINTER(Camera), ctypes.POINTER(Plane), D, I, I, I],
     "sv_batch_pipeline_mode": [P, I],
+    "sv_batch_pipeline_planes": [P, ctypes.POINTER(Camera), D, I, I, I],
+    "sv_batch_read_frame_plane": [P, I, P],
     "sv_batch_sync": [P],
     "sv_batch_last_ms": [P, I, PF],
     "sv_batch_timing": [P, I, ctypes.POINTER(D), PI64],

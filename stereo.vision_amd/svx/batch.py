@@ -108,6 +108,18 @@ class Batch:
         _abi.call("sv_batch_pipeline", self._h, ctypes.byref(cam), ctypes.byref(pl), float(point_thr),
                   int(hist_thr), int(chunk), int(sync))
 
+    def pipeline_planes(self, point_thr=0.05, hist_thr=10, camera=None, chunk=0, sync=True):
+        """The pipeline with each frame's own RANSAC plane (after ransac()); no plane -> no points."""
+        cam = camera or CAMERA
+        _abi.call("sv_batch_pipeline_planes", self._h, ctypes.byref(cam), float(point_thr), int(hist_thr),
+                  int(chunk), int(sync))
+
+    def read_frame_plane(self, frame):
+        """(a, b, c, |abc|) of the frame's plane as the kernels use it; |abc| = -1 without a plane."""
+        out = np.empty(4, np.float64)
+        _abi.call("sv_batch_read_frame_plane", self._h, frame, _abi.ptr(out))
+        return out
+
     def sync(self):
         _abi.call("sv_batch_sync", self._h)
 

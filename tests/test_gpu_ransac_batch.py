@@ -176,3 +176,38 @@ def test_batch_degenerate_frame_gives_up(svb):
         assert r0["trial"] == -1 and r0["flags"] & 8
         ref = _oracle_frame(b.read_maskpoints(1), 3, 1, k=100)
         _check(b.read_ransac(1), *ref, what="good frame")
+
+
+def test_pipeline_with_frame_planes(svb):
+    """stereovision.py:84-113 per frame on the device: RANSAC's plane of each
+    frame drives that frame's threshold / histogram / compaction. Each frame's
+    output equals the oracle chain run with that frame's plane; a frame with
+    no plane keeps nothing (the reference's plane step raises)."""
+    m = carmask()
+    frames = 4
+    sparse = _sparse_frame(300, 9)   # 300 points: fewer than 600 -> no plane
+    with svb.Batch(frames, H=H, W=W, step=2, with_bgr=True, with_points=True) as b:
+        b.synth(30)
+        _, bgr3 = oracle.synth_frame(33)
+        b.upload(3, sparse, bgr3)
+        b.set_mask(m)
+        b.ransac(seed_base=5, trials=60)
+        b.pipeline_planes()
+        counts = b.read_counts()
+        for f in range(frames):
+            res = b.read_ransac(f)
+            fp = b.read_frame_plane(f)
+            disp, bgr = (sparse, bgr3) if f == 3 else oracle.synth_frame(30 + f)
+            if f == 3:
+                assert res["trial"] == -1 and fp[3] == -1.0
+                assert tuple(counts[f][1:3]) == (0, 0)
+                continue
+            a, bb, c = res["abc"]
+            assert np.array_equal(fp[:3], res["abc"])
+            assert fp[3] == np.sqrt(a * a + bb * bb + c * c)       # device sqrt == the reference's math.sqrt
+            ref = oracle.pipeline_frame(disp, bgr, 2, abc=res["abc"])
+            xyz, pts = b.read_points(f)
+            assert tuple(int(v) for v in counts[f][:3]) == ref["counts"], f
+            assert np.array_equal(b.read_hist(f)[:1000], ref["hist"][:1000]), f
+            assert np.array_equal(pts, ref["pts"]), f
+            np.testing.assert_allclose(xyz, ref["xyz2"], rtol=1e-5, atol=0)
