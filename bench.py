@@ -113,8 +113,9 @@ def _timed(b, fn, reps):
 def extras(b, sb, args, device, with_cpu):
     """SURVEY §8f components on the same resident batch (after the headline runs):
     road raster + non-zero walk of the pipeline's points, the disparity pre-pass
-    (fillDisparity recurrence + carmask) over the batch, and the RANSAC drop-in
-    on one frame's masked points (600 trials) next to the CPU restatement."""
+    (fillDisparity recurrence + carmask) over the batch, the RANSAC drop-in
+    on one frame's masked points (600 trials) next to the CPU restatement, the
+    batched RANSAC of every frame and the pipeline driven by those planes."""
     import random
 
     from svx import ransac
@@ -153,6 +154,19 @@ def extras(b, sb, args, device, with_cpu):
         r["cpu_restatement_ms_per_call"] = round((time.perf_counter() - t0) * 1e3, 1)
     random.setstate(st)
     ex["ransac_dropin"] = r
+    # batched RANSAC of every frame (maskpoints + seeded CPython-random replay on the device), then the
+    # pipeline driven by each frame's own plane: stereovision.py:84-113 for the whole batch
+    ms = _timed(b, lambda: b.ransac(seed_base=0, trials=600, sync=False), 2)
+    rb = {"frames": b.frames, "trials": 600, "ms_per_batch": round(ms, 2),
+          "us_per_frame": round(ms / b.frames * 1e3, 2), "kernels": "maskpoints_kernel + ransac_batch_kernel",
+          "rng": "random.seed(frame) per frame"}
+    if "cpu_restatement_ms_per_call" in r:
+        rb["cpu_restatement_ms_per_frame"] = r["cpu_restatement_ms_per_call"]
+    ex["ransac_batch"] = rb
+    ms = _timed(b, lambda: b.pipeline_planes(sync=False), 3)
+    ex["pipeline_frame_planes"] = {"ms_per_batch": round(ms, 3), "frames": b.frames,
+                                   "kept_points": int(b.read_counts()[:, 2].sum()),
+                                   "kernels": "frame_planes_kernel + stage_kernel<PF> + offsets_kernel"}
     return ex
 
 
