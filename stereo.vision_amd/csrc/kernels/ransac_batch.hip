@@ -246,30 +246,45 @@ __device__ void rb_draw_below(RansacShared& sh, RbStream& st, uint32_t n, int kb
     }
 }
 
+// outputs [pos, pos + span) available, span <= 128 (two twist slots suffice)
+__device__ __forceinline__ void rb_ensure_span(RansacShared& sh, RbStream& st, uint32_t span) {
+    while (st.pos + span > 624 * st.twists) {
+        rb_twist(sh.mt, sh.tout[st.twists & 1]);
+        ++st.twists;
+    }
+}
+
 // wave 0: random.sample(range(n), k) into idx (set branch), then clear the bits.
+// One LDS round trip per 64 draws: atomicOr claims each accepted draw's bit and
+// its return says whether the bit was already set. A set bit means either an
+// index selected by an earlier batch (rejected) or a value drawn twice in this
+// batch; those (rare) values are resolved by ballots: if some lane saw the bit
+// clear, the value is new and its lowest lane (earliest draw) wins, otherwise it
+// was selected before and every lane drawing it is rejected. The next window is
+// read while this one is processed.
 __device__ void rb_sample_set(RansacShared& sh, RbStream& st, uint32_t n, int kb, int k, int32_t* idx) {
     const int lane = lane_id();
     int have = 0;
+    rb_ensure_span(sh, st, 128);
+    uint32_t w = rb_word(sh, st.pos + lane);
     while (have < k && st.pos < kRBMaxDraws) {
-        rb_ensure(sh, st);
-        const uint32_t r = rb_word(sh, st.pos + lane) >> (32 - kb);
+        const uint32_t wn = rb_word(sh, st.pos + 64 + lane);   // the next window, in flight
+        const uint32_t r = w >> (32 - kb);
         const bool acc = r < n;
         const uint32_t bit = 1u << (r & 31);
-        const uint32_t word = acc ? sh.bitmap[r >> 5] : 0u;
-        const bool cand = acc && !(word & bit);
-        // claim the candidates' bits; a candidate whose bit was already set by
-        // this same batch repeats an earlier or later lane's draw
-        const uint32_t old = cand ? atomicOr(&sh.bitmap[r >> 5], bit) : 0u;
-        uint64_t col = __ballot(cand && (old & bit));
-        uint64_t dups = 0;
-        while (col) {   // rare: resolve each repeated value in lane (= stream) order
-            const int l = __builtin_ctzll(col);
+        const uint32_t old = acc ? atomicOr(&sh.bitmap[r >> 5], bit) : 0u;
+        const bool hit = acc && (old & bit);
+        uint64_t hm = __ballot(hit);
+        uint64_t rej = hm;
+        while (hm) {   // rare
+            const int l = __builtin_ctzll(hm);
             const uint32_t v = __shfl(r, l, kWave);
-            const uint64_t eq = __ballot(cand && r == v);
-            dups |= eq & (eq - 1);   // all but the lowest lane
-            col &= ~eq;
+            const uint64_t eq = __ballot(acc && r == v);
+            const uint64_t fresh = __ballot(acc && r == v && !(old & bit));
+            hm &= ~eq;
+            rej = fresh ? ((rej & ~eq) | (eq & (eq - 1))) : (rej | eq);
         }
-        const bool sel = cand && !((dups >> lane) & 1ull);
+        const bool sel = acc && !((rej >> lane) & 1ull);
         const uint64_t sm = __ballot(sel);
         const int need = k - have;
         int cut = 63;   // the last lane this sample consumes
@@ -285,6 +300,10 @@ __device__ void rb_sample_set(RansacShared& sh, RbStream& st, uint32_t n, int kb
         have += __builtin_popcountll(cut == 63 ? sm : sm & ((2ull << cut) - 1));
         st.pos += (uint32_t)(cut + 1);
         rb_wave_lds_sync();   // the next batch reads bits set/cleared by other lanes
+        if (have < k) {       // the whole window was consumed: wn is the next one
+            w = wn;
+            rb_ensure_span(sh, st, 128);
+        }
     }
     for (int q = lane; q < have; q += kWave) {
         const uint32_t r = (uint32_t)idx[q];
@@ -317,7 +336,8 @@ __global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restr
                                                            double* __restrict__ out_abc, double* __restrict__ out_err,
                                                            int32_t* __restrict__ out_trial,
                                                            uint32_t* __restrict__ out_flags,
-                                                           int32_t* __restrict__ trace, int trace_trials) {
+                                                           int32_t* __restrict__ trace, int trace_trials,
+                                                           int ablate) {
     __shared__ RansacShared sh;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.x;
@@ -355,7 +375,7 @@ __global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restr
     // step s: wave 0 draws trial s (s < trials), waves 1-3 evaluate trial s - 1
     for (int s = 0; s <= trials; ++s) {
         const int buf = s & 1;
-        if (wave == 0 && s < trials) {
+        if (wave == 0 && s < trials && !((ablate & 2) && s >= 2)) {   // DIAGNOSTIC 2: draw 2 trials only
             int32_t* idx = sh.idx[buf];
             if (pool) rb_sample_pool(sh, st, n, k, idx);
             else rb_sample_set(sh, st, n, kb, k, idx);
@@ -416,15 +436,25 @@ __global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restr
                 sh.tri[buf][4] = fl;
             }
         }
-        if (wave != 0 && s > 0) {
+        if (wave != 0 && s > 0 && !(ablate & 1)) {   // DIAGNOSTIC 1: no evaluation
             const int pb = buf ^ 1;
             const double a = sh.tri[pb][0], b = sh.tri[pb][1], c = sh.tri[pb][2], d = sh.tri[pb][3];
             const double fl = sh.tri[pb][4];
             double sum = 0.0;
-            if (fl != 1.0) {
-                for (int j = tid - 64; j < k; j += 192) {
-                    const double* q = fp + 3 * (int64_t)sh.idx[pb][j];
-                    sum += fabs((q[0] * a + q[1] * b + q[2] * c - 1.0) / d);
+            if (fl != 1.0) {   // 4 points per lane per step, every gather in flight before the arithmetic
+                for (int j0 = tid - 64; j0 < k; j0 += 4 * 192) {
+                    double qx[4], qy[4], qz[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int j = j0 + 192 * u;
+                        const double* q = fp + 3 * (int64_t)(j < k ? sh.idx[pb][j] : 0);
+                        qx[u] = q[0];
+                        qy[u] = q[1];
+                        qz[u] = q[2];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (j0 + 192 * u < k) sum += fabs((qx[u] * a + qy[u] * b + qz[u] * c - 1.0) / d);
                 }
             }
 #pragma unroll
@@ -472,11 +502,12 @@ __global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restr
 
 hipError_t launch_ransac_batch(const double* pts, int64_t cap, const int64_t* counts, uint64_t seed_base,
                                int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
-                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, hipStream_t s) {
+                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, int ablate,
+                               hipStream_t s) {
     if (frames <= 0) return hipSuccess;
     if (k < 1 || k > kRBMaxK || cap > (int64_t)kRBBitmapWords * 32) return hipErrorInvalidValue;
     hipLaunchKernelGGL(ransac_batch_kernel, dim3(frames), dim3(256), 0, s, pts, cap, counts, seed_base, first_frame,
-                       trials, k, abc, err, trial, flags, trace, trace ? trace_trials : 0);
+                       trials, k, abc, err, trial, flags, trace, trace ? trace_trials : 0, ablate);
     return hipGetLastError();
 }
 

@@ -991,6 +991,13 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 // batched RANSAC (stereovision.py:85-94 per frame, seeded per frame)
 // ---------------------------------------------------------------------------
 
+// DIAGNOSTIC ONLY (env SVX_RANSAC_ABLATE, documented in DESIGN.md): 1 skips the trial evaluation,
+// 2 draws only the first two trials; results are invalid.
+static int ransac_ablate() {
+    const char* e = std::getenv("SVX_RANSAC_ABLATE");
+    return e ? std::atoi(e) : 0;
+}
+
 int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame, int trials, int k,
                     int sync) {
     if (!b || !cam || trials < 0 || k < 1 || k > 1024 || first_frame < 0)
@@ -1018,7 +1025,7 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
     }
     b->trace_k = k;
     HIP_TRY(launch_ransac_batch(b->mpts.as<double>(), mcap, r.mcount, seed_base, first_frame, b->frames, trials, k,
-                                r.abc, r.err, r.trial, r.flags, trace, b->trace_trials, b->stream));
+                                r.abc, r.err, r.trial, r.flags, trace, b->trace_trials, ransac_ablate(), b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }

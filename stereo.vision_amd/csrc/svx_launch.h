@@ -105,7 +105,8 @@ hipError_t launch_maskpoints(const uint8_t* disp, const uint8_t* mask_ff, int fr
 // frame_planes: the keep1 plane fields of every frame from its RANSAC result.
 hipError_t launch_ransac_batch(const double* pts, int64_t cap, const int64_t* counts, uint64_t seed_base,
                                int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
-                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, hipStream_t s);
+                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, int ablate,
+                               hipStream_t s);
 hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, double f, FramePlane* out,
                                hipStream_t s);
 
