@@ -167,6 +167,20 @@ def extras(b, sb, args, device, with_cpu):
     ex["pipeline_frame_planes"] = {"ms_per_batch": round(ms, 3), "frames": b.frames,
                                    "kept_points": int(b.read_counts()[:, 2].sum()),
                                    "kernels": "frame_planes_kernel + stage_kernel<PF> + offsets_kernel"}
+
+    # the whole per-frame loop of stereovision.py:53-136 that is not cv2, back to back on the resident batch:
+    # fill + mask pre-pass, maskpoints + RANSAC, the pipeline with each frame's plane, road raster + walk
+    def frame_loop():
+        b.prepass("previous", sync=False)
+        b.ransac(seed_base=0, trials=600, sync=False)
+        b.pipeline_planes(sync=False)
+        b.road_raster(sync=False)
+        b.nonzero(sync=False)
+    ms = _timed(b, frame_loop, 2)
+    ex["device_frame_loop"] = {"ms_per_batch": round(ms, 2), "frames": b.frames,
+                               "frames_per_s": round(b.frames / ms * 1e3, 1),
+                               "stages": "prepass(previous+mask) -> maskpoints+RANSAC(600) -> pipeline(per-frame "
+                                         "planes) -> road raster -> non-zero walk"}
     return ex
 
 

@@ -4,7 +4,8 @@
 //      projectDisparityTo3d(maskDisparity(disparity), 128) = the fp64 X, Y, Z of
 //      every d > 0 grid point of the masked disparity on the reference's step-2
 //      grid (functions.py:185-193), in raster order, same arithmetic as the
-//      drop-in (bit-identical). One workgroup per frame, running offset.
+//      drop-in (bit-identical). One workgroup per frame, running offset,
+//      LDS-staged coalesced output.
 //  * ransac_batch_kernel — functions.py:278-298 for every frame, with the
 //      batch RNG contract: frame F draws CPython's stream after
 //      random.seed(seed_base + F). One workgroup per frame:
@@ -30,62 +31,88 @@ namespace svx {
 // ---------------------------------------------------------------------------
 // maskpoints: step-2 grid of the (optionally masked) disparity -> fp64 XYZ
 // ---------------------------------------------------------------------------
+// One lane = one quad (4 consecutive grid points of a row): an 8-byte load of
+// the row's pixels 8q..8q+7 holds the quad's 4 step-2 disparities (and one of
+// the mask). The chunk's fp64 X, Y, Z go to LDS in output order, then out as
+// contiguous doubles (coalesced).
+struct MaskpointsShared {
+    uint32_t wtot[4];
+    double stage[3 * 1024];
+};
+
 __global__ __launch_bounds__(256) void maskpoints_kernel(const uint8_t* __restrict__ disp,
                                                          const uint8_t* __restrict__ mask_ff, int64_t frame_px,
                                                          int H, int W, KParams p, double* __restrict__ out,
                                                          int64_t cap, int64_t* __restrict__ counts) {
-    __shared__ uint32_t wtot[4];
+    __shared__ MaskpointsShared sh;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.x;
     const uint8_t* fd = disp + (int64_t)frame * frame_px;
     double* fo = out + (int64_t)frame * cap * 3;
-    const int Hg = (H - 1 + 1) / 2, Wg = (W - 1 + 1) / 2;   // range(0, H-1, 2) x range(0, W-1, 2)
-    const int64_t ng = (int64_t)Hg * Wg;
+    const int Hg = H / 2, Wg = W / 2;   // range(0, H-1, 2) x range(0, W-1, 2)
+    const int Wq = (Wg + 3) / 4;
+    const int64_t nq = (int64_t)Hg * Wq;
+    const bool wide = (W % 4) == 0 && (reinterpret_cast<uintptr_t>(fd) & 7) == 0 &&
+                      (!mask_ff || (reinterpret_cast<uintptr_t>(mask_ff) & 7) == 0);   // uniform
     uint32_t running = 0;
-    for (int64_t base = 0; base < ng; base += 256 * 4) {
-        uint32_t dv[4];
-        int gyv[4], gxv[4];
-        uint32_t m = 0;
+    for (int64_t base = 0; base < nq; base += 256) {
+        const int64_t qi = base + tid;
+        uint32_t dv[4] = {0, 0, 0, 0};
+        int gy = 0, gx0 = 0;
+        if (qi < nq) {
+            gy = (int)(qi / Wq);
+            gx0 = 4 * (int)(qi - (int64_t)gy * Wq);
+            const int64_t px = (int64_t)(2 * gy) * W + 2 * gx0;
+            if (wide && gx0 + 3 < Wg) {
+                uint2 d8 = *reinterpret_cast<const uint2*>(fd + px);
+                if (mask_ff) {
+                    const uint2 m8 = *reinterpret_cast<const uint2*>(mask_ff + px);
+                    d8.x &= m8.x;
+                    d8.y &= m8.y;
+                }
+                dv[0] = d8.x & 0xFF;
+                dv[1] = (d8.x >> 16) & 0xFF;
+                dv[2] = d8.y & 0xFF;
+                dv[3] = (d8.y >> 16) & 0xFF;
+            } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t i = base + 4 * tid + k;
-            dv[k] = 0;
-            gyv[k] = gxv[k] = 0;
-            if (i < ng) {
-                const int gy = (int)(i / Wg), gx = (int)(i - (int64_t)gy * Wg);
-                const int64_t px = (int64_t)(2 * gy) * W + 2 * gx;
-                uint32_t d = fd[px];
-                if (mask_ff) d &= mask_ff[px];
-                dv[k] = d;
-                gyv[k] = gy;
-                gxv[k] = gx;
-                m |= (d != 0) << k;
+                for (int k = 0; k < 4; ++k) {
+                    if (gx0 + k >= Wg) break;
+                    uint32_t d = fd[px + 2 * k];
+                    if (mask_ff) d &= mask_ff[px + 2 * k];
+                    dv[k] = d;
+                }
             }
         }
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m |= (dv[k] != 0) << k;
         const uint32_t cnt = __builtin_popcount(m);
         const uint32_t inc = wave_incl_scan(cnt);
-        if (lane == 63) wtot[wave] = inc;
-        __syncthreads();
+        if (lane == 63) sh.wtot[wave] = inc;
+        __syncthreads();   // also: the previous chunk's writes have read sh.stage
         uint32_t wbase = 0, tot = 0;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-            wbase += w < wave ? wtot[w] : 0u;
-            tot += wtot[w];
+            wbase += w < wave ? sh.wtot[w] : 0u;
+            tot += sh.wtot[w];
         }
-        __syncthreads();
-        uint32_t o = running + wbase + inc - cnt;
+        uint32_t o = wbase + inc - cnt;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!(m & (1u << k))) continue;
-            const int y = 2 * gyv[k], x = 2 * gxv[k];
+            const int y = 2 * gy, x = 2 * (gx0 + k);
             const double Z = p.fB / (double)dv[k];           // functions.py:191
             const double X = (((double)x - p.cw) * Z) / p.f;  // :192
             const double Y = (((double)y - p.ch) * Z) / p.f;  // :193
-            fo[3 * (int64_t)o + 0] = X;
-            fo[3 * (int64_t)o + 1] = Y;
-            fo[3 * (int64_t)o + 2] = Z;
+            sh.stage[3 * o + 0] = X;
+            sh.stage[3 * o + 1] = Y;
+            sh.stage[3 * o + 2] = Z;
             ++o;
         }
+        __syncthreads();   // sh.stage complete; sh.wtot free
+        double* dst = fo + 3 * (int64_t)running;
+        for (uint32_t j = tid; j < 3 * tot; j += 256) __builtin_nontemporal_store(sh.stage[j], dst + j);
         running += tot;
     }
     if (tid == 0) counts[frame] = running;

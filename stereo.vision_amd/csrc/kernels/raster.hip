@@ -8,12 +8,16 @@
 //  * nonzero_kernel  — the pixel walk that ends sanitiseRoadImage
 //                      (functions.py:359-365): [j, i] of every non-zero pixel
 //                      in raster order. One workgroup per image; chunks of
-//                      256 lanes x 16 pixels; a block scan orders the lanes and
-//                      a running offset orders the chunks, so the list is
-//                      written once, in order, with no cross-workgroup sync.
+//                      256 lanes x 16 pixels; a block scan orders the lanes,
+//                      LDS holds the chunk's pixels in output order and a
+//                      running offset orders the chunks, so the list is
+//                      written once, in order, coalesced, with no
+//                      cross-workgroup sync.
 #include "../svx_launch.h"
 
 namespace svx {
+
+typedef int v2i __attribute__((ext_vector_type(2)));
 
 // points: frames x cap x 2 int32 (x, y); counts[frame * cstride + cidx] = points of the frame
 __global__ __launch_bounds__(256) void raster_kernel(const int32_t* __restrict__ pts, const int64_t* __restrict__ counts,
@@ -45,24 +49,36 @@ hipError_t launch_raster(const int32_t* pts, const int64_t* counts, int cstride,
 
 struct NonzeroShared {
     uint32_t wtot[4];
+    uint32_t stage[256 * 16];   // the chunk's non-zero pixel indices, in output order
 };
 
-// img: frames x frame_px u8 (frame_px % 4 == 0); out: frames x cap x 2 int32 ([j, i]); counts[frame]
+// img: frames x frame_px u8 (frame_px % 4 == 0); out: frames x cap x 2 int32 ([j, i]); counts[frame].
+// Per chunk of 4096 pixels: each lane finds its 16 pixels' non-zero bits, a
+// block scan orders them, lanes put the pixel indices into LDS in output order,
+// then the whole chunk's [j, i] pairs are written contiguously (coalesced,
+// non-temporal: written once, read by the caller later).
 __global__ __launch_bounds__(256) void nonzero_kernel(const uint8_t* __restrict__ img, int64_t frame_px, int W,
                                                       uint64_t W_m40, int32_t* __restrict__ out, int64_t cap,
                                                       int64_t* __restrict__ counts) {
     __shared__ NonzeroShared sh;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.x;
-    const uint32_t* fi = reinterpret_cast<const uint32_t*>(img + (int64_t)frame * frame_px);
+    const uint8_t* fb = img + (int64_t)frame * frame_px;
+    const uint32_t* fi = reinterpret_cast<const uint32_t*>(fb);
     int2* fo = reinterpret_cast<int2*>(out) + (int64_t)frame * cap;
     const int64_t words = frame_px / 4, vecs = (words + 3) / 4;   // lane = 4 words = 16 pixels
+    const bool vec16 = (reinterpret_cast<uintptr_t>(fb) & 15) == 0;   // uniform
     uint32_t running = 0;
     for (int64_t base = 0; base < vecs; base += 256) {
         const int64_t v = base + tid;
         uint32_t w[4];
+        if (vec16 && 4 * v + 3 < words) {
+            const uint4 q = *reinterpret_cast<const uint4*>(fi + 4 * v);
+            w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = 4 * v + k < words ? fi[4 * v + k] : 0u;
+            for (int k = 0; k < 4; ++k) w[k] = 4 * v + k < words ? fi[4 * v + k] : 0u;
+        }
         uint32_t bits = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -73,7 +89,7 @@ __global__ __launch_bounds__(256) void nonzero_kernel(const uint8_t* __restrict_
         const uint32_t cnt = __builtin_popcount(bits);
         const uint32_t inc = wave_incl_scan(cnt);
         if (lane == 63) sh.wtot[wave] = inc;
-        __syncthreads();
+        __syncthreads();   // also: the previous chunk's writes have read sh.stage
         uint32_t wbase = 0, tot = 0;
 #pragma unroll
         for (int w4 = 0; w4 < 4; ++w4) {
@@ -81,15 +97,19 @@ __global__ __launch_bounds__(256) void nonzero_kernel(const uint8_t* __restrict_
             wbase += w4 < wave ? t : 0u;
             tot += t;
         }
-        __syncthreads();   // sh.wtot is rewritten next chunk
-        uint32_t o = running + wbase + inc - cnt;
-        const int64_t p0 = v * 16;
+        uint32_t o = wbase + inc - cnt;
+        const uint32_t p0 = (uint32_t)(v * 16);
         while (bits) {
             const int b = __builtin_ctz(bits);
             bits &= bits - 1;
-            const int64_t p = p0 + b;
+            sh.stage[o++] = p0 + (uint32_t)b;
+        }
+        __syncthreads();   // sh.wtot is rewritten next chunk; sh.stage is complete
+        v2i* dst = reinterpret_cast<v2i*>(fo + running);
+        for (uint32_t j = tid; j < tot; j += 256) {
+            const uint32_t p = sh.stage[j];
             const int y = fastdiv40((int)p, W_m40);
-            fo[o++] = make_int2((int)(p - (int64_t)y * W), y);
+            __builtin_nontemporal_store((v2i){(int)(p - (uint32_t)y * (uint32_t)W), y}, dst + j);
         }
         running += tot;
     }
