@@ -100,6 +100,25 @@ int sv_road_raster(const int32_t* pts, int64_t n, int H, int W, uint8_t* out_img
  * out = [j, i] (int32) of every non-zero pixel, raster order. W <= 4096. */
 int sv_nonzero_points(const uint8_t* img, int H, int W, int32_t* out, int64_t cap, int64_t* out_n);
 
+/* ---- the stages a2-a6 one by one (the stage drop-ins) ---------------------- */
+
+/* calculatePointErrors (functions.py:300-312): out[i] = |(P_i . abc - 1) / d|
+ * in fp64 with P.abc = fma(z, c, fma(x, a, y * b)) (OpenBLAS dgemv's order for
+ * (N,3) x (3,1)); abcd = {a, b, c, d}, d as the reference's
+ * math.sqrt computes it. xyz: n rows of stride ld >= 3 doubles. */
+int sv_point_errors(const double* xyz, int64_t n, int64_t ld, const double* abcd, double* out);
+/* BGRtoHSVHue + calculateColourHistogram (functions.py:73-78, :215-226): the
+ * hue bin rint(h * 1000) of every (R, G, B) row (stride ld bytes; out_bins
+ * nullable), the count of every bin (out_hist[1000]) and the index of its
+ * first row (out_first[1000], -1 if empty; the dict's insertion order). */
+int sv_hue_histogram(const uint8_t* rgb, int64_t n, int64_t ld, int16_t* out_bins, uint32_t* out_hist,
+                     int64_t* out_first);
+/* computePlanarThreshold (functions.py:314-323): indices i with vals[i] < thr
+ * (NaN never), in order. filterPointsByHistogram (functions.py:228-230): indices
+ * i with ok[bins[i]] != 0 (ok[1000] = hist[bin] > threshold), in order. */
+int sv_select_less(const double* vals, int64_t n, double thr, int64_t* out_idx, int64_t* out_n);
+int sv_select_bins(const int16_t* bins, int64_t n, const uint8_t* ok, int64_t* out_idx, int64_t* out_n);
+
 /* ---- RANSAC plane fit --------------------------------- */
 
 /* The draws of functions.py:278-298 RANSAC(points, trials), replayed exactly

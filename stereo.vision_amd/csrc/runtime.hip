@@ -1123,6 +1123,110 @@ int sv_ransac(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld, int 
 }
 
 // ---------------------------------------------------------------------------
+// a2-a6 as separate calls (functions.py:212-230, :300-323) for the stage drop-ins
+// ---------------------------------------------------------------------------
+namespace {
+struct Locked {   // the current device's scratch + stream, under its mutex
+    Device* d = nullptr;
+    std::unique_lock<std::mutex> lk;
+};
+int lock_current(Locked& L) {
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    if (int rc = dev_get(dev, &L.d)) return rc;
+    L.lk = std::unique_lock<std::mutex>(L.d->mu);
+    return SV_OK;
+}
+}  // namespace
+
+int sv_point_errors(const double* xyz, int64_t n, int64_t ld, const double* abcd, double* out) {
+    if (n < 0 || ld < 3 || !abcd || (n > 0 && (!xyz || !out))) return fail(SV_E_ARG, "sv_point_errors: bad arguments");
+    if (n == 0) return SV_OK;
+    Locked L;
+    if (int rc = lock_current(L)) return rc;
+    hipStream_t s = L.d->stream;
+    HIP_TRY(L.d->xyz.ensure(sizeof(double) * (size_t)n * ld));
+    HIP_TRY(L.d->aux.ensure(sizeof(double) * (size_t)n));
+    HIP_TRY(hipMemcpyAsync(L.d->xyz.p, xyz, sizeof(double) * (size_t)n * ld, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_point_errors(L.d->xyz.as<double>(), n, ld, abcd, L.d->aux.as<double>(), s));
+    HIP_TRY(hipMemcpyAsync(out, L.d->aux.p, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SV_OK;
+}
+
+int sv_hue_histogram(const uint8_t* rgb, int64_t n, int64_t ld, int16_t* out_bins, uint32_t* out_hist,
+                     int64_t* out_first) {
+    if (n < 0 || ld < 3 || n >= INT32_MAX || (n > 0 && !rgb) || !out_hist || !out_first)
+        return fail(SV_E_ARG, "sv_hue_histogram: bad arguments");
+    for (int k = 0; k < 1000; ++k) {
+        out_hist[k] = 0;
+        out_first[k] = -1;
+    }
+    if (n == 0) return SV_OK;
+    Locked L;
+    if (int rc = lock_current(L)) return rc;
+    hipStream_t s = L.d->stream;
+    HIP_TRY(L.d->rgb.ensure((size_t)n * ld));
+    HIP_TRY(L.d->aux.ensure(sizeof(int16_t) * (size_t)n + 8192));
+    int16_t* bins = L.d->aux.as<int16_t>();
+    uint32_t* hist = reinterpret_cast<uint32_t*>(L.d->aux.as<char>() + (sizeof(int16_t) * (size_t)n + 15) / 16 * 16);
+    int32_t* first = reinterpret_cast<int32_t*>(hist + 1000);
+    HIP_TRY(hipMemcpyAsync(L.d->rgb.p, rgb, (size_t)n * ld, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(hist, 0, sizeof(uint32_t) * 1000, s));
+    HIP_TRY(hipMemsetAsync(first, 0x7f, sizeof(int32_t) * 1000, s));   // 0x7f7f7f7f > any index
+    HIP_TRY(launch_hue_hist(L.d->rgb.as<uint8_t>(), n, ld, out_bins ? bins : nullptr, hist, first, s));
+    std::vector<int32_t> f(1000);
+    HIP_TRY(hipMemcpyAsync(out_hist, hist, sizeof(uint32_t) * 1000, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(f.data(), first, sizeof(int32_t) * 1000, hipMemcpyDeviceToHost, s));
+    if (out_bins) HIP_TRY(hipMemcpyAsync(out_bins, bins, sizeof(int16_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int k = 0; k < 1000; ++k) out_first[k] = out_hist[k] ? (int64_t)f[k] : -1;
+    return SV_OK;
+}
+
+static int select_impl(int mode, const double* vals, double thr, const int16_t* bins, const uint8_t* ok, int64_t n,
+                       int64_t* out_idx, int64_t* out_n) {
+    if (n < 0 || !out_n || (n > 0 && !out_idx) || (mode == 0 && n > 0 && !vals) ||
+        (mode == 1 && (!ok || (n > 0 && !bins))))
+        return fail(SV_E_ARG, "sv_select: bad arguments");
+    *out_n = 0;
+    if (n == 0) return SV_OK;
+    Locked L;
+    if (int rc = lock_current(L)) return rc;
+    hipStream_t s = L.d->stream;
+    const size_t in_bytes = mode == 0 ? sizeof(double) * (size_t)n : sizeof(int16_t) * (size_t)n;
+    HIP_TRY(L.d->aux.ensure((in_bytes + 15) / 16 * 16 + 1024));
+    HIP_TRY(L.d->aux2.ensure(sizeof(int64_t) * ((size_t)n + 1)));
+    char* in = L.d->aux.as<char>();
+    uint8_t* dok = reinterpret_cast<uint8_t*>(in + (in_bytes + 15) / 16 * 16);
+    int64_t* idx = L.d->aux2.as<int64_t>();
+    int64_t* cnt = idx + n;
+    HIP_TRY(hipMemcpyAsync(in, mode == 0 ? (const void*)vals : (const void*)bins, in_bytes, hipMemcpyHostToDevice, s));
+    if (mode == 1) HIP_TRY(hipMemcpyAsync(dok, ok, 1000, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_select(mode, reinterpret_cast<const double*>(in), thr, reinterpret_cast<const int16_t*>(in), dok, n,
+                          idx, cnt, s));
+    int64_t k = 0;
+    HIP_TRY(hipMemcpyAsync(&k, cnt, sizeof k, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (k) {
+        HIP_TRY(hipMemcpyAsync(out_idx, idx, sizeof(int64_t) * (size_t)k, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    *out_n = k;
+    return SV_OK;
+}
+
+int sv_select_less(const double* vals, int64_t n, double thr, int64_t* out_idx, int64_t* out_n) {
+    return select_impl(0, vals, thr, nullptr, nullptr, n, out_idx, out_n);
+}
+
+int sv_select_bins(const int16_t* bins, int64_t n, const uint8_t* ok, int64_t* out_idx, int64_t* out_n) {
+    for (int64_t i = 0; bins && i < n; ++i)
+        if (bins[i] < 0 || bins[i] >= 1000) return fail(SV_E_ARG, "sv_select_bins: bin %d out of range", (int)bins[i]);
+    return select_impl(1, nullptr, 0.0, bins, ok, n, out_idx, out_n);
+}
+
+// ---------------------------------------------------------------------------
 // verification helpers
 // ---------------------------------------------------------------------------
 int sv_hue_lut(int device, int16_t* out_lut) {

@@ -110,4 +110,15 @@ hipError_t launch_ransac_batch(const double* pts, int64_t cap, const int64_t* co
 hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, double f, FramePlane* out,
                                hipStream_t s);
 
+// kernels/stages.hip -------------------------------------------------------
+// a2: |(P.abc - 1) / d| per point (abcd = a, b, c, d); a4/a5: hue bin per point,
+// bin counts and first point per bin (hist zeroed, first INT32_MAX-filled);
+// a3/a6: stable selection (mode 0: vals < thr, mode 1: ok[bins] != 0).
+hipError_t launch_point_errors(const double* xyz, int64_t n, int64_t ld, const double* abcd, double* out,
+                               hipStream_t s);
+hipError_t launch_hue_hist(const uint8_t* rgb, int64_t n, int64_t ld, int16_t* bins, uint32_t* hist, int32_t* first,
+                           hipStream_t s);
+hipError_t launch_select(int mode, const double* vals, double thr, const int16_t* bins, const uint8_t* ok, int64_t n,
+                         int64_t* out_idx, int64_t* out_n, hipStream_t s);
+
 }  // namespace svx

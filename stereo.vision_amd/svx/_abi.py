@@ -54,6 +54,10 @@ SIGNATURES = {
     "sv_batch_road_raster": [P, I],
     "sv_batch_nonzero": [P, I],
     "sv_batch_read_road": [P, I, P, P, I64, PI64],
+    "sv_point_errors": [P, I64, I64, P, P],
+    "sv_hue_histogram": [P, I64, I64, P, P, P],
+    "sv_select_less": [P, I64, D, P, PI64],
+    "sv_select_bins": [P, I64, P, P, PI64],
     "sv_ransac_draw": [P, P, I64, I64, I, I, P, P, ctypes.POINTER(I)],
     "sv_ransac": [P, P, I64, I64, I, I, P, P, P, P, P, ctypes.POINTER(I)],
     "sv_batch_ransac": [P, ctypes.POINTER(Camera), ctypes.c_uint64, I64, I, I, I],

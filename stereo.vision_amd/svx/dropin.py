@@ -25,6 +25,10 @@ reference:
   ``nonzero_points(img)`` gives sanitiseRoadImage's final pixel walk.
 * ``RANSAC(points, trials)`` (functions.py:278-298): see svx/ransac.py — same
   draws from the global ``random`` stream, trials on the GPU, same plane bits.
+* ``calculatePointErrors``, ``computePlanarThreshold``,
+  ``calculateColourHistogram``, ``filterPointsByHistogram`` (functions.py:
+  212-230, :300-323): see svx/stages.py — one device call each, same return
+  types, dict order and errors as the reference.
 * disparity pre-pass (functions.py:141-172): ``fillDisparity`` (new array, or
   the input itself when there is no previous frame), ``fillAltDisparity`` (in
   place, returns its argument), ``maskDisparity`` (new array; the mask is the
@@ -91,43 +95,7 @@ def project_frame(disparity, rgb=None, step=REFERENCE_STEP, camera=None):
     return xyz[:k], (out_rgb[:k] if out_rgb is not None else None)
 
 
-class PointList(list):
-    """The list of row views projectDisparityTo3d returns, remembering the (N, 3|6)
-    array behind it while the list is unmodified, so later GPU stages (RANSAC,
-    back-projection) skip re-stacking N Python rows. Any list mutation drops it;
-    writes through a row view write the array itself, so they stay consistent."""
-
-    __slots__ = ("_array",)
-
-    def __init__(self, array):
-        super().__init__(array)
-        self._array = array
-
-    def array(self):
-        a = self._array
-        return a if a is not None and len(a) == len(self) else None
-
-    def _drop(name):  # noqa: N805
-        base = getattr(list, name)
-
-        def f(self, *a, **k):
-            self._array = None
-            return base(self, *a, **k)
-        f.__name__ = name
-        return f
-
-    for _n in ("append", "extend", "insert", "remove", "pop", "clear", "sort", "reverse", "__setitem__",
-               "__delitem__", "__iadd__", "__imul__"):
-        locals()[_n] = _drop(_n)
-    del _n, _drop
-
-
-def as_points_array(points):
-    """(N, >=3) float64 C-contiguous array of a point sequence (zero-copy for a PointList)."""
-    if isinstance(points, PointList) and points.array() is not None:
-        return points.array()
-    arr = points if isinstance(points, np.ndarray) else np.asarray(points)
-    return np.ascontiguousarray(arr, dtype=np.float64)
+from .points import PointList, as_points_array  # noqa: E402,F401  (re-exported)
 
 
 def projectDisparityTo3d(disparity, max_disparity, rgb=[]):  # noqa: N802,B006 (reference signature)
@@ -254,9 +222,12 @@ project_disparity_to_3d = projectDisparityTo3d
 project_3D_points_to_2D = project3DPointsTo2DImagePoints
 
 from .ransac import RANSAC  # noqa: E402  (functions.py:278-298)
+from .stages import (calculateColourHistogram, calculatePointErrors, computePlanarThreshold,  # noqa: E402,F401
+                     filterPointsByHistogram)
 
 PATCHED = ("projectDisparityTo3d", "project3DPointsTo2DImagePoints", "fillDisparity", "fillAltDisparity",
-           "maskDisparity", "capDisparity", "generatePointsAsImage", "RANSAC")
+           "maskDisparity", "capDisparity", "generatePointsAsImage", "RANSAC", "calculatePointErrors",
+           "computePlanarThreshold", "calculateColourHistogram", "filterPointsByHistogram")
 ALIASES = {"project_disparity_to_3d": "projectDisparityTo3d",
            "project_3D_points_to_2D": "project3DPointsTo2DImagePoints"}
 _saved = {}

@@ -111,3 +111,20 @@ def test_point_list_tracks_its_array():
     assert pl2.array() is None and np.array_equal(as_points_array(pl2), a[1:])
     import random
     assert len(random.Random(0).sample(PointList(a), 2)) == 2
+
+
+def test_hue_keys_match_reference_strings():
+    """svx.stages.bin_key(k) is the reference's str(round(h, 3)) for bin k, and every key the
+    reference produced in tests/golden/stages.json is one of them (CPU only)."""
+    import json
+    import os
+
+    import numpy as np
+
+    from conftest import GOLDEN
+    from svx import stages
+    keys = [stages.bin_key(k) for k in range(1000)]
+    assert keys == [str(round(np.float64(k / 1000), 3)) for k in range(1000)]
+    fx = json.load(open(os.path.join(GOLDEN, "stages.json")))
+    seen = {key for c in fx["crops"].values() for key, _ in c["hist_items"] + c["default_hist_items"]}
+    assert seen <= set(keys) and len(seen) > 900
