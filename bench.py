@@ -168,6 +168,44 @@ def extras(b, sb, args, device, with_cpu):
                                    "kept_points": int(b.read_counts()[:, 2].sum()),
                                    "kernels": "frame_planes_kernel + stage_kernel<PF> + offsets_kernel"}
 
+    # stereovision.py:84-113 for one host frame through the installed drop-ins (what a user of the
+    # reference sees after svx.dropin.install(functions)): 2 projections, RANSAC(600), the four stages,
+    # back-projection and the int32 cast; step 2 as the reference hard-codes
+    import types
+
+    from svx import dropin
+    fmod = types.SimpleNamespace(camera_focal_length_px=399.9745178222656, stereo_camera_baseline_m=0.2090607502,
+                                 image_centre_w=474.5, image_centre_h=262.0, carmask=mask)
+    dropin.install(fmod)
+    try:
+        disp, bgr = oracle.synth_frame(0)
+
+        def chain():
+            points = fmod.projectDisparityTo3d(disp, 128, bgr)
+            maskpoints = fmod.projectDisparityTo3d(fmod.maskDisparity(disp), 128)
+            _, abc = fmod.RANSAC(maskpoints, 600)
+            diffs = fmod.calculatePointErrors(abc, points)
+            points = fmod.computePlanarThreshold(points, diffs, 0.05)
+            hist = fmod.calculateColourHistogram(points)
+            points = fmod.filterPointsByHistogram(points, hist, 10)
+            pp = np.array(fmod.project3DPointsTo2DImagePoints(points), np.int32).reshape((-1, 1, 2))
+            return len(pp)
+        st = random.getstate()
+        random.seed(0)
+        chain()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            n_pp = chain()
+        ex["dropin_frame_chain"] = {"ms_per_frame": round((time.perf_counter() - t0) / 5 * 1e3, 2),
+                                    "plane_points": n_pp,
+                                    "stages": "stereovision.py:84-113 via installed drop-ins, step 2, RANSAC 600",
+                                    "reference_ms_per_frame_survey": "~1,450 (SURVEY §8a, measured in the "
+                                                                     "build container: a1 2x150-180, a2 30, a3 55, "
+                                                                     "a5 300, a6 300, a7 45, a8 16, RANSAC ~380)"}
+        random.setstate(st)
+    finally:
+        dropin.uninstall()
+
     # the whole per-frame loop of stereovision.py:53-136 that is not cv2, back to back on the resident batch:
     # fill + mask pre-pass, maskpoints + RANSAC, the pipeline with each frame's plane, road raster + walk
     def frame_loop():

@@ -20,7 +20,6 @@
 // re-decides them with the reference's own numpy calls (it also re-derives the
 // winner's plane that way, so the plane it returns is bit-identical).
 #include <cmath>
-#include <unordered_set>
 #include <vector>
 
 #include "../svx_launch.h"
@@ -69,8 +68,11 @@ struct PyMT {
 };
 
 // random.sample(range(n), k) -> out[0..k). Caller guarantees 0 <= k <= n.
+// The set branch's `selected` is a bitmap of n bits (cleared bit by bit after
+// the sample): membership is what the reference's set answers, at a fraction
+// of a hash set's cost.
 static void py_sample(PyMT& rng, uint32_t n, int k, int32_t* out, std::vector<uint32_t>& pool,
-                      std::unordered_set<uint32_t>& selected) {
+                      std::vector<uint64_t>& selected) {
     int64_t setsize = 21;
     if (k > 5) setsize += (int64_t)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
     if ((int64_t)n <= setsize) {
@@ -82,13 +84,14 @@ static void py_sample(PyMT& rng, uint32_t n, int k, int32_t* out, std::vector<ui
             pool[j] = pool[n - i - 1];
         }
     } else {
-        selected.clear();
+        if (selected.size() < (n + 63) / 64) selected.assign((n + 63) / 64, 0);
         for (int i = 0; i < k; ++i) {
             uint32_t j = rng.randbelow(n);
-            while (selected.count(j)) j = rng.randbelow(n);
-            selected.insert(j);
+            while ((selected[j >> 6] >> (j & 63)) & 1) j = rng.randbelow(n);
+            selected[j >> 6] |= 1ull << (j & 63);
             out[i] = (int32_t)j;
         }
+        for (int i = 0; i < k; ++i) selected[(uint32_t)out[i] >> 6] = 0;   // every word that got a bit
     }
 }
 
@@ -108,8 +111,7 @@ int ransac_draw(uint32_t* state625, const double* pts, int64_t n, int64_t ld, in
     for (int i = 0; i < 624; ++i) rng.mt[i] = state625[i];
     rng.index = (int)state625[624];
     std::vector<uint32_t> pool;
-    std::unordered_set<uint32_t> selected;
-    selected.reserve(2 * (size_t)k + 16);
+    std::vector<uint64_t> selected;
     for (int t = 0; t < trials; ++t) {
         py_sample(rng, (uint32_t)n, k, sidx + (int64_t)t * k, pool, selected);
         uint32_t i1, i2, i3;

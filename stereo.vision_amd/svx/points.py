@@ -1,7 +1,19 @@
 """The point lists the drop-ins pass between stages (functions.py:178-323):
 a Python list of row views, as the reference's callers expect, that remembers
 the array behind it so the next GPU stage does not re-stack rows."""
+import operator
+
 import numpy as np
+
+
+def select_rows(seq, idx):
+    """[seq[i] for i in idx] with the per-item work in C (operator.itemgetter)."""
+    idx = [int(i) for i in idx] if not isinstance(idx, np.ndarray) else idx.tolist()
+    if not idx:
+        return []
+    if len(idx) == 1:
+        return [seq[idx[0]]]
+    return list(operator.itemgetter(*idx)(seq))
 
 
 class PointList(list):
@@ -26,7 +38,7 @@ class PointList(list):
     @classmethod
     def subset(cls, parent, idx):
         out = list.__new__(cls)
-        list.__init__(out, (parent[i] for i in idx))
+        list.__init__(out, select_rows(parent, idx))
         base = parent.array() if isinstance(parent, PointList) else None
         out._array = base
         out._idx = np.asarray(idx, np.int64) if base is not None else None

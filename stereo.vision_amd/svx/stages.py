@@ -31,7 +31,7 @@ import math
 import numpy as np
 
 from . import _abi
-from .points import PointList, as_points_array
+from .points import PointList, as_points_array, select_rows
 
 BINS = 1000
 
@@ -75,7 +75,7 @@ def _hue(points, bins):
 def _select(points, idx):
     if isinstance(points, PointList):
         return PointList.subset(points, idx)
-    return [points[int(i)] for i in idx]
+    return select_rows(points, idx)
 
 
 def calculatePointErrors(abc, points):  # noqa: N802 (reference signature)
