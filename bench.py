@@ -346,8 +346,8 @@ def main():
                        if args.frames >= 512 else "tiled: stage_kernel + offsets_kernel",
         }
 
-    if want_pipe and not args.no_extras:
-        out["extras"] = extras(b, sb, args, local, rank == 0 and world == 1 and not args.no_cpu)
+    if want_pipe and not args.no_extras and world == 1:   # §8f component timings: the N=1 run only
+        out["extras"] = extras(b, sb, args, local, not args.no_cpu)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
