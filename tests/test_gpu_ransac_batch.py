@@ -211,3 +211,24 @@ def test_pipeline_with_frame_planes(svb):
             assert np.array_equal(b.read_hist(f)[:1000], ref["hist"][:1000]), f
             assert np.array_equal(pts, ref["pts"]), f
             np.testing.assert_allclose(xyz, ref["xyz2"], rtol=1e-5, atol=0)
+
+
+def test_batch_shard_invariance(svb):
+    """Frames sharded across ranks (contiguous global ids, seeds by global id, as
+    svx.dist.shard lays them out) give each frame the result of the whole batch."""
+    m = carmask()
+    full = []
+    with svb.Batch(6, H=H, W=W, step=2, with_bgr=False) as b:
+        b.synth(40)
+        b.set_mask(m)
+        b.ransac(seed_base=77, trials=30, first_frame=40)
+        full = [b.read_ransac(f) for f in range(6)]
+    for first, count in ((40, 2), (42, 4)):
+        with svb.Batch(count, H=H, W=W, step=2, with_bgr=False) as b:
+            b.synth(first)
+            b.set_mask(m)
+            b.ransac(seed_base=77, trials=30, first_frame=first)
+            for f in range(count):
+                r, ref = b.read_ransac(f), full[first - 40 + f]
+                assert r["trial"] == ref["trial"] and r["flags"] == ref["flags"]
+                assert r["err"] == ref["err"] and np.array_equal(r["abc"], ref["abc"])
