@@ -6,7 +6,7 @@
  * cpu_baseline leg. The product path (stereo.vision_amd/svx + libsvx.so) never
  * links, loads or calls this file.
  *
- * Parity: pinned against tests/golden/* — fixtures produced by running the
+ * Parity: pinned against tests/golden/ — fixtures produced by running the
  * reference's own Python functions (tests/golden/make_golden.py, container
  * only) — and against the SURVEY.md §8c digests.
  *
