@@ -36,19 +36,26 @@
 
 namespace svx {
 
-constexpr int kRMaxChunks = 256;
-constexpr int kRStage = 4096;   // LDS staging slots; a power of two (wrap-around below)
+constexpr int kRMaxChunks = 256;   // chunks per frame at the default 4 quads per lane (= maxchunks_of<4>)
 constexpr int kRBins = 1000;    // bins 0..999: t < 1000 - 1000/(6*255) so rint(t) <= 999
 
 
-template <int STEP>
+template <int STEP, int QP>
 struct RCfg {
-    static constexpr int QPL = STEP == 1 ? 4 : 2;   // quads per lane per chunk
+    static constexpr int QPL = QP;                 // quads per lane per chunk
     static constexpr int CW = 3 * STEP;            // BGR dwords per quad
 };
+template <int STEP>
+constexpr int default_qpl() { return STEP == 1 ? 4 : 2; }
+// Per-workgroup chunk = 256 lanes x QP quads = 1024 * QP grid points; the LDS
+// stage holds one chunk's outputs; a frame has at most 2^20 quads.
+template <int QP>
+constexpr int stage_of() { return 1024 * QP; }
+template <int QP>
+constexpr int maxchunks_of() { return 1024 / QP; }
 
-int resident_chunks_per_frame(const KParams& p) {
-    const int per = 256 * (p.step == 1 ? 4 : 2);
+int resident_chunks_per_frame(const KParams& p, int qpl) {
+    const int per = 256 * qpl;
     return (p.frame_quads + per - 1) / per;
 }
 
@@ -103,15 +110,15 @@ struct RParams {      // what the streaming kernel needs (kept small: SGPR budge
     float B32, fB32, cw_hi, cw_lo, ch_hi, ch_lo;
 };
 
-template <int STEP>
+template <int STEP, int QP>
 struct RQuads {   // this lane's quads of one chunk
-    int gy[RCfg<STEP>::QPL];   // grid row, -1 past the frame end
-    int q[RCfg<STEP>::QPL];    // quad within the row
+    int gy[RCfg<STEP, QP>::QPL];   // grid row, -1 past the frame end
+    int q[RCfg<STEP, QP>::QPL];    // quad within the row
 };
 
-template <int STEP>
-__device__ __forceinline__ void r_geometry(int c, int tid, const RParams& p, RQuads<STEP>& g) {
-    constexpr int QPL = RCfg<STEP>::QPL;
+template <int STEP, int QP>
+__device__ __forceinline__ void r_geometry(int c, int tid, const RParams& p, RQuads<STEP, QP>& g) {
+    constexpr int QPL = RCfg<STEP, QP>::QPL;
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
         const int qi = (c * QPL + i) * 256 + tid;
@@ -124,17 +131,17 @@ __device__ __forceinline__ void r_geometry(int c, int tid, const RParams& p, RQu
 }
 
 // byte offset of quad (gy, q) in a frame plane with `bpp` bytes per pixel
-template <int STEP>
+template <int STEP, int QP>
 __device__ __forceinline__ uint32_t r_off(int gy, int q, int bpp, const RParams& p) {
     return (uint32_t)(((gy < 0 ? 0 : gy) * STEP) * p.W + 4 * STEP * q) * (uint32_t)bpp;
 }
 
-template <int STEP>
-__device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<STEP>& g, const RParams& p,
-                                            uint32_t (&dw)[RCfg<STEP>::QPL][STEP]) {
+template <int STEP, int QP>
+__device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<STEP, QP>& g, const RParams& p,
+                                            uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP]) {
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
-        const uint8_t* a = fdisp + r_off<STEP>(g.gy[i], g.q[i], 1, p);
+    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
+        const uint8_t* a = fdisp + r_off<STEP, QP>(g.gy[i], g.q[i], 1, p);
         if constexpr (STEP == 1) {
             dw[i][0] = *reinterpret_cast<const uint32_t*>(a);
         } else {
@@ -145,22 +152,22 @@ __device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<S
     }
 }
 
-template <int STEP>
-__device__ __forceinline__ void r_load_tab(const uint16_t* tab, const RQuads<STEP>& g, const RParams& p,
-                                           uint2 (&tw)[RCfg<STEP>::QPL]) {
+template <int STEP, int QP>
+__device__ __forceinline__ void r_load_tab(const uint16_t* tab, const RQuads<STEP, QP>& g, const RParams& p,
+                                           uint2 (&tw)[RCfg<STEP, QP>::QPL]) {
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
+    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
         const int gy = g.gy[i] < 0 ? 0 : g.gy[i];
         tw[i] = *reinterpret_cast<const uint2*>(tab + (uint32_t)(gy * p.pitch + 4 * g.q[i]));
     }
 }
 
-template <int STEP>
-__device__ __forceinline__ void r_load_bgr(const uint8_t* fbgr, const RQuads<STEP>& g, const RParams& p,
-                                           uint32_t (&cw)[RCfg<STEP>::QPL][RCfg<STEP>::CW]) {
+template <int STEP, int QP>
+__device__ __forceinline__ void r_load_bgr(const uint8_t* fbgr, const RQuads<STEP, QP>& g, const RParams& p,
+                                           uint32_t (&cw)[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW]) {
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
-        const uint8_t* a = fbgr + r_off<STEP>(g.gy[i], g.q[i], 3, p);
+    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
+        const uint8_t* a = fbgr + r_off<STEP, QP>(g.gy[i], g.q[i], 3, p);
         if constexpr (STEP == 1) {
             const uint32_t* cp = reinterpret_cast<const uint32_t*>(a);
             cw[i][0] = cp[0];
@@ -175,17 +182,17 @@ __device__ __forceinline__ void r_load_bgr(const uint8_t* fbgr, const RQuads<STE
 }
 
 // disparity byte of point k of a quad
-template <int STEP>
+template <int STEP, int QP>
 __device__ __forceinline__ uint32_t r_d(const uint32_t (&w)[STEP], int k) {
     if constexpr (STEP == 1) return (w[0] >> (8 * k)) & 0xFF;
     else return (w[k >> 1] >> (16 * (k & 1))) & 0xFF;
 }
 
 // colour (B | G<<8 | R<<16, top byte junk) of point k of a quad
-template <int STEP>
-__device__ __forceinline__ uint32_t r_col(const uint32_t (&c)[RCfg<STEP>::CW], int k) {
+template <int STEP, int QP>
+__device__ __forceinline__ uint32_t r_col(const uint32_t (&c)[RCfg<STEP, QP>::CW], int k) {
     const int o = 3 * STEP * k, w = o >> 2, sh = o & 3;
-    const uint32_t hi = (w + 1 < RCfg<STEP>::CW) ? c[w + 1] : 0u;
+    const uint32_t hi = (w + 1 < RCfg<STEP, QP>::CW) ? c[w + 1] : 0u;
     return sh == 0 ? c[w] : __builtin_amdgcn_alignbyte(hi, c[w], sh);
 }
 
@@ -198,17 +205,17 @@ __device__ __forceinline__ int r_bin(uint32_t col) {
 }
 
 // keep1 bits of this lane's chunk (bit 4i+k = point k of quad i): lo <= d <= hi.
-template <int STEP>
-__device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP>::QPL][STEP],
-                                            const uint2 (&tw)[RCfg<STEP>::QPL], const RQuads<STEP>& g) {
+template <int STEP, int QP>
+__device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP],
+                                            const uint2 (&tw)[RCfg<STEP, QP>::QPL], const RQuads<STEP, QP>& g) {
     uint32_t keep = 0;
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
+    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
         uint32_t k4 = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t t = (k < 2 ? tw[i].x : tw[i].y) >> (16 * (k & 1));
-            const uint32_t d = r_d<STEP>(dw[i], k);
+            const uint32_t d = r_d<STEP, QP>(dw[i], k);
             k4 |= (uint32_t)(d >= (t & 0xFF) && d <= ((t >> 8) & 0xFF)) << k;
         }
         keep |= (g.gy[i] >= 0 ? k4 : 0u) << (4 * i);
@@ -217,12 +224,12 @@ __device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP>::QPL
 }
 
 // grid points with d != 0 in this lane's chunk (pad columns and rows past the end excluded)
-template <int STEP>
-__device__ __forceinline__ uint32_t r_nvalid(const uint32_t (&dw)[RCfg<STEP>::QPL][STEP], const RQuads<STEP>& g,
+template <int STEP, int QP>
+__device__ __forceinline__ uint32_t r_nvalid(const uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP], const RQuads<STEP, QP>& g,
                                              const RParams& p) {
     uint32_t n = 0;
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
+    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
         const int nin = g.gy[i] < 0 ? 0 : min(4, p.Wg - 4 * g.q[i]);
         uint32_t v;   // the quad's 4 disparity bytes, point k at byte k
         if constexpr (STEP == 1) v = dw[i][0];
@@ -236,19 +243,19 @@ __device__ __forceinline__ uint32_t r_nvalid(const uint32_t (&dw)[RCfg<STEP>::QP
 
 // Pack the colours of the keep bits into this wave's LDS region, in (lane, bit)
 // order; returns the wave's total and this lane's first slot.
-template <int STEP>
+template <int STEP, int QP>
 __device__ __forceinline__ uint32_t r_stage_colours(uint32_t keep,
-                                                    const uint32_t (&cw)[RCfg<STEP>::QPL][RCfg<STEP>::CW],
+                                                    const uint32_t (&cw)[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW],
                                                     uint32_t* wstage, uint32_t& pos0) {
     const uint32_t cnt = __builtin_popcount(keep);
     const uint32_t inc = wave_incl_scan(cnt);
     pos0 = inc - cnt;
     uint32_t pos = pos0;
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP>::QPL; ++i) {
+    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (keep & (1u << (4 * i + k))) wstage[pos++] = r_col<STEP>(cw[i], k);
+            if (keep & (1u << (4 * i + k))) wstage[pos++] = r_col<STEP, QP>(cw[i], k);
         }
     }
     return __shfl(inc, 63, kWave);
@@ -257,49 +264,49 @@ __device__ __forceinline__ uint32_t r_stage_colours(uint32_t keep,
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 
-template <int STEP>
+template <int STEP, int QP>
 struct P1Regs {
-    RQuads<STEP> g;
-    uint32_t dw[RCfg<STEP>::QPL][STEP];
-    uint32_t cw[RCfg<STEP>::QPL][RCfg<STEP>::CW];
-    uint2 tw[RCfg<STEP>::QPL];
+    RQuads<STEP, QP> g;
+    uint32_t dw[RCfg<STEP, QP>::QPL][STEP];
+    uint32_t cw[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW];
+    uint2 tw[RCfg<STEP, QP>::QPL];
 };
 
-template <int STEP>
+template <int STEP, int QP>
 struct P2Regs {
-    RQuads<STEP> g;
-    uint32_t dw[RCfg<STEP>::QPL][STEP];
-    uint2 tw[RCfg<STEP>::QPL];
+    RQuads<STEP, QP> g;
+    uint32_t dw[RCfg<STEP, QP>::QPL][STEP];
+    uint2 tw[RCfg<STEP, QP>::QPL];
 };
 
-template <int STEP>
-__device__ __forceinline__ void p1_load(P1Regs<STEP>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
+template <int STEP, int QP>
+__device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
                                         const uint16_t* tab, const RParams& p) {
-    r_geometry<STEP>(c, tid, p, r.g);
-    r_load_disp<STEP>(fdisp, r.g, p, r.dw);
-    r_load_tab<STEP>(tab, r.g, p, r.tw);
-    r_load_bgr<STEP>(fbgr, r.g, p, r.cw);
+    r_geometry<STEP, QP>(c, tid, p, r.g);
+    r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
+    r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
+    r_load_bgr<STEP, QP>(fbgr, r.g, p, r.cw);
 }
 
-template <int STEP>
-__device__ __forceinline__ void p2_load(P2Regs<STEP>& r, int c, int tid, const uint8_t* fdisp, const uint16_t* tab,
+template <int STEP, int QP>
+__device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint16_t* tab,
                                         const RParams& p) {
-    r_geometry<STEP>(c, tid, p, r.g);
-    r_load_disp<STEP>(fdisp, r.g, p, r.dw);
-    r_load_tab<STEP>(tab, r.g, p, r.tw);
+    r_geometry<STEP, QP>(c, tid, p, r.g);
+    r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
+    r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
 }
 
 // pass 1 of one chunk: keep1, valid/kept counts, dense hue binning into hist,
 // candidate mark into dirty. Wave-local (no barrier).
-template <int STEP>
-__device__ __forceinline__ void p1_chunk(const P1Regs<STEP>& r, int c, uint32_t* hist, uint32_t* dirty,
+template <int STEP, int QP>
+__device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint32_t* hist, uint32_t* dirty,
                                          uint32_t* wstage, const RParams& p, uint32_t& nvalid, uint32_t& nkept) {
     const int lane = lane_id();
-    const uint32_t keep = r_keep1<STEP>(r.dw, r.tw, r.g);
-    nvalid += r_nvalid<STEP>(r.dw, r.g, p);
+    const uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
+    nvalid += r_nvalid<STEP, QP>(r.dw, r.g, p);
     nkept += __builtin_popcount(keep);
     uint32_t pos0;
-    const uint32_t wtotal = r_stage_colours<STEP>(keep, r.cw, wstage, pos0);
+    const uint32_t wtotal = r_stage_colours<STEP, QP>(keep, r.cw, wstage, pos0);
     bool cand = false;
     for (uint32_t j = lane; j < ((p.ablate & 512) ? 0u : wtotal); j += kWave) {   // ablate: DIAGNOSTIC ONLY
         const int bin = r_bin(wstage[j]);
@@ -313,38 +320,48 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 // Write outputs [a, b) of the frame from their LDS descriptors (slot = g mod
-// kRStage). Group = 4 outputs at a 16-byte-aligned position; lane j takes
-// groups j, j + 256, ... The next group's descriptors and delta-table words are
-// fetched before this group's stores: vmcnt counts loads and stores in issue
-// order, so a load issued after a store would wait for it.
-template <int STEP>
+// the stage size); groups of 4 outputs at 16-byte-aligned positions. The P
+// plane is written in whole lines: lane l's group (outputs
+// 4l..4l+3 of its wave's 256-output block) gives the X, Y, Z stores, and the
+// lane also produces the (x, y) pairs of outputs 2l, 2l+1 and 128+2l, 129+2l of
+// the block, so each of the two P stores covers 1 KiB contiguous (with one
+// group per lane, every P store would cover 2 KiB half-filled). The loop runs
+// over wave blocks, uniform per wave.
+template <int STEP, int QP>
 __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint32_t b, const PipeBuffers& bf,
-                                         float* oX, float* oY, float* oZ, int32_t* oP, const RParams& p) {
+                                               float* oX, float* oY, float* oZ, int32_t* oP, const RParams& p) {
+    constexpr uint32_t SM = stage_of<QP>() - 1;
     const uint32_t first = a & ~3u;
-    const uint32_t groups = (p.ablate & 16384) ? 0u : (b - first + 3) >> 2;   // ablate: DIAGNOSTIC ONLY
-    uint32_t m = threadIdx.x;
-    uint32_t u[4], wx[4], wy[4];
-    auto fetch = [&](uint32_t mm) {
-        const uint32_t g = first + 4 * mm;
-        const uint4 u4 = *reinterpret_cast<const uint4*>(&stage[g & (kRStage - 1)]);
-        u[0] = u4.x; u[1] = u4.y; u[2] = u4.z; u[3] = u4.w;
+    const uint32_t groups = (b - first + 3) >> 2;
+    const int lane = lane_id();
+    uint32_t m0 = threadIdx.x & ~63u;   // this wave's first group
+    uint32_t pu[4], wx[4], wy[4];       // P outputs 2l, 2l+1, 128+2l, 129+2l of the block
+    auto fetch = [&](uint32_t mm0) {
+        const uint32_t o = first + 4 * mm0 + 2 * lane;
+        const uint2 lo = *reinterpret_cast<const uint2*>(&stage[o & SM]);
+        const uint2 hi = *reinterpret_cast<const uint2*>(&stage[(o + 128) & SM]);
+        pu[0] = lo.x; pu[1] = lo.y; pu[2] = hi.x; pu[3] = hi.y;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            if (!(g + e >= a && g + e < b)) u[e] = 1u << 24;   // d = 1 at (0, 0): harmless filler
-            const uint32_t d = u[e] >> 24;
-            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
-            const int x = (int)(u[e] & 0xFFF) * STEP;
-            wx[e] = (p.ablate & 8192) ? 0u : bf.dxbits[d * p.dx_words + (x >> 5)];
-            wy[e] = (p.ablate & 8192) ? 0u : bf.dybits[d * p.dy_words + (y >> 5)];
+            const uint32_t oe = o + (e >> 1) * 128 + (e & 1);
+            if (!(oe >= a && oe < b)) pu[e] = 1u << 24;   // d = 1 at (0, 0): harmless filler
+            const uint32_t d = pu[e] >> 24;
+            const int y = (int)((pu[e] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(pu[e] & 0xFFF) * STEP;
+            wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
+            wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
         }
     };
-    if (m < groups) fetch(m);
-    while (m < groups) {
+    if (m0 < groups) fetch(m0);
+    while (m0 < groups) {   // uniform per wave
+        const uint32_t m = m0 + lane;
+        const uint32_t g = first + 4 * m;
+        const uint4 u4 = *reinterpret_cast<const uint4*>(&stage[g & SM]);
+        const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
         float X[4], Y[4], Z[4];
-        int PX[4], PY[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const uint32_t d = u[e] >> 24;
+            const uint32_t d = (u[e] >> 24) | (g + e < b ? 0u : 1u);   // no rcp(0) on slots past the end
             const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
             const int x = (int)(u[e] & 0xFFF) * STEP;
             const float rr = __builtin_amdgcn_rcpf((float)d);
@@ -352,53 +369,69 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
             X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
             Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
             Z[e] = p.fB32 * rr;
+        }
+        int PX[4], PY[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int y = (int)((pu[e] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(pu[e] & 0xFFF) * STEP;
             PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
             PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
         }
-        const uint32_t g = first + 4 * m;
-        const bool full = g >= a && g + 3 < b;
-        const uint32_t mn = m + 256;
+        const uint32_t o = first + 4 * m0 + 2 * lane;
+        const uint32_t mn = m0 + 256;
         if (mn < groups) fetch(mn);   // before the stores below
-        if (p.ablate & 4096) {   // diagnostic: keep the math live, no stores
-            if (X[0] == 12345.f) oX[g] = X[1] + Y[2] + Z[3] + (float)(PX[0] + PY[1] + PX[2] + PY[3]);
-        } else if (full) {   // 16-byte non-temporal stores: whole groups, lines filled in order
-            __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + g));
-            __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + g));
-            __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + g));
-            __builtin_nontemporal_store((v4i){PX[0], PY[0], PX[1], PY[1]}, reinterpret_cast<v4i*>(oP + 2 * (size_t)g));
-            __builtin_nontemporal_store((v4i){PX[2], PY[2], PX[3], PY[3]}, reinterpret_cast<v4i*>(oP + 2 * (size_t)g + 4));
-        } else {                // a frame's last group, or a rare early tail
+        if (m < groups) {
+            if (g >= a && g + 3 < b) {
+                __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + g));
+                __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + g));
+                __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + g));
+            } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (!(g + e >= a && g + e < b)) continue;
-                oX[g + e] = X[e];
-                oY[g + e] = Y[e];
-                oZ[g + e] = Z[e];
-                *reinterpret_cast<int2*>(oP + 2 * (size_t)(g + e)) = make_int2(PX[e], PY[e]);
+                for (int e = 0; e < 4; ++e) {
+                    if (!(g + e >= a && g + e < b)) continue;
+                    oX[g + e] = X[e];
+                    oY[g + e] = Y[e];
+                    oZ[g + e] = Z[e];
+                }
             }
         }
-        m = mn;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t oh = o + 128 * h;
+            if (oh >= a && oh + 1 < b) {
+                __builtin_nontemporal_store((v4i){PX[2 * h], PY[2 * h], PX[2 * h + 1], PY[2 * h + 1]},
+                                            reinterpret_cast<v4i*>(oP + 2 * (size_t)oh));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    if (oh + e >= a && oh + e < b)
+                        *reinterpret_cast<int2*>(oP + 2 * (size_t)(oh + e)) = make_int2(PX[2 * h + e], PY[2 * h + e]);
+                }
+            }
+        }
+        m0 = mn;
     }
 }
 
 // pass 2 of one chunk: keep2, block scan, descriptor scatter, then the
 // chunk's whole output groups. Two barriers. Loads chunk c + 1 into r before
 // the stores (PF).
-template <int STEP, bool PF, class SH>
-__device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, const uint32_t* hist,
+template <int STEP, int QP, bool PF, class SH>
+__device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, const uint32_t* hist,
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
                                          const uint8_t* fdisp, const uint8_t* fbgr, const uint16_t* tab,
                                          const PipeBuffers& bf, float* oX, int32_t* oP, uint32_t& running,
                                          uint32_t& flushed, const RParams& p) {
-    constexpr int QPL = RCfg<STEP>::QPL;
+    constexpr int QPL = RCfg<STEP, QP>::QPL;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    uint32_t keep = r_keep1<STEP>(r.dw, r.tw, r.g);
+    uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
     if ((dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: candidate chunk (rare)
-        uint32_t cw[QPL][RCfg<STEP>::CW];
-        r_load_bgr<STEP>(fbgr, r.g, p, cw);
+        uint32_t cw[QPL][RCfg<STEP, QP>::CW];
+        r_load_bgr<STEP, QP>(fbgr, r.g, p, cw);
         __syncthreads();   // every wave is done writing the previous chunk: sh.stage is free
         uint32_t pos0;
-        const uint32_t wtotal = r_stage_colours<STEP>(keep, cw, wstage, pos0);
+        const uint32_t wtotal = r_stage_colours<STEP, QP>(keep, cw, wstage, pos0);
         for (uint32_t j = lane; j < wtotal; j += kWave) {
             const int bin = r_bin(wstage[j]);
             wstage[j] = (int64_t)hist[bin] > (int64_t)p.hist_thr ? 1u : 0u;
@@ -440,9 +473,9 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, cons
                        (uint32_t)((tot >> 32) & 0xFFFF) + (uint32_t)((tot >> 48) & 0xFFFF);
     float* oY = oX + bf.cap;
     float* oZ = oY + bf.cap;
-    if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (kRStage - 1)] = sh.red[tid];   // the tail
-    if (T > (uint32_t)kRStage - (running - flushed)) {
-        p2_write<STEP>(sh.stage, flushed, running, bf, oX, oY, oZ, oP, p);
+    if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (stage_of<QP>() - 1)] = sh.red[tid];   // the tail
+    if (T > (uint32_t)stage_of<QP>() - (running - flushed)) {
+        p2_write<STEP, QP>(sh.stage, flushed, running, bf, oX, oY, oZ, oP, p);
         flushed = running;
     }
     uint32_t rowbase = running;
@@ -453,56 +486,65 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP>& r, int c, bool more, cons
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (keep & (1u << (4 * i + k))) {
-                const uint32_t d = r_d<STEP>(r.dw[i], k);
-                sh.stage[(o++) & (kRStage - 1)] = (d << 24) | ((uint32_t)r.g.gy[i] << 12) | (uint32_t)(4 * r.g.q[i] + k);
+                const uint32_t d = r_d<STEP, QP>(r.dw[i], k);
+                sh.stage[(o++) & (stage_of<QP>() - 1)] = (d << 24) | ((uint32_t)r.g.gy[i] << 12) | (uint32_t)(4 * r.g.q[i] + k);
             }
         }
     }
-    if (PF && more) p2_load<STEP>(r, c + 1, tid, fdisp, tab, p);   // next chunk in flight before the stores
+    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, p);   // next chunk in flight before the stores
     __syncthreads();
     running += T;
     const uint32_t upto = more ? (running & ~3u) : running;   // the last chunk flushes its tail
     // keep the new tail (< 4 descriptors) out of sh.stage's way: the next
     // chunk's dirty path may reuse sh.stage before its scatter restores them
-    if (tid < (int)(running - upto)) sh.red[tid] = sh.stage[(upto + tid) & (kRStage - 1)];
+    if (tid < (int)(running - upto)) sh.red[tid] = sh.stage[(upto + tid) & (stage_of<QP>() - 1)];
     if (upto > flushed) {
-        p2_write<STEP>(sh.stage, flushed, upto, bf, oX, oY, oZ, oP, p);
+        p2_write<STEP, QP>(sh.stage, flushed, upto, bf, oX, oY, oZ, oP, p);
         flushed = upto;
     }
 }
 
 // ---------------------------------------------------------------------------
-// One workgroup = one frame: pass 1 over all chunks, then pass 2 (grid = frames).
+// One frame's two passes as workgroup-level device functions. pass 1 leaves
+// the histogram and dirty bits in LDS and the valid/kept counts in sh.red.
 // ---------------------------------------------------------------------------
+template <int QP>
 struct FusedShared {
     uint32_t hist[kRBins];
-    uint32_t dirty[kRMaxChunks / 32];
+    uint32_t dirty[maxchunks_of<QP>() / 32];
     uint64_t wtot[4];
     uint32_t red[8];
-    uint32_t stage[kRStage];
+    uint32_t stage[stage_of<QP>()];
 };
-static_assert(sizeof(FusedShared) <= 20480, "8 workgroups per CU (160 KiB LDS)");
+static_assert(sizeof(FusedShared<4>) <= 20480, "8 workgroups per CU (160 KiB LDS)");
 
-template <int STEP, bool PF>
-__global__ __launch_bounds__(256) void resident_fused_kernel(PipeBuffers bf, const uint16_t* __restrict__ tab,
-                                                             RParams p) {
-    constexpr int QPL = RCfg<STEP>::QPL;
-    constexpr int WREGION = 64 * QPL * 4;
-    __shared__ FusedShared sh;
+template <int STEP, int QP, bool PF1 = false>
+__device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, const PipeBuffers& bf,
+                                            const uint16_t* tab, const RParams& p) {
+    constexpr int WREGION = 64 * RCfg<STEP, QP>::QPL * 4;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.x;
-    const int nch = p.nchunks;
     const uint8_t* fdisp = bf.disp + (int64_t)frame * p.frame_px;
     const uint8_t* fbgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
     uint32_t* wstage = sh.stage + wave * WREGION;
     for (int i = tid; i < kRBins; i += 256) sh.hist[i] = 0;
-    if (tid < kRMaxChunks / 32) sh.dirty[tid] = 0;
+    if (tid < maxchunks_of<QP>() / 32) sh.dirty[tid] = 0;
     __syncthreads();
     uint32_t nvalid = 0, nkept = 0;
-    for (int c = 0; c < ((p.ablate & 128) ? 0 : nch); ++c) {   // ablate: DIAGNOSTIC ONLY
-        P1Regs<STEP> r1;
-        p1_load<STEP>(r1, c, tid, fdisp, fbgr, tab, p);
-        p1_chunk<STEP>(r1, c, sh.hist, sh.dirty, wstage, p, nvalid, nkept);
+    const int n1 = (p.ablate & 128) ? 0 : p.nchunks;   // ablate: DIAGNOSTIC ONLY
+    if constexpr (PF1) {   // chunk c + 1's loads in flight while chunk c is binned (pass 1 stores nothing)
+        P1Regs<STEP, QP> r1;
+        if (n1 > 0) p1_load<STEP, QP>(r1, 0, tid, fdisp, fbgr, tab, p);
+        for (int c = 0; c < n1; ++c) {
+            P1Regs<STEP, QP> cur = r1;
+            if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, tab, p);
+            p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, wstage, p, nvalid, nkept);
+        }
+    } else {
+        for (int c = 0; c < n1; ++c) {
+            P1Regs<STEP, QP> r1;
+            p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, tab, p);
+            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, wstage, p, nvalid, nkept);
+        }
     }
     nvalid = wave_sum(nvalid);
     nkept = wave_sum(nkept);
@@ -511,45 +553,69 @@ __global__ __launch_bounds__(256) void resident_fused_kernel(PipeBuffers bf, con
         sh.red[4 + wave] = nkept;
     }
     __syncthreads();   // histogram, dirty bits, counts complete
-    {
-        uint32_t* gh = bf.hist + (int64_t)frame * kBins;
-        for (int b = tid; b < kBins; b += 256) gh[b] = b < kRBins ? sh.hist[b] : 0u;
-        if (tid == 0) {
-            int64_t* cn = bf.counts + 4 * (int64_t)frame;
-            cn[0] = (int64_t)sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
-            cn[1] = (int64_t)sh.red[4] + sh.red[5] + sh.red[6] + sh.red[7];
-        }
-    }
+}
+
+template <int STEP, int QP, bool PF>
+__device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, const PipeBuffers& bf,
+                                            const uint16_t* tab, const RParams& p) {
+    constexpr int WREGION = 64 * RCfg<STEP, QP>::QPL * 4;
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const uint8_t* fdisp = bf.disp + (int64_t)frame * p.frame_px;
+    const uint8_t* fbgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
+    uint32_t* wstage = sh.stage + wave * WREGION;
     float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap;
     int32_t* oP = bf.pts + (int64_t)frame * bf.cap * 2;
     uint32_t running = 0, flushed = 0;
-    const int n2 = (p.ablate & 256) ? 0 : nch;
-    P2Regs<STEP> r2;
-    if (PF && n2 > 0) p2_load<STEP>(r2, 0, tid, fdisp, tab, p);
+    const int n2 = (p.ablate & 256) ? 0 : p.nchunks;
+    P2Regs<STEP, QP> r2;
+    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, p);
     for (int c = 0; c < n2; ++c) {
-        if (!PF) p2_load<STEP>(r2, c, tid, fdisp, tab, p);
-        p2_chunk<STEP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
+        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, p);
+        p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
                            running, flushed, p);
     }
     if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;
 }
 
-bool resident_supported(const KParams& p) {
-    return (p.step == 1 || p.step == 2) && p.Wg <= 4096 && p.Hg <= 4096 &&
-           resident_chunks_per_frame(p) <= kRMaxChunks && p.frame_px * 3 < (1ll << 31);
+// ---------------------------------------------------------------------------
+// One workgroup = one frame: pass 1 over all chunks, then pass 2 (grid = frames).
+// ---------------------------------------------------------------------------
+template <int STEP, int QP, bool PF, bool PF1>
+__device__ __forceinline__ void fused_body(const PipeBuffers& bf, const uint16_t* __restrict__ tab, const RParams& p,
+                                           FusedShared<QP>& sh) {
+    const int tid = threadIdx.x;
+    const int frame = blockIdx.x;
+    frame_pass1<STEP, QP, PF1>(frame, sh, bf, tab, p);
+    uint32_t* gh = bf.hist + (int64_t)frame * kBins;
+    for (int b = tid; b < kBins; b += 256) gh[b] = b < kRBins ? sh.hist[b] : 0u;
+    if (tid == 0) {
+        int64_t* cn = bf.counts + 4 * (int64_t)frame;
+        cn[0] = (int64_t)sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
+        cn[1] = (int64_t)sh.red[4] + sh.red[5] + sh.red[6] + sh.red[7];
+    }
+    frame_pass2<STEP, QP, PF>(frame, sh, bf, tab, p);
 }
 
-hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, const uint16_t* tab, int frames,
-                                    bool prefetch, hipStream_t s) {
-    if (frames <= 0) return hipSuccess;
-    if (!resident_supported(kp)) return hipErrorInvalidValue;
+template <int STEP, int QP, bool PF, bool PF1 = false>
+__global__ __launch_bounds__(256) void resident_fused_kernel(PipeBuffers bf, const uint16_t* __restrict__ tab,
+                                                             RParams p) {
+    __shared__ FusedShared<QP> sh;
+    fused_body<STEP, QP, PF, PF1>(bf, tab, p, sh);
+}
+
+bool resident_supported(const KParams& p) {   // frame_quads <= 2^20: every QP's chunk count fits its dirty bits
+    return (p.step == 1 || p.step == 2) && p.Wg <= 4096 && p.Hg <= 4096 &&
+           resident_chunks_per_frame(p, 4) <= kRMaxChunks && p.frame_px * 3 < (1ll << 31);
+}
+
+static RParams resident_params(const KParams& kp, int qpl) {
     RParams p;
     p.W = kp.W;
     p.Wg = kp.Wg;
     p.Q = kp.Q;
     p.pitch = kp.pitch;
     p.frame_quads = kp.frame_quads;
-    p.nchunks = resident_chunks_per_frame(kp);
+    p.nchunks = resident_chunks_per_frame(kp, qpl);
     p.hist_thr = kp.hist_thr;
     p.dx_words = kp.dx_words;
     p.dy_words = kp.dy_words;
@@ -562,12 +628,24 @@ hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, con
     p.cw_lo = kp.cw_lo;
     p.ch_hi = kp.ch_hi;
     p.ch_lo = kp.ch_lo;
+    return p;
+}
+
+hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, const uint16_t* tab, int frames,
+                                    bool prefetch, hipStream_t s, bool prefetch1) {
+    if (frames <= 0) return hipSuccess;
+    if (!resident_supported(kp)) return hipErrorInvalidValue;
+    const dim3 grid(frames), block(256);
     if (kp.step == 1) {
-        if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, true>), dim3(frames), dim3(256), 0, s, b, tab, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<1, false>), dim3(frames), dim3(256), 0, s, b, tab, p);
+        const RParams p = resident_params(kp, 4);
+        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true>), grid, block, 0, s, b, tab, p);
+        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true>), grid, block, 0, s, b, tab, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, false>), grid, block, 0, s, b, tab, p);
     } else {
-        if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<2, true>), dim3(frames), dim3(256), 0, s, b, tab, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<2, false>), dim3(frames), dim3(256), 0, s, b, tab, p);
+        const RParams p = resident_params(kp, 2);
+        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<2, 2, true, true>), grid, block, 0, s, b, tab, p);
+        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<2, 2, true>), grid, block, 0, s, b, tab, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<2, 2, false>), grid, block, 0, s, b, tab, p);
     }
     return hipGetLastError();
 }

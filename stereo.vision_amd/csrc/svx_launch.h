@@ -61,7 +61,7 @@ hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, hip
 // One workgroup per frame (pass 1 then pass 2); prefetch = pass 2 loads the
 // next chunk before issuing this chunk's stores (costs registers).
 hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, const uint16_t* tab, int frames,
-                                    bool prefetch, hipStream_t s);
+                                    bool prefetch, hipStream_t s, bool prefetch1 = false);
 
 // kernels/prepass.hip ------------------------------------------------------
 // fillDisparity frame recurrence / fillAltDisparity row means / maskDisparity.

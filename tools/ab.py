@@ -4,7 +4,8 @@
 pipeline modes, alternated round-robin; prints the median ms per variant.
 DIAGNOSTIC: ablated runs produce invalid results.
 
-usage: ab.py --ablate 0,128,8320 --modes resident --rounds 5 --reps 3
+usage: ab.py --ablate 0,128,8320 --modes resident,split:512,split:1024 --rounds 5 --reps 3
+(a mode "split:L" runs the split schedule with SVX_SPLIT_LAG=L)
 """
 import argparse
 import json
@@ -24,6 +25,7 @@ def main():
     ap.add_argument("--frames", type=int, default=4096)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--k1", action="store_true", help="time K1 (project) instead of the pipeline")
     a = ap.parse_args()
     b = sb.Batch(a.frames, step=1, with_bgr=True, with_points=True)
     b.synth(0)
@@ -32,12 +34,16 @@ def main():
     for _ in range(a.rounds):
         for mode, abl in variants:
             os.environ["SVX_ABLATE"] = str(abl)
-            b.pipeline_mode(mode)
-            b.pipeline(sync=True)
+            m, _, lag = mode.partition(":")
+            if lag:
+                os.environ["SVX_SPLIT_LAG"] = lag
+            b.pipeline_mode(m)
+            run = (lambda sync: b.project(sync=sync)) if a.k1 else (lambda sync: b.pipeline(sync=sync))
+            run(True)
             b.reset_timing()
             for _ in range(a.reps):
-                b.pipeline(sync=False)
-            ms, n = b.timing("pipeline")
+                run(False)
+            ms, n = b.timing("project" if a.k1 else "pipeline")
             res[(mode, abl)].append(ms / n)
     os.environ["SVX_ABLATE"] = "0"
     for (mode, abl), v in res.items():

@@ -8,7 +8,7 @@ from collections import defaultdict
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 acc = defaultdict(lambda: defaultdict(list))
 dur = defaultdict(list)
-for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
+for f in sorted(set(glob.glob(f"{root}/p*/run_counter_collection.csv") + glob.glob(f"{root}/run_counter_collection.csv") + glob.glob(f"{root}/*/run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")[:48]
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
