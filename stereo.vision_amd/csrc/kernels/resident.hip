@@ -196,13 +196,6 @@ __device__ __forceinline__ uint32_t r_col(const uint32_t (&c)[RCfg<STEP, QP>::CW
     return sh == 0 ? c[w] : __builtin_amdgcn_alignbyte(hi, c[w], sh);
 }
 
-__device__ __forceinline__ int r_bin(uint32_t col) {
-    bool near;
-    int bin = hue_bin_fast(col, near);
-    if (__builtin_expect(near, 0))
-        bin = hue_bin((int)((col >> 16) & 0xFF), (int)((col >> 8) & 0xFF), (int)(col & 0xFF));
-    return bin;
-}
 
 // keep1 bits of this lane's chunk (bit 4i+k = point k of quad i): lo <= d <= hi.
 template <int STEP, int QP>
@@ -241,12 +234,32 @@ __device__ __forceinline__ uint32_t r_nvalid(const uint32_t (&dw)[RCfg<STEP, QP>
     return n;
 }
 
-// Pack the colours of the keep bits into this wave's LDS region, in (lane, bit)
-// order; returns the wave's total and this lane's first slot.
+// Hue bin as hue_bin_fast (svx_device.h), with the sector select written as
+// value selects so that no lane mask is branched on; the +-4e-4 band around a
+// half-integer takes the exact integer/fp64 path (hue_bin).
+__device__ __forceinline__ int r_bin_sel(uint32_t col) {
+    const int b = (int)(col & 0xFF), g = (int)((col >> 8) & 0xFF), r = (int)((col >> 16) & 0xFF);
+    const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
+    const int rng = mx - mn;
+    const int nr = g - b, ng = 2 * rng + b - r, nb = 4 * rng + r - g;
+    const int n = (r == mx) ? nr : ((g == mx) ? ng : nb);
+    const float t = ((float)n * __builtin_amdgcn_rcpf((float)rng)) * (500.0f / 3.0f);
+    const float rt = __builtin_rintf(t);
+    const bool near = __builtin_fabsf(t - rt) > 0.5f - 4e-4f;   // NaN (grey) -> false
+    int bin = (int)rt + (n < 0 ? 1000 : 0);
+    bin = rng == 0 ? 0 : bin;
+    if (__builtin_expect(near, 0)) bin = hue_bin(r, g, b);
+    return bin;
+}
+
+// Pack the colours of the keep bits into this wave's LDS region, (lane, bit)
+// order, without branching on lane masks: a point that is not kept writes its
+// colour to this lane's private dump slot instead. Returns the wave's total
+// and this lane's first slot.
 template <int STEP, int QP>
-__device__ __forceinline__ uint32_t r_stage_colours(uint32_t keep,
-                                                    const uint32_t (&cw)[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW],
-                                                    uint32_t* wstage, uint32_t& pos0) {
+__device__ __forceinline__ uint32_t r_stage_colours_sel(uint32_t keep,
+                                                        const uint32_t (&cw)[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW],
+                                                        uint32_t* wstage, uint32_t* dump, uint32_t& pos0) {
     const uint32_t cnt = __builtin_popcount(keep);
     const uint32_t inc = wave_incl_scan(cnt);
     pos0 = inc - cnt;
@@ -255,7 +268,9 @@ __device__ __forceinline__ uint32_t r_stage_colours(uint32_t keep,
     for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (keep & (1u << (4 * i + k))) wstage[pos++] = r_col<STEP, QP>(cw[i], k);
+            const uint32_t bit = (keep >> (4 * i + k)) & 1u;
+            *(bit ? wstage + pos : dump) = r_col<STEP, QP>(cw[i], k);
+            pos += bit;
         }
     }
     return __shfl(inc, 63, kWave);
@@ -300,18 +315,28 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, con
 // candidate mark into dirty. Wave-local (no barrier).
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint32_t* hist, uint32_t* dirty,
-                                         uint32_t* wstage, const RParams& p, uint32_t& nvalid, uint32_t& nkept) {
+                                         uint32_t* wstage, uint32_t* dump, const RParams& p, uint32_t& nvalid,
+                                         uint32_t& nkept) {
     const int lane = lane_id();
     const uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
     nvalid += r_nvalid<STEP, QP>(r.dw, r.g, p);
     nkept += __builtin_popcount(keep);
     uint32_t pos0;
-    const uint32_t wtotal = r_stage_colours<STEP, QP>(keep, r.cw, wstage, pos0);
     bool cand = false;
-    for (uint32_t j = lane; j < ((p.ablate & 512) ? 0u : wtotal); j += kWave) {   // ablate: DIAGNOSTIC ONLY
-        const int bin = r_bin(wstage[j]);
-        const uint32_t old = atomicAdd(&hist[bin], 1u);
-        cand |= (int64_t)old < (int64_t)p.hist_thr;
+    {
+        const uint32_t wtotal = r_stage_colours_sel<STEP, QP>(keep, r.cw, wstage, dump, pos0);
+        // a point is a candidate while its bin holds fewer than hist_thr points (never for hist_thr < 0)
+        const uint32_t lim = p.hist_thr < 0 ? 0u : (uint32_t)p.hist_thr;
+        for (uint32_t j = lane; j < ((p.ablate & 512) ? 0u : wtotal); j += 2 * kWave) {   // two colours in flight
+            const bool v1 = j + kWave < wtotal;
+            const uint32_t c0 = wstage[j];
+            const uint32_t c1 = wstage[v1 ? j + kWave : j];
+            const int b0 = r_bin_sel(c0), b1 = r_bin_sel(c1);
+            const uint32_t o0 = atomicAdd(&hist[b0], 1u);
+            uint32_t o1 = lim;
+            if (v1) o1 = atomicAdd(&hist[b1], 1u);
+            cand |= (o0 < lim) | (o1 < lim);
+        }
     }
     if (__ballot(cand) && lane == 0) atomicOr(&dirty[c >> 5], 1u << (c & 31));
 }
@@ -431,9 +456,9 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
         r_load_bgr<STEP, QP>(fbgr, r.g, p, cw);
         __syncthreads();   // every wave is done writing the previous chunk: sh.stage is free
         uint32_t pos0;
-        const uint32_t wtotal = r_stage_colours<STEP, QP>(keep, cw, wstage, pos0);
+        const uint32_t wtotal = r_stage_colours_sel<STEP, QP>(keep, cw, wstage, sh.dump + tid, pos0);
         for (uint32_t j = lane; j < wtotal; j += kWave) {
-            const int bin = r_bin(wstage[j]);
+            const int bin = r_bin_sel(wstage[j]);
             wstage[j] = (int64_t)hist[bin] > (int64_t)p.hist_thr ? 1u : 0u;
         }
         uint32_t pos = pos0;
@@ -515,8 +540,9 @@ struct FusedShared {
     uint64_t wtot[4];
     uint32_t red[8];
     uint32_t stage[stage_of<QP>()];
+    uint32_t dump[256];   // pass 1: one slot per lane for the colours of points that are not kept
 };
-static_assert(sizeof(FusedShared<4>) <= 20480, "8 workgroups per CU (160 KiB LDS)");
+static_assert(sizeof(FusedShared<4>) <= 32768, "5 workgroups per CU (160 KiB LDS); 4 are VGPR-resident");
 
 template <int STEP, int QP, bool PF1 = false>
 __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, const PipeBuffers& bf,
@@ -537,13 +563,13 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> cur = r1;
             if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, tab, p);
-            p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, wstage, p, nvalid, nkept);
+            p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, wstage, sh.dump + tid, p, nvalid, nkept);
         }
     } else {
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> r1;
             p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, tab, p);
-            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, wstage, p, nvalid, nkept);
+            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, wstage, sh.dump + tid, p, nvalid, nkept);
         }
     }
     nvalid = wave_sum(nvalid);
