@@ -363,63 +363,79 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
     float* oY = oX + bf.cap;
     float* oZ = oY + bf.cap;
     int32_t* oP = bf.pts + ((int64_t)frame * bf.cap + g0) * 2;
+    // Groups of 4 outputs at 16-byte-aligned slots: lane l of a wave stores the
+    // X, Y, Z of group m0 + l, and the (x, y) pairs of slots 4 m0 + 2l, +1 and
+    // 4 m0 + 128 + 2l, +1, so every store instruction covers 1 KiB contiguous
+    // (one group per lane would leave each P store's lines half-filled).
     const uint32_t groups = (end + 3) >> 2;
-    for (uint32_t m = tid; m < groups; m += 256) {
-        const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.desc[4 * m]);
-        const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
-        uint32_t wx[4], wy[4];
-        bool ok[4];
+    for (uint32_t m0 = tid & ~63u; m0 < groups; m0 += 256) {   // uniform per wave
+        const uint32_t m = m0 + lane;
+        const uint32_t sp = 4 * m0 + 2 * lane;   // first P slot of this lane
+        uint32_t pu[4], wx[4], wy[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {   // all table loads of the group in flight together
-            const uint32_t s_ = 4 * m + e;
-            ok[e] = s_ >= lead && s_ < end;
-            const uint32_t uu = ok[e] ? u[e] : (1u << 24);
+        for (int e = 0; e < 4; ++e) {   // all table loads in flight together
+            const uint32_t se = sp + (e >> 1) * 128 + (e & 1);
+            const uint32_t uu = (se >= lead && se < end) ? sh.desc[se] : (1u << 24);
+            pu[e] = uu;
             const uint32_t d = uu >> 24;
             const int y = (int)((uu >> 12) & 0xFFF) * STEP;
             const int x = (int)(uu & 0xFFF) * STEP;
-            wx[e] = (p.ablate & 8) ? 0u : bf.dxbits[d * p.dx_words + (x >> 5)];
-            wy[e] = (p.ablate & 8) ? 0u : bf.dybits[d * p.dy_words + (y >> 5)];
+            wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
+            wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
         }
-        float X[4], Y[4], Z[4];
+        if (m < groups) {
+            const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.desc[4 * m]);
+            const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
+            float X[4], Y[4], Z[4];
+            bool ok[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t s_ = 4 * m + e;
+                ok[e] = s_ >= lead && s_ < end;
+                const uint32_t uu = ok[e] ? u[e] : (1u << 24);
+                const uint32_t d = uu >> 24;
+                const int y = (int)((uu >> 12) & 0xFFF) * STEP;
+                const int x = (int)(uu & 0xFFF) * STEP;
+                const float r = __builtin_amdgcn_rcpf((float)d);
+                const float K = p.B32 * r;
+                X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
+                Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
+                Z[e] = p.fB32 * r;
+            }
+            if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
+                __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + 4 * m));
+                __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + 4 * m));
+                __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + 4 * m));
+            } else {                // the tile's first / last group
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (!ok[e]) continue;
+                    oX[4 * m + e] = X[e];
+                    oY[4 * m + e] = Y[e];
+                    oZ[4 * m + e] = Z[e];
+                }
+            }
+        }
         int PX[4], PY[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const uint32_t uu = ok[e] ? u[e] : (1u << 24);
-            const uint32_t d = uu >> 24;
-            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
-            const int x = (int)(uu & 0xFFF) * STEP;
-            const float r = __builtin_amdgcn_rcpf((float)d);
-            const float K = p.B32 * r;
-            X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
-            Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
-            Z[e] = p.fB32 * r;
+            const int y = (int)((pu[e] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(pu[e] & 0xFFF) * STEP;
             PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
             PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
         }
-        if (p.ablate & 4) {
-            if (X[0] == 12345.f) oX[4 * m] = X[1] + Y[2] + Z[3] + (float)(PX[0] + PY[1]);   // keep the math live
-            continue;
-        }
-        if (ok[0] && ok[3] && (p.ablate & 16)) {   // diagnostic: plain stores
-            *reinterpret_cast<v4f*>(oX + 4 * m) = (v4f){X[0], X[1], X[2], X[3]};
-            *reinterpret_cast<v4f*>(oY + 4 * m) = (v4f){Y[0], Y[1], Y[2], Y[3]};
-            *reinterpret_cast<v4f*>(oZ + 4 * m) = (v4f){Z[0], Z[1], Z[2], Z[3]};
-            *reinterpret_cast<v4i*>(oP + 8 * m) = (v4i){PX[0], PY[0], PX[1], PY[1]};
-            *reinterpret_cast<v4i*>(oP + 8 * m + 4) = (v4i){PX[2], PY[2], PX[3], PY[3]};
-        } else if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
-            __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + 4 * m));
-            __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + 4 * m));
-            __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + 4 * m));
-            __builtin_nontemporal_store((v4i){PX[0], PY[0], PX[1], PY[1]}, reinterpret_cast<v4i*>(oP + 8 * m));
-            __builtin_nontemporal_store((v4i){PX[2], PY[2], PX[3], PY[3]}, reinterpret_cast<v4i*>(oP + 8 * m + 4));
-        } else {                // the tile's first / last group
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (!ok[e]) continue;
-                oX[4 * m + e] = X[e];
-                oY[4 * m + e] = Y[e];
-                oZ[4 * m + e] = Z[e];
-                *reinterpret_cast<int2*>(oP + 2 * (4 * m + e)) = make_int2(PX[e], PY[e]);
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t sh_ = sp + 128 * h;
+            if (sh_ >= lead && sh_ + 1 < end) {
+                __builtin_nontemporal_store((v4i){PX[2 * h], PY[2 * h], PX[2 * h + 1], PY[2 * h + 1]},
+                                            reinterpret_cast<v4i*>(oP + 2 * (size_t)sh_));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    if (sh_ + e >= lead && sh_ + e < end)
+                        *reinterpret_cast<int2*>(oP + 2 * (size_t)(sh_ + e)) = make_int2(PX[2 * h + e], PY[2 * h + e]);
+                }
             }
         }
     }

@@ -666,7 +666,7 @@ hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, con
         const RParams p = resident_params(kp, 4);
         if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true>), grid, block, 0, s, b, tab, p);
         else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true>), grid, block, 0, s, b, tab, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, false>), grid, block, 0, s, b, tab, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, false>), grid, block, 0, s, b, tab, p);   // no prefetch
     } else {
         const RParams p = resident_params(kp, 2);
         if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<2, 2, true, true>), grid, block, 0, s, b, tab, p);

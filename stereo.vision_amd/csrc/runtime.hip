@@ -228,8 +228,8 @@ struct sv_batch {
     bool have_ms[2] = {false, false};
     int qpl = 1;               // K1 quads per lane (1, 2 or 4)
     int nontemporal = 1;       // K1 store flavour (non-temporal: measured faster)
-    int pipe_mode = 0;         // 0 auto, 1 tiled (pipeline.hip), 2 frame-resident (resident.hip),
-                               // 3 same without pass-2 prefetch, 4 same with pass-1 prefetch
+    int pipe_mode = 0;         // 0 auto, 1 tiled (pipeline.hip), 2 frame-resident (resident.hip, both
+                               // passes prefetch the next chunk), 3 same without prefetch, 4 pass-2 prefetch only
     // per-launch timing accumulator: event pairs recorded on the batch stream
     std::vector<hipEvent_t> pool;
     std::vector<std::pair<int, int>> pending[2];  // (start idx, end idx) per op kind
@@ -556,7 +556,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
         HIP_TRY(hipMemcpyAsync(b->ktab_err_host, terr, 4, hipMemcpyDeviceToHost, b->stream));
         HIP_TRY(hipStreamSynchronize(b->stream));
         if (*b->ktab_err_host) goto tiled;   // a keep set that is not one interval: exact tiled kernels
-        HIP_TRY(launch_pipeline_resident(p, bf, tab, b->frames, mode != 3, b->stream, mode == 4));
+        HIP_TRY(launch_pipeline_resident(p, bf, tab, b->frames, mode != 3, b->stream, mode == 2));
         HIP_TRY(b->timed_event(&t1));
         HIP_TRY(hipEventRecord(b->ev[3], b->stream));
         b->pending[1].push_back({t0, t1});
@@ -622,8 +622,8 @@ int sv_batch_read_frame_plane(sv_batch* b, int frame, double* out4) {
 int sv_batch_pipeline_mode(sv_batch* b, int mode) {
     if (!b) return fail(SV_E_ARG, "null batch");
     if (mode < 0 || mode > 4)
-        return fail(SV_E_ARG, "pipeline mode must be 0 (auto), 1 (tiled), 2 (resident), 3 (resident, no pass-2 "
-                              "prefetch) or 4 (resident, pass-1 prefetch)");
+        return fail(SV_E_ARG, "pipeline mode must be 0 (auto), 1 (tiled), 2 (resident), 3 (resident, no prefetch) "
+                              "or 4 (resident, pass-2 prefetch only)");
     b->pipe_mode = mode;
     return SV_OK;
 }

@@ -70,7 +70,7 @@ class Batch:
         """K1 launch shape: quads per lane (1, 2, 4) and non-temporal stores."""
         _abi.call("sv_batch_tune", self._h, int(qpl), int(nontemporal))
 
-    PIPE_MODES = {"auto": 0, "tiled": 1, "resident": 2, "resident_nopf": 3, "pf1": 4}
+    PIPE_MODES = {"auto": 0, "tiled": 1, "resident": 2, "resident_nopf": 3, "resident_pf2": 4}
 
     def pipeline_mode(self, mode="auto"):
         """Pipeline kernel family: "auto", "tiled" (tiles across workgroups) or

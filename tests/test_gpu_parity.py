@@ -219,7 +219,7 @@ def _pipe(svx_mod, kind, disp, bgr, step, **kw):
         return dict(counts=tuple(int(v) for v in b.read_counts()[0]), hist=b.read_hist(0), pts=pts, xyz2=xyz)
 
 
-KINDS = ["frame", "resident", "resident_nopf", "pf1"]
+KINDS = ["frame", "resident", "resident_nopf", "resident_pf2"]
 
 
 @pytest.mark.parametrize("kind", KINDS)
@@ -305,7 +305,7 @@ def test_batch_dense_projection(svx_mod, step, tune):
 @pytest.mark.parametrize("step,chunk,mode", [(1, 16, "tiled"), (1, 3, "tiled"), (2, 1, "tiled"),
                                              (2, 5, "tiled"), (1, 0, "resident"), (2, 0, "resident"),
                                              (1, 0, "resident_nopf"), (1, 3, "resident_nopf"), (2, 2, "resident_nopf"),
-                                             (1, 0, "pf1"), (2, 0, "pf1")])
+                                             (1, 0, "resident_pf2"), (2, 0, "resident_pf2")])
 def test_batch_pipeline(svx_mod, step, chunk, mode):
     frames, first = 7, 1000
     with svx_mod.batch.Batch(frames, step=step, with_bgr=True, with_points=True) as b:
@@ -354,7 +354,7 @@ def test_batch_baseline_size_properties(svx_mod):
         assert np.array_equal(b.read_hist(4095), h16)
         x29, p29 = b.read_points(4095)
         assert np.array_equal(p29, p16) and np.array_equal(x29, x16)
-        for mode in ("resident", "resident_nopf", "pf1"):
+        for mode in ("resident", "resident_nopf", "resident_pf2"):
             b.pipeline_mode(mode)
             b.pipeline()
             assert np.array_equal(b.read_counts(), c16)
