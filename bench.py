@@ -52,7 +52,7 @@ def parse():
                     help="untimed K1 launches before the warmup steps, to let clocks settle")
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-latency", action="store_true",
-                    help="skip the 1-frame latency probe (keeps K1's rocprof average = 4096-frame launches)")
+                    help="skip the 1-frame latency probe")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the SURVEY §8f component timings")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -225,6 +225,10 @@ def extras(b, sb, args, device, with_cpu):
 def latency_1frame(sb, step, first, device):
     """configs[1]: one 1024x544 frame, step 1: K1 kernel time (HIP events), us."""
     with sb.Batch(1, H, W, step, with_bgr=False, device=device) as one:
+        # K1's plain-store instance (same grid, one quad per lane): its 1-frame
+        # launches are a rocprof row of their own, so the batch launches'
+        # average stays unmixed
+        one.tune(1, 0)
         one.synth(first)
         for _ in range(5):
             one.project(sync=False)

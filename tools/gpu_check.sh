@@ -11,14 +11,17 @@ TESTS="${TESTS:-tests}"
 timeout -k 10 "${PYTEST_LIMIT:-900}" python -m pytest $TESTS -m gpu -q ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -25 "$OUT/pytest_gpu.log"; stop_if_fatal $rc pytest
 [ "${SKIP_BENCH:-0}" = 1 ] && exit 0
-timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 5} > "$OUT/bench.log" 2>&1
-rc=$?; echo "bench rc=$rc"; tail -5 "$OUT/bench.log"; stop_if_fatal $rc bench
-if [ "${SKIP_PROF:-0}" != 1 ]; then
+# The bench runs once, under rocprofv3 --kernel-trace --stats, so the JSON line
+# (HIP-event kernel times) and the kernel stats come from the same process.
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-  python3 bench.py --steps 5 --warmup 1 --no-cpu --no-latency > "$OUT/prof.log" 2>&1
-rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"; stop_if_fatal $rc rocprof
-find "$OUT/prof" -name "*stats*" | head
+if [ "${SKIP_PROF:-0}" != 1 ]; then
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+    python3 bench.py ${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 10} > "$OUT/bench.log" 2>&1
+  rc=$?; echo "bench (rocprof) rc=$rc"; tail -2 "$OUT/bench.log"; stop_if_fatal $rc bench
+  find "$OUT/prof" -name "*stats*" | head
+else
+  timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 2 --cpu-seconds 10} > "$OUT/bench.log" 2>&1
+  rc=$?; echo "bench rc=$rc"; tail -2 "$OUT/bench.log"; stop_if_fatal $rc bench
 fi
 if [ -n "${SWEEP:-}" ]; then
   timeout -k 10 600 python tools/sweep.py $SWEEP > "$OUT/sweep.log" 2>&1
