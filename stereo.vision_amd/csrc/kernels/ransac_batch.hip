@@ -28,6 +28,12 @@
 
 namespace svx {
 
+// A maskpoint as (x, y, d) pixel coordinates in one word: x | y << 12 | d << 24
+// (W, H <= 4096). Its fp64 X, Y, Z are a function of these (functions.py:191-193).
+__device__ __forceinline__ uint32_t rb_pack(int x, int y, uint32_t d) {
+    return (uint32_t)x | ((uint32_t)y << 12) | (d << 24);
+}
+
 // ---------------------------------------------------------------------------
 // maskpoints: step-2 grid of the (optionally masked) disparity -> fp64 XYZ
 // ---------------------------------------------------------------------------
@@ -38,17 +44,20 @@ namespace svx {
 struct MaskpointsShared {
     uint32_t wtot[4];
     double stage[3 * 1024];
+    uint32_t pk[1024];
 };
 
 __global__ __launch_bounds__(256) void maskpoints_kernel(const uint8_t* __restrict__ disp,
                                                          const uint8_t* __restrict__ mask_ff, int64_t frame_px,
                                                          int H, int W, KParams p, double* __restrict__ out,
-                                                         int64_t cap, int64_t* __restrict__ counts) {
+                                                         uint32_t* __restrict__ packed, int64_t cap,
+                                                         int64_t* __restrict__ counts) {
     __shared__ MaskpointsShared sh;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.x;
     const uint8_t* fd = disp + (int64_t)frame * frame_px;
     double* fo = out + (int64_t)frame * cap * 3;
+    uint32_t* fpk = packed + (int64_t)frame * cap;
     const int Hg = H / 2, Wg = W / 2;   // range(0, H-1, 2) x range(0, W-1, 2)
     const int Wq = (Wg + 3) / 4;
     const int64_t nq = (int64_t)Hg * Wq;
@@ -108,21 +117,24 @@ __global__ __launch_bounds__(256) void maskpoints_kernel(const uint8_t* __restri
             sh.stage[3 * o + 0] = X;
             sh.stage[3 * o + 1] = Y;
             sh.stage[3 * o + 2] = Z;
+            sh.pk[o] = rb_pack(x, y, dv[k]);
             ++o;
         }
         __syncthreads();   // sh.stage complete; sh.wtot free
         double* dst = fo + 3 * (int64_t)running;
         for (uint32_t j = tid; j < 3 * tot; j += 256) __builtin_nontemporal_store(sh.stage[j], dst + j);
+        for (uint32_t j = tid; j < tot; j += 256) fpk[running + j] = sh.pk[j];
         running += tot;
     }
     if (tid == 0) counts[frame] = running;
 }
 
 hipError_t launch_maskpoints(const uint8_t* disp, const uint8_t* mask_ff, int frames, int H, int W, const KParams& p,
-                             double* out, int64_t cap, int64_t* counts, hipStream_t s) {
+                             double* out, uint32_t* packed, int64_t cap, int64_t* counts, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
+    if (H > 4096 || W > 4096) return hipErrorInvalidValue;   // rb_pack's 12-bit coordinates
     hipLaunchKernelGGL(maskpoints_kernel, dim3(frames), dim3(256), 0, s, disp, mask_ff, (int64_t)H * W, H, W, p, out,
-                       cap, counts);
+                       packed, cap, counts);
     return hipGetLastError();
 }
 
@@ -143,7 +155,7 @@ constexpr uint32_t kRBMaxDraws = 1u << 28;
 
 struct RansacShared {
     uint32_t mt[624];
-    uint32_t tout[2][624];                    // tempered outputs of twists t (slot t & 1)
+    uint32_t tout[3][624];                    // tempered outputs of twists t (slot t % 3)
     union {
         uint32_t bitmap[kRBBitmapWords];      // set branch: selected indices of the current sample
         int32_t pool[kRBBitmapWords];         // pool branch: the shrinking list
@@ -151,7 +163,9 @@ struct RansacShared {
     int32_t idx[2][kRBMaxK];                  // per trial (double-buffered): the sample
     double tri[2][12];                        // abc[3], d, flag, then P1..P3 unused (padding)
     double red[4];
+    double bnd[4];
     uint32_t misc[8];
+    uint32_t dummy[64];                       // claims of rejected draws (one word a lane)
 };
 static_assert(sizeof(RansacShared) <= 40960, "4 workgroups per CU");
 
@@ -199,34 +213,44 @@ __device__ __forceinline__ uint32_t rb_temper(uint32_t y) {
     return y;
 }
 
-// One MT19937 twist of mt (in place, one wave, ascending 64-word steps: every
-// step reads its inputs before writing, which is what the sequential in-place
-// recurrence needs) and its tempered outputs into out.
-__device__ void rb_twist(uint32_t* mt, uint32_t* out) {
+// One MT19937 twist of mt (in place, one wave) and its tempered outputs into
+// out. The sequential in-place recurrence new[kk] = f(old[kk], old[kk+1],
+// src) reads src = old[kk+397] for kk < 227 and new[kk-227] above, so it has
+// three dependency levels: [0, 227) from old words only, [227, 454) from level
+// 1, [454, 624) from level 2 (word 623 also reads new[0]). Within a level every
+// lane reads all its inputs (up to 4 words a lane) before any lane writes, so
+// no read sees a word of its own level already replaced.
+__device__ __forceinline__ void rb_twist_level(uint32_t* mt, uint32_t* out, int lo, int hi) {
     constexpr uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, A = 0x9908b0dfu;
     const int lane = lane_id();
-    for (int b = 0; b < 623; b += 64) {
-        const int kk = b + lane;
-        uint32_t nv = 0;
-        if (kk < 623) {
-            const uint32_t y = (mt[kk] & UPPER) | (mt[kk + 1] & LOWER);
+    uint32_t nv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int kk = lo + lane + 64 * j;
+        nv[j] = 0;
+        if (kk < hi) {
+            const uint32_t nxt = mt[kk == 623 ? 0 : kk + 1];
+            const uint32_t y = (mt[kk] & UPPER) | (nxt & LOWER);
             const uint32_t src = kk < 227 ? mt[kk + 397] : mt[kk - 227];
-            nv = src ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+            nv[j] = src ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
         }
-        rb_wave_lds_sync();   // every read of this step before any write of it
-        if (kk < 623) mt[kk] = nv;
-        rb_wave_lds_sync();   // later steps read kk - 227 and kk + 1 written here
     }
-    if (lane == 0) {
-        const uint32_t y = (mt[623] & UPPER) | (mt[0] & LOWER);
-        mt[623] = mt[396] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    rb_wave_lds_sync();   // every read of this level before any write of it
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int kk = lo + lane + 64 * j;
+        if (kk < hi) {
+            mt[kk] = nv[j];
+            out[kk] = rb_temper(nv[j]);
+        }
     }
-    rb_wave_lds_sync();
-    for (int b = 0; b < 624; b += 64) {
-        const int kk = b + lane;
-        if (kk < 624) out[kk] = rb_temper(mt[kk]);
-    }
-    rb_wave_lds_sync();
+    rb_wave_lds_sync();   // the next level reads this one's words
+}
+
+__device__ void rb_twist(uint32_t* mt, uint32_t* out) {
+    rb_twist_level(mt, out, 0, 227);
+    rb_twist_level(mt, out, 227, 454);
+    rb_twist_level(mt, out, 454, 624);
 }
 
 struct RbStream {   // wave 0's view of the frame's output stream
@@ -237,13 +261,13 @@ struct RbStream {   // wave 0's view of the frame's output stream
 // make outputs [pos, pos + 64) available (at most one new twist per call)
 __device__ __forceinline__ void rb_ensure(RansacShared& sh, RbStream& st) {
     while (st.pos + 64 > 624 * st.twists) {
-        rb_twist(sh.mt, sh.tout[st.twists & 1]);
+        rb_twist(sh.mt, sh.tout[st.twists % 3]);
         ++st.twists;
     }
 }
 
 __device__ __forceinline__ uint32_t rb_word(const RansacShared& sh, uint32_t q) {
-    return sh.tout[(q / 624) & 1][q % 624];
+    return sh.tout[(q / 624) % 3][q % 624];
 }
 
 // numpy.cross(P1 - P2, P2 - P3) all zero (functions.py:255-258); products rounded first
@@ -266,75 +290,99 @@ __device__ void rb_draw_below(RansacShared& sh, RbStream& st, uint32_t n, int kb
         while (acc && got < m) {
             const int l = __builtin_ctzll(acc);
             acc &= acc - 1;
-            out[got++] = __shfl(r, l, kWave);
+            out[got++] = __builtin_amdgcn_readlane(r, l);   // l is wave-uniform: a scalar read
             last = l;
         }
         st.pos += (got == m) ? (uint32_t)(last + 1) : 64u;
     }
 }
 
-// outputs [pos, pos + span) available, span <= 128 (two twist slots suffice)
+// outputs [pos, pos + span) available, span <= 1024 (three twist slots suffice)
 __device__ __forceinline__ void rb_ensure_span(RansacShared& sh, RbStream& st, uint32_t span) {
     while (st.pos + span > 624 * st.twists) {
-        rb_twist(sh.mt, sh.tout[st.twists & 1]);
+        rb_twist(sh.mt, sh.tout[st.twists % 3]);
         ++st.twists;
     }
 }
 
 // wave 0: random.sample(range(n), k) into idx (set branch), then clear the bits.
-// One LDS round trip per 64 draws: atomicOr claims each accepted draw's bit and
-// its return says whether the bit was already set. A set bit means either an
-// index selected by an earlier batch (rejected) or a value drawn twice in this
-// batch; those (rare) values are resolved by ballots: if some lane saw the bit
-// clear, the value is new and its lowest lane (earliest draw) wins, otherwise it
-// was selected before and every lane drawing it is rejected. The next window is
-// read while this one is processed.
+// A round takes kRBWin windows of 64 draws (stream positions pos + 64 w + lane):
+// every accepted draw claims its index bit with atomicOr, whose return says
+// whether the bit was already set. LDS executes one wave's operations in
+// order, so a window sees the claims of every earlier window; a set bit means
+// an index selected earlier (rejected) or a value drawn twice in the same
+// window, resolved by ballots: if some lane saw the bit clear, the value is new
+// and its lowest lane (earliest draw) wins, otherwise every lane drawing it is
+// rejected. The k-th selection in stream order ends the sample; bits claimed
+// past it are released and the stream resumes right after it.
+constexpr int kRBWin = 12;   // 768 draws a round: two rounds for a 600-point sample at n ~ 65k points
+
 __device__ void rb_sample_set(RansacShared& sh, RbStream& st, uint32_t n, int kb, int k, int32_t* idx) {
     const int lane = lane_id();
-    int have = 0;
-    rb_ensure_span(sh, st, 128);
-    uint32_t w = rb_word(sh, st.pos + lane);
+    int have = 0, round0 = 0;   // round0: picks made before the current round
+    uint32_t keptm = 0;         // this lane's picks of the current round (bit w: window w)
+    uint32_t r[kRBWin];
     while (have < k && st.pos < kRBMaxDraws) {
-        const uint32_t wn = rb_word(sh, st.pos + 64 + lane);   // the next window, in flight
-        const uint32_t r = w >> (32 - kb);
-        const bool acc = r < n;
-        const uint32_t bit = 1u << (r & 31);
-        const uint32_t old = acc ? atomicOr(&sh.bitmap[r >> 5], bit) : 0u;
-        const bool hit = acc && (old & bit);
-        uint64_t hm = __ballot(hit);
-        uint64_t rej = hm;
-        while (hm) {   // rare
-            const int l = __builtin_ctzll(hm);
-            const uint32_t v = __shfl(r, l, kWave);
-            const uint64_t eq = __ballot(acc && r == v);
-            const uint64_t fresh = __ballot(acc && r == v && !(old & bit));
-            hm &= ~eq;
-            rej = fresh ? ((rej & ~eq) | (eq & (eq - 1))) : (rej | eq);
+        round0 = have;
+        keptm = 0;
+        rb_ensure_span(sh, st, 64 * kRBWin);
+        const uint32_t* ring = &sh.tout[0][0];    // outputs q at ring[q mod 3 * 624]
+        const uint32_t base = st.pos % (3 * 624);
+        uint32_t old[kRBWin];
+#pragma unroll
+        for (int w = 0; w < kRBWin; ++w) {
+            uint32_t i = base + 64 * w + lane;
+            i -= i >= 3 * 624 ? 3 * 624 : 0;
+            r[w] = ring[i] >> (32 - kb);
         }
-        const bool sel = acc && !((rej >> lane) & 1ull);
-        const uint64_t sm = __ballot(sel);
-        const int need = k - have;
-        int cut = 63;   // the last lane this sample consumes
-        if (__builtin_popcountll(sm) >= need) {
-            uint64_t t = sm;
-            for (int q = 1; q < need; ++q) t &= t - 1;
-            cut = __builtin_ctzll(t);
+#pragma unroll
+        for (int w = 0; w < kRBWin; ++w) {   // claims issued in window order; rejected draws or a lane's dummy word
+            const bool acc = r[w] < n;
+            uint32_t* a = acc ? &sh.bitmap[r[w] >> 5] : &sh.dummy[lane];
+            old[w] = atomicOr(a, acc ? 1u << (r[w] & 31) : 0u);
         }
-        if (sel) {
-            if (lane <= cut) idx[have + __builtin_popcountll(sm & ((1ull << lane) - 1))] = (int32_t)r;
-            else atomicAnd(&sh.bitmap[r >> 5], ~bit);   // drawn by the next consumer, not this sample
+        // Selections are numbered in stream order from `have`; number q < k is the
+        // sample's q-th pick, q >= k was drawn past the sample's end (its claim is
+        // released). The pick numbered k - 1 fixes where the stream resumes.
+        uint32_t consumed = 64u * kRBWin;
+        int q0 = have;
+#pragma unroll
+        for (int w = 0; w < kRBWin; ++w) {
+            const bool acc = r[w] < n;
+            const uint32_t bit = 1u << (r[w] & 31);
+            uint64_t hm = __ballot(acc && (old[w] & bit));
+            uint64_t rej = hm;
+            while (hm) {   // rare
+                const int l = __builtin_ctzll(hm);
+                const uint32_t v = __builtin_amdgcn_readlane(r[w], l);   // uniform lane: no LDS round trip
+                const uint64_t eq = __ballot(acc && r[w] == v);
+                const uint64_t fresh = __ballot(acc && r[w] == v && !(old[w] & bit));
+                hm &= ~eq;
+                rej = fresh ? ((rej & ~eq) | (eq & (eq - 1))) : (rej | eq);
+            }
+            const bool sel = acc && !((rej >> lane) & 1ull);
+            const uint64_t sm = __ballot(sel);
+            const int q = q0 + (int)__builtin_popcountll(sm & ((1ull << lane) - 1));
+            if (sel) {
+                if (q < k) idx[q] = (int32_t)r[w];
+                else atomicAnd(&sh.bitmap[r[w] >> 5], ~bit);
+            }
+            keptm |= (uint32_t)(sel && q < k) << w;
+            const uint64_t lastm = __ballot(sel && q == k - 1);
+            if (lastm) consumed = 64u * w + (uint32_t)__builtin_ctzll(lastm) + 1u;
+            q0 += (int)__builtin_popcountll(sm);
         }
-        have += __builtin_popcountll(cut == 63 ? sm : sm & ((2ull << cut) - 1));
-        st.pos += (uint32_t)(cut + 1);
-        rb_wave_lds_sync();   // the next batch reads bits set/cleared by other lanes
-        if (have < k) {       // the whole window was consumed: wn is the next one
-            w = wn;
-            rb_ensure_span(sh, st, 128);
-        }
+        have = q0 < k ? q0 : k;
+        st.pos += consumed;
+        rb_wave_lds_sync();   // the next round reads bits set/cleared by other lanes
     }
-    for (int q = lane; q < have; q += kWave) {
-        const uint32_t r = (uint32_t)idx[q];
-        atomicAnd(&sh.bitmap[r >> 5], ~(1u << (r & 31)));
+    // clear the sample's bits: the last round's picks from registers, earlier ones from idx
+#pragma unroll
+    for (int w = 0; w < kRBWin; ++w)
+        if ((keptm >> w) & 1u) atomicAnd(&sh.bitmap[r[w] >> 5], ~(1u << (r[w] & 31)));
+    for (int q = lane; q < round0; q += kWave) {
+        const uint32_t v = (uint32_t)idx[q];
+        atomicAnd(&sh.bitmap[v >> 5], ~(1u << (v & 31)));
     }
     rb_wave_lds_sync();
 }
@@ -357,8 +405,10 @@ __device__ void rb_sample_pool(RansacShared& sh, RbStream& st, uint32_t n, int k
     rb_wave_lds_sync();   // idx (and the trace) read by every lane next
 }
 
-__global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restrict__ pts, int64_t cap,
-                                                           const int64_t* __restrict__ counts, uint64_t seed_base,
+__global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __restrict__ pts,
+                                                           const uint32_t* __restrict__ packed, int64_t cap,
+                                                           KParams cp, const int64_t* __restrict__ counts,
+                                                           uint64_t seed_base,
                                                            int64_t first_frame, int trials, int k,
                                                            double* __restrict__ out_abc, double* __restrict__ out_err,
                                                            int32_t* __restrict__ out_trial,
@@ -370,6 +420,7 @@ __global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restr
     const int frame = blockIdx.x;
     const int64_t n64 = counts[frame];
     const double* fp = pts + (int64_t)frame * cap * 3;
+    const uint32_t* fpk = packed + (int64_t)frame * cap;
     if (n64 < k || trials <= 0) {   // every trial's random.sample raises: (None, None)
         if (tid == 0) {
             out_trial[frame] = -1;
@@ -406,6 +457,7 @@ __global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restr
             int32_t* idx = sh.idx[buf];
             if (pool) rb_sample_pool(sh, st, n, k, idx);
             else rb_sample_set(sh, st, n, kb, k, idx);
+
             uint32_t t3[3] = {0, 0, 0};
             const double *p1, *p2, *p3;
             int attempts = 0;
@@ -463,38 +515,97 @@ __global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restr
                 sh.tri[buf][4] = fl;
             }
         }
+        // Waves 1-3 screen trial s - 1 in fp32 from the packed points (one 4-byte
+        // gather a point), with a rigorous bound on the difference to the fp64
+        // mean; only a trial that could beat (or tie within 1e-9) the best so
+        // far is then evaluated in fp64 exactly as before (functions.py:289-293).
+        // A random sequence sets a new minimum ~ln(trials) times, so nearly
+        // every trial is decided by the screen.
         if (wave != 0 && s > 0 && !(ablate & 1)) {   // DIAGNOSTIC 1: no evaluation
             const int pb = buf ^ 1;
-            const double a = sh.tri[pb][0], b = sh.tri[pb][1], c = sh.tri[pb][2], d = sh.tri[pb][3];
             const double fl = sh.tri[pb][4];
-            double sum = 0.0;
-            if (fl != 1.0) {   // 4 points per lane per step, every gather in flight before the arithmetic
+            double sum = 0.0, bnd = 0.0;
+            if (fl != 1.0) {
+                const float a = (float)sh.tri[pb][0], b = (float)sh.tri[pb][1], c = (float)sh.tri[pb][2];
+                const float fa = __builtin_fabsf(a), fb = __builtin_fabsf(b), fc = __builtin_fabsf(c);
                 for (int j0 = tid - 64; j0 < k; j0 += 4 * 192) {
-                    double qx[4], qy[4], qz[4];
+                    uint32_t u[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int j = j0 + 192 * u;
-                        const double* q = fp + 3 * (int64_t)(j < k ? sh.idx[pb][j] : 0);
-                        qx[u] = q[0];
-                        qy[u] = q[1];
-                        qz[u] = q[2];
+                    for (int v = 0; v < 4; ++v) {
+                        const int j = j0 + 192 * v;
+                        u[v] = fpk[j < k ? sh.idx[pb][j] : 0];
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (j0 + 192 * u < k) sum += fabs((qx[u] * a + qy[u] * b + qz[u] * c - 1.0) / d);
+                    for (int v = 0; v < 4; ++v) {
+                        if (j0 + 192 * v >= k) continue;
+                        const int x = (int)(u[v] & 0xFFF), y = (int)((u[v] >> 12) & 0xFFF);
+                        const float rr = __builtin_amdgcn_rcpf((float)(u[v] >> 24));
+                        const float K = cp.B32 * rr;
+                        const float X = centred(x, cp.cw_hi, cp.cw_lo) * K;
+                        const float Y = centred(y, cp.ch_hi, cp.ch_lo) * K;
+                        const float Z = cp.fB32 * rr;
+                        const float dot = __builtin_fmaf(Z, c, __builtin_fmaf(X, a, Y * b));
+                        sum += (double)__builtin_fabsf(dot - 1.0f);
+                        bnd += (double)(__builtin_fmaf(fa, __builtin_fabsf(X),
+                                                       __builtin_fmaf(fb, __builtin_fabsf(Y), fc * Z)) + 1.0f);
+                    }
                 }
             }
 #pragma unroll
-            for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
-            if (lane == 0) sh.red[wave] = sum;
+            for (int o = kWave / 2; o > 0; o >>= 1) {
+                sum += __shfl_xor(sum, o, kWave);
+                bnd += __shfl_xor(bnd, o, kWave);
+            }
+            if (lane == 0) {
+                sh.red[wave] = sum;
+                sh.bnd[wave] = bnd;
+            }
         }
         __syncthreads();
-        if (tid == 64 && s > 0) {   // one lane of wave 1 keeps the decision (trial order, strict <)
+        if (tid == 64 && s > 0) {   // the screen: can trial s - 1 matter?
             const int pb = buf ^ 1;
             const double fl = sh.tri[pb][4];
+            uint32_t full = 0;
             if (fl == 1.0) {
                 flags |= 1u;
             } else {
+                // |dist32 - dist64| <= (|Xa| + |Yb| + |Zc| + 1) 2^-18 / |abc| a point (fp32 X, Y, Z within
+                // 2^-21 relative, fp32 a, b, c and the two fmas, |abc| in fp32); sums in fp64
+                const double d = sh.tri[pb][3];
+                const double e32 = (sh.red[1] + sh.red[2] + sh.red[3]) / (d * k);
+                const double eb = (sh.bnd[1] + sh.bnd[2] + sh.bnd[3]) * 0x1p-18 / (d * k);
+                full = (ablate & 4) || !(e32 - eb > best * (1.0 + 1e-9));   // NaN / inf: evaluate in fp64
+                if (ablate & 1) full = 0;   // DIAGNOSTIC 1: no evaluation at all
+            }
+            sh.misc[1] = full;
+        }
+        __syncthreads();
+        if (s > 0 && sh.misc[1]) {   // uniform: the fp64 evaluation of trial s - 1 (rare)
+            const int pb = buf ^ 1;
+            if (wave != 0) {
+                const double a = sh.tri[pb][0], b = sh.tri[pb][1], c = sh.tri[pb][2], d = sh.tri[pb][3];
+                double sum = 0.0;
+                for (int j0 = tid - 64; j0 < k; j0 += 4 * 192) {   // every gather in flight before the arithmetic
+                    double qx[4], qy[4], qz[4];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const int j = j0 + 192 * v;
+                        const double* q = fp + 3 * (int64_t)(j < k ? sh.idx[pb][j] : 0);
+                        qx[v] = q[0];
+                        qy[v] = q[1];
+                        qz[v] = q[2];
+                    }
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        if (j0 + 192 * v < k) sum += fabs((qx[v] * a + qy[v] * b + qz[v] * c - 1.0) / d);
+                }
+#pragma unroll
+                for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
+                if (lane == 0) sh.red[wave] = sum;
+            }
+            __syncthreads();
+            if (tid == 64) {   // one lane keeps the decision (trial order, strict <)
+                const double fl = sh.tri[pb][4];
                 const double e = (sh.red[1] + sh.red[2] + sh.red[3]) / k;
                 if (e < best) {
                     second = best;
@@ -527,14 +638,14 @@ __global__ __launch_bounds__(256) void ransac_batch_kernel(const double* __restr
     }
 }
 
-hipError_t launch_ransac_batch(const double* pts, int64_t cap, const int64_t* counts, uint64_t seed_base,
-                               int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
-                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, int ablate,
-                               hipStream_t s) {
+hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
+                               const int64_t* counts, uint64_t seed_base, int64_t first_frame, int frames, int trials,
+                               int k, double* abc, double* err, int32_t* trial, uint32_t* flags, int32_t* trace,
+                               int trace_trials, int ablate, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
     if (k < 1 || k > kRBMaxK || cap > (int64_t)kRBBitmapWords * 32) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(ransac_batch_kernel, dim3(frames), dim3(256), 0, s, pts, cap, counts, seed_base, first_frame,
-                       trials, k, abc, err, trial, flags, trace, trace ? trace_trials : 0, ablate);
+    hipLaunchKernelGGL(ransac_batch_kernel, dim3(frames), dim3(256), 0, s, pts, packed, cap, cp, counts, seed_base,
+                       first_frame, trials, k, abc, err, trial, flags, trace, trace ? trace_trials : 0, ablate);
     return hipGetLastError();
 }
 

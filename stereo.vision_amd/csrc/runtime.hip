@@ -212,6 +212,7 @@ struct sv_batch {
     DevBuf mdisp, carmask;      // pre-pass: masked disparity (frames x H x W), 0x00/0xFF mask (H x W)
     DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
     DevBuf mpts, rres;          // maskpoints (frames x mcap x 3 fp64) + counts; batched RANSAC results
+    DevBuf mpk;                 // maskpoints packed (frames x mcap words x | y << 12 | d << 24): RANSAC's fp32 screen
     DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
     DevBuf fplanes;             // per-frame keep1 plane fields (FramePlane) for sv_batch_pipeline_planes
     int64_t mcap = 0;
@@ -406,7 +407,7 @@ int sv_batch_destroy(sv_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks, &b->ktab,
-                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->rres, &b->rtrace, &b->fplanes})
+                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes})
         if (x->p) (void)hipFree(x->p);
     if (b->ktab_err_host) (void)hipHostFree(b->ktab_err_host);
     for (auto& ev : b->ev)
@@ -994,7 +995,8 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 // ---------------------------------------------------------------------------
 
 // DIAGNOSTIC ONLY (env SVX_RANSAC_ABLATE, documented in DESIGN.md): 1 skips the trial evaluation,
-// 2 draws only the first two trials; results are invalid.
+// 2 draws only the first two trials (results invalid); 4 evaluates every trial in fp64 (no fp32
+// screen; results valid, for A/B).
 static int ransac_ablate() {
     const char* e = std::getenv("SVX_RANSAC_ABLATE");
     return e ? std::atoi(e) : 0;
@@ -1011,14 +1013,16 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
                     (long long)mcap);
     HIP_TRY(hipSetDevice(b->device));
     const size_t F = (size_t)b->frames;
+    if (b->H > 4096 || b->W > 4096) return fail(SV_E_ARG, "sv_batch_ransac: frames up to 4096 x 4096");
     HIP_TRY(b->mpts.ensure(sizeof(double) * 3 * (size_t)(mcap > 0 ? mcap : 1) * F));
+    HIP_TRY(b->mpk.ensure(sizeof(uint32_t) * (size_t)(mcap > 0 ? mcap : 1) * F));
     HIP_TRY(b->rres.ensure(F * (sizeof(double) * 4 + sizeof(int64_t) + sizeof(int32_t) + sizeof(uint32_t))));
     b->mcap = mcap;
     const RansacRes r = ransac_res(b);
     const KParams p = make_params(b->H, b->W, 2, *cam);
     const uint8_t* mff = b->have_mask ? b->carmask.as<uint8_t>() : nullptr;
-    HIP_TRY(launch_maskpoints(b->disp.as<uint8_t>(), mff, b->frames, b->H, b->W, p, b->mpts.as<double>(), mcap,
-                              r.mcount, b->stream));
+    HIP_TRY(launch_maskpoints(b->disp.as<uint8_t>(), mff, b->frames, b->H, b->W, p, b->mpts.as<double>(),
+                              b->mpk.as<uint32_t>(), mcap, r.mcount, b->stream));
     int32_t* trace = nullptr;
     if (b->trace_trials > 0) {
         HIP_TRY(b->rtrace.ensure(sizeof(int32_t) * F * b->trace_trials * (size_t)(k + 3)));
@@ -1026,8 +1030,9 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
         trace = b->rtrace.as<int32_t>();
     }
     b->trace_k = k;
-    HIP_TRY(launch_ransac_batch(b->mpts.as<double>(), mcap, r.mcount, seed_base, first_frame, b->frames, trials, k,
-                                r.abc, r.err, r.trial, r.flags, trace, b->trace_trials, ransac_ablate(), b->stream));
+    HIP_TRY(launch_ransac_batch(b->mpts.as<double>(), b->mpk.as<uint32_t>(), mcap, p, r.mcount, seed_base,
+                                first_frame, b->frames, trials, k, r.abc, r.err, r.trial, r.flags, trace,
+                                b->trace_trials, ransac_ablate(), b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }

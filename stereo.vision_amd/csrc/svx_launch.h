@@ -96,17 +96,19 @@ hipError_t launch_ransac_eval(const double* pts, int64_t ld, const int32_t* sidx
 // kernels/ransac_batch.hip -------------------------------------------------
 // maskpoints of every frame: fp64 XYZ of the d > 0 points of (disp & mask_ff)
 // on the step-2 grid, raster order; out frames x cap x 3, counts[frame].
+// packed (optional use by RANSAC): frames x cap words x | y << 12 | d << 24 (H, W <= 4096).
 hipError_t launch_maskpoints(const uint8_t* disp, const uint8_t* mask_ff, int frames, int H, int W, const KParams& p,
-                             double* out, int64_t cap, int64_t* counts, hipStream_t s);
+                             double* out, uint32_t* packed, int64_t cap, int64_t* counts, hipStream_t s);
 // RANSAC of every frame with random.seed(seed_base + first_frame + frame):
 // abc (frames x 3), err, winning trial (-1: none ran), flags (1 a singular
 // trial, 2 ill-conditioned winner, 4 near-tie). cap <= 163,840, k <= 1024.
 // trace (optional): frames x trace_trials x (k + 3) drawn indices (sample, then P1..P3).
 // frame_planes: the keep1 plane fields of every frame from its RANSAC result.
-hipError_t launch_ransac_batch(const double* pts, int64_t cap, const int64_t* counts, uint64_t seed_base,
-                               int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
-                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, int ablate,
-                               hipStream_t s);
+// cp: the camera's fp32 fields (B32, fB32, cw/ch hi-lo) for the fp32 screen of every trial.
+hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
+                               const int64_t* counts, uint64_t seed_base, int64_t first_frame, int frames, int trials,
+                               int k, double* abc, double* err, int32_t* trial, uint32_t* flags, int32_t* trace,
+                               int trace_trials, int ablate, hipStream_t s);
 hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, double f, FramePlane* out,
                                hipStream_t s);
 
