@@ -153,21 +153,34 @@ constexpr int kRBMaxAttempts = 1 << 16;
 constexpr uint32_t kRBMaxDraws = 1u << 28;
 // the pool branch's list shares the bitmap: n <= setsize(k <= 1024) = 21 + 4096 = 4117 < 5120 words
 
-struct RansacShared {
+// LDS of one frame: a fixed part (static) and, in dynamic LDS sized by the
+// launch for the batch's largest frame, the sample bitmap (set branch) or the
+// pool list (pool branch) and the two trial samples. RansacShared is the view
+// (pointers into LDS, kept in registers) the device functions take.
+struct RansacFixed {
     uint32_t mt[624];
     uint32_t tout[3][624];                    // tempered outputs of twists t (slot t % 3)
-    union {
-        uint32_t bitmap[kRBBitmapWords];      // set branch: selected indices of the current sample
-        int32_t pool[kRBBitmapWords];         // pool branch: the shrinking list
-    };
-    int32_t idx[2][kRBMaxK];                  // per trial (double-buffered): the sample
-    double tri[2][12];                        // abc[3], d, flag, then P1..P3 unused (padding)
-    double red[4];
-    double bnd[4];
+    double tri[2][12];                        // abc[3], d, flag, then padding
+    double red[2];
+    double bnd[2];
     uint32_t misc[8];
     uint32_t dummy[64];                       // claims of rejected draws (one word a lane)
 };
-static_assert(sizeof(RansacShared) <= 40960, "4 workgroups per CU");
+
+struct RansacShared {
+    uint32_t* mt;
+    uint32_t (*tout)[624];
+    uint32_t* bitmap;                         // set branch: selected indices of the current sample
+    int32_t* pool;                            // pool branch: the shrinking list (same words)
+    int32_t* idx0;                            // per trial (double-buffered): the samples, k apart
+    int k;
+    __device__ int32_t* idx(int b) const { return idx0 + b * k; }
+    double (*tri)[12];
+    double* red;
+    double* bnd;
+    uint32_t* misc;
+    uint32_t* dummy;
+};
 
 // CPython's init_genrand + init_by_array (Modules/_randommodule.c) for a
 // non-negative seed < 2^64: key = its 32-bit words, little-endian, at least one.
@@ -405,7 +418,10 @@ __device__ void rb_sample_pool(RansacShared& sh, RbStream& st, uint32_t n, int k
     rb_wave_lds_sync();   // idx (and the trace) read by every lane next
 }
 
-__global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __restrict__ pts,
+constexpr int kRBThreads = 128;   // wave 0 replays the stream, wave 1 evaluates
+constexpr int kRBGather = 10;     // screen gathers a lane keeps in flight
+
+__global__ __launch_bounds__(kRBThreads) void ransac_batch_kernel(const double* __restrict__ pts,
                                                            const uint32_t* __restrict__ packed, int64_t cap,
                                                            KParams cp, const int64_t* __restrict__ counts,
                                                            uint64_t seed_base,
@@ -414,8 +430,21 @@ __global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __re
                                                            int32_t* __restrict__ out_trial,
                                                            uint32_t* __restrict__ out_flags,
                                                            int32_t* __restrict__ trace, int trace_trials,
-                                                           int ablate) {
-    __shared__ RansacShared sh;
+                                                           int ablate, int bitmap_words) {
+    __shared__ RansacFixed fx;
+    extern __shared__ uint32_t rb_dyn[];   // [bitmap_words] bitmap / pool, then idx[2][k]
+    RansacShared sh;
+    sh.mt = fx.mt;
+    sh.tout = fx.tout;
+    sh.bitmap = rb_dyn;
+    sh.pool = reinterpret_cast<int32_t*>(rb_dyn);
+    sh.idx0 = reinterpret_cast<int32_t*>(rb_dyn + bitmap_words);
+    sh.k = k;
+    sh.tri = fx.tri;
+    sh.red = fx.red;
+    sh.bnd = fx.bnd;
+    sh.misc = fx.misc;
+    sh.dummy = fx.dummy;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.x;
     const int64_t n64 = counts[frame];
@@ -432,14 +461,8 @@ __global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __re
     }
     const uint32_t n = (uint32_t)n64;
     const int kb = 32 - __builtin_clz(n);
-    int64_t setsize = 21;
-    if (k > 5) {
-        int64_t pw = 1;
-        while (pw < 3ll * k) pw *= 4;   // 4 ** ceil(log4(3k)); 3k is never a power of 4
-        setsize += pw;
-    }
-    const bool pool = (int64_t)n <= setsize;
-    for (int q = tid; q < kRBBitmapWords; q += 256) sh.bitmap[q] = 0;
+    const bool pool = (int64_t)n <= ransac_setsize(k);
+    for (int q = tid; q < bitmap_words; q += kRBThreads) sh.bitmap[q] = 0;
     if (tid == 0) {
         sh.misc[0] = 0;
         rb_seed(sh.mt, seed_base + (uint64_t)(first_frame + frame));
@@ -450,11 +473,11 @@ __global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __re
     int best_t = -1;
     uint32_t flags = 0;
     double babc[3] = {0, 0, 0};
-    // step s: wave 0 draws trial s (s < trials), waves 1-3 evaluate trial s - 1
+    // step s: wave 0 draws trial s (s < trials), wave 1 evaluates trial s - 1
     for (int s = 0; s <= trials; ++s) {
         const int buf = s & 1;
         if (wave == 0 && s < trials && !((ablate & 2) && s >= 2)) {   // DIAGNOSTIC 2: draw 2 trials only
-            int32_t* idx = sh.idx[buf];
+            int32_t* idx = sh.idx(buf);
             if (pool) rb_sample_pool(sh, st, n, k, idx);
             else rb_sample_set(sh, st, n, kb, k, idx);
 
@@ -515,7 +538,7 @@ __global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __re
                 sh.tri[buf][4] = fl;
             }
         }
-        // Waves 1-3 screen trial s - 1 in fp32 from the packed points (one 4-byte
+        // Wave 1 screens trial s - 1 in fp32 from the packed points (one 4-byte
         // gather a point), with a rigorous bound on the difference to the fp64
         // mean; only a trial that could beat (or tie within 1e-9) the best so
         // far is then evaluated in fp64 exactly as before (functions.py:289-293).
@@ -528,16 +551,16 @@ __global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __re
             if (fl != 1.0) {
                 const float a = (float)sh.tri[pb][0], b = (float)sh.tri[pb][1], c = (float)sh.tri[pb][2];
                 const float fa = __builtin_fabsf(a), fb = __builtin_fabsf(b), fc = __builtin_fabsf(c);
-                for (int j0 = tid - 64; j0 < k; j0 += 4 * 192) {
-                    uint32_t u[4];
+                for (int j0 = lane; j0 < k; j0 += kRBGather * kWave) {   // one batch for k <= 640
+                    uint32_t u[kRBGather];
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        const int j = j0 + 192 * v;
-                        u[v] = fpk[j < k ? sh.idx[pb][j] : 0];
+                    for (int v = 0; v < kRBGather; ++v) {
+                        const int j = j0 + kWave * v;
+                        u[v] = fpk[j < k ? sh.idx(pb)[j] : 0];
                     }
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        if (j0 + 192 * v >= k) continue;
+                    for (int v = 0; v < kRBGather; ++v) {
+                        if (j0 + kWave * v >= k) continue;
                         const int x = (int)(u[v] & 0xFFF), y = (int)((u[v] >> 12) & 0xFFF);
                         const float rr = __builtin_amdgcn_rcpf((float)(u[v] >> 24));
                         const float K = cp.B32 * rr;
@@ -572,8 +595,8 @@ __global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __re
                 // |dist32 - dist64| <= (|Xa| + |Yb| + |Zc| + 1) 2^-18 / |abc| a point (fp32 X, Y, Z within
                 // 2^-21 relative, fp32 a, b, c and the two fmas, |abc| in fp32); sums in fp64
                 const double d = sh.tri[pb][3];
-                const double e32 = (sh.red[1] + sh.red[2] + sh.red[3]) / (d * k);
-                const double eb = (sh.bnd[1] + sh.bnd[2] + sh.bnd[3]) * 0x1p-18 / (d * k);
+                const double e32 = sh.red[1] / (d * k);
+                const double eb = sh.bnd[1] * 0x1p-18 / (d * k);
                 full = (ablate & 4) || !(e32 - eb > best * (1.0 + 1e-9));   // NaN / inf: evaluate in fp64
                 if (ablate & 1) full = 0;   // DIAGNOSTIC 1: no evaluation at all
             }
@@ -585,19 +608,19 @@ __global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __re
             if (wave != 0) {
                 const double a = sh.tri[pb][0], b = sh.tri[pb][1], c = sh.tri[pb][2], d = sh.tri[pb][3];
                 double sum = 0.0;
-                for (int j0 = tid - 64; j0 < k; j0 += 4 * 192) {   // every gather in flight before the arithmetic
+                for (int j0 = lane; j0 < k; j0 += 4 * kWave) {   // every gather in flight before the arithmetic
                     double qx[4], qy[4], qz[4];
 #pragma unroll
                     for (int v = 0; v < 4; ++v) {
-                        const int j = j0 + 192 * v;
-                        const double* q = fp + 3 * (int64_t)(j < k ? sh.idx[pb][j] : 0);
+                        const int j = j0 + kWave * v;
+                        const double* q = fp + 3 * (int64_t)(j < k ? sh.idx(pb)[j] : 0);
                         qx[v] = q[0];
                         qy[v] = q[1];
                         qz[v] = q[2];
                     }
 #pragma unroll
                     for (int v = 0; v < 4; ++v)
-                        if (j0 + 192 * v < k) sum += fabs((qx[v] * a + qy[v] * b + qz[v] * c - 1.0) / d);
+                        if (j0 + kWave * v < k) sum += fabs((qx[v] * a + qy[v] * b + qz[v] * c - 1.0) / d);
                 }
 #pragma unroll
                 for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
@@ -606,7 +629,7 @@ __global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __re
             __syncthreads();
             if (tid == 64) {   // one lane keeps the decision (trial order, strict <)
                 const double fl = sh.tri[pb][4];
-                const double e = (sh.red[1] + sh.red[2] + sh.red[3]) / k;
+                const double e = sh.red[1] / k;
                 if (e < best) {
                     second = best;
                     best = e;
@@ -639,13 +662,20 @@ __global__ __launch_bounds__(256, 4) void ransac_batch_kernel(const double* __re
 }
 
 hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
-                               const int64_t* counts, uint64_t seed_base, int64_t first_frame, int frames, int trials,
-                               int k, double* abc, double* err, int32_t* trial, uint32_t* flags, int32_t* trace,
-                               int trace_trials, int ablate, hipStream_t s) {
+                               const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
+                               int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
+                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, int ablate,
+                               hipStream_t s) {
     if (frames <= 0) return hipSuccess;
-    if (k < 1 || k > kRBMaxK || cap > (int64_t)kRBBitmapWords * 32) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(ransac_batch_kernel, dim3(frames), dim3(256), 0, s, pts, packed, cap, cp, counts, seed_base,
-                       first_frame, trials, k, abc, err, trial, flags, trace, trace ? trace_trials : 0, ablate);
+    if (k < 1 || k > kRBMaxK || cap > (int64_t)kRBBitmapWords * 32 || max_n > cap) return hipErrorInvalidValue;
+    // dynamic LDS: the set branch's bitmap (n bits) or the pool branch's list (n words), for the largest frame
+    int64_t words = (max_n + 31) / 32;
+    if (max_pool_n > words) words = max_pool_n;
+    if (words < 1) words = 1;
+    const size_t dyn = sizeof(uint32_t) * ((size_t)words + 2 * (size_t)k);
+    hipLaunchKernelGGL(ransac_batch_kernel, dim3(frames), dim3(kRBThreads), dyn, s, pts, packed, cap, cp, counts,
+                       seed_base, first_frame, trials, k, abc, err, trial, flags, trace, trace ? trace_trials : 0, ablate,
+                       (int)words);
     return hipGetLastError();
 }
 

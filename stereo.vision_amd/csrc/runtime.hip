@@ -1030,8 +1030,18 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
         trace = b->rtrace.as<int32_t>();
     }
     b->trace_k = k;
-    HIP_TRY(launch_ransac_batch(b->mpts.as<double>(), b->mpk.as<uint32_t>(), mcap, p, r.mcount, seed_base,
-                                first_frame, b->frames, trials, k, r.abc, r.err, r.trial, r.flags, trace,
+    // the largest frame sizes the kernel's LDS (bitmap / pool list): one small read-back
+    std::vector<int64_t> cnt(F);
+    HIP_TRY(hipMemcpyAsync(cnt.data(), r.mcount, sizeof(int64_t) * F, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    int64_t max_n = 0, max_pool_n = 0;
+    const int64_t setsize = ransac_setsize(k);
+    for (int64_t c : cnt) {
+        max_n = std::max(max_n, c);
+        if (c >= k && c <= setsize) max_pool_n = std::max(max_pool_n, c);
+    }
+    HIP_TRY(launch_ransac_batch(b->mpts.as<double>(), b->mpk.as<uint32_t>(), mcap, p, r.mcount, max_n, max_pool_n,
+                                seed_base, first_frame, b->frames, trials, k, r.abc, r.err, r.trial, r.flags, trace,
                                 b->trace_trials, ransac_ablate(), b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;

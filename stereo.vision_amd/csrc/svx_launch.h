@@ -105,10 +105,23 @@ hipError_t launch_maskpoints(const uint8_t* disp, const uint8_t* mask_ff, int fr
 // trace (optional): frames x trace_trials x (k + 3) drawn indices (sample, then P1..P3).
 // frame_planes: the keep1 plane fields of every frame from its RANSAC result.
 // cp: the camera's fp32 fields (B32, fB32, cw/ch hi-lo) for the fp32 screen of every trial.
+// random.sample's set-branch threshold: 21 + 4 ** ceil(log4(3k)) for k > 5 (3k is never a power of 4)
+__host__ __device__ inline int64_t ransac_setsize(int k) {
+    int64_t setsize = 21;
+    if (k > 5) {
+        int64_t pw = 1;
+        while (pw < 3ll * k) pw *= 4;
+        setsize += pw;
+    }
+    return setsize;
+}
+// max_n: the largest frame's point count; max_pool_n: the largest count that takes random.sample's pool
+// branch (n <= setsize(k)), 0 if none (both size the dynamic LDS).
 hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
-                               const int64_t* counts, uint64_t seed_base, int64_t first_frame, int frames, int trials,
-                               int k, double* abc, double* err, int32_t* trial, uint32_t* flags, int32_t* trace,
-                               int trace_trials, int ablate, hipStream_t s);
+                               const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
+                               int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
+                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, int ablate,
+                               hipStream_t s);
 hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, double f, FramePlane* out,
                                hipStream_t s);
 
