@@ -182,8 +182,10 @@ int sv_batch_read_frame_plane(sv_batch* b, int frame, double* out4);
 /* Pipeline kernel family: 0 = auto (frame-resident for >= 512 frames when the
  * frame fits, else tiled), 1 = tiled (tiles of 4096 points across workgroups,
  * offsets kernel between the passes), 2 = frame-resident (one workgroup per
- * frame, LDS histogram; frames of <= 1M grid points at step 1). Results are
- * identical; only the speed differs. */
+ * frame, LDS histogram; frames of <= 1M grid points at step 1; both passes
+ * prefetch the next chunk), 3 = frame-resident without prefetch, 4 =
+ * frame-resident with the pass-2 prefetch only. Results are identical; only
+ * the speed differs. */
 int sv_batch_pipeline_mode(sv_batch* b, int mode);
 
 /* Pre-pass over the batch's frames in order (stereovision.py:53-76): option
@@ -217,7 +219,9 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
  * LAPACK-based choice; 8: every triple drawn in 65,536 attempts was collinear
  * — the reference never returns there — trial = -1; 16: more than 2^28
  * draws in one frame, trial = -1). Step-2 grids of
- * <= 163,840 points; 1 <= k <= 1024. */
+ * <= 163,840 points, frames up to 4096 x 4096; 1 <= k <= 1024. The call
+ * waits for the maskpoints counts (one small read-back: the largest frame
+ * sizes the RANSAC kernel's LDS); `sync` then applies to the RANSAC kernel. */
 int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame, int trials, int k,
                     int sync);
 int sv_batch_read_ransac(sv_batch* b, int frame, double* abc, double* err, int32_t* trial, uint32_t* flags);
