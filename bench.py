@@ -225,10 +225,9 @@ def extras(b, sb, args, device, with_cpu):
 def latency_1frame(sb, step, first, device):
     """configs[1]: one 1024x544 frame, step 1: K1 kernel time (HIP events), us."""
     with sb.Batch(1, H, W, step, with_bgr=False, device=device) as one:
-        # K1's plain-store instance (same grid, one quad per lane): its 1-frame
-        # launches are a rocprof row of their own, so the batch launches'
-        # average stays unmixed
-        one.tune(1, 0)
+        # the same K1 as a separately named instance: its 1-frame launches are a
+        # rocprof row of their own, so the batch launches' average stays unmixed
+        one.tune(1, 2)
         one.synth(first)
         for _ in range(5):
             one.project(sync=False)

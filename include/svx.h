@@ -150,7 +150,9 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
 int sv_batch_destroy(sv_batch* b);
 int sv_batch_info(const sv_batch* b, int64_t* out8); /* Hg, Wg, pitch, Ng, bytes, frames, H, W */
 /* K1 launch shape: qpl = quads (4 grid points) per lane, 1, 2 or 4 (0 = 1);
- * nontemporal = 1 for non-temporal (streaming) stores. */
+ * nontemporal = 1 for non-temporal (streaming) stores, 2 for the same kernel
+ * (qpl 1, non-temporal) as a separately named instance: a profiler keeps its
+ * launches in a statistics row of their own. */
 int sv_batch_tune(sv_batch* b, int qpl, int nontemporal);
 
 /* Counter-based synthetic frames for global frame ids first..first+frames-1

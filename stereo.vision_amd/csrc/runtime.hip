@@ -440,6 +440,7 @@ int sv_batch_tune(sv_batch* b, int qpl, int nontemporal) {
     if (!b) return fail(SV_E_ARG, "null batch");
     if (qpl == 0) qpl = 1;
     if (qpl != 1 && qpl != 2 && qpl != 4) return fail(SV_E_ARG, "qpl must be 1, 2 or 4");
+    if (nontemporal < 0 || nontemporal > 2) return fail(SV_E_ARG, "nontemporal must be 0, 1 or 2");
     b->qpl = qpl;
     b->nontemporal = nontemporal;
     return SV_OK;

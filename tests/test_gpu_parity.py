@@ -286,7 +286,7 @@ def test_pipeline_random_colours_and_planes(svx_mod, kind):
 # batched device-resident API
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("step", [1, 2])
-@pytest.mark.parametrize("tune", [(1, 0), (1, 1), (2, 1), (4, 1)])
+@pytest.mark.parametrize("tune", [(1, 0), (1, 1), (2, 1), (4, 1), (1, 2)])
 def test_batch_dense_projection(svx_mod, step, tune):
     first = 40
     with svx_mod.batch.Batch(6, step=step, with_bgr=False) as b:
