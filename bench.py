@@ -229,7 +229,7 @@ def latency_1frame(sb, step, first, device):
         # rocprof row of their own, so the batch launches' average stays unmixed
         one.tune(1, 2)
         one.synth(first)
-        for _ in range(5):
+        for _ in range(200):
             one.project(sync=False)
         one.reset_timing()
         for _ in range(50):
@@ -251,6 +251,8 @@ def main():
     first, count = dist.shard(args.frames * world, world, rank)
     want_pipe = not args.no_pipeline
 
+    # configs[1]: one frame, before the 4096-frame batch exists (its own warm-up inside)
+    lat_us = None if args.no_latency else latency_1frame(sb, args.step, first, local)
     b = sb.Batch(count, H, W, args.step, with_bgr=want_pipe, with_points=want_pipe, device=local)
     b.tune(args.qpl, args.nt)
     b.synth(first)
@@ -308,9 +310,9 @@ def main():
                      "bytes_per_point": K1_BYTES_PER_POINT},
     }
 
-    # ---- config 2: single-frame latency ------------------------------------
-    if not args.no_latency:
-        out["latency_1frame_us"] = latency_1frame(sb, args.step, first, local)
+    # ---- config 2: single-frame latency (measured first, before the batch) ----
+    if lat_us is not None:
+        out["latency_1frame_us"] = lat_us
 
     # ---- config 4/5: pipeline ----------------------------------------------
     if want_pipe:
