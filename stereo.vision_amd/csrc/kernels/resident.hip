@@ -38,6 +38,20 @@ namespace svx {
 
 constexpr int kRMaxChunks = 256;   // chunks per frame at the default 4 quads per lane (= maxchunks_of<4>)
 constexpr int kRBins = 1000;    // bins 0..999: t < 1000 - 1000/(6*255) so rint(t) <= 999
+// Pass 2 stages the back-projection delta words (tables.hip: dx bits [256][dx_words],
+// dy bits [256][dy_words]) of kRDN consecutive disparities — the chunk's keep1
+// range, recorded by pass 1 — in LDS: dx rows at stride 33 words (bank spread),
+// then the kRDN dy words of the chunk's first 32-row word. Outputs outside the
+// staged range (a carried tail, a wide range, dx_words > 32) gather from HBM/L2.
+constexpr int kRDN = 16;
+constexpr int kRDxStride = 33;
+constexpr int kRDyOff = kRDN * kRDxStride;
+constexpr int kRDeltaWords = kRDyOff + kRDN;
+
+// both 16-bit halves: max
+__device__ __forceinline__ uint32_t pk_max16(uint32_t a, uint32_t b) {
+    return (max(a >> 16, b >> 16) << 16) | max(a & 0xFFFFu, b & 0xFFFFu);
+}
 
 
 template <int STEP, int QP>
@@ -292,6 +306,9 @@ struct P2Regs {
     RQuads<STEP, QP> g;
     uint32_t dw[RCfg<STEP, QP>::QPL][STEP];
     uint2 tw[RCfg<STEP, QP>::QPL];
+    uint32_t fx0, fx1, fy;   // the chunk's staged delta words (this lane's share)
+    int dlo, ywb;            // first staged disparity; the chunk's first 32-row word
+    bool narrow;             // the chunk's keep1 range fits the stage
 };
 
 template <int STEP, int QP>
@@ -305,22 +322,76 @@ __device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, con
 
 template <int STEP, int QP>
 __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint16_t* tab,
-                                        const RParams& p) {
+                                        const uint32_t* crange, const PipeBuffers& bf, const RParams& p) {
     r_geometry<STEP, QP>(c, tid, p, r.g);
     r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
     r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
+    // delta words of the chunk's keep1 disparities (pass 1's range), written to
+    // LDS at the chunk's start; every index is clamped in range, so the loads
+    // are unconditional (whatever crange holds)
+    const uint4 cr = *reinterpret_cast<const uint4*>(crange + 4 * c);
+    const uint32_t w = pk_max16(pk_max16(cr.x, cr.y), pk_max16(cr.z, cr.w));
+    const int dmn = max(0, 255 - (int)(w >> 16)), dmx = (int)(w & 0xFFFFu);
+    const int dlo = min(dmn, 256 - kRDN);
+    const int ywb = (fastdiv40(c * RCfg<STEP, QP>::QPL * 256, p.Q_m40) * STEP) >> 5;
+    r.dlo = dlo;
+    r.ywb = ywb;
+    r.narrow = !(p.ablate & 1024) && p.dx_words <= 32 && dmx >= dmn && dmx - dlo < kRDN;   // 1024: DIAGNOSTIC A/B
+    const int xw = min(tid & 31, p.dx_words - 1);
+    r.fx0 = bf.dxbits[(dlo + (tid >> 5)) * p.dx_words + xw];
+    r.fx1 = bf.dxbits[(dlo + 8 + (tid >> 5)) * p.dx_words + xw];
+    r.fy = bf.dybits[(dlo + (tid & (kRDN - 1))) * p.dy_words + min(ywb, p.dy_words - 1)];
+}
+
+// stage the chunk's delta words (loaded by p2_load) into dl: dx word (d, xw) at
+// (d - dlo) * kRDxStride + xw, dy word of d at kRDyOff + d - dlo
+template <int STEP, int QP>
+__device__ __forceinline__ void p2_stage_deltas(const P2Regs<STEP, QP>& r, uint32_t* dl) {
+    const int tid = threadIdx.x;
+    dl[(tid >> 5) * kRDxStride + (tid & 31)] = r.fx0;
+    dl[(8 + (tid >> 5)) * kRDxStride + (tid & 31)] = r.fx1;
+    if (tid < kRDN) dl[kRDyOff + tid] = r.fy;
+}
+
+// this wave's keep1 disparity range of the chunk as (255 - dmin) << 16 | dmax
+// (0 when nothing is kept): byte masks from the keep nibbles, no per-point branch
+template <int STEP, int QP>
+__device__ __forceinline__ uint32_t r_keep_range(const uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP], uint32_t keep) {
+    uint32_t dmn = 255, dmx = 0;
+#pragma unroll
+    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
+        uint32_t v;   // the quad's 4 disparity bytes, point k at byte k
+        if constexpr (STEP == 1) v = dw[i][0];
+        else v = __builtin_amdgcn_perm(dw[i][1], dw[i][0], 0x06040200u);
+        const uint32_t nib = (keep >> (4 * i)) & 0xFu;
+        const uint32_t m = ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;   // bit k -> byte k
+        const uint32_t vx = v & m, vn = v | ~m;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            dmx = max(dmx, (vx >> (8 * k)) & 0xFFu);
+            dmn = min(dmn, (vn >> (8 * k)) & 0xFFu);
+        }
+    }
+    uint32_t w = ((255u - dmn) << 16) | dmx;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) w = pk_max16(w, __shfl_xor(w, o, kWave));
+    return w;
 }
 
 // pass 1 of one chunk: keep1, valid/kept counts, dense hue binning into hist,
-// candidate mark into dirty. Wave-local (no barrier).
+// candidate mark into dirty, keep1 disparity range into crange. Wave-local (no barrier).
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint32_t* hist, uint32_t* dirty,
-                                         uint32_t* wstage, uint32_t* dump, const RParams& p, uint32_t& nvalid,
-                                         uint32_t& nkept) {
+                                         uint32_t* crange, uint32_t* wstage, uint32_t* dump, const RParams& p,
+                                         uint32_t& nvalid, uint32_t& nkept) {
     const int lane = lane_id();
     const uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
     nvalid += r_nvalid<STEP, QP>(r.dw, r.g, p);
     nkept += __builtin_popcount(keep);
+    {
+        const uint32_t w = r_keep_range<STEP, QP>(r.dw, keep);
+        if (lane == 0) crange[4 * c + (threadIdx.x >> 6)] = w;
+    }
     uint32_t pos0;
     bool cand = false;
     {
@@ -354,13 +425,16 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 // over wave blocks, uniform per wave.
 template <int STEP, int QP>
 __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint32_t b, const PipeBuffers& bf,
-                                               float* oX, float* oY, float* oZ, int32_t* oP, const RParams& p) {
+                                         float* oX, float* oY, float* oZ, int32_t* oP, const uint32_t* dl, int dlo,
+                                         int ywb, bool narrow, const RParams& p) {
     constexpr uint32_t SM = stage_of<QP>() - 1;
     const uint32_t first = a & ~3u;
     const uint32_t groups = (b - first + 3) >> 2;
     const int lane = lane_id();
     uint32_t m0 = threadIdx.x & ~63u;   // this wave's first group
     uint32_t pu[4], wx[4], wy[4];       // P outputs 2l, 2l+1, 128+2l, 129+2l of the block
+    // delta words from the chunk's LDS stage; an output outside it (rare) gathers
+    // from the tables in memory — only then does the loop wait on a load
     auto fetch = [&](uint32_t mm0) {
         const uint32_t o = first + 4 * mm0 + 2 * lane;
         const uint2 lo = *reinterpret_cast<const uint2*>(&stage[o & SM]);
@@ -369,12 +443,17 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const uint32_t oe = o + (e >> 1) * 128 + (e & 1);
-            if (!(oe >= a && oe < b)) pu[e] = 1u << 24;   // d = 1 at (0, 0): harmless filler
+            const bool ok = oe >= a && oe < b;   // else a stale slot: its words are never used
             const uint32_t d = pu[e] >> 24;
             const int y = (int)((pu[e] >> 12) & 0xFFF) * STEP;
             const int x = (int)(pu[e] & 0xFFF) * STEP;
-            wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
-            wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
+            const uint32_t dd = d - (uint32_t)dlo;
+            const bool lx = ok && narrow && dd < (uint32_t)kRDN;   // x < 32 * dx_words <= 1024 here
+            const bool ly = lx && (y >> 5) == ywb;
+            wx[e] = dl[lx ? dd * kRDxStride + (uint32_t)(x >> 5) : 0u];
+            wy[e] = dl[kRDyOff + (ly ? dd : 0u)];
+            if (ok && !lx) wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
+            if (ok && !ly) wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
         }
     };
     if (m0 < groups) fetch(m0);
@@ -451,6 +530,12 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     constexpr int QPL = RCfg<STEP, QP>::QPL;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
+    // this chunk's delta words into LDS (read by the write phases below, after
+    // the barriers; the other buffer may still be read by chunk c - 1's writes)
+    uint32_t* dl = sh.dlt[c & 1];
+    p2_stage_deltas<STEP, QP>(r, dl);
+    const int dlo = r.dlo, ywb = r.ywb;
+    const bool narrow = r.narrow;
     if ((dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: candidate chunk (rare)
         uint32_t cw[QPL][RCfg<STEP, QP>::CW];
         r_load_bgr<STEP, QP>(fbgr, r.g, p, cw);
@@ -500,7 +585,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     float* oZ = oY + bf.cap;
     if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (stage_of<QP>() - 1)] = sh.red[tid];   // the tail
     if (T > (uint32_t)stage_of<QP>() - (running - flushed)) {
-        p2_write<STEP, QP>(sh.stage, flushed, running, bf, oX, oY, oZ, oP, p);
+        p2_write<STEP, QP>(sh.stage, flushed, running, bf, oX, oY, oZ, oP, dl, dlo, ywb, narrow, p);
         flushed = running;
     }
     uint32_t rowbase = running;
@@ -516,7 +601,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
             }
         }
     }
-    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, p);   // next chunk in flight before the stores
+    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p);   // in flight before the stores
     __syncthreads();
     running += T;
     const uint32_t upto = more ? (running & ~3u) : running;   // the last chunk flushes its tail
@@ -524,7 +609,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     // chunk's dirty path may reuse sh.stage before its scatter restores them
     if (tid < (int)(running - upto)) sh.red[tid] = sh.stage[(upto + tid) & (stage_of<QP>() - 1)];
     if (upto > flushed) {
-        p2_write<STEP, QP>(sh.stage, flushed, upto, bf, oX, oY, oZ, oP, p);
+        p2_write<STEP, QP>(sh.stage, flushed, upto, bf, oX, oY, oZ, oP, dl, dlo, ywb, narrow, p);
         flushed = upto;
     }
 }
@@ -541,6 +626,10 @@ struct FusedShared {
     uint32_t red[8];
     uint32_t stage[stage_of<QP>()];
     uint32_t dump[256];   // pass 1: one slot per lane for the colours of points that are not kept
+    // pass 1 -> pass 2: per chunk and wave, the keep1 disparity range as
+    // (255 - dmin) << 16 | dmax (0 = no kept point)
+    alignas(16) uint32_t crange[maxchunks_of<QP>() * 4];
+    uint32_t dlt[2][kRDeltaWords];   // pass 2: the chunk's delta words, double-buffered by chunk parity
 };
 static_assert(sizeof(FusedShared<4>) <= 32768, "5 workgroups per CU (160 KiB LDS); 4 are VGPR-resident");
 
@@ -563,13 +652,13 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> cur = r1;
             if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, tab, p);
-            p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, wstage, sh.dump + tid, p, nvalid, nkept);
+            p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept);
         }
     } else {
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> r1;
             p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, tab, p);
-            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, wstage, sh.dump + tid, p, nvalid, nkept);
+            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept);
         }
     }
     nvalid = wave_sum(nvalid);
@@ -594,9 +683,9 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     uint32_t running = 0, flushed = 0;
     const int n2 = (p.ablate & 256) ? 0 : p.nchunks;
     P2Regs<STEP, QP> r2;
-    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, p);
+    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, sh.crange, bf, p);
     for (int c = 0; c < n2; ++c) {
-        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, p);
+        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, sh.crange, bf, p);
         p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
                            running, flushed, p);
     }
