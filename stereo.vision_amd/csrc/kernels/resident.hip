@@ -48,9 +48,10 @@ constexpr int kRDxStride = 33;
 constexpr int kRDyOff = kRDN * kRDxStride;
 constexpr int kRDeltaWords = kRDyOff + kRDN;
 
-// both 16-bit halves: max
+// both 16-bit halves: max (v_pk_max_u16)
 __device__ __forceinline__ uint32_t pk_max16(uint32_t a, uint32_t b) {
-    return (max(a >> 16, b >> 16) << 16) | max(a & 0xFFFFu, b & 0xFFFFu);
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
 }
 
 
@@ -311,6 +312,12 @@ struct P2Regs {
     bool narrow;             // the chunk's keep1 range fits the stage
 };
 
+// a global load waited for at once (rare fallback paths; hidden from the compiler)
+__device__ __forceinline__ uint32_t load_now_b32(const uint32_t* a) {
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
                                         const uint16_t* tab, const RParams& p) {
@@ -338,9 +345,12 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, con
     r.ywb = ywb;
     r.narrow = !(p.ablate & 1024) && p.dx_words <= 32 && dmx >= dmn && dmx - dlo < kRDN;   // 1024: DIAGNOSTIC A/B
     const int xw = min(tid & 31, p.dx_words - 1);
-    r.fx0 = bf.dxbits[(dlo + (tid >> 5)) * p.dx_words + xw];
-    r.fx1 = bf.dxbits[(dlo + 8 + (tid >> 5)) * p.dx_words + xw];
-    r.fy = bf.dybits[(dlo + (tid & (kRDN - 1))) * p.dy_words + min(ywb, p.dy_words - 1)];
+    const uint32_t* ax0 = bf.dxbits + (dlo + (tid >> 5)) * p.dx_words + xw;
+    const uint32_t* ax1 = bf.dxbits + (dlo + 8 + (tid >> 5)) * p.dx_words + xw;
+    const uint32_t* ay = bf.dybits + (dlo + (tid & (kRDN - 1))) * p.dy_words + min(ywb, p.dy_words - 1);
+    r.fx0 = *ax0;
+    r.fx1 = *ax1;
+    r.fy = *ay;
 }
 
 // stage the chunk's delta words (loaded by p2_load) into dl: dx word (d, xw) at
@@ -372,10 +382,9 @@ __device__ __forceinline__ uint32_t r_keep_range(const uint32_t (&dw)[RCfg<STEP,
             dmn = min(dmn, (vn >> (8 * k)) & 0xFFu);
         }
     }
-    uint32_t w = ((255u - dmn) << 16) | dmx;
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) w = pk_max16(w, __shfl_xor(w, o, kWave));
-    return w;
+    // max-scan (identity 0) of both halves; lane 63 holds the wave's
+    const uint32_t w = wave_scan_dpp(((255u - dmn) << 16) | dmx, pk_max16);
+    return __builtin_amdgcn_readlane(w, 63);
 }
 
 // pass 1 of one chunk: keep1, valid/kept counts, dense hue binning into hist,
@@ -452,8 +461,11 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
             const bool ly = lx && (y >> 5) == ywb;
             wx[e] = dl[lx ? dd * kRDxStride + (uint32_t)(x >> 5) : 0u];
             wy[e] = dl[kRDyOff + (ly ? dd : 0u)];
-            if (ok && !lx) wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
-            if (ok && !ly) wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
+            // the fallback in asm: as plain code, hipcc merges it with the LDS read
+            // above into one flat load (select of the two addresses), which the
+            // loop then waits for with vmcnt(0) behind every store
+            if (ok && !lx) wx[e] = load_now_b32(bf.dxbits + d * p.dx_words + (x >> 5));
+            if (ok && !ly) wy[e] = load_now_b32(bf.dybits + d * p.dy_words + (y >> 5));
         }
     };
     if (m0 < groups) fetch(m0);
@@ -558,12 +570,10 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     uint64_t cnt = 0;
 #pragma unroll
     for (int i = 0; i < QPL; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
-    uint64_t inc = cnt;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint64_t t = __shfl_up(inc, o, kWave);
-        if (lane >= o) inc += t;
-    }
+    // the four 16-bit row counts never carry (<= 256 each): two 32-bit DPP scans
+    const auto add = [](uint32_t a, uint32_t b) { return a + b; };
+    const uint64_t inc = (uint64_t)wave_scan_dpp((uint32_t)cnt, add) |
+                         ((uint64_t)wave_scan_dpp((uint32_t)(cnt >> 32), add) << 32);
     if (lane == 63) sh.wtot[wave] = inc;
     __syncthreads();
     uint64_t wbase = 0, tot = 0;
@@ -575,8 +585,8 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     }
     const uint64_t excl = wbase + inc - cnt;
     // LDS slot of output g = g mod kRStage. Outputs [flushed, running) are the
-    // previous chunk's unwritten tail (< 4, restored from sh.red), so every
-    // group of 4 written below is whole and 16-byte aligned. If this chunk's
+    // previous chunk's unwritten tail (< 32, restored from sh.red), so every
+    // group of 4 written below is whole and the writes start on a 128-byte line. If this chunk's
     // points would wrap onto that tail (almost every point kept), the tail is
     // written first as a partial group (uniform, rare).
     const uint32_t T = (uint32_t)((tot >> 0) & 0xFFFF) + (uint32_t)((tot >> 16) & 0xFFFF) +
@@ -604,8 +614,10 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p);   // in flight before the stores
     __syncthreads();
     running += T;
-    const uint32_t upto = more ? (running & ~3u) : running;   // the last chunk flushes its tail
-    // keep the new tail (< 4 descriptors) out of sh.stage's way: the next
+    // write whole 128-byte lines: outputs up to a multiple of 32 (X, Y, Z: 32 floats a line; P: 16 pairs),
+    // the rest (< 32) carried to the next chunk; the last chunk flushes its tail
+    const uint32_t upto = more ? (running & ~31u) : running;
+    // keep the new tail (< 32 descriptors) out of sh.stage's way: the next
     // chunk's dirty path may reuse sh.stage before its scatter restores them
     if (tid < (int)(running - upto)) sh.red[tid] = sh.stage[(upto + tid) & (stage_of<QP>() - 1)];
     if (upto > flushed) {
@@ -623,7 +635,7 @@ struct FusedShared {
     uint32_t hist[kRBins];
     uint32_t dirty[maxchunks_of<QP>() / 32];
     uint64_t wtot[4];
-    uint32_t red[8];
+    uint32_t red[32];   // pass 1: valid/kept counts per wave; pass 2: the carried output tail (< 32)
     uint32_t stage[stage_of<QP>()];
     uint32_t dump[256];   // pass 1: one slot per lane for the colours of points that are not kept
     // pass 1 -> pass 2: per chunk and wave, the keep1 disparity range as
@@ -687,7 +699,7 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     for (int c = 0; c < n2; ++c) {
         if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, sh.crange, bf, p);
         p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
-                           running, flushed, p);
+                                   running, flushed, p);
     }
     if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;
 }

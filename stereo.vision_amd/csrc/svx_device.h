@@ -201,14 +201,25 @@ __device__ __forceinline__ int hue_bin_fast(uint32_t col, bool& near) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o, kWave);
-        if (lane >= o) v += t;
-    }
+// Inclusive wave64 scan of an operation with identity 0 (add, unsigned max, ...)
+// in six DPP steps: row_shr 1/2/4/8 (Hillis-Steele inside each 16-lane row),
+// then row_bcast 15 (rows 1, 3) and row_bcast 31 (rows 2, 3). A lane whose
+// source is outside its row (or a row the mask leaves out) reads the identity.
+// One VALU op a step instead of a ds_bpermute + compare + select (shfl_up).
+// All 64 lanes must be active.
+template <class Op>
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v, Op op) {
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));   // row_bcast:31
     return v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    return wave_scan_dpp(v, [](uint32_t a, uint32_t b) { return a + b; });
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {

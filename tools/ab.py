@@ -26,10 +26,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--k1", action="store_true", help="time K1 (project) instead of the pipeline")
+    ap.add_argument("--with-k1", action="store_true", help="also time K1 (a per-box reference)")
     a = ap.parse_args()
     b = sb.Batch(a.frames, step=1, with_bgr=True, with_points=True)
     b.synth(0)
     variants = [(m, int(x)) for m in a.modes.split(",") for x in a.ablate.split(",")]
+    if a.with_k1:   # K1 beside the variants: the box's HBM speed, to compare runs across boxes
+        variants.append(("k1", 0))
     res = {v: [] for v in variants}
     for _ in range(a.rounds):
         for mode, abl in variants:
@@ -37,13 +40,15 @@ def main():
             m, _, lag = mode.partition(":")
             if lag:
                 os.environ["SVX_SPLIT_LAG"] = lag
-            b.pipeline_mode(m)
-            run = (lambda sync: b.project(sync=sync)) if a.k1 else (lambda sync: b.pipeline(sync=sync))
+            k1 = a.k1 or m == "k1"
+            if not k1:
+                b.pipeline_mode(m)
+            run = (lambda sync: b.project(sync=sync)) if k1 else (lambda sync: b.pipeline(sync=sync))
             run(True)
             b.reset_timing()
             for _ in range(a.reps):
                 run(False)
-            ms, n = b.timing("project" if a.k1 else "pipeline")
+            ms, n = b.timing("project" if k1 else "pipeline")
             res[(mode, abl)].append(ms / n)
     os.environ["SVX_ABLATE"] = "0"
     for (mode, abl), v in res.items():
