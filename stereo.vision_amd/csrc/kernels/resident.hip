@@ -41,9 +41,11 @@ constexpr int kRBins = 1000;    // bins 0..999: t < 1000 - 1000/(6*255) so rint(
 // Pass 2 stages the back-projection delta words (tables.hip: dx bits [256][dx_words],
 // dy bits [256][dy_words]) of kRDN consecutive disparities — the chunk's keep1
 // range, recorded by pass 1 — in LDS: dx rows at stride 33 words (bank spread),
-// then the kRDN dy words of the chunk's first 32-row word. Outputs outside the
-// staged range (a carried tail, a wide range, dx_words > 32) gather from HBM/L2.
-constexpr int kRDN = 16;
+// then the kRDN dy words of the chunk's 32-row word. The scatter looks up each
+// kept point's two delta bits there ("narrow" chunk: keep1 range within kRDN
+// disparities, one row word, dx_words <= 32) or in the tables in memory, and
+// packs them into its descriptor (rdesc).
+constexpr int kRDN = 32;
 constexpr int kRDxStride = 33;
 constexpr int kRDyOff = kRDN * kRDxStride;
 constexpr int kRDeltaWords = kRDyOff + kRDN;
@@ -307,17 +309,11 @@ struct P2Regs {
     RQuads<STEP, QP> g;
     uint32_t dw[RCfg<STEP, QP>::QPL][STEP];
     uint2 tw[RCfg<STEP, QP>::QPL];
-    uint32_t fx0, fx1, fy;   // the chunk's staged delta words (this lane's share)
-    int dlo, ywb;            // first staged disparity; the chunk's first 32-row word
-    bool narrow;             // the chunk's keep1 range fits the stage
+    uint32_t fx[kRDN / 8], fy;   // the chunk's staged delta words (this lane's share)
+    int dlo, ywb;                // first staged disparity; the chunk's 32-row word
+    bool narrow;                 // the chunk's keep1 range and rows fit the stage
 };
 
-// a global load waited for at once (rare fallback paths; hidden from the compiler)
-__device__ __forceinline__ uint32_t load_now_b32(const uint32_t* a) {
-    uint32_t v;
-    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-    return v;
-}
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
                                         const uint16_t* tab, const RParams& p) {
@@ -340,17 +336,16 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, con
     const uint32_t w = pk_max16(pk_max16(cr.x, cr.y), pk_max16(cr.z, cr.w));
     const int dmn = max(0, 255 - (int)(w >> 16)), dmx = (int)(w & 0xFFFFu);
     const int dlo = min(dmn, 256 - kRDN);
-    const int ywb = (fastdiv40(c * RCfg<STEP, QP>::QPL * 256, p.Q_m40) * STEP) >> 5;
+    constexpr int per = RCfg<STEP, QP>::QPL * 256;   // quads per chunk
+    const int ywb = (fastdiv40(c * per, p.Q_m40) * STEP) >> 5;
+    const int ywl = (fastdiv40(min((c + 1) * per, p.frame_quads) - 1, p.Q_m40) * STEP) >> 5;
     r.dlo = dlo;
     r.ywb = ywb;
-    r.narrow = !(p.ablate & 1024) && p.dx_words <= 32 && dmx >= dmn && dmx - dlo < kRDN;   // 1024: DIAGNOSTIC A/B
+    r.narrow = !(p.ablate & 1024) && p.dx_words <= 32 && dmx - dlo < kRDN && ywl == ywb;   // 1024: DIAGNOSTIC A/B
     const int xw = min(tid & 31, p.dx_words - 1);
-    const uint32_t* ax0 = bf.dxbits + (dlo + (tid >> 5)) * p.dx_words + xw;
-    const uint32_t* ax1 = bf.dxbits + (dlo + 8 + (tid >> 5)) * p.dx_words + xw;
-    const uint32_t* ay = bf.dybits + (dlo + (tid & (kRDN - 1))) * p.dy_words + min(ywb, p.dy_words - 1);
-    r.fx0 = *ax0;
-    r.fx1 = *ax1;
-    r.fy = *ay;
+#pragma unroll
+    for (int j = 0; j < kRDN / 8; ++j) r.fx[j] = bf.dxbits[(dlo + 8 * j + (tid >> 5)) * p.dx_words + xw];
+    r.fy = bf.dybits[(dlo + (tid & (kRDN - 1))) * p.dy_words + min(ywb, p.dy_words - 1)];
 }
 
 // stage the chunk's delta words (loaded by p2_load) into dl: dx word (d, xw) at
@@ -358,8 +353,8 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, con
 template <int STEP, int QP>
 __device__ __forceinline__ void p2_stage_deltas(const P2Regs<STEP, QP>& r, uint32_t* dl) {
     const int tid = threadIdx.x;
-    dl[(tid >> 5) * kRDxStride + (tid & 31)] = r.fx0;
-    dl[(8 + (tid >> 5)) * kRDxStride + (tid & 31)] = r.fx1;
+#pragma unroll
+    for (int j = 0; j < kRDN / 8; ++j) dl[(8 * j + (tid >> 5)) * kRDxStride + (tid & 31)] = r.fx[j];
     if (tid < kRDN) dl[kRDyOff + tid] = r.fy;
 }
 
@@ -424,6 +419,13 @@ __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint3
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 
+// A kept point's LDS descriptor: gx | dx << 11 | gy << 12 | dy << 23 | d << 24
+// (grid coordinates < 2048; dx, dy = the back-projection deltas of §2 item 2:
+// the int32 (x, y) is (x - dx, y - dy)).
+__device__ __forceinline__ uint32_t rdesc(uint32_t d, uint32_t gy, uint32_t gx, uint32_t dx, uint32_t dy) {
+    return (d << 24) | (dy << 23) | (gy << 12) | (dx << 11) | gx;
+}
+
 // Write outputs [a, b) of the frame from their LDS descriptors (slot = g mod
 // the stage size); groups of 4 outputs at 16-byte-aligned positions. The P
 // plane is written in whole lines: lane l's group (outputs
@@ -431,42 +433,22 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 // lane also produces the (x, y) pairs of outputs 2l, 2l+1 and 128+2l, 129+2l of
 // the block, so each of the two P stores covers 1 KiB contiguous (with one
 // group per lane, every P store would cover 2 KiB half-filled). The loop runs
-// over wave blocks, uniform per wave.
+// over wave blocks, uniform per wave. No global loads: the next block's
+// descriptors are read from LDS before the stores.
 template <int STEP, int QP>
-__device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint32_t b, const PipeBuffers& bf,
-                                         float* oX, float* oY, float* oZ, int32_t* oP, const uint32_t* dl, int dlo,
-                                         int ywb, bool narrow, const RParams& p) {
+__device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint32_t b, float* oX, float* oY,
+                                         float* oZ, int32_t* oP, const RParams& p) {
     constexpr uint32_t SM = stage_of<QP>() - 1;
     const uint32_t first = a & ~3u;
     const uint32_t groups = (b - first + 3) >> 2;
     const int lane = lane_id();
     uint32_t m0 = threadIdx.x & ~63u;   // this wave's first group
-    uint32_t pu[4], wx[4], wy[4];       // P outputs 2l, 2l+1, 128+2l, 129+2l of the block
-    // delta words from the chunk's LDS stage; an output outside it (rare) gathers
-    // from the tables in memory — only then does the loop wait on a load
+    uint32_t pu[4];                     // P outputs 2l, 2l+1, 128+2l, 129+2l of the block
     auto fetch = [&](uint32_t mm0) {
         const uint32_t o = first + 4 * mm0 + 2 * lane;
         const uint2 lo = *reinterpret_cast<const uint2*>(&stage[o & SM]);
         const uint2 hi = *reinterpret_cast<const uint2*>(&stage[(o + 128) & SM]);
         pu[0] = lo.x; pu[1] = lo.y; pu[2] = hi.x; pu[3] = hi.y;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint32_t oe = o + (e >> 1) * 128 + (e & 1);
-            const bool ok = oe >= a && oe < b;   // else a stale slot: its words are never used
-            const uint32_t d = pu[e] >> 24;
-            const int y = (int)((pu[e] >> 12) & 0xFFF) * STEP;
-            const int x = (int)(pu[e] & 0xFFF) * STEP;
-            const uint32_t dd = d - (uint32_t)dlo;
-            const bool lx = ok && narrow && dd < (uint32_t)kRDN;   // x < 32 * dx_words <= 1024 here
-            const bool ly = lx && (y >> 5) == ywb;
-            wx[e] = dl[lx ? dd * kRDxStride + (uint32_t)(x >> 5) : 0u];
-            wy[e] = dl[kRDyOff + (ly ? dd : 0u)];
-            // the fallback in asm: as plain code, hipcc merges it with the LDS read
-            // above into one flat load (select of the two addresses), which the
-            // loop then waits for with vmcnt(0) behind every store
-            if (ok && !lx) wx[e] = load_now_b32(bf.dxbits + d * p.dx_words + (x >> 5));
-            if (ok && !ly) wy[e] = load_now_b32(bf.dybits + d * p.dy_words + (y >> 5));
-        }
     };
     if (m0 < groups) fetch(m0);
     while (m0 < groups) {   // uniform per wave
@@ -478,8 +460,8 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const uint32_t d = (u[e] >> 24) | (g + e < b ? 0u : 1u);   // no rcp(0) on slots past the end
-            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
-            const int x = (int)(u[e] & 0xFFF) * STEP;
+            const int y = (int)((u[e] >> 12) & 0x7FF) * STEP;
+            const int x = (int)(u[e] & 0x7FF) * STEP;
             const float rr = __builtin_amdgcn_rcpf((float)d);
             const float K = p.B32 * rr;
             X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
@@ -489,10 +471,8 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
         int PX[4], PY[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int y = (int)((pu[e] >> 12) & 0xFFF) * STEP;
-            const int x = (int)(pu[e] & 0xFFF) * STEP;
-            PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
-            PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
+            PX[e] = (int)(pu[e] & 0x7FF) * STEP - (int)((pu[e] >> 11) & 1);
+            PY[e] = (int)((pu[e] >> 12) & 0x7FF) * STEP - (int)((pu[e] >> 23) & 1);
         }
         const uint32_t o = first + 4 * m0 + 2 * lane;
         const uint32_t mn = m0 + 256;
@@ -542,11 +522,11 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     constexpr int QPL = RCfg<STEP, QP>::QPL;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
-    // this chunk's delta words into LDS (read by the write phases below, after
-    // the barriers; the other buffer may still be read by chunk c - 1's writes)
-    uint32_t* dl = sh.dlt[c & 1];
+    // this chunk's delta words into LDS, read by its scatter after the next
+    // barrier (every wave has finished chunk c - 1's scatter)
+    uint32_t* dl = sh.dlt;
     p2_stage_deltas<STEP, QP>(r, dl);
-    const int dlo = r.dlo, ywb = r.ywb;
+    const int dlo = r.dlo;
     const bool narrow = r.narrow;
     if ((dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: candidate chunk (rare)
         uint32_t cw[QPL][RCfg<STEP, QP>::CW];
@@ -595,20 +575,43 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     float* oZ = oY + bf.cap;
     if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (stage_of<QP>() - 1)] = sh.red[tid];   // the tail
     if (T > (uint32_t)stage_of<QP>() - (running - flushed)) {
-        p2_write<STEP, QP>(sh.stage, flushed, running, bf, oX, oY, oZ, oP, dl, dlo, ywb, narrow, p);
+        p2_write<STEP, QP>(sh.stage, flushed, running, oX, oY, oZ, oP, p);
         flushed = running;
     }
+    // descriptors (rdesc) with the back-projection delta bits of each point,
+    // branch-free: a slot that is not kept writes to this lane's dump word
     uint32_t rowbase = running;
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
         uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
         rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
+        const uint32_t gy = (uint32_t)max(r.g.gy[i], 0), y = gy * STEP;
+        uint32_t dv[4], bx[4], by[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dv[k] = r_d<STEP, QP>(r.dw[i], k);
+        if (narrow) {   // uniform: every kept d in [dlo, dlo + kRDN), the chunk's rows in word ywb
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t dd = min(dv[k] - (uint32_t)dlo, (uint32_t)kRDN - 1);   // clamp: slots not kept
+                const uint32_t x = (uint32_t)(4 * r.g.q[i] + k) * STEP;
+                bx[k] = (dl[dd * kRDxStride + (x >> 5)] >> (x & 31)) & 1u;
+                by[k] = (dl[kRDyOff + dd] >> (y & 31)) & 1u;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t x = (uint32_t)(4 * r.g.q[i] + k) * STEP;
+                const uint32_t xw = min(x >> 5, (uint32_t)p.dx_words - 1);   // pad columns
+                bx[k] = (bf.dxbits[dv[k] * p.dx_words + xw] >> (x & 31)) & 1u;
+                by[k] = (bf.dybits[dv[k] * p.dy_words + (y >> 5)] >> (y & 31)) & 1u;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (keep & (1u << (4 * i + k))) {
-                const uint32_t d = r_d<STEP, QP>(r.dw[i], k);
-                sh.stage[(o++) & (stage_of<QP>() - 1)] = (d << 24) | ((uint32_t)r.g.gy[i] << 12) | (uint32_t)(4 * r.g.q[i] + k);
-            }
+            const uint32_t bit = (keep >> (4 * i + k)) & 1u;
+            *(bit ? &sh.stage[o & (stage_of<QP>() - 1)] : sh.dump + tid) =
+                rdesc(dv[k], gy, (uint32_t)(4 * r.g.q[i] + k), bx[k], by[k]);
+            o += bit;
         }
     }
     if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p);   // in flight before the stores
@@ -621,7 +624,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     // chunk's dirty path may reuse sh.stage before its scatter restores them
     if (tid < (int)(running - upto)) sh.red[tid] = sh.stage[(upto + tid) & (stage_of<QP>() - 1)];
     if (upto > flushed) {
-        p2_write<STEP, QP>(sh.stage, flushed, upto, bf, oX, oY, oZ, oP, dl, dlo, ywb, narrow, p);
+        p2_write<STEP, QP>(sh.stage, flushed, upto, oX, oY, oZ, oP, p);
         flushed = upto;
     }
 }
@@ -641,7 +644,7 @@ struct FusedShared {
     // pass 1 -> pass 2: per chunk and wave, the keep1 disparity range as
     // (255 - dmin) << 16 | dmax (0 = no kept point)
     alignas(16) uint32_t crange[maxchunks_of<QP>() * 4];
-    uint32_t dlt[2][kRDeltaWords];   // pass 2: the chunk's delta words, double-buffered by chunk parity
+    uint32_t dlt[kRDeltaWords];   // pass 2: the chunk's delta words (scatter lookups)
 };
 static_assert(sizeof(FusedShared<4>) <= 32768, "5 workgroups per CU (160 KiB LDS); 4 are VGPR-resident");
 
@@ -731,7 +734,7 @@ __global__ __launch_bounds__(256) void resident_fused_kernel(PipeBuffers bf, con
 }
 
 bool resident_supported(const KParams& p) {   // frame_quads <= 2^20: every QP's chunk count fits its dirty bits
-    return (p.step == 1 || p.step == 2) && p.Wg <= 4096 && p.Hg <= 4096 &&
+    return (p.step == 1 || p.step == 2) && p.pitch <= 2048 && p.Hg <= 2048 &&   // rdesc: 11-bit coordinates
            resident_chunks_per_frame(p, 4) <= kRMaxChunks && p.frame_px * 3 < (1ll << 31);
 }
 
