@@ -122,6 +122,7 @@ hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, hip
 // ---------------------------------------------------------------------------
 struct RParams {      // what the streaming kernel needs (kept small: SGPR budget)
     int W, Wg, Q, pitch, frame_quads, nchunks, hist_thr, dx_words, dy_words, ablate;
+    int drow, dq;   // a chunk's quads (QPL * 256) as whole rows + quads
     uint64_t Q_m40;
     int64_t frame_px;
     float B32, fB32, cw_hi, cw_lo, ch_hi, ch_lo;
@@ -147,10 +148,29 @@ __device__ __forceinline__ void r_geometry(int c, int tid, const RParams& p, RQu
     }
 }
 
+// the geometry of chunk c from that of chunk c - 1 (all its quads inside the
+// frame): every quad slot advances by drow rows and dq quads, no division
+template <int STEP, int QP>
+__device__ __forceinline__ void r_geometry_next(int c, int tid, const RParams& p, RQuads<STEP, QP>& g) {
+    constexpr int QPL = RCfg<STEP, QP>::QPL;
+#pragma unroll
+    for (int i = 0; i < QPL; ++i) {
+        int q = g.q[i] + p.dq, gy = g.gy[i] + p.drow;
+        const bool wrap = q >= p.Q;
+        q -= wrap ? p.Q : 0;
+        gy += wrap ? 1 : 0;
+        const bool ok = (c * QPL + i) * 256 + tid < p.frame_quads;
+        g.q[i] = ok ? q : p.Q - 1;   // past the end: an in-range load address (row 0), gy = -1
+        g.gy[i] = ok ? gy : -1;
+    }
+}
+
 // byte offset of quad (gy, q) in a frame plane with `bpp` bytes per pixel
+// (24-bit multiplies: full-rate, operands < 2^24 for frames the resident kernel takes)
 template <int STEP, int QP>
 __device__ __forceinline__ uint32_t r_off(int gy, int q, int bpp, const RParams& p) {
-    return (uint32_t)(((gy < 0 ? 0 : gy) * STEP) * p.W + 4 * STEP * q) * (uint32_t)bpp;
+    const uint32_t px = __umul24((uint32_t)(gy < 0 ? 0 : gy) * STEP, (uint32_t)p.W) + 4u * STEP * (uint32_t)q;
+    return bpp == 3 ? 3u * px : px;
 }
 
 template <int STEP, int QP>
@@ -175,7 +195,7 @@ __device__ __forceinline__ void r_load_tab(const uint16_t* tab, const RQuads<STE
 #pragma unroll
     for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
         const int gy = g.gy[i] < 0 ? 0 : g.gy[i];
-        tw[i] = *reinterpret_cast<const uint2*>(tab + (uint32_t)(gy * p.pitch + 4 * g.q[i]));
+        tw[i] = *reinterpret_cast<const uint2*>(tab + (__umul24((uint32_t)gy, (uint32_t)p.pitch) + 4u * (uint32_t)g.q[i]));
     }
 }
 
@@ -316,8 +336,9 @@ struct P2Regs {
 
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
-                                        const uint16_t* tab, const RParams& p) {
-    r_geometry<STEP, QP>(c, tid, p, r.g);
+                                        const uint16_t* tab, const RParams& p, bool next) {
+    if (next) r_geometry_next<STEP, QP>(c, tid, p, r.g);   // r.g holds chunk c - 1
+    else r_geometry<STEP, QP>(c, tid, p, r.g);
     r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
     r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
     r_load_bgr<STEP, QP>(fbgr, r.g, p, r.cw);
@@ -325,8 +346,9 @@ __device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, con
 
 template <int STEP, int QP>
 __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint16_t* tab,
-                                        const uint32_t* crange, const PipeBuffers& bf, const RParams& p) {
-    r_geometry<STEP, QP>(c, tid, p, r.g);
+                                        const uint32_t* crange, const PipeBuffers& bf, const RParams& p, bool next) {
+    if (next) r_geometry_next<STEP, QP>(c, tid, p, r.g);   // r.g holds chunk c - 1
+    else r_geometry<STEP, QP>(c, tid, p, r.g);
     r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
     r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
     // delta words of the chunk's keep1 disparities (pass 1's range), written to
@@ -369,7 +391,8 @@ __device__ __forceinline__ uint32_t r_keep_range(const uint32_t (&dw)[RCfg<STEP,
         if constexpr (STEP == 1) v = dw[i][0];
         else v = __builtin_amdgcn_perm(dw[i][1], dw[i][0], 0x06040200u);
         const uint32_t nib = (keep >> (4 * i)) & 0xFu;
-        const uint32_t m = ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;   // bit k -> byte k
+        // bit k -> byte k = 0xFF: v_perm selector 0x0C gives a 0x00 byte, 0x0D a 0xFF byte
+        const uint32_t m = __builtin_amdgcn_perm(0u, 0u, ((__umul24(nib, 0x00204081u) & 0x01010101u) + 0x0C0C0C0Cu));
         const uint32_t vx = v & m, vn = v | ~m;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -614,7 +637,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
             o += bit;
         }
     }
-    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p);   // in flight before the stores
+    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p, true);   // in flight before the stores
     __syncthreads();
     running += T;
     // write whole 128-byte lines: outputs up to a multiple of 32 (X, Y, Z: 32 floats a line; P: 16 pairs),
@@ -663,16 +686,16 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
     const int n1 = (p.ablate & 128) ? 0 : p.nchunks;   // ablate: DIAGNOSTIC ONLY
     if constexpr (PF1) {   // chunk c + 1's loads in flight while chunk c is binned (pass 1 stores nothing)
         P1Regs<STEP, QP> r1;
-        if (n1 > 0) p1_load<STEP, QP>(r1, 0, tid, fdisp, fbgr, tab, p);
+        if (n1 > 0) p1_load<STEP, QP>(r1, 0, tid, fdisp, fbgr, tab, p, false);
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> cur = r1;
-            if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, tab, p);
+            if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, tab, p, true);
             p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept);
         }
     } else {
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> r1;
-            p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, tab, p);
+            p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, tab, p, false);
             p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept);
         }
     }
@@ -698,9 +721,9 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     uint32_t running = 0, flushed = 0;
     const int n2 = (p.ablate & 256) ? 0 : p.nchunks;
     P2Regs<STEP, QP> r2;
-    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, sh.crange, bf, p);
+    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, sh.crange, bf, p, false);
     for (int c = 0; c < n2; ++c) {
-        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, sh.crange, bf, p);
+        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, sh.crange, bf, p, c > 0);
         p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
                                    running, flushed, p);
     }
@@ -746,6 +769,8 @@ static RParams resident_params(const KParams& kp, int qpl) {
     p.pitch = kp.pitch;
     p.frame_quads = kp.frame_quads;
     p.nchunks = resident_chunks_per_frame(kp, qpl);
+    p.drow = 256 * qpl / kp.Q;
+    p.dq = 256 * qpl % kp.Q;
     p.hist_thr = kp.hist_thr;
     p.dx_words = kp.dx_words;
     p.dy_words = kp.dy_words;
