@@ -482,7 +482,7 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
         float X[4], Y[4], Z[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const uint32_t d = (u[e] >> 24) | (g + e < b ? 0u : 1u);   // no rcp(0) on slots past the end
+            const uint32_t d = u[e] >> 24;   // a stale slot past b may give rcp(0) = inf: never stored
             const int y = (int)((u[e] >> 12) & 0x7FF) * STEP;
             const int x = (int)(u[e] & 0x7FF) * STEP;
             const float rr = __builtin_amdgcn_rcpf((float)d);
