@@ -82,7 +82,7 @@ int resident_chunks_per_frame(const KParams& p, int qpl) {
 // One lane per grid point, brute force over d = 1..255.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void keep_table_kernel(uint16_t* __restrict__ tab, uint32_t* __restrict__ err,
-                                                         KParams p) {
+                                                         uint32_t* __restrict__ cany, int chunk_quads, KParams p) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= p.Hg * p.pitch) return;
     const int gy = i / p.pitch, gx = i - gy * p.pitch;
@@ -105,15 +105,17 @@ __global__ __launch_bounds__(256) void keep_table_kernel(uint16_t* __restrict__ 
         if (cnt) {
             if (cnt == hi - lo + 1) entry = (uint32_t)lo | ((uint32_t)hi << 8);
             else atomicOr(err, 1u);   // not an interval: the caller uses the tiled kernels
+            cany[(gy * p.Q + (gx >> 2)) / chunk_quads] = 1u;   // the chunk can keep a point (same value from all)
         }
     }
     tab[i] = (uint16_t)entry;
 }
 
-hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, hipStream_t s) {
+hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, uint32_t* cany, hipStream_t s) {
     const int n = p.Hg * p.pitch;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(keep_table_kernel, dim3((n + 255) / 256), dim3(256), 0, s, tab, err, p);
+    const int chunk_quads = 256 * (p.step == 1 ? default_qpl<1>() : default_qpl<2>());
+    hipLaunchKernelGGL(keep_table_kernel, dim3((n + 255) / 256), dim3(256), 0, s, tab, err, cany, chunk_quads, p);
     return hipGetLastError();
 }
 
@@ -336,19 +338,23 @@ struct P2Regs {
 
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
-                                        const uint16_t* tab, const RParams& p, bool next) {
+                                        const uint16_t* tab, const RParams& p, bool next, bool any) {
     if (next) r_geometry_next<STEP, QP>(c, tid, p, r.g);   // r.g holds chunk c - 1
     else r_geometry<STEP, QP>(c, tid, p, r.g);
     r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
-    r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
-    r_load_bgr<STEP, QP>(fbgr, r.g, p, r.cw);
+    if (any) {   // uniform: a chunk no grid point of which can be kept needs only its valid count
+        r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
+        r_load_bgr<STEP, QP>(fbgr, r.g, p, r.cw);
+    }
 }
 
 template <int STEP, int QP>
 __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint16_t* tab,
-                                        const uint32_t* crange, const PipeBuffers& bf, const RParams& p, bool next) {
+                                        const uint32_t* crange, const PipeBuffers& bf, const RParams& p, bool next,
+                                        bool run) {
     if (next) r_geometry_next<STEP, QP>(c, tid, p, r.g);   // r.g holds chunk c - 1
     else r_geometry<STEP, QP>(c, tid, p, r.g);
+    if (!run) return;   // uniform: a chunk pass 2 skips (none of its grid points can be kept)
     r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
     r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
     // delta words of the chunk's keep1 disparities (pass 1's range), written to
@@ -410,10 +416,14 @@ __device__ __forceinline__ uint32_t r_keep_range(const uint32_t (&dw)[RCfg<STEP,
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint32_t* hist, uint32_t* dirty,
                                          uint32_t* crange, uint32_t* wstage, uint32_t* dump, const RParams& p,
-                                         uint32_t& nvalid, uint32_t& nkept) {
+                                         uint32_t& nvalid, uint32_t& nkept, bool any) {
     const int lane = lane_id();
-    const uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
     nvalid += r_nvalid<STEP, QP>(r.dw, r.g, p);
+    if (!any) {   // uniform: no grid point of the chunk can be kept (keep table): nothing to bin
+        if (lane == 0) crange[4 * c + (threadIdx.x >> 6)] = 0u;
+        return;
+    }
+    const uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
     nkept += __builtin_popcount(keep);
     {
         const uint32_t w = r_keep_range<STEP, QP>(r.dw, keep);
@@ -541,7 +551,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
                                          const uint8_t* fdisp, const uint8_t* fbgr, const uint16_t* tab,
                                          const PipeBuffers& bf, float* oX, int32_t* oP, uint32_t& running,
-                                         uint32_t& flushed, const RParams& p) {
+                                         uint32_t& flushed, bool next_run, const RParams& p) {
     constexpr int QPL = RCfg<STEP, QP>::QPL;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
@@ -637,7 +647,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
             o += bit;
         }
     }
-    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p, true);   // in flight before the stores
+    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p, true, next_run);   // in flight before the stores
     __syncthreads();
     running += T;
     // write whole 128-byte lines: outputs up to a multiple of 32 (X, Y, Z: 32 floats a line; P: 16 pairs),
@@ -686,17 +696,19 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
     const int n1 = (p.ablate & 128) ? 0 : p.nchunks;   // ablate: DIAGNOSTIC ONLY
     if constexpr (PF1) {   // chunk c + 1's loads in flight while chunk c is binned (pass 1 stores nothing)
         P1Regs<STEP, QP> r1;
-        if (n1 > 0) p1_load<STEP, QP>(r1, 0, tid, fdisp, fbgr, tab, p, false);
+        if (n1 > 0) p1_load<STEP, QP>(r1, 0, tid, fdisp, fbgr, tab, p, false, bf.cany[0] != 0);
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> cur = r1;
-            if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, tab, p, true);
-            p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept);
+            if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, tab, p, true, bf.cany[c + 1] != 0);
+            p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept,
+                               bf.cany[c] != 0);
         }
     } else {
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> r1;
-            p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, tab, p, false);
-            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept);
+            const bool any = bf.cany[c] != 0;
+            p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, tab, p, false, any);
+            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept, any);
         }
     }
     nvalid = wave_sum(nvalid);
@@ -720,12 +732,19 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     int32_t* oP = bf.pts + (int64_t)frame * bf.cap * 2;
     uint32_t running = 0, flushed = 0;
     const int n2 = (p.ablate & 256) ? 0 : p.nchunks;
+    // a chunk none of whose grid points can be kept (keep table) adds no output and
+    // is skipped, loads included; the last chunk always runs (it flushes the tail)
+    const auto run = [&](int c) { return c + 1 == n2 || bf.cany[c] != 0; };
     P2Regs<STEP, QP> r2;
-    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, sh.crange, bf, p, false);
+    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, sh.crange, bf, p, false, run(0));
     for (int c = 0; c < n2; ++c) {
-        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, sh.crange, bf, p, c > 0);
+        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, sh.crange, bf, p, c > 0, run(c));
+        if (!run(c)) {   // uniform; c + 1 < n2 here
+            if (PF) p2_load<STEP, QP>(r2, c + 1, tid, fdisp, tab, sh.crange, bf, p, true, run(c + 1));
+            continue;
+        }
         p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
-                                   running, flushed, p);
+                               running, flushed, c + 1 < n2 && run(c + 1), p);
     }
     if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;
 }

@@ -547,14 +547,16 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     int t0, t1;
     if (mode >= 2) {   // every output word (hist, counts, points) is rewritten: no memset
         const size_t tab_bytes = sizeof(uint16_t) * (size_t)p.Hg * p.pitch;
-        HIP_TRY(b->ktab.ensure(tab_bytes + 64));
+        HIP_TRY(b->ktab.ensure(tab_bytes + 16 + 64 + 2048));
         if (!b->ktab_err_host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&b->ktab_err_host), 64));
         uint16_t* tab = b->ktab.as<uint16_t>();
         uint32_t* terr = reinterpret_cast<uint32_t*>(b->ktab.as<char>() + (tab_bytes + 15) / 16 * 16);
         HIP_TRY(hipEventRecord(b->ev[2], b->stream));
         HIP_TRY(b->timed_event(&t0));
-        HIP_TRY(hipMemsetAsync(terr, 0, 4, b->stream));
-        HIP_TRY(launch_keep_table(p, tab, terr, b->stream));
+        uint32_t* cany = terr + 16;   // 512 chunk flags (the resident kernels' chunks per frame <= 512)
+        HIP_TRY(hipMemsetAsync(terr, 0, 64 + 2048, b->stream));
+        HIP_TRY(launch_keep_table(p, tab, terr, cany, b->stream));
+        bf.cany = cany;
         HIP_TRY(hipMemcpyAsync(b->ktab_err_host, terr, 4, hipMemcpyDeviceToHost, b->stream));
         HIP_TRY(hipStreamSynchronize(b->stream));
         if (*b->ktab_err_host) goto tiled;   // a keep set that is not one interval: exact tiled kernels

@@ -44,6 +44,7 @@ struct PipeBuffers {
     const uint32_t* dybits;
     int64_t cap;         // points per frame (Ng)
     const FramePlane* planes = nullptr;   // per-frame planes (tiled kernels), or the KParams plane
+    const uint32_t* cany = nullptr;       // resident kernel: per chunk, can any grid point be kept (keep table)
 };
 int pipeline_tiles_per_frame(const KParams& p);
 // The whole chain for frames [0, frames) in chunks: chunks + 2 fused stage
@@ -57,7 +58,9 @@ hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, i
 // keep1 from a per-call interval table (uint16 lo | hi << 8 per grid point of
 // Hg x pitch); *err is set when some grid point's keep set is not an interval.
 bool resident_supported(const KParams& p);
-hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, hipStream_t s);
+// cany[chunk] = 1 where some grid point of the resident kernel's chunk can be kept
+// (zeroed by the caller; 512 words).
+hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, uint32_t* cany, hipStream_t s);
 // One workgroup per frame (pass 1 then pass 2); prefetch = pass 2 loads the
 // next chunk before issuing this chunk's stores (costs registers).
 hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, const uint16_t* tab, int frames,
