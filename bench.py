@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the SURVEY §8f component timings")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--traffic-pipeline", default=os.path.join(REPO, "profiles", "traffic_pipeline.json"))
     return ap.parse_args()
 
 
@@ -97,6 +98,18 @@ def cpu_baseline(budget_s):
                       f"({pts} grid points, {dt:.1f} s): oracle/cpu_loop.py nested loop "
                       f"(functions.py:178-198 semantics)",
             "c_restatement_mpts": pts / dtc / 1e6, "cpu": model}
+
+
+def pipeline_traffic(path, frames, step):
+    """PMC HBM bytes per pipeline call (tools/traffic.py output), if measured at this workload."""
+    try:
+        with open(path) as fh:
+            tj = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if tj.get("frames") != frames or tj.get("step") != step:
+        return None
+    return tj.get("pipeline_hbm_bytes_per_call")
 
 
 def _timed(b, fn, reps):
@@ -345,11 +358,19 @@ def main():
             "achieved_GBps": round(pbytes / p_avg_s / 1e9, 1),
             "frac": round(pbytes / p_avg_s / 1e9 / PEAK_HBM_GBS, 4),
             "algorithmic_bytes_per_call": pbytes,
+            "bytes_note": "algorithmic = SURVEY 8d config 4: 4 B read per grid point (disparity + BGR) + 20 B per "
+                          "kept point + 4 KB histogram per frame; the resident kernel does not read the BGR (nor, "
+                          "in pass 2, the disparity) of chunks the keep table rules out, so it moves fewer bytes "
+                          "(traffic = PMC bytes per call, frac_of_traffic = traffic / time / peak)",
             "counts_total": {"valid": int(counts[0]), "kept": int(counts[1]), "kept2": n_kept2},
             "plane_broadcast": "RCCL ncclBroadcast over xGMI, every step" if comm else "n/a (single process)",
             "kernels": "keep_table_kernel (per call) + resident_fused_kernel (one workgroup per frame)"
                        if args.frames >= 512 else "tiled: stage_kernel + offsets_kernel",
         }
+        ptraffic = pipeline_traffic(args.traffic_pipeline, count, args.step)
+        if ptraffic:
+            out["pipeline"]["traffic"] = ptraffic
+            out["pipeline"]["frac_of_traffic"] = round(ptraffic / p_avg_s / 1e9 / PEAK_HBM_GBS, 4)
 
     if want_pipe and not args.no_extras and world == 1:   # §8f component timings: the N=1 run only
         out["extras"] = extras(b, sb, args, local, not args.no_cpu)
