@@ -732,9 +732,13 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     int32_t* oP = bf.pts + (int64_t)frame * bf.cap * 2;
     uint32_t running = 0, flushed = 0;
     const int n2 = (p.ablate & 256) ? 0 : p.nchunks;
-    // a chunk none of whose grid points can be kept (keep table) adds no output and
-    // is skipped, loads included; the last chunk always runs (it flushes the tail)
-    const auto run = [&](int c) { return c + 1 == n2 || bf.cany[c] != 0; };
+    // a chunk in which pass 1 kept no point (its keep1 range is 0 in every wave;
+    // always so where the keep table rules the chunk out) adds no output and is
+    // skipped, loads included; the last chunk always runs (it flushes the tail)
+    const auto run = [&](int c) {
+        const uint4 cr = *reinterpret_cast<const uint4*>(sh.crange + 4 * c);
+        return c + 1 == n2 || (cr.x | cr.y | cr.z | cr.w) != 0u;
+    };
     P2Regs<STEP, QP> r2;
     if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, sh.crange, bf, p, false, run(0));
     for (int c = 0; c < n2; ++c) {
