@@ -184,7 +184,8 @@ int sv_batch_read_frame_plane(sv_batch* b, int frame, double* out4);
 /* Pipeline kernel family: 0 = auto (frame-resident for >= 512 frames when the
  * frame fits, else tiled), 1 = tiled (tiles of 4096 points across workgroups,
  * offsets kernel between the passes), 2 = frame-resident (one workgroup per
- * frame, LDS histogram; frames of <= 1M grid points at step 1; both passes
+ * frame, LDS histogram; frames of <= 1M grid points and <= 2048 grid points a
+ * side, else SV_E_ARG; chunks the keep table rules out are skipped; both passes
  * prefetch the next chunk), 3 = frame-resident without prefetch, 4 =
  * frame-resident with the pass-2 prefetch only. Results are identical; only
  * the speed differs. */
