@@ -268,6 +268,18 @@ def test_pipeline_edge_frames(svx_mod, kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("plane", [(0.0, -3.0, -0.5), (0.0, 2.87, 0.44), (0.02, 2.9, -0.3)])
+def test_pipeline_chunk_skipping(svx_mod, kind, plane):
+    """Planes under which the keep table rules out none, some or all of the
+    resident kernel's chunks (those chunks are skipped): the valid count still
+    covers every grid point and the outputs equal the oracle's."""
+    disp, bgr = oracle.synth_frame(5)
+    for step in (1, 2):
+        got = _pipe(svx_mod, kind, disp, bgr, step, plane=plane)
+        _check_pipe(got, oracle.pipeline_frame(disp, bgr, step, abc=np.array(plane)))
+
+
+@pytest.mark.parametrize("kind", KINDS)
 def test_pipeline_random_colours_and_planes(svx_mod, kind):
     """Uniformly random BGR (every hue bin, exact ties included) and random
     disparity, under planes that put many points near the keep1 boundary."""
