@@ -107,6 +107,27 @@ __device__ __forceinline__ const uint8_t* row_ptr(const uint8_t* base, int gy, i
     return base + (int64_t)(g * STEP) * p.W * bpp;
 }
 
+// Can any grid point of the tile be kept by the plane (keep1)? P.abc = u / d with
+// u = B (a (x - cw) + b (y - ch) + c f), so keep1 <=> |u / d - 1| < t, t = thr |abc|
+// (functions.py:300-323). u is affine in (x, y): over the tile's rows and the whole
+// width its extremes are at the corners. For t < 0.99 no d in [1, 255] is kept when
+// u_max < 1 - t or u_min > 255 (1 + t); the margins (1e-9 relative) dwarf the
+// reference's fp64 rounding (~1e-15). Uniform per tile; false -> skip its colours.
+__device__ __forceinline__ bool tile_keepable(int tile, const KParams& p) {
+    const int q0 = tile * 256 * kQPT, q1 = min(q0 + 256 * kQPT, p.frame_quads) - 1;
+    const double y0 = (double)(fastdiv40(q0, p.Q_m40) * p.step), y1 = (double)(fastdiv40(q1, p.Q_m40) * p.step);
+    const double ax0 = p.a * (0.0 - p.cw), ax1 = p.a * ((double)((p.Wg - 1) * p.step) - p.cw);
+    const double by0 = p.b * (y0 - p.ch), by1 = p.b * (y1 - p.ch);
+    const double cf = p.c * p.f;
+    const double umax = p.B * (fmax(ax0, ax1) + fmax(by0, by1) + cf);
+    const double umin = p.B * (fmin(ax0, ax1) + fmin(by0, by1) + cf);
+    const double t = p.thr * p.nrm;
+    if (!(t < 0.99)) return true;   // (NaN too): no skipping
+    if (umax < (1.0 - t) * (1.0 - 1e-9) - 1e-12) return false;
+    if (umin > 255.0 * (1.0 + t) * (1.0 + 1e-9) + 1e-9) return false;
+    return true;
+}
+
 struct PipeShared {   // pass 1
     uint32_t hist[kBins];
     uint32_t cnt[2];
@@ -131,11 +152,12 @@ __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int 
     const uint8_t* bgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
     int gy[kQPT], q[kQPT];
     tile_geometry(tile * 256 * kQPT, tid, p, gy, q);
+    live = live && tile_keepable(tile, p);   // uniform: a tile the plane rules out needs only its valid count
     QuadIn<STEP> in[kQPT];
 #pragma unroll
     for (int i = 0; i < kQPT; ++i) {   // all loads in flight before any use
         load_disp<STEP>(row_ptr<STEP>(disp, gy[i], 1, p), q[i], in[i].d);
-        load_bgr<STEP>(row_ptr<STEP>(bgr, gy[i], 3, p), q[i], in[i]);
+        if (live) load_bgr<STEP>(row_ptr<STEP>(bgr, gy[i], 3, p), q[i], in[i]);
     }
     for (int i = tid; i < kBins; i += 256) sh.hist[i] = 0;
     if (tid < 2) sh.cnt[tid] = 0;
@@ -308,6 +330,7 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
                                              const KParams& p, CompactShared& sh) {
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int64_t slot = (int64_t)frame * tiles + t;
+    if (bf.tcount[slot] == 0) return;   // uniform: no keep1 point, so no output (no barrier skipped by part of the block)
     const uint8_t* disp = bf.disp + (int64_t)frame * p.frame_px;
     const uint32_t keep = bf.kbits[slot * 256 + tid];
     const uint32_t toff = bf.toff[slot];
