@@ -330,7 +330,8 @@ template <int STEP, int QP>
 struct P2Regs {
     RQuads<STEP, QP> g;
     uint32_t dw[RCfg<STEP, QP>::QPL][STEP];
-    uint2 tw[RCfg<STEP, QP>::QPL];
+    uint2 tw[RCfg<STEP, QP>::QPL];   // step 2: keep-table words (step 1: the keep1 bits of pass 1 in kb)
+    uint32_t kb;
     uint32_t fx[kRDN / 8], fy;   // the chunk's staged delta words (this lane's share)
     int dlo, ywb;                // first staged disparity; the chunk's 32-row word
     bool narrow;                 // the chunk's keep1 range and rows fit the stage
@@ -351,12 +352,13 @@ __device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, con
 template <int STEP, int QP>
 __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint16_t* tab,
                                         const uint32_t* crange, const PipeBuffers& bf, const RParams& p, bool next,
-                                        bool run) {
+                                        bool run, const uint16_t* fkb) {
     if (next) r_geometry_next<STEP, QP>(c, tid, p, r.g);   // r.g holds chunk c - 1
     else r_geometry<STEP, QP>(c, tid, p, r.g);
     if (!run) return;   // uniform: a chunk pass 2 skips (none of its grid points can be kept)
     r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
-    r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
+    if constexpr (STEP == 1) r.kb = fkb[c * 256 + tid];   // pass 1's keep1 bits (this lane wrote them)
+    else r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
     // delta words of the chunk's keep1 disparities (pass 1's range), written to
     // LDS at the chunk's start; every index is clamped in range, so the loads
     // are unconditional (whatever crange holds)
@@ -416,14 +418,15 @@ __device__ __forceinline__ uint32_t r_keep_range(const uint32_t (&dw)[RCfg<STEP,
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint32_t* hist, uint32_t* dirty,
                                          uint32_t* crange, uint32_t* wstage, uint32_t* dump, const RParams& p,
-                                         uint32_t& nvalid, uint32_t& nkept, bool any) {
+                                         uint32_t& nvalid, uint32_t& nkept, bool any, uint16_t* fkb) {
     const int lane = lane_id();
     nvalid += r_nvalid<STEP, QP>(r.dw, r.g, p);
+    const uint32_t keep = any ? r_keep1<STEP, QP>(r.dw, r.tw, r.g) : 0u;
+    if constexpr (STEP == 1) fkb[c * 256 + threadIdx.x] = (uint16_t)keep;   // for pass 2 (read back by this lane)
     if (!any) {   // uniform: no grid point of the chunk can be kept (keep table): nothing to bin
         if (lane == 0) crange[4 * c + (threadIdx.x >> 6)] = 0u;
         return;
     }
-    const uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
     nkept += __builtin_popcount(keep);
     {
         const uint32_t w = r_keep_range<STEP, QP>(r.dw, keep);
@@ -551,10 +554,12 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
                                          const uint8_t* fdisp, const uint8_t* fbgr, const uint16_t* tab,
                                          const PipeBuffers& bf, float* oX, int32_t* oP, uint32_t& running,
-                                         uint32_t& flushed, bool next_run, const RParams& p) {
+                                         uint32_t& flushed, bool next_run, const uint16_t* fkb, const RParams& p) {
     constexpr int QPL = RCfg<STEP, QP>::QPL;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    uint32_t keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
+    uint32_t keep;
+    if constexpr (STEP == 1) keep = r.kb;
+    else keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
     // this chunk's delta words into LDS, read by its scatter after the next
     // barrier (every wave has finished chunk c - 1's scatter)
     uint32_t* dl = sh.dlt;
@@ -647,7 +652,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
             o += bit;
         }
     }
-    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p, true, next_run);   // in flight before the stores
+    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p, true, next_run, fkb);   // in flight before the stores
     __syncthreads();
     running += T;
     // write whole 128-byte lines: outputs up to a multiple of 32 (X, Y, Z: 32 floats a line; P: 16 pairs),
@@ -693,6 +698,7 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
     if (tid < maxchunks_of<QP>() / 32) sh.dirty[tid] = 0;
     __syncthreads();
     uint32_t nvalid = 0, nkept = 0;
+    uint16_t* fkb = bf.kbits + (int64_t)frame * p.nchunks * 256;   // step 1: keep1 bits per chunk and lane
     const int n1 = (p.ablate & 128) ? 0 : p.nchunks;   // ablate: DIAGNOSTIC ONLY
     if constexpr (PF1) {   // chunk c + 1's loads in flight while chunk c is binned (pass 1 stores nothing)
         P1Regs<STEP, QP> r1;
@@ -701,14 +707,14 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
             P1Regs<STEP, QP> cur = r1;
             if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, tab, p, true, bf.cany[c + 1] != 0);
             p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept,
-                               bf.cany[c] != 0);
+                               bf.cany[c] != 0, fkb);
         }
     } else {
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> r1;
             const bool any = bf.cany[c] != 0;
             p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, tab, p, false, any);
-            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept, any);
+            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept, any, fkb);
         }
     }
     nvalid = wave_sum(nvalid);
@@ -739,16 +745,17 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
         const uint4 cr = *reinterpret_cast<const uint4*>(sh.crange + 4 * c);
         return c + 1 == n2 || (cr.x | cr.y | cr.z | cr.w) != 0u;
     };
+    const uint16_t* fkb = bf.kbits + (int64_t)frame * p.nchunks * 256;
     P2Regs<STEP, QP> r2;
-    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, sh.crange, bf, p, false, run(0));
+    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, sh.crange, bf, p, false, run(0), fkb);
     for (int c = 0; c < n2; ++c) {
-        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, sh.crange, bf, p, c > 0, run(c));
+        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, sh.crange, bf, p, c > 0, run(c), fkb);
         if (!run(c)) {   // uniform; c + 1 < n2 here
-            if (PF) p2_load<STEP, QP>(r2, c + 1, tid, fdisp, tab, sh.crange, bf, p, true, run(c + 1));
+            if (PF) p2_load<STEP, QP>(r2, c + 1, tid, fdisp, tab, sh.crange, bf, p, true, run(c + 1), fkb);
             continue;
         }
         p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
-                               running, flushed, c + 1 < n2 && run(c + 1), p);
+                               running, flushed, c + 1 < n2 && run(c + 1), fkb, p);
     }
     if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;
 }
