@@ -684,7 +684,7 @@ struct FusedShared {
     alignas(16) uint32_t crange[maxchunks_of<QP>() * 4];
     uint32_t dlt[kRDeltaWords];   // pass 2: the chunk's delta words (scatter lookups)
 };
-static_assert(sizeof(FusedShared<4>) <= 32768, "5 workgroups per CU (160 KiB LDS); 4 are VGPR-resident");
+static_assert(sizeof(FusedShared<4>) <= 32768, "5 workgroups per CU (160 KiB LDS), as many as 93 VGPRs allow");
 
 template <int STEP, int QP, bool PF1 = false>
 __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, const PipeBuffers& bf,
