@@ -254,6 +254,16 @@ int sv_batch_read_hist(sv_batch* b, int frame, uint32_t* hist /* 1024 */);
 int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64_t cap, int64_t* n);
 
 /* ---- verification helpers (device computes, host compares) -------------- */
+/* Per-frame verification digests of the batch's current outputs (test and
+ * bench support, not timed): which = 0 checks the K1 dense planes, 1 the
+ * pipeline outputs. out = frames x 8 uint64: n_valid, n_kept, n_kept2,
+ * disp_hash, hist_hash, pts_hash, bad, 0 — the definitions of
+ * oracle/svx_oracle.c svo_frame_digest, recomputed on the device from the
+ * outputs (kernels/digest.hip); `bad` counts outputs outside 1e-5 relative of
+ * the fp64 reference values or inconsistent with the disparity. Synchronous. */
+int sv_batch_digest(sv_batch* b, const sv_camera* cam, int which, uint64_t* out);
+
+
 /* Hue bin of all 2^24 colours, index R<<16|G<<8|B (for exhaustive tests). */
 int sv_hue_lut(int device, int16_t* out_lut);
 /* Back-projection delta tables as computed on the device: dx[d][x], dy[d][y]. */

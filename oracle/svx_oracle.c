@@ -16,6 +16,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 typedef struct { double f, B, cw, ch; } svo_camera;
@@ -280,4 +281,68 @@ int svo_pipeline_frame(const uint8_t* disp, const uint8_t* bgr, int H, int W, in
     counts[1] = n1;
     counts[2] = n2;
     return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * Per-frame digests: the checker's summary of one full-size synthetic frame.
+ * The device computes the same summary of its own outputs (digest kernels,
+ * sv_batch_digest), so EVERY frame of a batch is checked at full size without
+ * moving the outputs off the GPU. Definitions (the spec shared with
+ * stereo.vision_amd/csrc/kernels/digest.hip; sums mod 2^64):
+ *   disp_hash = sum_j mix64(j << 32 | word_j), word_j = little-endian u32 j of
+ *               the frame's disparity (H*W % 4 == 0)
+ *   hist_hash = sum_{k<1000} mix64((k + 65536) << 32 | hist[k])
+ *   pts_hash  = sum_i mix64(A_i ^ mix64(i)) over the surviving points in
+ *               order, A_i = (x | y << 12 | d << 24) << 32 | (px & 0xFFFF) |
+ *               (py & 0xFFFF) << 16: source pixel (x, y), its disparity d and
+ *               its int32 back-projection (px, py) (functions.py:201-209,
+ *               stereovision.py:112)
+ * counts = svo_pipeline_frame's (N_valid, N_kept, N_kept2).
+ * --------------------------------------------------------------------- */
+uint64_t svo_digest_mix(uint64_t z) { return svo_mix64(z); }
+
+int svo_frame_digest(int64_t frame_id, int H, int W, int step, const svo_camera* cam, const double* abc,
+                     double point_thr, int hist_thr, int64_t* counts, uint64_t* hashes) {
+    const int Hg = (H - 1 + step - 1) / step, Wg = (W - 1 + step - 1) / step;
+    const size_t cap = (size_t)(Hg > 0 && Wg > 0 ? Hg * Wg : 1);
+    const size_t px = (size_t)H * W;
+    uint8_t* disp = malloc(px);
+    uint8_t* bgr = malloc(px * 3);
+    int32_t* pts = malloc(cap * 2 * sizeof(int32_t));
+    int32_t* src2 = malloc(cap * 2 * sizeof(int32_t));
+    double* s_xyz = malloc(cap * 3 * sizeof(double));
+    uint8_t* s_rgb = malloc(cap * 3);
+    int32_t* s_src = malloc(cap * 2 * sizeof(int32_t));
+    uint8_t* s_keep = malloc(cap);
+    int16_t* s_bin = malloc(cap * sizeof(int16_t));
+    uint32_t hist[1024];
+    int rc = -1;
+    if (!disp || !bgr || !pts || !src2 || !s_xyz || !s_rgb || !s_src || !s_keep || !s_bin || (px % 4) ||
+        W > 4096 || H > 4096)
+        goto out;
+    svo_synth_frame(frame_id, H, W, disp, bgr);
+    svo_pipeline_frame(disp, bgr, H, W, step, cam, abc, point_thr, hist_thr, counts, hist, NULL, pts, src2,
+                       s_xyz, s_rgb, s_src, s_keep, s_bin);
+    uint64_t hd = 0, hh = 0, hp = 0;
+    for (size_t j = 0; j < px / 4; ++j) {
+        uint32_t w = (uint32_t)disp[4 * j] | ((uint32_t)disp[4 * j + 1] << 8) | ((uint32_t)disp[4 * j + 2] << 16) |
+                     ((uint32_t)disp[4 * j + 3] << 24);
+        hd += svo_mix64(((uint64_t)j << 32) | w);
+    }
+    for (uint64_t k = 0; k < 1000; ++k) hh += svo_mix64(((k + 65536) << 32) | hist[k]);
+    for (int64_t i = 0; i < counts[2]; ++i) {
+        const uint32_t y = (uint32_t)src2[2 * i], x = (uint32_t)src2[2 * i + 1];
+        const uint32_t d = disp[(size_t)y * W + x];
+        const uint64_t a = ((uint64_t)(x | (y << 12) | (d << 24)) << 32) |
+                           (uint64_t)(((uint32_t)pts[2 * i] & 0xFFFFu) | (((uint32_t)pts[2 * i + 1] & 0xFFFFu) << 16));
+        hp += svo_mix64(a ^ svo_mix64((uint64_t)i));
+    }
+    hashes[0] = hd;
+    hashes[1] = hh;
+    hashes[2] = hp;
+    rc = 0;
+out:
+    free(disp); free(bgr); free(pts); free(src2);
+    free(s_xyz); free(s_rgb); free(s_src); free(s_keep); free(s_bin);
+    return rc;
 }

@@ -1,0 +1,184 @@
+// Per-frame verification digests (gfx950): test / bench support, never timed.
+//
+// The checker's summary of a frame (oracle/svx_oracle.c svo_frame_digest) is
+// recomputed here from the device's own outputs, so every frame of a
+// 4096-frame (or, per shard, 32,768-frame) batch is compared with the oracle at
+// full size without copying gigabytes of points off the GPU. Definitions
+// (sums mod 2^64, mix64 = the splitmix64 finaliser of the frame generator):
+//   disp_hash = sum_j mix64(j << 32 | word_j) over the frame's disparity words
+//   hist_hash = sum_{k<1000} mix64((k + 65536) << 32 | hist[k])
+//   pts_hash  = sum_i mix64(A_i ^ mix64(i)), A_i = (x | y << 12 | d << 24) << 32
+//               | (px & 0xFFFF) | (py & 0xFFFF) << 16 for output i
+// For the pipeline the source pixel (x, y) and d of output i are recovered from
+// its fp32 X, Y, Z (d = rint(fB / Z), x = rint(X f / Z + cw), y = rint(Y f / Z
+// + ch): fp32 XYZ are within 1e-6 relative, so the recovery is exact); `bad`
+// counts outputs whose recovery is out of range, whose disparity at (x, y) is
+// not d, or whose X, Y, Z are not within 1e-5 relative of the fp64 reference
+// values (functions.py:191-193). For K1 (dense planes) `bad` counts grid points
+// whose Z = 0 marking disagrees with d = 0 or whose X, Y, Z are not within 1e-5
+// relative; n_valid counts the Z != 0 points.
+#include "../svx_launch.h"
+
+namespace svx {
+
+namespace {
+
+__device__ __forceinline__ uint64_t dmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+constexpr double kRtol = 1e-5;
+
+__device__ __forceinline__ bool close_rel(float got, double want) {
+    return __builtin_fabs((double)got - want) <= kRtol * __builtin_fabs(want);
+}
+
+// block-wide sum of n u64 accumulators (256 threads); result valid in thread 0
+template <int N>
+__device__ __forceinline__ void block_sum(uint64_t (&v)[N], uint64_t (*red)[N]) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        uint64_t x = v[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t lo = __shfl_xor((uint32_t)x, o, 64), hi = __shfl_xor((uint32_t)(x >> 32), o, 64);
+            x += ((uint64_t)hi << 32) | lo;
+        }
+        if (lane == 0) red[wave][k] = x;
+    }
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+    }
+}
+
+__device__ __forceinline__ uint64_t disp_hash_part(const uint32_t* fd, int64_t words) {
+    uint64_t h = 0;
+    for (int64_t j = threadIdx.x; j < words; j += 256) h += dmix64(((uint64_t)j << 32) | fd[j]);
+    return h;
+}
+
+// one workgroup per frame: out[8 * frame + ...] (see sv_batch_digest)
+__global__ __launch_bounds__(256) void digest_pipe_kernel(const uint8_t* __restrict__ disp,
+                                                          const uint32_t* __restrict__ hist,
+                                                          const int64_t* __restrict__ counts,
+                                                          const float* __restrict__ xyz,
+                                                          const int32_t* __restrict__ pts, int64_t cap, KParams p,
+                                                          uint64_t* __restrict__ out) {
+    __shared__ uint64_t red[4][4];
+    const int frame = blockIdx.x, tid = threadIdx.x;
+    const uint8_t* fd = disp + (int64_t)frame * p.frame_px;
+    const int64_t n2 = counts[4 * (int64_t)frame + 2];
+    const float* oX = xyz + (int64_t)frame * 3 * cap;
+    const float* oY = oX + cap;
+    const float* oZ = oY + cap;
+    const int32_t* oP = pts + (int64_t)frame * 2 * cap;
+    uint64_t acc[4] = {disp_hash_part(reinterpret_cast<const uint32_t*>(fd), p.frame_px / 4), 0, 0, 0};
+    for (int k = tid; k < 1000; k += 256)
+        acc[1] += dmix64(((uint64_t)(k + 65536) << 32) | hist[(int64_t)frame * kBins + k]);
+    for (int64_t i = tid; i < (n2 <= cap ? n2 : 0); i += 256) {
+        const float X = oX[i], Y = oY[i], Z = oZ[i];
+        const double Zd = (double)Z;
+        const double dr = __builtin_rint(p.fB / Zd);
+        const double xr = __builtin_rint((double)X * p.f / Zd + p.cw);
+        const double yr = __builtin_rint((double)Y * p.f / Zd + p.ch);
+        bool ok = Z > 0.0f && dr >= 1.0 && dr <= 255.0 && xr >= 0.0 && xr < (double)p.W && yr >= 0.0 &&
+                  yr < (double)p.H;
+        uint32_t x = 0, y = 0, d = 0;
+        if (ok) {
+            x = (uint32_t)xr;
+            y = (uint32_t)yr;
+            d = (uint32_t)dr;
+            ok = fd[(int64_t)y * p.W + x] == d;
+            const double Z64 = p.fB / (double)d;
+            const double X64 = (((double)x - p.cw) * Z64) / p.f;
+            const double Y64 = (((double)y - p.ch) * Z64) / p.f;
+            ok = ok && close_rel(X, X64) && close_rel(Y, Y64) && close_rel(Z, Z64);
+        }
+        const uint32_t px = (uint32_t)oP[2 * i], py = (uint32_t)oP[2 * i + 1];
+        const uint64_t a = ((uint64_t)(x | (y << 12) | (d << 24)) << 32) | (uint64_t)((px & 0xFFFFu) | ((py & 0xFFFFu) << 16));
+        acc[2] += dmix64(a ^ dmix64((uint64_t)i));
+        acc[3] += ok ? 0u : 1u;
+    }
+    block_sum<4>(acc, red);
+    if (tid == 0) {
+        uint64_t* o = out + 8 * (int64_t)frame;
+        o[0] = (uint64_t)counts[4 * (int64_t)frame + 0];
+        o[1] = (uint64_t)counts[4 * (int64_t)frame + 1];
+        o[2] = (uint64_t)n2;
+        o[3] = acc[0];
+        o[4] = acc[1];
+        o[5] = acc[2];
+        o[6] = acc[3] + (n2 > cap ? 1u : 0u);
+        o[7] = 0;
+    }
+}
+
+// K1 outputs: three planes of frames x Hg x pitch fp32
+__global__ __launch_bounds__(256) void digest_dense_kernel(const uint8_t* __restrict__ disp,
+                                                           const float* __restrict__ Xp, const float* __restrict__ Yp,
+                                                           const float* __restrict__ Zp, KParams p,
+                                                           uint64_t* __restrict__ out) {
+    __shared__ uint64_t red[4][3];
+    const int frame = blockIdx.x, tid = threadIdx.x;
+    const uint8_t* fd = disp + (int64_t)frame * p.frame_px;
+    const int64_t per = (int64_t)p.Hg * p.pitch, base = per * frame;
+    uint64_t acc[3] = {disp_hash_part(reinterpret_cast<const uint32_t*>(fd), p.frame_px / 4), 0, 0};
+    for (int64_t i = tid; i < per; i += 256) {
+        const int gy = (int)(i / p.pitch), gx = (int)(i - (int64_t)gy * p.pitch);
+        const float X = Xp[base + i], Y = Yp[base + i], Z = Zp[base + i];
+        bool ok;
+        if (gx >= p.Wg) {
+            ok = Z == 0.0f;
+        } else {
+            const int x = gx * p.step, y = gy * p.step;
+            const uint32_t d = fd[(int64_t)y * p.W + x];
+            if (d == 0) {
+                ok = Z == 0.0f;
+            } else {
+                const double Z64 = p.fB / (double)d;
+                const double X64 = (((double)x - p.cw) * Z64) / p.f;
+                const double Y64 = (((double)y - p.ch) * Z64) / p.f;
+                ok = Z != 0.0f && close_rel(X, X64) && close_rel(Y, Y64) && close_rel(Z, Z64);
+                acc[1] += 1;
+            }
+        }
+        acc[2] += ok ? 0u : 1u;
+    }
+    block_sum<3>(acc, red);
+    if (tid == 0) {
+        uint64_t* o = out + 8 * (int64_t)frame;
+        o[0] = acc[1];
+        o[1] = 0;
+        o[2] = 0;
+        o[3] = acc[0];
+        o[4] = 0;
+        o[5] = 0;
+        o[6] = acc[2];
+        o[7] = 0;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_digest_pipe(const KParams& p, const uint8_t* disp, const uint32_t* hist, const int64_t* counts,
+                              const float* xyz, const int32_t* pts, int64_t cap, int frames, uint64_t* out,
+                              hipStream_t s) {
+    if (frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(digest_pipe_kernel, dim3(frames), dim3(256), 0, s, disp, hist, counts, xyz, pts, cap, p, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_digest_dense(const KParams& p, const uint8_t* disp, const float* X, const float* Y, const float* Z,
+                               int frames, uint64_t* out, hipStream_t s) {
+    if (frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(digest_dense_kernel, dim3(frames), dim3(256), 0, s, disp, X, Y, Z, p, out);
+    return hipGetLastError();
+}
+
+}  // namespace svx

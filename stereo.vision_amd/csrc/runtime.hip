@@ -732,6 +732,30 @@ int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64
     return SV_OK;
 }
 
+int sv_batch_digest(sv_batch* b, const sv_camera* cam, int which, uint64_t* out) {
+    if (!b || !cam || !out || which < 0 || which > 1) return fail(SV_E_ARG, "sv_batch_digest: bad args");
+    if (which == 0 && !b->Z.p) return fail(SV_E_STATE, "sv_batch_digest: nothing projected");
+    if (which == 1 && !b->pts.p) return fail(SV_E_STATE, "sv_batch_digest: no pipeline outputs");
+    if ((b->kp.frame_px % 4) != 0) return fail(SV_E_ARG, "sv_batch_digest: H * W must be a multiple of 4");
+    HIP_TRY(hipSetDevice(b->device));
+    KParams p = make_params(b->H, b->W, b->step, *cam);
+    DevBuf buf;
+    HIP_TRY(buf.ensure(sizeof(uint64_t) * 8 * (size_t)b->frames));
+    hipError_t e;
+    if (which == 0)
+        e = launch_digest_dense(p, b->disp.as<uint8_t>(), b->X.as<float>(), b->Y.as<float>(), b->Z.as<float>(),
+                                b->frames, buf.as<uint64_t>(), b->stream);
+    else
+        e = launch_digest_pipe(p, b->disp.as<uint8_t>(), b->hist, b->counts, b->xyz.as<float>(), b->pts.as<int32_t>(),
+                               (int64_t)b->cap, b->frames, buf.as<uint64_t>(), b->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, buf.p, sizeof(uint64_t) * 8 * (size_t)b->frames, hipMemcpyDeviceToHost,
+                                            b->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(b->stream);
+    (void)hipFree(buf.p);
+    HIP_TRY(e);
+    return SV_OK;
+}
+
 // ---------------------------------------------------------------------------
 // fused one-frame chain (stereovision.py:84,97-113) through a cached batch
 // ---------------------------------------------------------------------------

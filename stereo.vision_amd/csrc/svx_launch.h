@@ -139,4 +139,12 @@ hipError_t launch_hue_hist(const uint8_t* rgb, int64_t n, int64_t ld, int16_t* b
 hipError_t launch_select(int mode, const double* vals, double thr, const int16_t* bins, const uint8_t* ok, int64_t n,
                          int64_t* out_idx, int64_t* out_n, hipStream_t s);
 
+// kernels/digest.hip -------------------------------------------------------
+// Per-frame verification digests (out: frames x 8 u64, see sv_batch_digest).
+hipError_t launch_digest_pipe(const KParams& p, const uint8_t* disp, const uint32_t* hist, const int64_t* counts,
+                              const float* xyz, const int32_t* pts, int64_t cap, int frames, uint64_t* out,
+                              hipStream_t s);
+hipError_t launch_digest_dense(const KParams& p, const uint8_t* disp, const float* X, const float* Y, const float* Z,
+                               int frames, uint64_t* out, hipStream_t s);
+
 }  // namespace svx

@@ -84,6 +84,7 @@ SIGNATURES = {
     "sv_batch_read_counts": [P, P],
     "sv_batch_read_hist": [P, I, P],
     "sv_batch_read_points": [P, I, P, P, I64, PI64],
+    "sv_batch_digest": [P, ctypes.POINTER(Camera), I, P],
     "sv_hue_lut": [I, P],
     "sv_delta_tables": [I, I, I, ctypes.POINTER(Camera), P, P],
     "sv_synth_frame": [I, I64, I, I, P, P],

@@ -193,6 +193,17 @@ class Batch:
         _abi.call("sv_batch_read_maskpoints", self._h, frame, _abi.ptr(xyz), cap, ctypes.byref(n))
         return xyz[: n.value]
 
+    DIGEST_FIELDS = ("n_valid", "n_kept", "n_kept2", "disp_hash", "hist_hash", "pts_hash", "bad")
+
+    def digest(self, which="pipeline", camera=None):
+        """Per-frame verification digests of the current outputs (which = "dense" for K1's
+        planes, "pipeline" for the pipeline's points): a (frames, 8) uint64 array with the
+        columns of DIGEST_FIELDS (see sv_batch_digest); computed on the device."""
+        cam = camera or CAMERA
+        out = np.empty((self.frames, 8), np.uint64)
+        _abi.call("sv_batch_digest", self._h, ctypes.byref(cam), 0 if which == "dense" else 1, _abi.ptr(out))
+        return out
+
     # -- outputs -------------------------------------------------------------------
     def read_dense(self, frame):
         shape = (self.Hg, self.pitch)

@@ -1,0 +1,82 @@
+"""Every frame at BASELINE.json's full sizes against the oracle.
+
+The device summarises its own outputs per frame (sv_batch_digest,
+kernels/digest.hip): the counts, hashes of the disparity, of the hue histogram
+and of the surviving points in order (source pixel, disparity, int32
+back-projection) and a count of outputs whose fp32 X, Y, Z are not within 1e-5
+relative of the fp64 reference values. Those rows must equal
+tests/golden/frame_digests.npz, written by the pinned C oracle
+(tests/golden/make_frame_digests.py), for EVERY frame:
+  * configs[2]: K1 dense projection of 4096 frames (counts, disparity, tolerance)
+  * configs[3]: the pipeline over 4096 frames, resident and tiled kernels, steps 1 and 2
+  * configs[4]: all 32,768 frames, generated and processed shard by shard as
+    the 8 ranks would (4096 frames each, global frame ids), on one GPU."""
+import os
+import types
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("n_valid", "n_kept", "n_kept2", "disp_hash", "hist_hash", "pts_hash")
+
+
+@pytest.fixture(scope="module")
+def env():
+    import svx
+    from svx import batch
+    assert svx.device_count() >= 1
+    return types.SimpleNamespace(batch=batch, fd=np.load(os.path.join(GOLDEN, "frame_digests.npz")))
+
+
+def _mismatches(got, want, fields):
+    """frames whose digest row differs (field names), plus frames with bad outputs"""
+    bad = []
+    for k, name in enumerate(FIELDS):
+        if name in fields:
+            diff = np.flatnonzero(got[:, k] != want[name].astype(np.uint64))
+            bad += [(int(i), name) for i in diff[:5]]
+    nb = np.flatnonzero(got[:, 6] != 0)
+    bad += [(int(i), f"bad={int(got[i, 6])}") for i in nb[:5]]
+    return bad
+
+
+def test_dense_every_frame_step1(env):
+    frames = 4096
+    want = env.fd["step1"][:frames]
+    with env.batch.Batch(frames, step=1, with_bgr=False) as b:
+        b.synth(0)
+        b.project()
+        got = b.digest("dense")
+    assert _mismatches(got, want, ("n_valid", "disp_hash")) == []
+
+
+@pytest.mark.parametrize("step", [1, 2])
+def test_pipeline_every_frame(env, step):
+    frames = 4096
+    want = env.fd[f"step{step}"][:frames]
+    with env.batch.Batch(frames, step=step, with_bgr=True, with_points=True) as b:
+        b.synth(0)
+        for mode in ("resident", "tiled"):
+            b.pipeline_mode(mode)
+            b.pipeline()
+            got = b.digest("pipeline")
+            assert _mismatches(got, want, FIELDS) == [], mode
+
+
+def test_config5_every_shard(env):
+    """32,768 frames = 8 shards of 4096 global frame ids (svx.dist.shard), each
+    generated on the device from its global ids and run through the pipeline."""
+    from svx import dist
+    want_all = env.fd["step1"]
+    with env.batch.Batch(4096, step=1, with_bgr=True, with_points=True) as b:
+        for rank in range(8):
+            first, count = dist.shard(32768, 8, rank)
+            assert count == 4096
+            b.synth(first)
+            b.pipeline()
+            got = b.digest("pipeline")
+            assert _mismatches(got, want_all[first:first + count], FIELDS) == [], f"shard {rank}"
