@@ -4,17 +4,32 @@
 Headline workload (BASELINE.json configs[2], the north-star target): a batch of
 4096 synthetic 1024x544 disparity maps per GPU, step 1 (555,489 grid points per
 frame), resident in HBM, projected by K1 into dense fp32 X/Y/Z planes. One
-"step" = one K1 pass over the whole batch. Multi-GPU (configs[4]): one process
-per GPU, 4096 frames per rank (weak scaling), frames sharded by global id, no
-data-path collective.
+"step" = one K1 pass over the whole batch. Multi-GPU (configs[4]): 4096 frames
+per GPU (weak scaling), frames sharded by global id, no data-path collective.
+
+How N GPUs are driven (`--gpus N`):
+  * under torchrun (WORLD_SIZE set; it must equal N): one process per GPU,
+    LOCAL_RANK's device, host control over TCP (svx/control.py), RCCL
+    communicator per rank;
+  * plain `python bench.py --gpus N`, N > 1: ONE process drives devices
+    0..N-1: one sv_batch per device, ncclCommInitAll, the plane
+    broadcast of all devices in one RCCL group (sv_multi_pipeline).
+Either way: barrier + device sync on both sides of the K timed steps, the
+max over ranks, `value` = grid points of all GPUs / that time.
 
 Also reported (same JSON line):
   pipeline      configs[3]/[4]: plane threshold + hue histogram + ordered
                 compaction + int32 back-projection over the same batch; for
-                N>1 each step starts with the RCCL broadcast of the plane.
+                N > 1 every step starts with the RCCL broadcast of the plane
+                into device memory (read there by the pipeline).
+  parity        every frame of every shard (K1 and pipeline outputs) checked
+                on the device against tests/golden/frame_digests.npz (the
+                pinned C oracle's per-frame digests, global frame ids).
   latency_1frame_us  configs[1]: one frame, step 1, K1 kernel time.
-  cpu_baseline  the nested-loop CPU port (oracle/cpu_loop.py, same numpy-scalar
-                semantics as functions.py:178-198), rank 0 at N=1 only.
+  cpu_baseline  configs[0]: the nested-loop CPU port (oracle/cpu_loop.py, the
+                numpy-scalar semantics of functions.py:178-323) on one pinned
+                host core: stereovision.py:84-113 for frame 0 at step 2, per
+                stage; rank 0 at N = 1 only.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -36,9 +51,11 @@ METRIC = "Mpoints/sec disparity→3D at 1024×544; achieved HBM GB/s vs peak"
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 H, W = 544, 1024
 K1_BYTES_PER_POINT = 13        # 1 B disparity read + 12 B fp32 XYZ written
+GOLDEN_DIGESTS = os.path.join(REPO, "tests", "golden", "frame_digests.npz")
+CARMASK = os.path.join(REPO, "tests", "golden", "carmask.npz")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -51,53 +68,124 @@ def parse():
     ap.add_argument("--ramp-ms", type=float, default=300.0,
                     help="untimed K1 launches before the warmup steps, to let clocks settle")
     ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--no-latency", action="store_true",
-                    help="skip the 1-frame latency probe")
+    ap.add_argument("--no-latency", action="store_true", help="skip the 1-frame latency probe")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the SURVEY §8f component timings")
+    ap.add_argument("--no-parity", action="store_true", help="skip the per-frame digest check")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--traffic-pipeline", default=os.path.join(REPO, "profiles", "traffic_pipeline.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def plan(gpus, environ):
+    """How this process takes part in an N-GPU run:
+    mode "ranks" (torchrun: one process per GPU), "multi" (one process, N GPUs)
+    or "single". Returns dict(mode, n_gpus, rank, world, devices, shard_base):
+    this process drives `devices`, which hold global shards shard_base.. of n_gpus."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    if "WORLD_SIZE" in environ:
+        world = int(environ["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: launched with WORLD_SIZE={world} but --gpus {gpus}; "
+                             f"use torchrun --nproc-per-node {gpus} (one process per GPU) or run "
+                             f"`python bench.py --gpus {gpus}` without a launcher (one process, {gpus} GPUs)")
+        rank, local = int(environ.get("RANK", 0)), int(environ.get("LOCAL_RANK", 0))
+        return dict(mode="ranks", n_gpus=world, rank=rank, world=world, devices=[local], shard_base=rank)
+    if gpus == 1:
+        return dict(mode="single", n_gpus=1, rank=0, world=1, devices=[0], shard_base=0)
+    return dict(mode="multi", n_gpus=gpus, rank=0, world=1, devices=list(range(gpus)), shard_base=0)
+
+
+def shards_of(pl, frames_per_gpu):
+    """(device, first global frame id, frames) of each GPU this process drives."""
+    from svx.dist import shard
+    total = frames_per_gpu * pl["n_gpus"]
+    return [(dev, *shard(total, pl["n_gpus"], pl["shard_base"] + j)) for j, dev in enumerate(pl["devices"])]
+
+
+def aggregate(ctrl, n_gpus, points_local, steps, dt_local):
+    """Whole-job rate: all GPUs' grid points over the max-over-ranks wall time."""
+    dt = float(ctrl.max([dt_local])[0])
+    points = float(ctrl.sum([points_local])[0]) * steps
+    return {"n_gpus": n_gpus, "value": points / dt / 1e6, "ms_per_step": dt / steps * 1e3, "points": points}
+
+
+def carmask():
+    z = np.load(CARMASK)
+    shape = tuple(int(v) for v in z["shape"])
+    return np.unpackbits(z["bits"])[: shape[0] * shape[1]].reshape(shape).astype(np.uint8) * 255
 
 
 def cpu_baseline(budget_s):
-    """Nested-loop port (oracle/cpu_loop.py) on 1 core; bounded sample of whole frames."""
+    """configs[0]: stereovision.py:84-113 for synthetic frame 0 at step 2 through the
+    nested-loop port (oracle/cpu_loop.py, oracle/ransac.py) on ONE pinned host core,
+    per stage; then a bounded step-1 projection sample (the headline workload's unit)."""
+    import random
+
     import oracle
     from oracle import cpu_loop
+    from oracle import ransac as oransac
     try:
-        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+        cpu = sorted(os.sched_getaffinity(0))[0]
+        os.sched_setaffinity(0, {cpu})
     except (AttributeError, OSError):
-        pass
-    pts = 0
-    frames = 0
-    t0 = time.perf_counter()
-    while True:
-        disp, _ = oracle.synth_frame(frames)
-        rows = cpu_loop.project(disp, None, step=1)
-        pts += (H - 1) * (W - 1)
-        frames += 1
-        assert len(rows) > 0
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    # C restatement, 1 thread, same frames (for scale; not the reported baseline)
-    t1 = time.perf_counter()
-    for f in range(frames):
-        disp, _ = oracle.synth_frame(f)
-        oracle.project(disp, None, 1)
-    dtc = time.perf_counter() - t1
+        cpu = None
     model = ""
     try:
         with open("/proc/cpuinfo") as fh:
             model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
     except OSError:
         pass
-    return {"value": pts / dt / 1e6, "unit": "Mpoints/s", "cores": 1, "kind": "port",
-            "sample": f"{frames} synthetic 1024x544 frames, step 1, projection only "
-                      f"({pts} grid points, {dt:.1f} s): oracle/cpu_loop.py nested loop "
-                      f"(functions.py:178-198 semantics)",
-            "c_restatement_mpts": pts / dtc / 1e6, "cpu": model}
+    disp, bgr = oracle.synth_frame(0)
+    mask = carmask()
+    abc_syn = np.asarray(oracle.synthetic_plane(), np.float64).reshape(3, 1)
+    ng2 = ((H - 1 + 1) // 2) * ((W - 1 + 1) // 2)   # grid of range(0,H-1,2) x range(0,W-1,2)
+
+    def stage(fn):
+        t = time.perf_counter()
+        out = fn()
+        return out, (time.perf_counter() - t) * 1e3
+
+    reps, st = 0, {}
+    t_all = time.perf_counter()
+    while True:
+        s = {}
+        points, s["a1_project_rgb"] = stage(lambda: cpu_loop.project(disp, bgr, 2))           # stereovision.py:84
+        mpts, s["a1_project_masked"] = stage(lambda: cpu_loop.project(oracle.mask_disparity(disp, mask), None, 2))
+        random.seed(0)
+        (abc, _), s["ransac_600"] = stage(lambda: oransac.ransac(np.asarray(mpts), 600))     # :94
+        abc = abc if abc is not None else abc_syn
+        dist, s["a2_point_errors"] = stage(lambda: cpu_loop.point_errors(abc, points))       # :97
+        kept, s["a3_planar_threshold"] = stage(lambda: cpu_loop.plane_keep(points, dist, 0.05))
+        hist, s["a5_colour_histogram"] = stage(lambda: cpu_loop.colour_hist(kept))
+        kept2, s["a6_histogram_filter"] = stage(lambda: cpu_loop.hist_keep(kept, hist, 10))
+        _, s["a7_a8_backproject_int32"] = stage(
+            lambda: np.array(cpu_loop.backproject(kept2), np.int32).reshape((-1, 1, 2)))
+        for k, v in s.items():
+            st.setdefault(k, []).append(v)
+        reps += 1
+        if time.perf_counter() - t_all >= budget_s * 0.7 or reps >= 5:
+            break
+    med = {k: round(float(np.median(v)), 1) for k, v in st.items()}
+    chain_ms = round(sum(med.values()), 1)
+    # bounded step-1 projection sample: the headline workload's unit of work
+    t1, frames1, pts1 = time.perf_counter(), 0, 0
+    while frames1 == 0 or time.perf_counter() - t1 < budget_s * 0.3:
+        d1, _ = oracle.synth_frame(frames1)
+        cpu_loop.project(d1, None, step=1)
+        pts1 += (H - 1) * (W - 1)
+        frames1 += 1
+    s1 = time.perf_counter() - t1
+    return {"value": round(ng2 / med["a1_project_rgb"] / 1e3, 4), "unit": "Mpoints/s", "cores": 1, "kind": "port",
+            "sample": f"configs[0]: synthetic frame 0, step 2 ({ng2} grid points), stereovision.py:84-113 "
+                      f"through oracle/cpu_loop.py + oracle/ransac.py (functions.py:178-323 semantics), "
+                      f"median of {reps} runs on one pinned core; value = grid points / projectDisparityTo3d time",
+            "config1_stage_ms": med, "config1_chain_ms_per_frame": chain_ms,
+            "step1_projection": {"Mpoints_per_s": round(pts1 / s1 / 1e6, 4), "frames": frames1,
+                                 "seconds": round(s1, 1)},
+            "cpu": model, "cpu_index": cpu}
 
 
 def pipeline_traffic(path, frames, step):
@@ -123,15 +211,61 @@ def _timed(b, fn, reps):
     return (time.perf_counter() - t0) / reps * 1e3
 
 
-def extras(b, sb, args, device, with_cpu):
+def dropin_chain(fmod, disp, bgr, reps=5):
+    """stereovision.py:84-113 for one host frame through the installed drop-ins,
+    per stage (ms, median of reps): what a user of the reference sees after
+    svx.dropin.install(functions), step 2 as the reference hard-codes."""
+    import random
+    st = {}
+    n_pp = 0
+    state = random.getstate()
+    random.seed(0)
+    for r in range(reps + 1):
+        s = {}
+        t = time.perf_counter()
+        points = fmod.projectDisparityTo3d(disp, 128, bgr)
+        s["a1_project_rgb"] = time.perf_counter() - t
+        t = time.perf_counter()
+        maskpoints = fmod.projectDisparityTo3d(fmod.maskDisparity(disp), 128)
+        s["a1_project_masked"] = time.perf_counter() - t
+        t = time.perf_counter()
+        _, abc = fmod.RANSAC(maskpoints, 600)
+        s["ransac_600"] = time.perf_counter() - t
+        t = time.perf_counter()
+        diffs = fmod.calculatePointErrors(abc, points)
+        s["a2_point_errors"] = time.perf_counter() - t
+        t = time.perf_counter()
+        points = fmod.computePlanarThreshold(points, diffs, 0.05)
+        s["a3_planar_threshold"] = time.perf_counter() - t
+        t = time.perf_counter()
+        hist = fmod.calculateColourHistogram(points)
+        s["a5_colour_histogram"] = time.perf_counter() - t
+        t = time.perf_counter()
+        points = fmod.filterPointsByHistogram(points, hist, 10)
+        s["a6_histogram_filter"] = time.perf_counter() - t
+        t = time.perf_counter()
+        pp = np.array(fmod.project3DPointsTo2DImagePoints(points), np.int32).reshape((-1, 1, 2))
+        s["a7_a8_backproject_int32"] = time.perf_counter() - t
+        n_pp = len(pp)
+        if r > 0:   # the first run warms the device buffers
+            for k, v in s.items():
+                st.setdefault(k, []).append(v * 1e3)
+    random.setstate(state)
+    med = {k: round(float(np.median(v)), 2) for k, v in st.items()}
+    return {"ms_per_frame": round(sum(med.values()), 2), "stage_ms": med, "plane_points": n_pp,
+            "stages": "stereovision.py:84-113 via installed drop-ins, step 2, RANSAC 600"}
+
+
+def extras(b, args, with_cpu):
     """SURVEY §8f components on the same resident batch (after the headline runs):
     road raster + non-zero walk of the pipeline's points, the disparity pre-pass
     (fillDisparity recurrence + carmask) over the batch, the RANSAC drop-in
     on one frame's masked points (600 trials) next to the CPU restatement, the
     batched RANSAC of every frame and the pipeline driven by those planes."""
     import random
+    import types
 
-    from svx import ransac
+    from svx import dropin, ransac
 
     import oracle
     from oracle import ransac as oransac
@@ -142,8 +276,7 @@ def extras(b, sb, args, device, with_cpu):
     byts = px + 8 * n2 + px + 8 * n2          # raster: zero + point reads (+1 B each); walk: image + [j,i]
     ex["road_raster_nonzero"] = {"ms_per_batch": round(ms, 3), "approx_GBps": round(byts / ms / 1e6, 1),
                                  "points": n2, "kernels": "raster_kernel + nonzero_kernel"}
-    mask = np.zeros((H, W), np.uint8)
-    mask[H // 3:, 64:W - 64] = 255            # a carmask-like region (timing only)
+    mask = carmask()
     b.set_mask(mask)
     ms = _timed(b, lambda: b.prepass("previous", sync=False), 3)
     ex["prepass_fill_previous_masked"] = {"ms_per_batch": round(ms, 3), "GBps": round(3 * px / ms / 1e6, 1),
@@ -176,46 +309,20 @@ def extras(b, sb, args, device, with_cpu):
     if "cpu_restatement_ms_per_call" in r:
         rb["cpu_restatement_ms_per_frame"] = r["cpu_restatement_ms_per_call"]
     ex["ransac_batch"] = rb
+    b.reset_timing()
     ms = _timed(b, lambda: b.pipeline_planes(sync=False), 3)
-    ex["pipeline_frame_planes"] = {"ms_per_batch": round(ms, 3), "frames": b.frames,
-                                   "kept_points": int(b.read_counts()[:, 2].sum()),
-                                   "kernels": "frame_planes_kernel + stage_kernel<PF> + offsets_kernel"}
+    k_ms, k_n = b.timing("pipeline")
+    ex["pipeline_frame_planes"] = {"ms_per_batch": round(ms, 3), "gpu_ms_per_call": round(k_ms / max(k_n, 1), 4),
+                                   "frames": b.frames, "kept_points": int(b.read_counts()[:, 2].sum()),
+                                   "kernels": "frame_planes_kernel + resident_fused_kernel (each frame's plane)"
+                                   if b.frames >= 512 else "frame_planes_kernel + tiled kernels"}
 
-    # stereovision.py:84-113 for one host frame through the installed drop-ins (what a user of the
-    # reference sees after svx.dropin.install(functions)): 2 projections, RANSAC(600), the four stages,
-    # back-projection and the int32 cast; step 2 as the reference hard-codes
-    import types
-
-    from svx import dropin
     fmod = types.SimpleNamespace(camera_focal_length_px=399.9745178222656, stereo_camera_baseline_m=0.2090607502,
                                  image_centre_w=474.5, image_centre_h=262.0, carmask=mask)
     dropin.install(fmod)
     try:
-        disp, bgr = oracle.synth_frame(0)
-
-        def chain():
-            points = fmod.projectDisparityTo3d(disp, 128, bgr)
-            maskpoints = fmod.projectDisparityTo3d(fmod.maskDisparity(disp), 128)
-            _, abc = fmod.RANSAC(maskpoints, 600)
-            diffs = fmod.calculatePointErrors(abc, points)
-            points = fmod.computePlanarThreshold(points, diffs, 0.05)
-            hist = fmod.calculateColourHistogram(points)
-            points = fmod.filterPointsByHistogram(points, hist, 10)
-            pp = np.array(fmod.project3DPointsTo2DImagePoints(points), np.int32).reshape((-1, 1, 2))
-            return len(pp)
-        st = random.getstate()
-        random.seed(0)
-        chain()
-        t0 = time.perf_counter()
-        for _ in range(5):
-            n_pp = chain()
-        ex["dropin_frame_chain"] = {"ms_per_frame": round((time.perf_counter() - t0) / 5 * 1e3, 2),
-                                    "plane_points": n_pp,
-                                    "stages": "stereovision.py:84-113 via installed drop-ins, step 2, RANSAC 600",
-                                    "reference_ms_per_frame_survey": "~1,450 (SURVEY §8a, measured in the "
-                                                                     "build container: a1 2x150-180, a2 30, a3 55, "
-                                                                     "a5 300, a6 300, a7 45, a8 16, RANSAC ~380)"}
-        random.setstate(st)
+        d0, bgr0 = oracle.synth_frame(0)
+        ex["dropin_frame_chain"] = dropin_chain(fmod, d0, bgr0)
     finally:
         dropin.uninstall()
 
@@ -235,9 +342,9 @@ def extras(b, sb, args, device, with_cpu):
     return ex
 
 
-def latency_1frame(sb, step, first, device):
+def latency_1frame(sb, first, device):
     """configs[1]: one 1024x544 frame, step 1: K1 kernel time (HIP events), us."""
-    with sb.Batch(1, H, W, step, with_bgr=False, device=device) as one:
+    with sb.Batch(1, H, W, 1, with_bgr=False, device=device) as one:
         # the same K1 as a separately named instance: its 1-frame launches are a
         # rocprof row of their own, so the batch launches' average stays unmixed
         one.tune(1, 2)
@@ -251,49 +358,86 @@ def latency_1frame(sb, step, first, device):
         return round(ms / n * 1e3, 2)
 
 
-def main():
-    args = parse()
+def check_parity(batches, shards, what, step):
+    """Every frame's device digest vs the oracle's (global frame ids); (frames checked, mismatching)."""
+    if step not in (1, 2) or not os.path.exists(GOLDEN_DIGESTS):
+        return 0, 0
+    gold = np.load(GOLDEN_DIGESTS)[f"step{step}"]
+    checked = bad = 0
+    fields = ("n_valid", "disp_hash") if what == "dense" else \
+        ("n_valid", "n_kept", "n_kept2", "disp_hash", "hist_hash", "pts_hash")
+    for b, (_, first, count) in zip(batches, shards):
+        if first + count > len(gold):
+            continue
+        got = b.digest(what)
+        want = gold[first:first + count]
+        ok = got[:, 6] == 0
+        for k, name in enumerate(("n_valid", "n_kept", "n_kept2", "disp_hash", "hist_hash", "pts_hash")):
+            if name in fields:
+                ok &= got[:, k] == want[name].astype(np.uint64)
+        checked += count
+        bad += int((~ok).sum())
+    return checked, bad
+
+
+def main(argv=None):
+    args = parse(argv)
+    pl = plan(args.gpus, os.environ)
     from svx import batch as sb
     from svx import dist
 
-    rank, world, local = dist.env_topology()
-    ctrl = dist.Control()
-    # RCCL whenever launched by torchrun (also at world size 1, so the device
-    # collective path is the one that runs), never for a plain `python bench.py`
-    comm = dist.RcclComm(ctrl, local) if "WORLD_SIZE" in os.environ else None
-    first, count = dist.shard(args.frames * world, world, rank)
+    import svx
+    ctrl = dist.Control(rank=pl["rank"], world=pl["world"])
+    if pl["mode"] == "multi" and svx.device_count() < args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but {svx.device_count()} GPU(s) visible")
     want_pipe = not args.no_pipeline
+    shards = shards_of(pl, args.frames)
+    comm = mcomm = None
+    if pl["mode"] == "ranks":   # RCCL over every rank (also at world size 1: the collective path runs)
+        comm = dist.RcclComm(ctrl, pl["devices"][0])
+    elif pl["mode"] == "multi":
+        mcomm = dist.MultiComm(pl["devices"])
 
     # configs[1]: one frame, before the 4096-frame batch exists (its own warm-up inside)
-    lat_us = None if args.no_latency else latency_1frame(sb, args.step, first, local)
-    b = sb.Batch(count, H, W, args.step, with_bgr=want_pipe, with_points=want_pipe, device=local)
-    b.tune(args.qpl, args.nt)
-    b.synth(first)
-    ng = b.Ng
-    points_rank = ng * count
+    lat_us = None if (args.no_latency or pl["n_gpus"] > 1) else latency_1frame(sb, shards[0][1], shards[0][0])
+    batches = []
+    for dev, first, count in shards:
+        b = sb.Batch(count, H, W, args.step, with_bgr=want_pipe, with_points=want_pipe, device=dev)
+        b.tune(args.qpl, args.nt)
+        b.synth(first)
+        batches.append(b)
+    ng = batches[0].Ng
+    points_local = sum(ng * b.frames for b in batches)
+
+    def sync_all():
+        for b in batches:
+            b.sync()
+
+    def timed_steps(fn, steps):
+        sync_all()
+        ctrl.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        sync_all()
+        ctrl.barrier()
+        return time.perf_counter() - t0
 
     # ---- headline: K1 dense projection --------------------------------------
     t_ramp = time.perf_counter()
     while (time.perf_counter() - t_ramp) * 1e3 < args.ramp_ms:
-        b.project(sync=True)
+        for b in batches:
+            b.project(sync=False)
+        sync_all()
     for _ in range(args.warmup):
-        b.project(sync=False)
-    b.sync()
-    b.reset_timing()
-    ctrl.barrier()
-    b.sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        b.project(sync=False)
-    b.sync()
-    ctrl.barrier()
-    dt = time.perf_counter() - t0
-    dt_max = float(ctrl.max([dt])[0])
-    k_ms, k_n = b.timing("project")
-    k_avg_s = float(ctrl.max([k_ms / max(k_n, 1) / 1e3])[0])
-    total_points = points_rank * world * args.steps
-    value = total_points / dt_max / 1e6
-    bytes_launch = K1_BYTES_PER_POINT * points_rank
+        for b in batches:
+            b.project(sync=False)
+    for b in batches:
+        b.reset_timing()
+    dt = timed_steps(lambda: [b.project(sync=False) for b in batches], args.steps)
+    agg = aggregate(ctrl, pl["n_gpus"], points_local, args.steps, dt)
+    k_avg_s = float(ctrl.max([max(ms / max(n, 1) for ms, n in (b.timing("project") for b in batches)) / 1e3])[0])
+    bytes_launch = K1_BYTES_PER_POINT * ng * batches[0].frames
     achieved = bytes_launch / k_avg_s / 1e9
 
     traffic = None
@@ -301,27 +445,37 @@ def main():
         try:
             with open(args.traffic) as fh:
                 tj = json.load(fh)
-            if tj.get("frames") == count and tj.get("step") == args.step:
+            if tj.get("frames") == batches[0].frames and tj.get("step") == args.step:
                 traffic = tj.get("k1_hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 
+    frames_gpu = batches[0].frames
+    par = {"ranks": f"one process per GPU (torchrun), RCCL communicator per rank",
+           "multi": f"one process, {pl['n_gpus']} GPUs (ncclCommInitAll)",
+           "single": "one process, one GPU"}[pl["mode"]]
     out = {
-        "metric": METRIC, "value": round(value, 1), "unit": "Mpoints/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+        "metric": METRIC, "value": round(agg["value"], 1), "unit": "Mpoints/s", "n_gpus": pl["n_gpus"],
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(agg["ms_per_step"], 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8->f32",
         "data": "synthetic (counter-based generator of SURVEY §8d, generated on device)",
-        "config": {"workload": f"configs[2]: batch={count}/GPU synthetic {W}x{H} disparity maps, "
-                               f"step {args.step}, dense fp32 XYZ planes (K1)",
-                   "frames_per_gpu": count, "global_frames": count * world, "H": H, "W": W,
+        "config": {"workload": f"configs[2]: batch={frames_gpu}/GPU synthetic {W}x{H} disparity maps, "
+                               f"step {args.step}, dense fp32 XYZ planes (K1)"
+                               + (f"; configs[4]: {frames_gpu * pl['n_gpus']} frames over {pl['n_gpus']} GPUs"
+                                  if pl["n_gpus"] > 1 else ""),
+                   "frames_per_gpu": frames_gpu, "global_frames": frames_gpu * pl["n_gpus"], "H": H, "W": W,
                    "step": args.step, "grid_points_per_frame": ng,
-                   "parallelism": f"frame-sharded x{world} (no data-path collective)"},
+                   "parallelism": f"frame-sharded x{pl['n_gpus']} (no data-path collective); {par}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                      "kernel": "project_dense_kernel", "kernel_ms": round(k_avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_point": K1_BYTES_PER_POINT},
     }
+    parity = {}
+    if not args.no_parity:
+        c, m = check_parity(batches, shards, "dense", args.step)
+        parity["k1"] = [c, m]
 
     # ---- config 2: single-frame latency (measured first, before the batch) ----
     if lat_us is not None:
@@ -330,61 +484,83 @@ def main():
     # ---- config 4/5: pipeline ----------------------------------------------
     if want_pipe:
         plane = sb.synthetic_plane()
-        for _ in range(max(1, args.warmup)):
-            b.pipeline(plane=plane, chunk=args.chunk, sync=False)
-        b.sync()
-        b.reset_timing()
-        ctrl.barrier()
-        b.sync()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            pl = comm.broadcast_plane(plane, root=0) if comm else plane
-            b.pipeline(plane=pl, chunk=args.chunk, sync=False)
-        b.sync()
-        ctrl.barrier()
-        pdt = float(ctrl.max([time.perf_counter() - t0])[0])
-        p_ms, p_n = b.timing("pipeline")
-        p_avg_s = float(ctrl.max([p_ms / max(p_n, 1) / 1e3])[0])
-        counts = b.read_counts().sum(axis=0)
         if comm:
-            counts = comm.allreduce_i64(counts)
-        n_kept2 = int(counts[2])
-        pbytes = 4 * points_rank + (20 * int(b.read_counts()[:, 2].sum())) + 4096 * count
+            def pipe_step():
+                dp = comm.broadcast_plane_dev(batches[0], plane, root=0)
+                batches[0].pipeline_dev(dp, chunk=args.chunk, sync=False)
+        elif mcomm:
+            def pipe_step():
+                mcomm.pipeline(batches, plane, root=0)
+        else:
+            def pipe_step():
+                batches[0].pipeline(plane=plane, chunk=args.chunk, sync=False)
+        for _ in range(max(1, args.warmup)):
+            pipe_step()
+        for b in batches:
+            b.reset_timing()
+        pdt = timed_steps(pipe_step, args.steps)
+        pagg = aggregate(ctrl, pl["n_gpus"], points_local, args.steps, pdt)
+        p_avg_s = float(ctrl.max([max(ms / max(n, 1) for ms, n in (b.timing("pipeline") for b in batches))
+                                  / 1e3])[0])
+        counts_local = np.sum([b.read_counts().sum(axis=0) for b in batches], axis=0).astype(np.float64)
+        counts = ctrl.sum(counts_local)
+        kept2_gpu0 = int(batches[0].read_counts()[:, 2].sum())
+        pbytes = 4 * ng * frames_gpu + 20 * kept2_gpu0 + 4096 * frames_gpu
         out["pipeline"] = {
             "workload": "configs[3]/[4]: same batch, plane threshold 0.05 + hue histogram (thr 10) "
                         "+ ordered compaction + int32 back-projection",
-            "value": round(points_rank * world * args.steps / pdt / 1e6, 1), "unit": "Mpoints/s",
-            "ms_per_step": round(pdt / args.steps * 1e3, 4), "gpu_ms_per_call": round(p_avg_s * 1e3, 4),
+            "value": round(pagg["value"], 1), "unit": "Mpoints/s",
+            "ms_per_step": round(pagg["ms_per_step"], 4), "gpu_ms_per_call": round(p_avg_s * 1e3, 4),
             "achieved_GBps": round(pbytes / p_avg_s / 1e9, 1),
             "frac": round(pbytes / p_avg_s / 1e9 / PEAK_HBM_GBS, 4),
             "algorithmic_bytes_per_call": pbytes,
-            "bytes_note": "algorithmic = SURVEY 8d config 4: 4 B read per grid point (disparity + BGR) + 20 B per "
-                          "kept point + 4 KB histogram per frame; the resident kernel does not read the BGR (nor, "
-                          "in pass 2, the disparity) of chunks the keep table rules out, so it moves fewer bytes "
+            "bytes_note": "algorithmic = SURVEY 8d config 4 per GPU: 4 B read per grid point (disparity + BGR) + 20 B "
+                          "per kept point + 4 KB histogram per frame; the resident kernel does not read the BGR (nor, "
+                          "in pass 2, the disparity) of chunks the plane rules out, so it moves fewer bytes "
                           "(traffic = PMC bytes per call, frac_of_traffic = traffic / time / peak)",
-            "counts_total": {"valid": int(counts[0]), "kept": int(counts[1]), "kept2": n_kept2},
-            "plane_broadcast": "RCCL ncclBroadcast over xGMI, every step" if comm else "n/a (single process)",
-            "kernels": "keep_table_kernel (per call) + resident_fused_kernel (one workgroup per frame)"
-                       if args.frames >= 512 else "tiled: stage_kernel + offsets_kernel",
+            "counts_total": {"valid": int(counts[0]), "kept": int(counts[1]), "kept2": int(counts[2])},
+            "plane_broadcast": {"ranks": "RCCL ncclBroadcast into device memory every step (sv_comm_broadcast_plane_dev)",
+                                "multi": "RCCL grouped ncclBroadcast to every device every step (sv_multi_pipeline)",
+                                "single": "host plane (single GPU)"}[pl["mode"]],
+            "kernels": "resident_fused_kernel (one workgroup per frame, keep1 from the plane in device memory)"
+                       if frames_gpu >= 512 else "tiled: stage_kernel + offsets_kernel",
         }
-        ptraffic = pipeline_traffic(args.traffic_pipeline, count, args.step)
+        ptraffic = pipeline_traffic(args.traffic_pipeline, frames_gpu, args.step)
         if ptraffic:
             out["pipeline"]["traffic"] = ptraffic
             out["pipeline"]["frac_of_traffic"] = round(ptraffic / p_avg_s / 1e9 / PEAK_HBM_GBS, 4)
+        if not args.no_parity:
+            c, m = check_parity(batches, shards, "pipeline", args.step)
+            parity["pipeline"] = [c, m]
 
-    if want_pipe and not args.no_extras and world == 1:   # §8f component timings: the N=1 run only
-        out["extras"] = extras(b, sb, args, local, not args.no_cpu)
+    if parity:
+        tot = ctrl.sum(np.array([v for pair in parity.values() for v in pair], np.float64))
+        keys = list(parity)
+        out["parity"] = {k: {"frames_checked": int(tot[2 * i]), "mismatched_frames": int(tot[2 * i + 1])}
+                         for i, k in enumerate(keys)}
+        out["parity"]["vs"] = "device per-frame digests vs tests/golden/frame_digests.npz (pinned C oracle, " \
+                              "global frame ids), every frame of every GPU"
+        out["parity"]["pass"] = all(v["mismatched_frames"] == 0 and v["frames_checked"] > 0
+                                    for k, v in out["parity"].items() if isinstance(v, dict))
 
-    if rank == 0 and world == 1 and not args.no_cpu:
+    single = pl["n_gpus"] == 1
+    if want_pipe and not args.no_extras and single:   # §8f component timings: the N=1 run only
+        out["extras"] = extras(batches[0], args, not args.no_cpu)
+
+    if pl["rank"] == 0 and single and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
 
-    b.close()
+    for b in batches:
+        b.close()
     if comm:
         comm.close()
+    if mcomm:
+        mcomm.close()
     ctrl.barrier()
-    if rank == 0:
+    if pl["rank"] == 0:
         print(json.dumps(out), flush=True)
     ctrl.close()
+    return out
 
 
 if __name__ == "__main__":

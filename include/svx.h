@@ -174,21 +174,26 @@ int sv_batch_pipeline(sv_batch* b, const sv_camera* cam, const sv_plane* plane,
 /* The pipeline with every frame's own plane: the plane the last
  * sv_batch_ransac found for it (stereovision.py:94-113 per frame). A frame
  * without a plane (trial -1: the reference's plane step raises) keeps no
- * points. Tiled kernels (the frame-resident family takes one plane per call).
- * sv_batch_read_frame_plane: a, b, c and |abc| (-1 without a plane) as the
- * kernels use them. */
+ * points. Same kernel families as sv_batch_pipeline (the frame-resident
+ * kernel reads each frame's plane). sv_batch_read_frame_plane: a, b, c and
+ * |abc| (-1 without a plane) as the kernels use them. */
 int sv_batch_pipeline_planes(sv_batch* b, const sv_camera* cam, double point_thr, int hist_thr, int chunk,
                              int sync);
+/* sv_batch_pipeline with the plane in DEVICE memory (3 doubles a, b, c on the
+ * batch's device, e.g. the buffer an RCCL broadcast wrote): read by the
+ * device, so the call needs no host copy of the plane and no host sync. */
+int sv_batch_pipeline_dev(sv_batch* b, const sv_camera* cam, const double* dplane, double point_thr, int hist_thr,
+                          int chunk, int sync);
 int sv_batch_read_frame_plane(sv_batch* b, int frame, double* out4);
 
 /* Pipeline kernel family: 0 = auto (frame-resident for >= 512 frames when the
  * frame fits, else tiled), 1 = tiled (tiles of 4096 points across workgroups,
  * offsets kernel between the passes), 2 = frame-resident (one workgroup per
  * frame, LDS histogram; frames of <= 1M grid points and <= 2048 grid points a
- * side, else SV_E_ARG; chunks the keep table rules out are skipped; both passes
- * prefetch the next chunk), 3 = frame-resident without prefetch, 4 =
- * frame-resident with the pass-2 prefetch only. Results are identical; only
- * the speed differs. */
+ * side, else SV_E_ARG; chunks the plane rules out are skipped; both passes
+ * prefetch the next chunk; no host sync), 3 = frame-resident without prefetch,
+ * 4 = frame-resident with the pass-2 prefetch only. Results are identical;
+ * only the speed differs. */
 int sv_batch_pipeline_mode(sv_batch* b, int mode);
 
 /* Pre-pass over the batch's frames in order (stereovision.py:53-76): option
@@ -232,9 +237,11 @@ int sv_batch_read_maskpoints(sv_batch* b, int frame, double* xyz, int64_t cap, i
 /* Draw-level verification: record the first `trials` trials' drawn indices of
  * every frame in later sv_batch_ransac calls (0 = off); read one frame's as
  * trials x (k + 3) int32 (the sample, then P1..P3 of the accepted triple;
- * -1 where a trial did not run). */
+ * -1 where a trial did not run), trials and k being those of the last
+ * sv_batch_ransac (*out_trials, *out_k; out NULL: sizes only; cap = int32
+ * capacity of out, SV_E_CAP if smaller). */
 int sv_batch_ransac_trace(sv_batch* b, int trials);
-int sv_batch_read_ransac_trace(sv_batch* b, int frame, int32_t* out);
+int sv_batch_read_ransac_trace(sv_batch* b, int frame, int32_t* out, int64_t cap, int* out_trials, int* out_k);
 
 int sv_batch_sync(sv_batch* b);
 /* ms of the last sv_batch_project / sv_batch_pipeline, from HIP events
@@ -272,14 +279,40 @@ int sv_delta_tables(int device, int H, int W, const sv_camera* cam, int8_t* dx, 
 int sv_synth_frame(int device, int64_t frame_id, int H, int W, uint8_t* disp, uint8_t* bgr);
 
 /* ---- multi-GPU: RCCL over xGMI ----------------------------- */
+/* Frames shard by contiguous global-id ranges (one sv_batch per GPU); the only
+ * device-data collective is the broadcast of the plane. Two drivers:
+ *   one process per GPU: rank 0's sv_comm_unique_id, handed to every rank
+ *     (svx/control.py), then sv_comm_init on each rank;
+ *   one process, every GPU: sv_comm_init_all, then
+ *     sv_multi_pipeline (or sv_comm_group_start / .._end around the per-device
+ *     sv_comm_broadcast_plane_dev calls). */
 typedef struct sv_comm sv_comm;
 #define SV_UNIQUE_ID_BYTES 128
 int sv_comm_unique_id(uint8_t* out_id /* SV_UNIQUE_ID_BYTES */);
 int sv_comm_init(int nranks, int rank, const uint8_t* id, int device, sv_comm** out);
+/* ncclCommInitAll over devices[0..n-1] (rank i on devices[i]); out[n]. */
+int sv_comm_init_all(int n, const int* devices, sv_comm** out);
 int sv_comm_destroy(sv_comm* c);
-/* Broadcast the plane coefficients from root over RCCL (device buffer). */
+/* ncclGroupStart / ncclGroupEnd (one process issuing the collectives of several devices). */
+int sv_comm_group_start(void);
+int sv_comm_group_end(void);
+/* Broadcast the plane coefficients from root over RCCL and back to the host
+ * (synchronous; reporting and tests). */
 int sv_comm_broadcast_plane(sv_comm* c, sv_plane* inout, int root);
-/* Sum int64 counters over ranks (reporting only). */
+/* Broadcast the plane from root into device memory, ordered on batch b's
+ * stream (b on the comm's device): the root passes its host plane, the other
+ * ranks NULL. *out_dplane = the comm's device buffer (3 doubles a, b, c),
+ * valid for stream-ordered use on b's stream (sv_batch_pipeline_dev). No host
+ * sync. Inside a group, the broadcast is enqueued at sv_comm_group_end: enqueue
+ * the pipelines after it. */
+int sv_comm_broadcast_plane_dev(sv_comm* c, sv_batch* b, const sv_plane* plane, int root, const double** out_dplane);
+/* One process, n GPUs (SURVEY §8b sv_multi_pipeline): one grouped broadcast
+ * of the root's plane to every device, then sv_batch_pipeline_dev on every
+ * batches[i] (comms[i]'s device) with that device's copy of the plane.
+ * Asynchronous unless sync != 0 (then every batch is synchronised). */
+int sv_multi_pipeline(int n, sv_comm* const* comms, sv_batch* const* batches, const sv_camera* cam,
+                      const sv_plane* plane, int root, double point_thr, int hist_thr, int sync);
+/* Sum int64 counters over ranks (reporting only; host buffers, synchronous). */
 int sv_comm_allreduce_i64(sv_comm* c, int64_t* inout, int n);
 
 #ifdef __cplusplus

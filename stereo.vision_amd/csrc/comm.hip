@@ -1,11 +1,18 @@
 // Multi-GPU plumbing: RCCL over xGMI.
 //
-// One process per GPU (launched by torchrun); the 128-byte ncclUniqueId is
-// created by rank 0 and handed to the other ranks by the Python driver over
-// the host control plane (torch.distributed gloo). The only device-data
-// collective of the path is the plane-coefficient broadcast (24 B); an int64
-// all-reduce of the per-rank counts is provided for reporting. Frames are
-// sharded by contiguous global-id ranges, so no point data ever moves.
+// Two ways to drive the GPUs of a node, both over the same sv_comm handles:
+//   * one process per GPU (torchrun): rank 0 creates the 128-byte ncclUniqueId
+//     and the Python driver hands it to the other ranks over its host control
+//     plane (svx/control.py, plain TCP); sv_comm_init per rank;
+//   * one process driving every GPU: sv_comm_init_all
+//     (ncclCommInitAll), collectives of all devices inside one
+//     sv_comm_group_start / sv_comm_group_end.
+// The only device-data collective of the path is the broadcast of the plane
+// (3 doubles) from the root, written straight into device memory on the
+// batch's stream (sv_comm_broadcast_plane_dev), where the pipeline reads it
+// (sv_batch_pipeline_dev): no host copy on the receivers and no host sync per
+// step. An int64 all-reduce of the per-rank counts is provided for reporting.
+// Frames are sharded by contiguous global-id ranges, so no point data moves.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -24,7 +31,19 @@ struct sv_comm {
     void* buf = nullptr;  // 4 KB device scratch
 };
 
-extern "C" int sv_comm_set_error(const char* msg);  // runtime.hip
+extern "C" int sv_comm_set_error(const char* msg);                                  // runtime.hip
+extern "C" int sv_batch_stream_internal(sv_batch* b, int* device, hipStream_t* stream);  // runtime.hip
+
+namespace {
+// The root's host plane into the comm's device buffer, on the batch stream.
+__global__ void store_abc_kernel(double a, double b, double c, double* __restrict__ dst) {
+    if (threadIdx.x == 0) {
+        dst[0] = a;
+        dst[1] = b;
+        dst[2] = c;
+    }
+}
+}  // namespace
 
 #define NCCL_TRY(expr)                                                              \
     do {                                                                            \
@@ -104,6 +123,84 @@ int sv_comm_broadcast_plane(sv_comm* c, sv_plane* inout, int root) {
     inout->a = h[0];
     inout->b = h[1];
     inout->c = h[2];
+    return SV_OK;
+}
+
+int sv_comm_init_all(int n, const int* devices, sv_comm** out) {
+    if (n < 1 || n > 64 || !devices || !out) return sv_comm_set_error("sv_comm_init_all: bad arguments"), SV_E_ARG;
+    ncclComm_t comms[64];
+    for (int i = 0; i < n; ++i) out[i] = nullptr;
+    NCCL_TRY(ncclCommInitAll(comms, n, devices));
+    for (int i = 0; i < n; ++i) {
+        sv_comm* c = new sv_comm;
+        c->comm = comms[i];
+        c->device = devices[i];
+        out[i] = c;
+        hipError_t e = hipSetDevice(devices[i]);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMalloc(&c->buf, 4096);
+        if (e != hipSuccess) {
+            for (int j = 0; j <= i; ++j) {
+                sv_comm_destroy(out[j]);
+                out[j] = nullptr;
+            }
+            for (int j = i + 1; j < n; ++j) ncclCommDestroy(comms[j]);
+            HIPC_TRY(e);
+        }
+    }
+    return SV_OK;
+}
+
+int sv_comm_group_start(void) {
+    NCCL_TRY(ncclGroupStart());
+    return SV_OK;
+}
+
+int sv_comm_group_end(void) {
+    NCCL_TRY(ncclGroupEnd());
+    return SV_OK;
+}
+
+int sv_comm_broadcast_plane_dev(sv_comm* c, sv_batch* b, const sv_plane* plane, int root, const double** out_dplane) {
+    if (!c || !b || !out_dplane) return sv_comm_set_error("sv_comm_broadcast_plane_dev: null"), SV_E_ARG;
+    int dev = -1;
+    hipStream_t s = nullptr;
+    if (sv_batch_stream_internal(b, &dev, &s) != SV_OK || dev != c->device)
+        return sv_comm_set_error("sv_comm_broadcast_plane_dev: batch and comm are on different devices"), SV_E_ARG;
+    int rank = -1;
+    NCCL_TRY(ncclCommUserRank(c->comm, &rank));
+    if (rank == root && !plane) return sv_comm_set_error("sv_comm_broadcast_plane_dev: the root needs the plane"), SV_E_ARG;
+    HIPC_TRY(hipSetDevice(c->device));
+    double* buf = static_cast<double*>(c->buf);
+    if (rank == root) {
+        hipLaunchKernelGGL(store_abc_kernel, dim3(1), dim3(64), 0, s, plane->a, plane->b, plane->c, buf);
+        HIPC_TRY(hipGetLastError());
+    }
+    NCCL_TRY(ncclBroadcast(buf, buf, 3, ncclDouble, root, c->comm, s));
+    *out_dplane = buf;
+    return SV_OK;
+}
+
+int sv_multi_pipeline(int n, sv_comm* const* comms, sv_batch* const* batches, const sv_camera* cam,
+                      const sv_plane* plane, int root, double point_thr, int hist_thr, int sync) {
+    if (n < 1 || !comms || !batches || !cam || !plane || root < 0 || root >= n)
+        return sv_comm_set_error("sv_multi_pipeline: bad arguments"), SV_E_ARG;
+    const double* dplane[64];
+    if (n > 64) return sv_comm_set_error("sv_multi_pipeline: at most 64 devices"), SV_E_ARG;
+    NCCL_TRY(ncclGroupStart());
+    for (int i = 0; i < n; ++i) {
+        const int rc = sv_comm_broadcast_plane_dev(comms[i], batches[i], i == root ? plane : nullptr, root, &dplane[i]);
+        if (rc != SV_OK) {
+            (void)ncclGroupEnd();
+            return rc;
+        }
+    }
+    NCCL_TRY(ncclGroupEnd());
+    for (int i = 0; i < n; ++i)
+        if (int rc = sv_batch_pipeline_dev(batches[i], cam, dplane[i], point_thr, hist_thr, 0, 0)) return rc;
+    if (sync)
+        for (int i = 0; i < n; ++i)
+            if (int rc = sv_batch_sync(batches[i])) return rc;
     return SV_OK;
 }
 

@@ -110,9 +110,8 @@ __device__ __forceinline__ const uint8_t* row_ptr(const uint8_t* base, int gy, i
 // Can any grid point of the tile be kept by the plane (keep1)? P.abc = u / d with
 // u = B (a (x - cw) + b (y - ch) + c f), so keep1 <=> |u / d - 1| < t, t = thr |abc|
 // (functions.py:300-323). u is affine in (x, y): over the tile's rows and the whole
-// width its extremes are at the corners. For t < 0.99 no d in [1, 255] is kept when
-// u_max < 1 - t or u_min > 255 (1 + t); the margins (1e-9 relative) dwarf the
-// reference's fp64 rounding (~1e-15). Uniform per tile; false -> skip its colours.
+// width its extremes are at the corners (urange_keepable, svx_device.h).
+// Uniform per tile; false -> skip its colours.
 __device__ __forceinline__ bool tile_keepable(int tile, const KParams& p) {
     const int q0 = tile * 256 * kQPT, q1 = min(q0 + 256 * kQPT, p.frame_quads) - 1;
     const double y0 = (double)(fastdiv40(q0, p.Q_m40) * p.step), y1 = (double)(fastdiv40(q1, p.Q_m40) * p.step);
@@ -121,11 +120,8 @@ __device__ __forceinline__ bool tile_keepable(int tile, const KParams& p) {
     const double cf = p.c * p.f;
     const double umax = p.B * (fmax(ax0, ax1) + fmax(by0, by1) + cf);
     const double umin = p.B * (fmin(ax0, ax1) + fmin(by0, by1) + cf);
-    const double t = p.thr * p.nrm;
-    if (!(t < 0.99)) return true;   // (NaN too): no skipping
-    if (umax < (1.0 - t) * (1.0 - 1e-9) - 1e-12) return false;
-    if (umin > 255.0 * (1.0 + t) * (1.0 + 1e-9) + 1e-9) return false;
-    return true;
+    const double mag = p.B * (fmax(fabs(ax0), fabs(ax1)) + fmax(fabs(by0), fabs(by1)) + fabs(cf));
+    return urange_keepable(umin, umax, p.thr * p.nrm, mag);
 }
 
 struct PipeShared {   // pass 1
@@ -144,7 +140,7 @@ __device__ __forceinline__ void hist_tile(const PipeBuffers& bf, int frame, int 
     KParams p = p0;
     bool live = true;
     if constexpr (PF) {   // this frame's plane (uniform: scalar loads)
-        const FramePlane fpl = bf.planes[frame];
+        const FramePlane fpl = bf.planes[(int64_t)frame * bf.plane_stride];
         apply_plane(p, fpl);
         live = fpl.valid != 0;
     }

@@ -681,23 +681,24 @@ hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_
 
 // keep1 plane fields of every frame (plane_fields, as the host's set_plane)
 __global__ void frame_planes_kernel(const double* __restrict__ abc, const int32_t* __restrict__ trial, int frames,
-                                    double f, FramePlane* __restrict__ out) {
+                                    KParams p, double thr, FramePlane* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= frames) return;
     FramePlane o;
-    if (trial[i] >= 0) {
-        plane_fields(o, abc[3 * i], abc[3 * i + 1], abc[3 * i + 2], f);
+    if (!trial || trial[i] >= 0) {
+        plane_fields(o, abc[3 * i], abc[3 * i + 1], abc[3 * i + 2], p.f, p.B, p.cw, p.ch, thr, p.W, p.H);
     } else {
-        plane_fields(o, 0.0, 0.0, 0.0, f);
+        plane_fields(o, 0.0, 0.0, 0.0, p.f, p.B, p.cw, p.ch, thr, p.W, p.H);
         o.valid = 0;
     }
     out[i] = o;
 }
 
-hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, double f, FramePlane* out,
-                               hipStream_t s) {
+hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, const KParams& p, double thr,
+                               FramePlane* out, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
-    hipLaunchKernelGGL(frame_planes_kernel, dim3((frames + 255) / 256), dim3(256), 0, s, abc, trial, frames, f, out);
+    hipLaunchKernelGGL(frame_planes_kernel, dim3((frames + 255) / 256), dim3(256), 0, s, abc, trial, frames, p, thr,
+                       out);
     return hipGetLastError();
 }
 

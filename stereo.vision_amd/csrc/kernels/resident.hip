@@ -6,14 +6,12 @@
 // (functions.py:228-230); the keep2 points in raster order as fp32 X, Y, Z +
 // int32 (x, y) back-projection (functions.py:201-209, stereovision.py:112).
 //
-// keep1 comes from a per-call interval table (keep_table_kernel): for grid
-// point (gy, gx) the reference keeps exactly the disparities d in [lo, hi].
-// The table is built once per call (plane, threshold, camera) by evaluating the
-// reference predicate for every d = 1..255 — fp32 with a rigorous guard, the
-// reference's fp64 arithmetic inside the guard — and checking that the kept
-// set is one interval (the exact predicate |B*L/d - 1| < t is quasi-convex in
-// d); if it is not, the call falls back to the tiled kernels. The streaming
-// loops then test keep1 with two byte compares and no floating point.
+// keep1 is evaluated per grid point from the frame's plane (FramePlane: the
+// per-call plane, the frame's own RANSAC plane, or a plane broadcast into
+// device memory): the division-free fp32 test |u - d| < t*d (keep1_lean) with
+// a rigorous guard, the reference's fp64 arithmetic inside the guard. A chunk
+// whose rows the plane rules out for every d in 1..255 (the u range at its
+// corners, rows_keepable) reads no BGR and evaluates no keep1.
 //
 // Because one workgroup walks its frame chunk by chunk (chunk = 256 lanes x
 // QPL quads x 4 grid points, raster order), nothing crosses workgroups: the
@@ -74,49 +72,6 @@ constexpr int maxchunks_of() { return 1024 / QP; }
 int resident_chunks_per_frame(const KParams& p, int qpl) {
     const int per = 256 * qpl;
     return (p.frame_quads + per - 1) / per;
-}
-
-// ---------------------------------------------------------------------------
-// keep1 interval table: one uint16 (lo | hi << 8) per grid point of a
-// Hg x pitch grid; lo = 255, hi = 0 for "never" (and for the pad columns).
-// One lane per grid point, brute force over d = 1..255.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void keep_table_kernel(uint16_t* __restrict__ tab, uint32_t* __restrict__ err,
-                                                         uint32_t* __restrict__ cany, int chunk_quads, KParams p) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= p.Hg * p.pitch) return;
-    const int gy = i / p.pitch, gx = i - gy * p.pitch;
-    uint32_t entry = 0x00FF;
-    if (gx < p.Wg) {
-        const int x = gx * p.step, y = gy * p.step;
-        const float xf = (float)x;
-        const float beta = __builtin_fmaf(p.bb32, (float)y, p.b032);
-        int lo = 256, hi = 0, cnt = 0;
-        for (int d = 1; d < 256; ++d) {
-            bool unc;
-            bool k = keep1_lean(xf, beta, (float)d, p, unc);
-            if (__builtin_expect(unc, 0)) k = keep1_f64(x, y, (uint32_t)d, p);
-            if (k) {
-                lo = min(lo, d);
-                hi = d;
-                ++cnt;
-            }
-        }
-        if (cnt) {
-            if (cnt == hi - lo + 1) entry = (uint32_t)lo | ((uint32_t)hi << 8);
-            else atomicOr(err, 1u);   // not an interval: the caller uses the tiled kernels
-            cany[(gy * p.Q + (gx >> 2)) / chunk_quads] = 1u;   // the chunk can keep a point (same value from all)
-        }
-    }
-    tab[i] = (uint16_t)entry;
-}
-
-hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, uint32_t* cany, hipStream_t s) {
-    const int n = p.Hg * p.pitch;
-    if (n <= 0) return hipSuccess;
-    const int chunk_quads = 256 * (p.step == 1 ? default_qpl<1>() : default_qpl<2>());
-    hipLaunchKernelGGL(keep_table_kernel, dim3((n + 255) / 256), dim3(256), 0, s, tab, err, cany, chunk_quads, p);
-    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -192,16 +147,6 @@ __device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<S
 }
 
 template <int STEP, int QP>
-__device__ __forceinline__ void r_load_tab(const uint16_t* tab, const RQuads<STEP, QP>& g, const RParams& p,
-                                           uint2 (&tw)[RCfg<STEP, QP>::QPL]) {
-#pragma unroll
-    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
-        const int gy = g.gy[i] < 0 ? 0 : g.gy[i];
-        tw[i] = *reinterpret_cast<const uint2*>(tab + (__umul24((uint32_t)gy, (uint32_t)p.pitch) + 4u * (uint32_t)g.q[i]));
-    }
-}
-
-template <int STEP, int QP>
 __device__ __forceinline__ void r_load_bgr(const uint8_t* fbgr, const RQuads<STEP, QP>& g, const RParams& p,
                                            uint32_t (&cw)[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW]) {
 #pragma unroll
@@ -236,21 +181,71 @@ __device__ __forceinline__ uint32_t r_col(const uint32_t (&c)[RCfg<STEP, QP>::CW
 }
 
 
-// keep1 bits of this lane's chunk (bit 4i+k = point k of quad i): lo <= d <= hi.
+// The reference's keep1 in fp64 (functions.py:191-193, :300-323), op for op.
+// Plane and camera are read from memory here (the rare path), so that they do
+// not occupy registers for the whole kernel.
+__device__ __forceinline__ bool r_keep1_f64(int x, int y, uint32_t d, const FramePlane* Lp) {
+    const double f = Lp->f, cw = Lp->cw, ch = Lp->ch;
+    const double Z = Lp->fB / (double)d;
+    const double X = (((double)x - cw) * Z) / f;
+    const double Y = (((double)y - ch) * Z) / f;
+    const double dot = __builtin_fma(Z, Lp->c, __builtin_fma(X, Lp->a, Y * Lp->b));
+    return __builtin_fabs((dot - 1.0) / Lp->nrm) < Lp->thr;
+}
+
+// The fp32 constants of keep1_lean for one frame (uniform, scalar registers).
+struct RLean {
+    float al, bb, b0, tn, g;
+};
+
+// keep1 bits of this lane's chunk (bit 4i+k = point k of quad i) under the
+// frame's plane: keep1_lean in fp32 (the same fp32 operations as keep1_lean,
+// svx_device.h), the fp64 reference arithmetic for the points inside its guard
+// (rare; one fp64 evaluation site, looped over the lane's uncertain points).
 template <int STEP, int QP>
-__device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP],
-                                            const uint2 (&tw)[RCfg<STEP, QP>::QPL], const RQuads<STEP, QP>& g) {
-    uint32_t keep = 0;
+__device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP], const RQuads<STEP, QP>& g,
+                                            const RLean& L, const FramePlane* Lp, int Wg) {
+    constexpr int QPL = RCfg<STEP, QP>::QPL;
+    uint32_t keep = 0, unc = 0;
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
-        uint32_t k4 = 0;
+    for (int i = 0; i < QPL; ++i) {
+        const float beta = __builtin_fmaf(L.bb, (float)(max(g.gy[i], 0) * STEP), L.b0);
+        uint32_t k4 = 0, u4 = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t t = (k < 2 ? tw[i].x : tw[i].y) >> (16 * (k & 1));
             const uint32_t d = r_d<STEP, QP>(dw[i], k);
-            k4 |= (uint32_t)(d >= (t & 0xFF) && d <= ((t >> 8) & 0xFF)) << k;
+            const float df = (float)d;
+            const float u = __builtin_fmaf(L.al, (float)((4 * g.q[i] + k) * STEP), beta);
+            const float s = u - df;
+            const float e = __builtin_fmaf(-L.tn, df, __builtin_fabsf(s));
+            k4 |= (uint32_t)(e < 0.0f) << k;
+            u4 |= (uint32_t)(!(__builtin_fabsf(e) > L.g) && d != 0) << k;
         }
-        keep |= (g.gy[i] >= 0 ? k4 : 0u) << (4 * i);
+        // rows past the frame end and the pad columns gx >= Wg (the grid stops at W - 1) keep nothing
+        const int nin = Wg - 4 * g.q[i];
+        const uint32_t in = g.gy[i] < 0 ? 0u : (nin >= 4 ? 0xFu : (1u << max(nin, 0)) - 1u);
+        keep |= (k4 & in) << (4 * i);
+        unc |= (u4 & in) << (4 * i);
+    }
+    if (__builtin_expect(__ballot(unc != 0) != 0, 0)) {
+        uint32_t m = unc;
+        while (m) {   // per lane
+            const uint32_t b = __builtin_ctz(m);
+            m &= m - 1;
+            int x = 0, y = 0;
+            uint32_t d = 0;
+#pragma unroll
+            for (int i = 0; i < QPL; ++i) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool hit = b == (uint32_t)(4 * i + k);
+                    x = hit ? (4 * g.q[i] + k) * STEP : x;
+                    y = hit ? g.gy[i] * STEP : y;
+                    d = hit ? r_d<STEP, QP>(dw[i], k) : d;
+                }
+            }
+            keep = r_keep1_f64(x, y, d, Lp) ? (keep | (1u << b)) : (keep & ~(1u << b));
+        }
     }
     return keep;
 }
@@ -275,8 +270,9 @@ __device__ __forceinline__ uint32_t r_nvalid(const uint32_t (&dw)[RCfg<STEP, QP>
 
 // Hue bin as hue_bin_fast (svx_device.h), with the sector select written as
 // value selects so that no lane mask is branched on; the +-4e-4 band around a
-// half-integer takes the exact integer/fp64 path (hue_bin).
-__device__ __forceinline__ int r_bin_sel(uint32_t col) {
+// half-integer takes the exact integer/fp64 path (hue_bin). (A 392 KB
+// (rng, n) -> bin table gather instead: 7.40 vs 6.32 ms per call)
+__device__ __forceinline__ uint32_t r_bin_sel(uint32_t col) {
     const int b = (int)(col & 0xFF), g = (int)((col >> 8) & 0xFF), r = (int)((col >> 16) & 0xFF);
     const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
     const int rng = mx - mn;
@@ -284,11 +280,11 @@ __device__ __forceinline__ int r_bin_sel(uint32_t col) {
     const int n = (r == mx) ? nr : ((g == mx) ? ng : nb);
     const float t = ((float)n * __builtin_amdgcn_rcpf((float)rng)) * (500.0f / 3.0f);
     const float rt = __builtin_rintf(t);
-    const bool near = __builtin_fabsf(t - rt) > 0.5f - 4e-4f;   // NaN (grey) -> false
+    const bool near = __builtin_fabsf(t - rt) > 0.5f - 4e-4f;
     int bin = (int)rt + (n < 0 ? 1000 : 0);
     bin = rng == 0 ? 0 : bin;
     if (__builtin_expect(near, 0)) bin = hue_bin(r, g, b);
-    return bin;
+    return (uint32_t)bin;
 }
 
 // Pack the colours of the keep bits into this wave's LDS region, (lane, bit)
@@ -323,15 +319,13 @@ struct P1Regs {
     RQuads<STEP, QP> g;
     uint32_t dw[RCfg<STEP, QP>::QPL][STEP];
     uint32_t cw[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW];
-    uint2 tw[RCfg<STEP, QP>::QPL];
 };
 
 template <int STEP, int QP>
 struct P2Regs {
     RQuads<STEP, QP> g;
     uint32_t dw[RCfg<STEP, QP>::QPL][STEP];
-    uint2 tw[RCfg<STEP, QP>::QPL];   // step 2: keep-table words (step 1: the keep1 bits of pass 1 in kb)
-    uint32_t kb;
+    uint32_t kb;                 // step 1: the keep1 bits of pass 1 (step 2 evaluates keep1 again)
     uint32_t fx[kRDN / 8], fy;   // the chunk's staged delta words (this lane's share)
     int dlo, ywb;                // first staged disparity; the chunk's 32-row word
     bool narrow;                 // the chunk's keep1 range and rows fit the stage
@@ -339,18 +333,15 @@ struct P2Regs {
 
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
-                                        const uint16_t* tab, const RParams& p, bool next, bool any) {
+                                        const RParams& p, bool next, bool any) {
     if (next) r_geometry_next<STEP, QP>(c, tid, p, r.g);   // r.g holds chunk c - 1
     else r_geometry<STEP, QP>(c, tid, p, r.g);
     r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
-    if (any) {   // uniform: a chunk no grid point of which can be kept needs only its valid count
-        r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
-        r_load_bgr<STEP, QP>(fbgr, r.g, p, r.cw);
-    }
+    if (any) r_load_bgr<STEP, QP>(fbgr, r.g, p, r.cw);   // uniform: a chunk the plane rules out needs only its valid count
 }
 
 template <int STEP, int QP>
-__device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint16_t* tab,
+__device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp,
                                         const uint32_t* crange, const PipeBuffers& bf, const RParams& p, bool next,
                                         bool run, const uint16_t* fkb) {
     if (next) r_geometry_next<STEP, QP>(c, tid, p, r.g);   // r.g holds chunk c - 1
@@ -358,7 +349,6 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, con
     if (!run) return;   // uniform: a chunk pass 2 skips (none of its grid points can be kept)
     r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
     if constexpr (STEP == 1) r.kb = fkb[c * 256 + tid];   // pass 1's keep1 bits (this lane wrote them)
-    else r_load_tab<STEP, QP>(tab, r.g, p, r.tw);
     // delta words of the chunk's keep1 disparities (pass 1's range), written to
     // LDS at the chunk's start; every index is clamped in range, so the loads
     // are unconditional (whatever crange holds)
@@ -418,12 +408,12 @@ __device__ __forceinline__ uint32_t r_keep_range(const uint32_t (&dw)[RCfg<STEP,
 template <int STEP, int QP>
 __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint32_t* hist, uint32_t* dirty,
                                          uint32_t* crange, uint32_t* wstage, uint32_t* dump, const RParams& p,
-                                         uint32_t& nvalid, uint32_t& nkept, bool any, uint16_t* fkb) {
+                                         uint32_t& nvalid, uint32_t& nkept, bool any, uint16_t* fkb,
+                                         uint32_t keep) {
     const int lane = lane_id();
     nvalid += r_nvalid<STEP, QP>(r.dw, r.g, p);
-    const uint32_t keep = any ? r_keep1<STEP, QP>(r.dw, r.tw, r.g) : 0u;
     if constexpr (STEP == 1) fkb[c * 256 + threadIdx.x] = (uint16_t)keep;   // for pass 2 (read back by this lane)
-    if (!any) {   // uniform: no grid point of the chunk can be kept (keep table): nothing to bin
+    if (!any) {   // uniform: the plane rules out every grid point of the chunk: nothing to bin
         if (lane == 0) crange[4 * c + (threadIdx.x >> 6)] = 0u;
         return;
     }
@@ -442,7 +432,7 @@ __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint3
             const bool v1 = j + kWave < wtotal;
             const uint32_t c0 = wstage[j];
             const uint32_t c1 = wstage[v1 ? j + kWave : j];
-            const int b0 = r_bin_sel(c0), b1 = r_bin_sel(c1);
+            const uint32_t b0 = r_bin_sel(c0), b1 = r_bin_sel(c1);
             const uint32_t o0 = atomicAdd(&hist[b0], 1u);
             uint32_t o1 = lim;
             if (v1) o1 = atomicAdd(&hist[b1], 1u);
@@ -552,14 +542,15 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
 template <int STEP, int QP, bool PF, class SH>
 __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, const uint32_t* hist,
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
-                                         const uint8_t* fdisp, const uint8_t* fbgr, const uint16_t* tab,
-                                         const PipeBuffers& bf, float* oX, int32_t* oP, uint32_t& running,
-                                         uint32_t& flushed, bool next_run, const uint16_t* fkb, const RParams& p) {
+                                         const uint8_t* fdisp, const uint8_t* fbgr, const RLean& L,
+                                         const FramePlane* Lp, const PipeBuffers& bf, float* oX, int32_t* oP,
+                                         uint32_t& running, uint32_t& flushed, bool next_run, const uint16_t* fkb,
+                                         const RParams& p) {
     constexpr int QPL = RCfg<STEP, QP>::QPL;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     uint32_t keep;
     if constexpr (STEP == 1) keep = r.kb;
-    else keep = r_keep1<STEP, QP>(r.dw, r.tw, r.g);
+    else keep = r_keep1<STEP, QP>(r.dw, r.g, L, Lp, p.Wg);   // chunks pass 2 runs: not ruled out, or the last
     // this chunk's delta words into LDS, read by its scatter after the next
     // barrier (every wave has finished chunk c - 1's scatter)
     uint32_t* dl = sh.dlt;
@@ -573,7 +564,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
         uint32_t pos0;
         const uint32_t wtotal = r_stage_colours_sel<STEP, QP>(keep, cw, wstage, sh.dump + tid, pos0);
         for (uint32_t j = lane; j < wtotal; j += kWave) {
-            const int bin = r_bin_sel(wstage[j]);
+            const uint32_t bin = r_bin_sel(wstage[j]);
             wstage[j] = (int64_t)hist[bin] > (int64_t)p.hist_thr ? 1u : 0u;
         }
         uint32_t pos = pos0;
@@ -652,7 +643,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
             o += bit;
         }
     }
-    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, tab, sh.crange, bf, p, true, next_run, fkb);   // in flight before the stores
+    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, sh.crange, bf, p, true, next_run, fkb);   // in flight before the stores
     __syncthreads();
     running += T;
     // write whole 128-byte lines: outputs up to a multiple of 32 (X, Y, Z: 32 floats a line; P: 16 pairs),
@@ -683,12 +674,39 @@ struct FusedShared {
     // (255 - dmin) << 16 | dmax (0 = no kept point)
     alignas(16) uint32_t crange[maxchunks_of<QP>() * 4];
     uint32_t dlt[kRDeltaWords];   // pass 2: the chunk's delta words (scatter lookups)
+    uint32_t cany[8];             // per chunk: can the frame's plane keep any of its grid points
 };
 static_assert(sizeof(FusedShared<4>) <= 32768, "5 workgroups per CU (160 KiB LDS), as many as 93 VGPRs allow");
 
+// sh.cany bit c: can the plane keep some grid point of chunk c (rows_keepable
+// over the chunk's rows)? One lane per chunk (nchunks <= 256), one ballot per wave.
+template <int STEP, int QP>
+__device__ __forceinline__ void chunk_keepable_bits(FusedShared<QP>& sh, const FramePlane* Lp, const RParams& p) {
+    constexpr int per = RCfg<STEP, QP>::QPL * 256;   // quads per chunk
+    const int c = threadIdx.x;
+    bool k = false;
+    const FramePlane L = *Lp;
+    if (c < p.nchunks && L.valid) {
+        const int gy0 = fastdiv40(c * per, p.Q_m40);
+        const int gy1 = fastdiv40(min((c + 1) * per, p.frame_quads) - 1, p.Q_m40);
+        k = rows_keepable(L, gy0, gy1, p.Wg, STEP);
+    }
+    const uint64_t m = __ballot(k);
+    if (lane_id() == 0) {
+        sh.cany[2 * (c >> 6)] = (uint32_t)m;
+        sh.cany[2 * (c >> 6) + 1] = (uint32_t)(m >> 32);
+    }
+}
+
+template <int QP>
+__device__ __forceinline__ bool chunk_any(const FusedShared<QP>& sh, int c) {   // uniform
+    return __builtin_amdgcn_readfirstlane((sh.cany[c >> 5] >> (c & 31)) & 1u) != 0;
+}
+
 template <int STEP, int QP, bool PF1 = false>
 __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, const PipeBuffers& bf,
-                                            const uint16_t* tab, const RParams& p) {
+                                            const RLean& L, const FramePlane* Lp,
+                                            const RParams& p) {
     constexpr int WREGION = 64 * RCfg<STEP, QP>::QPL * 4;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const uint8_t* fdisp = bf.disp + (int64_t)frame * p.frame_px;
@@ -696,25 +714,32 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
     uint32_t* wstage = sh.stage + wave * WREGION;
     for (int i = tid; i < kRBins; i += 256) sh.hist[i] = 0;
     if (tid < maxchunks_of<QP>() / 32) sh.dirty[tid] = 0;
+    chunk_keepable_bits<STEP, QP>(sh, Lp, p);
     __syncthreads();
     uint32_t nvalid = 0, nkept = 0;
     uint16_t* fkb = bf.kbits + (int64_t)frame * p.nchunks * 256;   // step 1: keep1 bits per chunk and lane
     const int n1 = (p.ablate & 128) ? 0 : p.nchunks;   // ablate: DIAGNOSTIC ONLY
     if constexpr (PF1) {   // chunk c + 1's loads in flight while chunk c is binned (pass 1 stores nothing)
         P1Regs<STEP, QP> r1;
-        if (n1 > 0) p1_load<STEP, QP>(r1, 0, tid, fdisp, fbgr, tab, p, false, bf.cany[0] != 0);
+        if (n1 > 0) p1_load<STEP, QP>(r1, 0, tid, fdisp, fbgr, p, false, chunk_any(sh, 0));
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> cur = r1;
-            if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, tab, p, true, bf.cany[c + 1] != 0);
+            // keep1 before chunk c + 1's loads are issued: its rare fp64 path then
+            // runs with one chunk's registers live, not two
+            const bool any = chunk_any(sh, c);
+            const uint32_t keep = any ? r_keep1<STEP, QP>(cur.dw, cur.g, L, Lp, p.Wg) : 0u;
+            if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, p, true, chunk_any(sh, c + 1));
             p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept,
-                               bf.cany[c] != 0, fkb);
+                               any, fkb, keep);
         }
     } else {
         for (int c = 0; c < n1; ++c) {
             P1Regs<STEP, QP> r1;
-            const bool any = bf.cany[c] != 0;
-            p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, tab, p, false, any);
-            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept, any, fkb);
+            const bool any = chunk_any(sh, c);
+            p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, p, false, any);
+            const uint32_t keep = any ? r_keep1<STEP, QP>(r1.dw, r1.g, L, Lp, p.Wg) : 0u;
+            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept, any, fkb,
+                               keep);
         }
     }
     nvalid = wave_sum(nvalid);
@@ -728,7 +753,8 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
 
 template <int STEP, int QP, bool PF>
 __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, const PipeBuffers& bf,
-                                            const uint16_t* tab, const RParams& p) {
+                                            const RLean& L, const FramePlane* Lp,
+                                            const RParams& p) {
     constexpr int WREGION = 64 * RCfg<STEP, QP>::QPL * 4;
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint8_t* fdisp = bf.disp + (int64_t)frame * p.frame_px;
@@ -739,7 +765,7 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     uint32_t running = 0, flushed = 0;
     const int n2 = (p.ablate & 256) ? 0 : p.nchunks;
     // a chunk in which pass 1 kept no point (its keep1 range is 0 in every wave;
-    // always so where the keep table rules the chunk out) adds no output and is
+    // always so where the plane rules the chunk out) adds no output and is
     // skipped, loads included; the last chunk always runs (it flushes the tail)
     const auto run = [&](int c) {
         const uint4 cr = *reinterpret_cast<const uint4*>(sh.crange + 4 * c);
@@ -747,14 +773,14 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     };
     const uint16_t* fkb = bf.kbits + (int64_t)frame * p.nchunks * 256;
     P2Regs<STEP, QP> r2;
-    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, tab, sh.crange, bf, p, false, run(0), fkb);
+    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, sh.crange, bf, p, false, run(0), fkb);
     for (int c = 0; c < n2; ++c) {
-        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, tab, sh.crange, bf, p, c > 0, run(c), fkb);
+        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, sh.crange, bf, p, c > 0, run(c), fkb);
         if (!run(c)) {   // uniform; c + 1 < n2 here
-            if (PF) p2_load<STEP, QP>(r2, c + 1, tid, fdisp, tab, sh.crange, bf, p, true, run(c + 1), fkb);
+            if (PF) p2_load<STEP, QP>(r2, c + 1, tid, fdisp, sh.crange, bf, p, true, run(c + 1), fkb);
             continue;
         }
-        p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, tab, bf, oX, oP,
+        p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oP,
                                running, flushed, c + 1 < n2 && run(c + 1), fkb, p);
     }
     if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;
@@ -762,13 +788,16 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
 
 // ---------------------------------------------------------------------------
 // One workgroup = one frame: pass 1 over all chunks, then pass 2 (grid = frames).
+// The frame's plane: bf.planes[frame * bf.plane_stride] (device memory).
 // ---------------------------------------------------------------------------
 template <int STEP, int QP, bool PF, bool PF1>
-__device__ __forceinline__ void fused_body(const PipeBuffers& bf, const uint16_t* __restrict__ tab, const RParams& p,
+__device__ __forceinline__ void fused_body(const PipeBuffers& bf, const RParams& p,
                                            FusedShared<QP>& sh) {
     const int tid = threadIdx.x;
     const int frame = blockIdx.x;
-    frame_pass1<STEP, QP, PF1>(frame, sh, bf, tab, p);
+    const FramePlane* Lp = bf.planes + (int64_t)frame * bf.plane_stride;
+    const RLean L{Lp->al32, Lp->bb32, Lp->b032, Lp->tn32, Lp->g32};
+    frame_pass1<STEP, QP, PF1>(frame, sh, bf, L, Lp, p);
     uint32_t* gh = bf.hist + (int64_t)frame * kBins;
     for (int b = tid; b < kBins; b += 256) gh[b] = b < kRBins ? sh.hist[b] : 0u;
     if (tid == 0) {
@@ -776,14 +805,13 @@ __device__ __forceinline__ void fused_body(const PipeBuffers& bf, const uint16_t
         cn[0] = (int64_t)sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
         cn[1] = (int64_t)sh.red[4] + sh.red[5] + sh.red[6] + sh.red[7];
     }
-    frame_pass2<STEP, QP, PF>(frame, sh, bf, tab, p);
+    frame_pass2<STEP, QP, PF>(frame, sh, bf, L, Lp, p);
 }
 
 template <int STEP, int QP, bool PF, bool PF1 = false>
-__global__ __launch_bounds__(256) void resident_fused_kernel(PipeBuffers bf, const uint16_t* __restrict__ tab,
-                                                             RParams p) {
+__global__ __launch_bounds__(256) void resident_fused_kernel(PipeBuffers bf, RParams p) {
     __shared__ FusedShared<QP> sh;
-    fused_body<STEP, QP, PF, PF1>(bf, tab, p, sh);
+    fused_body<STEP, QP, PF, PF1>(bf, p, sh);
 }
 
 bool resident_supported(const KParams& p) {   // frame_quads <= 2^20: every QP's chunk count fits its dirty bits
@@ -816,21 +844,32 @@ static RParams resident_params(const KParams& kp, int qpl) {
     return p;
 }
 
-hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, const uint16_t* tab, int frames,
+// A host plane into device memory, stream-ordered (no host buffer outlives the call).
+__global__ void store_plane_kernel(FramePlane v, FramePlane* __restrict__ dst) {
+    if (threadIdx.x == 0) *dst = v;
+}
+
+hipError_t launch_store_plane(const FramePlane& v, FramePlane* dst, hipStream_t s) {
+    hipLaunchKernelGGL(store_plane_kernel, dim3(1), dim3(64), 0, s, v, dst);
+    return hipGetLastError();
+}
+
+// b.planes must be set (device planes; one for every frame with plane_stride 0).
+hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, int frames,
                                     bool prefetch, hipStream_t s, bool prefetch1) {
     if (frames <= 0) return hipSuccess;
-    if (!resident_supported(kp)) return hipErrorInvalidValue;
+    if (!resident_supported(kp) || !b.planes) return hipErrorInvalidValue;
     const dim3 grid(frames), block(256);
     if (kp.step == 1) {
         const RParams p = resident_params(kp, 4);
-        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true>), grid, block, 0, s, b, tab, p);
-        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true>), grid, block, 0, s, b, tab, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, false>), grid, block, 0, s, b, tab, p);   // no prefetch
+        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true>), grid, block, 0, s, b, p);
+        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true>), grid, block, 0, s, b, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, false>), grid, block, 0, s, b, p);
     } else {
         const RParams p = resident_params(kp, 2);
-        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<2, 2, true, true>), grid, block, 0, s, b, tab, p);
-        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<2, 2, true>), grid, block, 0, s, b, tab, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<2, 2, false>), grid, block, 0, s, b, tab, p);
+        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<2, 2, true, true>), grid, block, 0, s, b, p);
+        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<2, 2, true>), grid, block, 0, s, b, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<2, 2, false>), grid, block, 0, s, b, p);
     }
     return hipGetLastError();
 }

@@ -122,31 +122,11 @@ KParams make_params(int H, int W, int step, const sv_camera& cam) {
 }
 
 void set_plane(KParams& p, const sv_plane& pl, double thr, int hist_thr) {
-    FramePlane fp;
-    plane_fields(fp, pl.a, pl.b, pl.c, p.f);
-    apply_plane(p, fp);
     p.thr = thr;
     p.thr32 = (float)thr;
-    // keep1_lean constants. u = B*(a*(x-cw) + b*(y-ch) + c*f) = al*x + bb*y + b0.
-    // fp32 error of e = |u - d| - t*d is <= 2^-21 * M with
-    // M = 2*U + 255*(1+t) + 255, U = |al|*W + |bb|*H + |b0| (derivation in
-    // DESIGN.md §2.3); the reference's own fp64 error is <= 2^-48 * M. The guard
-    // 2^-16 * M leaves a 32x margin; non-finite constants force the exact path.
-    {
-        const double al = p.B * pl.a, bb = p.B * pl.b;
-        const double b0 = p.B * pl.c * p.f - bb * p.ch - al * p.cw;
-        const double t = thr * p.nrm;
-        const double U = std::fabs(al) * p.W + std::fabs(bb) * p.H + std::fabs(b0);
-        const double M = 2.0 * U + 255.0 * (1.0 + std::fabs(t)) + 255.0;
-        p.al32 = (float)al;
-        p.bb32 = (float)bb;
-        p.b032 = (float)b0;
-        p.tn32 = (float)t;
-        const double g = std::ldexp(M, -16);
-        const bool finite = std::isfinite(g) && std::isfinite((double)p.al32) && std::isfinite((double)p.bb32) &&
-                            std::isfinite((double)p.b032) && std::isfinite((double)p.tn32);
-        p.g32 = finite ? (float)g : INFINITY;
-    }
+    FramePlane fp;
+    plane_fields(fp, pl.a, pl.b, pl.c, p.f, p.B, p.cw, p.ch, thr, p.W, p.H);
+    apply_plane(p, fp);
     p.hist_thr = hist_thr;
     // Diagnostic ablation for profiling only (documented in DESIGN.md): when set,
     // kernels skip parts of their work and the results are NOT valid.
@@ -208,17 +188,17 @@ struct sv_batch {
     hipStream_t stream = nullptr;    // K1, pass 1 (stream A)
     hipStream_t stream2 = nullptr;   // pipeline offsets kernels (stream B), beside the stage launches
     std::vector<hipEvent_t> sync_ev; // pipeline hand-offs between A and B (timing disabled)
-    DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks, ktab;
+    DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks;
     DevBuf mdisp, carmask;      // pre-pass: masked disparity (frames x H x W), 0x00/0xFF mask (H x W)
     DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
     DevBuf mpts, rres;          // maskpoints (frames x mcap x 3 fp64) + counts; batched RANSAC results
     DevBuf mpk;                 // maskpoints packed (frames x mcap words x | y << 12 | d << 24): RANSAC's fp32 screen
     DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
     DevBuf fplanes;             // per-frame keep1 plane fields (FramePlane) for sv_batch_pipeline_planes
+    DevBuf dplane;              // the FramePlane of a device plane (sv_batch_pipeline_dev)
     int64_t mcap = 0;
-    int trace_trials = 0, trace_k = 0;
+    int trace_trials = 0, trace_k = 0, traced_trials = 0;   // requested; k and trials of the recorded trace
     bool have_mask = false;
-    uint32_t* ktab_err_host = nullptr;   // pinned: keep-table "not an interval" flag
     // pipeline control block (one memset per call): hist | counts | err
     uint32_t* hist = nullptr;
     int64_t* counts = nullptr;
@@ -257,6 +237,14 @@ const char* sv_last_error(void) { return g_err.c_str(); }
 int sv_comm_set_error(const char* msg) {
     g_err = msg ? msg : "";
     return 0;
+}
+
+// comm.hip: a batch's device and stream (collectives are ordered on the batch's stream)
+int sv_batch_stream_internal(sv_batch* b, int* device, hipStream_t* stream) {
+    if (!b) return SV_E_ARG;
+    *device = b->device;
+    *stream = b->stream;
+    return SV_OK;
 }
 
 int sv_device_count(int* n) {
@@ -406,10 +394,9 @@ int sv_batch_destroy(sv_batch* b) {
     if (!b) return SV_OK;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
-    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks, &b->ktab,
-                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes})
+    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks,
+                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane})
         if (x->p) (void)hipFree(x->p);
-    if (b->ktab_err_host) (void)hipHostFree(b->ktab_err_host);
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : b->pool) (void)hipEventDestroy(ev);
@@ -508,8 +495,10 @@ RansacRes ransac_res(sv_batch* b) {
 }
 }  // namespace
 
+// planes: device planes, frame f uses planes[f * plane_stride] (NULL: the host plane)
 static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane* plane, double point_thr,
-                               int hist_thr, int chunk, int sync, Device* d, const FramePlane* planes = nullptr) {
+                               int hist_thr, int chunk, int sync, Device* d, const FramePlane* planes = nullptr,
+                               int plane_stride = 1) {
     if (!b->with_bgr) return fail(SV_E_ARG, "pipeline needs a batch created with bgr");
     KParams p = make_params(b->H, b->W, b->step, *cam);
     if (p.Wg > 4096 || p.Hg > 4096) return fail(SV_E_ARG, "pipeline supports grids up to 4096 x 4096");
@@ -540,45 +529,34 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     bf.dybits = d->tables.dy.as<uint32_t>();
     bf.cap = (int64_t)cap;
     bf.planes = planes;
-    int mode = planes ? 1 : b->pipe_mode;   // the resident kernels take one plane (its keep table) per call
+    bf.plane_stride = plane_stride;
+    int mode = b->pipe_mode;
     if (mode == 0) mode = (b->frames >= kResidentMinFrames && resident_supported(p)) ? 2 : 1;
     if (mode >= 2 && !resident_supported(p))
         return fail(SV_E_ARG, "frame-resident pipeline: frame too large (grid %d x %d)", p.Hg, p.Wg);
     int t0, t1;
-    if (mode >= 2) {   // every output word (hist, counts, points) is rewritten: no memset
-        const size_t tab_bytes = sizeof(uint16_t) * (size_t)p.Hg * p.pitch;
-        HIP_TRY(b->ktab.ensure(tab_bytes + 16 + 64 + 2048));
-        if (!b->ktab_err_host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&b->ktab_err_host), 64));
-        uint16_t* tab = b->ktab.as<uint16_t>();
-        uint32_t* terr = reinterpret_cast<uint32_t*>(b->ktab.as<char>() + (tab_bytes + 15) / 16 * 16);
-        HIP_TRY(hipEventRecord(b->ev[2], b->stream));
-        HIP_TRY(b->timed_event(&t0));
-        uint32_t* cany = terr + 16;   // 512 chunk flags (the resident kernels' chunks per frame <= 512)
-        HIP_TRY(hipMemsetAsync(terr, 0, 64 + 2048, b->stream));
-        HIP_TRY(launch_keep_table(p, tab, terr, cany, b->stream));
-        bf.cany = cany;
-        HIP_TRY(hipMemcpyAsync(b->ktab_err_host, terr, 4, hipMemcpyDeviceToHost, b->stream));
-        HIP_TRY(hipStreamSynchronize(b->stream));
-        if (*b->ktab_err_host) goto tiled;   // a keep set that is not one interval: exact tiled kernels
-        HIP_TRY(launch_pipeline_resident(p, bf, tab, b->frames, mode != 3, b->stream, mode == 2));
-        HIP_TRY(b->timed_event(&t1));
-        HIP_TRY(hipEventRecord(b->ev[3], b->stream));
-        b->pending[1].push_back({t0, t1});
-        b->have_ms[1] = true;
-        if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
-        return SV_OK;
-    }
     HIP_TRY(hipEventRecord(b->ev[2], b->stream));
     HIP_TRY(b->timed_event(&t0));
-tiled:
-    const int nchunks = (b->frames + chunk - 1) / chunk;
-    while ((int)b->sync_ev.size() < 2 * nchunks) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        b->sync_ev.push_back(e);
+    if (mode >= 2) {   // every output word (hist, counts, points) is rewritten: no memset, no host sync
+        if (!planes) {   // the host plane, stream-ordered into device memory
+            HIP_TRY(b->dplane.ensure(sizeof(FramePlane)));
+            FramePlane fp;
+            plane_fields(fp, plane->a, plane->b, plane->c, p.f, p.B, p.cw, p.ch, point_thr, p.W, p.H);
+            HIP_TRY(launch_store_plane(fp, b->dplane.as<FramePlane>(), b->stream));
+            bf.planes = b->dplane.as<FramePlane>();
+            bf.plane_stride = 0;
+        }
+        HIP_TRY(launch_pipeline_resident(p, bf, b->frames, mode != 3, b->stream, mode == 2));
+    } else {
+        const int nchunks = (b->frames + chunk - 1) / chunk;
+        while ((int)b->sync_ev.size() < 2 * nchunks) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            b->sync_ev.push_back(e);
+        }
+        HIP_TRY(hipMemsetAsync(b->ctrl.p, 0, b->ctrl_bytes, b->stream));
+        HIP_TRY(launch_pipeline(p, bf, b->frames, chunk, b->stream, b->stream2, b->sync_ev.data()));
     }
-    HIP_TRY(hipMemsetAsync(b->ctrl.p, 0, b->ctrl_bytes, b->stream));
-    HIP_TRY(launch_pipeline(p, bf, b->frames, chunk, b->stream, b->stream2, b->sync_ev.data()));
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[3], b->stream));
     b->pending[1].push_back({t0, t1});
@@ -601,12 +579,24 @@ int sv_batch_pipeline_planes(sv_batch* b, const sv_camera* cam, double point_thr
     if (!b->rres.p) return fail(SV_E_STATE, "no per-frame planes (sv_batch_ransac first)");
     Device* d;
     if (int rc = dev_get(b->device, &d)) return rc;
-    HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(b->fplanes.ensure(sizeof(FramePlane) * (size_t)b->frames));
     const RansacRes r = ransac_res(b);
-    HIP_TRY(launch_frame_planes(r.abc, r.trial, b->frames, cam->f, b->fplanes.as<FramePlane>(), b->stream));
+    const KParams kp = make_params(b->H, b->W, b->step, *cam);
+    HIP_TRY(launch_frame_planes(r.abc, r.trial, b->frames, kp, point_thr, b->fplanes.as<FramePlane>(), b->stream));
     const sv_plane none{0.0, 0.0, 0.0};   // per-frame planes replace it
     return batch_pipeline_impl(b, cam, &none, point_thr, hist_thr, chunk, sync, d, b->fplanes.as<FramePlane>());
+}
+
+int sv_batch_pipeline_dev(sv_batch* b, const sv_camera* cam, const double* dplane, double point_thr, int hist_thr,
+                          int chunk, int sync) {
+    if (!b || !cam || !dplane) return fail(SV_E_ARG, "null");
+    Device* d;
+    if (int rc = dev_get(b->device, &d)) return rc;
+    HIP_TRY(b->dplane.ensure(sizeof(FramePlane)));
+    const KParams kp = make_params(b->H, b->W, b->step, *cam);
+    HIP_TRY(launch_frame_planes(dplane, nullptr, 1, kp, point_thr, b->dplane.as<FramePlane>(), b->stream));
+    const sv_plane none{0.0, 0.0, 0.0};   // the device plane replaces it
+    return batch_pipeline_impl(b, cam, &none, point_thr, hist_thr, chunk, sync, d, b->dplane.as<FramePlane>(), 0);
 }
 
 int sv_batch_read_frame_plane(sv_batch* b, int frame, double* out4) {
@@ -1057,6 +1047,7 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
         trace = b->rtrace.as<int32_t>();
     }
     b->trace_k = k;
+    b->traced_trials = trace ? b->trace_trials : 0;   // what rtrace holds now (read back by sv_batch_read_ransac_trace)
     // the largest frame sizes the kernel's LDS (bitmap / pool list): one small read-back
     std::vector<int64_t> cnt(F);
     HIP_TRY(hipMemcpyAsync(cnt.data(), r.mcount, sizeof(int64_t) * F, hipMemcpyDeviceToHost, b->stream));
@@ -1093,12 +1084,16 @@ int sv_batch_ransac_trace(sv_batch* b, int trials) {
     return SV_OK;
 }
 
-int sv_batch_read_ransac_trace(sv_batch* b, int frame, int32_t* out) {
-    if (!b || frame < 0 || frame >= b->frames || !out) return fail(SV_E_ARG, "bad args");
-    if (!b->trace_trials || !b->rtrace.p) return fail(SV_E_STATE, "no trace (sv_batch_ransac_trace, then sv_batch_ransac)");
+int sv_batch_read_ransac_trace(sv_batch* b, int frame, int32_t* out, int64_t cap, int* out_trials, int* out_k) {
+    if (!b || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "bad args");
+    if (!b->traced_trials || !b->rtrace.p) return fail(SV_E_STATE, "no trace (sv_batch_ransac_trace, then sv_batch_ransac)");
+    const size_t per = (size_t)b->traced_trials * (b->trace_k + 3);
+    if (out_trials) *out_trials = b->traced_trials;
+    if (out_k) *out_k = b->trace_k;
+    if (!out) return SV_OK;   // sizes only
+    if (cap < (int64_t)per) return fail(SV_E_CAP, "trace needs %zu int32, buffer holds %lld", per, (long long)cap);
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
-    const size_t per = (size_t)b->trace_trials * (b->trace_k + 3);
     HIP_TRY(hipMemcpy(out, b->rtrace.as<int32_t>() + per * frame, sizeof(int32_t) * per, hipMemcpyDeviceToHost));
     return SV_OK;
 }

@@ -41,21 +41,35 @@ struct KParams {
     int ablate;                            // DIAGNOSTIC ONLY (env SVX_ABLATE): skip work, results invalid
 };
 
-// The plane-dependent fields of KParams used by keep1 (tiled pipeline), for
-// one frame of the per-frame-plane pipeline (planes from the batched RANSAC).
-// plane_fields is the single definition, shared by the host's set_plane and
-// the device's per-frame kernel, so both give the same bits.
+// The plane-dependent fields of KParams used by keep1, for one plane: the
+// per-call plane of sv_batch_pipeline, one frame's plane of the per-frame-plane
+// pipeline (planes from the batched RANSAC) or a plane broadcast into device
+// memory. plane_fields is the single definition, shared by the host's
+// set_plane and the device's plane kernels, so both give the same bits.
 struct FramePlane {
     double a, b, c, nrm;
+    // u = ual*x + ubb*y + ub0 (fp64) and t = thr*|abc|: keep1 <=> |u - d| < t*d
+    // (chunk/tile bounds; the fp32 copies below decide single points)
+    double ual, ubb, ub0, ut;
+    double f, fB, cw, ch, thr;   // camera and point threshold: the exact fp64 path reads them with the plane
     float a32, b32, c32, inv_nrm32, guard32, abs_a32, abs_b32, abs_cf32;
+    float al32, bb32, b032, tn32, g32;   // keep1_lean (see KParams)
     uint32_t valid;   // 0: RANSAC found no plane (the reference's plane step raises: no points)
 };
 
-__host__ __device__ inline void plane_fields(FramePlane& o, double a, double b, double c, double f) {
+// thr = point_thr (functions.py:314-323); W, H = the frame's size in pixels
+// (bound of |x|, |y| in the keep1_lean error analysis).
+__host__ __device__ inline void plane_fields(FramePlane& o, double a, double b, double c, double f, double B,
+                                             double cw, double ch, double thr, int W, int H) {
     o.a = a;
     o.b = b;
     o.c = c;
     o.nrm = __builtin_sqrt(a * a + b * b + c * c);   // functions.py:307 (correctly rounded, host and device)
+    o.f = f;
+    o.fB = f * B;   // functions.py:191 evaluates f*B in fp64 (as KParams::fB)
+    o.cw = cw;
+    o.ch = ch;
+    o.thr = thr;
     o.a32 = (float)a;
     o.b32 = (float)b;
     o.c32 = (float)c;
@@ -65,6 +79,29 @@ __host__ __device__ inline void plane_fields(FramePlane& o, double a, double b, 
     o.abs_a32 = (float)__builtin_fabs(a);
     o.abs_b32 = (float)__builtin_fabs(b);
     o.abs_cf32 = (float)(__builtin_fabs(c) * f);
+    // keep1_lean constants. u = B*(a*(x-cw) + b*(y-ch) + c*f) = al*x + bb*y + b0.
+    // fp32 error of e = |u - d| - t*d is <= 2^-21 * M with
+    // M = 2*U + 255*(1+t) + 255, U = |al|*W + |bb|*H + |b0| (derivation in
+    // DESIGN.md §2.3); the reference's own fp64 error is <= 2^-48 * M. The guard
+    // 2^-16 * M leaves a 32x margin; non-finite constants force the exact path.
+    const double al = B * a, bb = B * b;
+    const double b0 = B * c * f - bb * ch - al * cw;
+    const double t = thr * o.nrm;
+    const double U = __builtin_fabs(al) * W + __builtin_fabs(bb) * H + __builtin_fabs(b0);
+    const double M = 2.0 * U + 255.0 * (1.0 + __builtin_fabs(t)) + 255.0;
+    o.ual = al;
+    o.ubb = bb;
+    o.ub0 = b0;
+    o.ut = t;
+    o.al32 = (float)al;
+    o.bb32 = (float)bb;
+    o.b032 = (float)b0;
+    o.tn32 = (float)t;
+    const double g = M * 0x1p-16;
+    const bool finite = __builtin_isfinite(g) && __builtin_isfinite((double)o.al32) &&
+                        __builtin_isfinite((double)o.bb32) && __builtin_isfinite((double)o.b032) &&
+                        __builtin_isfinite((double)o.tn32);
+    o.g32 = finite ? (float)g : __builtin_inff();
     o.valid = 1;
 }
 
@@ -81,6 +118,37 @@ __host__ __device__ inline void apply_plane(KParams& p, const FramePlane& o) {
     p.abs_a32 = o.abs_a32;
     p.abs_b32 = o.abs_b32;
     p.abs_cf32 = o.abs_cf32;
+    p.al32 = o.al32;
+    p.bb32 = o.bb32;
+    p.b032 = o.b032;
+    p.tn32 = o.tn32;
+    p.g32 = o.g32;
+}
+
+// Can some grid point with u in [umin, umax] be kept for some d in 1..255?
+// keep1 <=> |u - d| < t*d (u affine in (x, y), so over a rectangle of grid
+// points its extremes are at the corners). For t < 0.99 no d in [1, 255] is
+// kept when u_max < 1 - t or u_min > 255 (1 + t). The margins (1e-9 relative,
+// plus 1e-12 of mag = the largest |term| summed into u) dwarf both the
+// reference's fp64 rounding and this bound's own (~1e-15 of mag). NaN:
+// keepable (no skipping).
+__host__ __device__ inline bool urange_keepable(double umin, double umax, double t, double mag) {
+    if (!(t < 0.99)) return true;
+    const double slack = 1e-12 + 1e-12 * mag;
+    if (umax < (1.0 - t) * (1.0 - 1e-9) - slack) return false;
+    if (umin > 255.0 * (1.0 + t) * (1.0 + 1e-9) + 1e-9 + slack) return false;
+    return true;
+}
+
+// The grid rows gy0..gy1 (all columns 0..Wg-1) of a frame under plane o: keepable?
+__host__ __device__ inline bool rows_keepable(const FramePlane& o, int gy0, int gy1, int Wg, int step) {
+    const double ax0 = 0.0, ax1 = o.ual * (double)((Wg - 1) * step);
+    const double by0 = __builtin_fma(o.ubb, (double)(gy0 * step), o.ub0);
+    const double by1 = __builtin_fma(o.ubb, (double)(gy1 * step), o.ub0);
+    const double umax = __builtin_fmax(ax0, ax1) + __builtin_fmax(by0, by1);
+    const double umin = __builtin_fmin(ax0, ax1) + __builtin_fmin(by0, by1);
+    const double mag = __builtin_fabs(ax1) + __builtin_fabs(o.ubb * (double)(gy1 * step)) + __builtin_fabs(o.ub0);
+    return urange_keepable(umin, umax, o.ut, mag);
 }
 
 // ---------------------------------------------------------------------------

@@ -43,8 +43,8 @@ struct PipeBuffers {
     const uint32_t* dxbits;
     const uint32_t* dybits;
     int64_t cap;         // points per frame (Ng)
-    const FramePlane* planes = nullptr;   // per-frame planes (tiled kernels), or the KParams plane
-    const uint32_t* cany = nullptr;       // resident kernel: per chunk, can any grid point be kept (keep table)
+    const FramePlane* planes = nullptr;   // device planes: frame f uses planes[f * plane_stride] (else the KParams plane)
+    int plane_stride = 1;                 // 0: one device plane for every frame (a broadcast plane)
 };
 int pipeline_tiles_per_frame(const KParams& p);
 // The whole chain for frames [0, frames) in chunks: chunks + 2 fused stage
@@ -55,16 +55,16 @@ hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, i
 
 // kernels/resident.hip -----------------------------------------------------
 // One workgroup per frame (both passes, LDS histogram, running output offset).
-// keep1 from a per-call interval table (uint16 lo | hi << 8 per grid point of
-// Hg x pitch); *err is set when some grid point's keep set is not an interval.
+// keep1 per grid point from the frame's plane (b.planes, device memory, required):
+// the fp32 division-free test with the fp64 reference arithmetic inside its
+// guard; chunks the plane rules out are skipped.
 bool resident_supported(const KParams& p);
-// cany[chunk] = 1 where some grid point of the resident kernel's chunk can be kept
-// (zeroed by the caller; 512 words).
-hipError_t launch_keep_table(const KParams& p, uint16_t* tab, uint32_t* err, uint32_t* cany, hipStream_t s);
 // One workgroup per frame (pass 1 then pass 2); prefetch = pass 2 loads the
 // next chunk before issuing this chunk's stores (costs registers).
-hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, const uint16_t* tab, int frames,
+hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, int frames,
                                     bool prefetch, hipStream_t s, bool prefetch1 = false);
+// *dst = v on stream s (the resident kernel reads its planes from device memory).
+hipError_t launch_store_plane(const FramePlane& v, FramePlane* dst, hipStream_t s);
 
 // kernels/prepass.hip ------------------------------------------------------
 // fillDisparity frame recurrence / fillAltDisparity row means / maskDisparity.
@@ -125,8 +125,10 @@ hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_
                                int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
                                int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, int ablate,
                                hipStream_t s);
-hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, double f, FramePlane* out,
-                               hipStream_t s);
+// out[i] = plane_fields of abc[3i..3i+2] (trial[i] < 0, or trial NULL and a NaN plane: valid = 0);
+// trial may be NULL (a device plane, e.g. the RCCL broadcast buffer).
+hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, const KParams& p, double thr,
+                               FramePlane* out, hipStream_t s);
 
 // kernels/stages.hip -------------------------------------------------------
 // a2: |(P.abc - 1) / d| per point (abcd = a, b, c, d); a4/a5: hue bin per point,

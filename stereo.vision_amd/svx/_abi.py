@@ -64,7 +64,7 @@ SIGNATURES = {
     "sv_batch_read_ransac": [P, I, P, P, P, P],
     "sv_batch_read_maskpoints": [P, I, P, I64, PI64],
     "sv_batch_ransac_trace": [P, I],
-    "sv_batch_read_ransac_trace": [P, I, P],
+    "sv_batch_read_ransac_trace": [P, I, P, I64, ctypes.POINTER(I), ctypes.POINTER(I)],
     "sv_batch_create": [I, I, I, I, I, I, I, ctypes.POINTER(P)],
     "sv_batch_destroy": [P],
     "sv_batch_info": [P, P],
@@ -75,6 +75,7 @@ SIGNATURES = {
     "sv_batch_pipeline": [P, ctypes.POINTER(Camera), ctypes.POINTER(Plane), D, I, I, I],
     "sv_batch_pipeline_mode": [P, I],
     "sv_batch_pipeline_planes": [P, ctypes.POINTER(Camera), D, I, I, I],
+    "sv_batch_pipeline_dev": [P, ctypes.POINTER(Camera), P, D, I, I, I],
     "sv_batch_read_frame_plane": [P, I, P],
     "sv_batch_sync": [P],
     "sv_batch_last_ms": [P, I, PF],
@@ -91,7 +92,12 @@ SIGNATURES = {
     "sv_comm_unique_id": [P],
     "sv_comm_init": [I, I, P, I, ctypes.POINTER(P)],
     "sv_comm_destroy": [P],
+    "sv_comm_init_all": [I, P, P],
+    "sv_comm_group_start": [],
+    "sv_comm_group_end": [],
     "sv_comm_broadcast_plane": [P, ctypes.POINTER(Plane), I],
+    "sv_comm_broadcast_plane_dev": [P, P, ctypes.POINTER(Plane), I, ctypes.POINTER(P)],
+    "sv_multi_pipeline": [I, P, P, ctypes.POINTER(Camera), ctypes.POINTER(Plane), I, D, I, I],
     "sv_comm_allreduce_i64": [P, P, I],
 }
 _RESTYPE = {"sv_version": ctypes.c_char_p, "sv_last_error": ctypes.c_char_p}
@@ -103,11 +109,16 @@ def lib():
     """The loaded libsvx.so (raises ImportError if it was never built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"libsvx.so not found at {LIB_PATH}: build it with "
+        # SVX_LIB: DIAGNOSTIC A/B only (tools/ab_lib.py times an older build of the
+        # library beside this one); symbols that build lacks are left unbound.
+        path = os.environ.get("SVX_LIB") or LIB_PATH
+        if not os.path.exists(path):
+            raise ImportError(f"libsvx.so not found at {path}: build it with "
                               "`python -c 'import __graft_entry__ as g; g.build()'`")
-        l = ctypes.CDLL(LIB_PATH)
+        l = ctypes.CDLL(path)
         for name, args in SIGNATURES.items():
+            if path != LIB_PATH and not hasattr(l, name):
+                continue
             fn = getattr(l, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, ctypes.c_int)

@@ -114,6 +114,13 @@ class Batch:
         _abi.call("sv_batch_pipeline_planes", self._h, ctypes.byref(cam), float(point_thr), int(hist_thr),
                   int(chunk), int(sync))
 
+    def pipeline_dev(self, dplane, point_thr=0.05, hist_thr=10, camera=None, chunk=0, sync=True):
+        """The pipeline with the plane in device memory (a device pointer to a, b, c
+        on this batch's device, e.g. RcclComm.broadcast_plane_dev's): no host copy."""
+        cam = camera or CAMERA
+        _abi.call("sv_batch_pipeline_dev", self._h, ctypes.byref(cam), ctypes.c_void_p(dplane), float(point_thr),
+                  int(hist_thr), int(chunk), int(sync))
+
     def read_frame_plane(self, frame):
         """(a, b, c, |abc|) of the frame's plane as the kernels use it; |abc| = -1 without a plane."""
         out = np.empty(4, np.float64)
@@ -176,13 +183,15 @@ class Batch:
 
     def ransac_trace(self, trials):
         """Record the first `trials` trials' drawn indices per frame in later ransac() calls."""
-        self._trace = int(trials)
         _abi.call("sv_batch_ransac_trace", self._h, int(trials))
 
-    def read_ransac_trace(self, frame, k=600):
-        """(trials, k + 3) int32: each traced trial's sample indices, then P1..P3."""
-        out = np.empty((self._trace, k + 3), np.int32)
-        _abi.call("sv_batch_read_ransac_trace", self._h, frame, _abi.ptr(out))
+    def read_ransac_trace(self, frame):
+        """(trials, k + 3) int32: each traced trial's sample indices, then P1..P3
+        (trials and k of the last ransac() call, as the library recorded them)."""
+        t, k = ctypes.c_int(0), ctypes.c_int(0)
+        _abi.call("sv_batch_read_ransac_trace", self._h, frame, None, 0, ctypes.byref(t), ctypes.byref(k))
+        out = np.empty((t.value, k.value + 3), np.int32)
+        _abi.call("sv_batch_read_ransac_trace", self._h, frame, _abi.ptr(out), out.size, None, None)
         return out
 
     def read_maskpoints(self, frame):

@@ -1,0 +1,94 @@
+"""bench.py's launch logic on the CPU: how `--gpus N` maps onto processes and
+devices (torchrun ranks vs one process driving N GPUs), that a launcher whose
+WORLD_SIZE disagrees with --gpus is refused, that the shards of every
+topology cover the global frame ids exactly once, and the TCP control plane
+at three ranks."""
+import multiprocessing as mp
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import PKG, REPO
+
+import bench
+
+
+def test_plan_single_and_multi_process():
+    p = bench.plan(1, {})
+    assert p["mode"] == "single" and p["n_gpus"] == 1 and p["devices"] == [0]
+    p = bench.plan(2, {})
+    assert p["mode"] == "multi" and p["n_gpus"] == 2 and p["devices"] == [0, 1] and p["world"] == 1
+    p = bench.plan(8, {})
+    assert p["devices"] == list(range(8)) and p["n_gpus"] == 8
+
+
+def test_plan_torchrun_ranks():
+    for rank in range(2):
+        env = {"WORLD_SIZE": "2", "RANK": str(rank), "LOCAL_RANK": str(rank)}
+        p = bench.plan(2, env)
+        assert p["mode"] == "ranks" and p["n_gpus"] == 2 and p["world"] == 2
+        assert p["devices"] == [rank] and p["shard_base"] == rank
+    p = bench.plan(1, {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p["mode"] == "ranks" and p["n_gpus"] == 1
+
+
+@pytest.mark.parametrize("gpus,world", [(8, 1), (1, 8), (2, 4)])
+def test_plan_refuses_mismatched_launcher(gpus, world):
+    with pytest.raises(SystemExit) as e:
+        bench.plan(gpus, {"WORLD_SIZE": str(world), "RANK": "0", "LOCAL_RANK": "0"})
+    assert "WORLD_SIZE" in str(e.value)
+    with pytest.raises(SystemExit):
+        bench.plan(0, {})
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_shards_cover_global_frames(n):
+    frames = 4096
+    multi = bench.shards_of(bench.plan(n, {}), frames)
+    ranks = [s for r in range(n)
+             for s in bench.shards_of(bench.plan(n, {"WORLD_SIZE": str(n), "RANK": str(r), "LOCAL_RANK": str(r)}),
+                                      frames)]
+    for shards in (multi, ranks):
+        assert [d for d, _, _ in shards] == list(range(n))
+        ids = np.concatenate([np.arange(f, f + c) for _, f, c in shards])
+        assert np.array_equal(ids, np.arange(frames * n))   # every global id once, in order
+        assert all(c == frames for _, _, c in shards)       # weak scaling: 4096 per GPU
+    assert multi == ranks
+
+
+def _tcp_worker(rank, world, path, q):
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from svx.control import TcpControl
+    c = TcpControl(rank, world, path=path, timeout=60)
+    try:
+        got = c.broadcast_bytes(bytes([7] * 128) if rank == 0 else b"")
+        mx = c.max([rank, -rank, 0.5])
+        sm = c.sum([rank, 1.0])
+        c.barrier()
+        q.put((rank, got, list(mx), list(sm)))
+    finally:
+        c.close()
+
+
+@pytest.mark.timeout(120)
+def test_tcp_control_three_ranks(tmp_path):
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    path = str(tmp_path / "rdzv")
+    procs = [ctx.Process(target=_tcp_worker, args=(r, world, path, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    for rank, got, mx, sm in res:
+        assert got == bytes([7] * 128)
+        assert mx == [2.0, 0.0, 0.5] and sm == [3.0, 3.0]
+    assert not os.path.exists(path)   # rank 0 removes the rendezvous file once everyone is in

@@ -1,14 +1,16 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the sharded driver's host
-logic: frame sharding, max-over-ranks timing, the RCCL unique-id hand-off
-path (bytes broadcast) and the per-frame independence the sharding relies on
-(checked with the oracle standing in for the device)."""
+"""Multi-process (world_size 2, CPU) tests of the sharded driver's host
+logic over both control planes — svx.control's TCP star (the default, no
+PyTorch) and a torch.distributed gloo group (SVX_CONTROL=gloo): frame
+sharding, max-over-ranks timing, the RCCL unique-id hand-off path (bytes
+broadcast), bench.py's whole-job aggregation and the per-frame independence
+the sharding relies on (checked with the oracle standing in for the device)."""
 import os
 import socket
 import sys
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
+import multiprocessing as mp
 
 from conftest import PKG, REPO
 
@@ -31,9 +33,9 @@ def test_shard_partitions_exactly():
             assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, control, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SVX_CONTROL=control)
     for p in (REPO, PKG):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -56,18 +58,22 @@ def _worker(rank, world, port, q):
             crop = (np.ascontiguousarray(d[180:260]), np.ascontiguousarray(c[180:260]))
             counts.append(oracle.pipeline_frame(*crop, 2, abc=oracle.synthetic_plane())["counts"])
         tot = ctrl.sum(np.array(counts, np.float64).sum(axis=0))
+        # bench.py's whole-job figure: all ranks' points over the slowest rank's time
+        import bench
+        agg = bench.aggregate(ctrl, world, 1000.0 * (rank + 1), 4, 0.5 + rank)
         ctrl.barrier()
-        q.put((rank, list(mx), list(sm), first, count, counts, list(tot)))
+        q.put((rank, list(mx), list(sm), first, count, counts, list(tot), agg))
     finally:
         ctrl.close()
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_control_plane_and_sharding():
+@pytest.mark.parametrize("control", ["tcp", "gloo"])
+def test_two_rank_control_plane_and_sharding(control):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, control, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in procs)
@@ -80,7 +86,9 @@ def test_two_rank_control_plane_and_sharding():
         d, c = oracle.synth_frame(f)
         crop = (np.ascontiguousarray(d[180:260]), np.ascontiguousarray(c[180:260]))
         ref.append(oracle.pipeline_frame(*crop, 2, abc=oracle.synthetic_plane())["counts"])
-    for rank, mx, sm, first, count, counts, tot in res:
+    for rank, mx, sm, first, count, counts, tot, agg in res:
+        assert agg["n_gpus"] == 2 and agg["points"] == 3000.0 * 4
+        assert abs(agg["value"] - 3000.0 * 4 / 1.5 / 1e6) < 1e-12 and abs(agg["ms_per_step"] - 1.5 / 4 * 1e3) < 1e-9
         assert mx == [2.0, 0.0] and sm == [2.0, 1.0]
         assert (first, count) == (2 * rank, 2)
         assert [tuple(c) for c in counts] == ref[first:first + count]

@@ -38,3 +38,37 @@ def test_sharded_batches_equal_one_batch():
             for j in range(count):
                 assert tuple(c[j]) == tuple(ref_counts[first + j])
                 assert np.array_equal(b.read_points(j)[1], ref_pts[first + j])
+
+
+@pytest.mark.parametrize("mode", ["resident", "tiled"])
+def test_device_plane_broadcast_drives_the_pipeline(mode):
+    """The plane broadcast into device memory (RCCL, world 1) and read there by
+    the pipeline gives exactly the host-plane pipeline's outputs; so does the
+    one-process driver (ncclCommInitAll + grouped broadcast, sv_multi_pipeline)."""
+    from svx import batch as sb
+    from svx import dist
+    plane = sb.synthetic_plane()
+    frames = 6
+    with sb.Batch(frames, step=1, with_bgr=True, with_points=True) as ref:
+        ref.pipeline_mode(mode)
+        ref.synth(300)
+        ref.pipeline(plane=plane)
+        want = ref.digest("pipeline")
+    ctrl = dist.Control(rank=0, world=1)
+    comm = dist.RcclComm(ctrl, device=0)
+    mcomm = dist.MultiComm([0])
+    try:
+        with sb.Batch(frames, step=1, with_bgr=True, with_points=True) as b:
+            b.pipeline_mode(mode)
+            b.synth(300)
+            for _ in range(2):   # the second call reuses the broadcast buffer
+                dp = comm.broadcast_plane_dev(b, plane, root=0)
+                assert dp
+                b.pipeline_dev(dp, sync=True)
+                assert np.array_equal(b.digest("pipeline"), want)
+            b.pipeline(plane=(0.0, 1.0, 0.0))          # something else in between
+            mcomm.pipeline([b], plane, root=0, sync=True)
+            assert np.array_equal(b.digest("pipeline"), want)
+    finally:
+        mcomm.close()
+        comm.close()

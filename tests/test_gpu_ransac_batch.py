@@ -63,7 +63,8 @@ def _check(res, ref_abc, ref_t, ref_e, what):
 
 
 def _check_draws(b, frame, pts, seed, trials, k=600):
-    tr = b.read_ransac_trace(frame, k)
+    tr = b.read_ransac_trace(frame)
+    assert tr.shape == (trials, k + 3)
     _, recs = oransac.ransac(pts, trials, k=k, rng=random.Random(seed))
     for t, rec in enumerate(recs[: len(tr)]):
         got = list(tr[t, :k])
@@ -178,15 +179,19 @@ def test_batch_degenerate_frame_gives_up(svb):
         _check(b.read_ransac(1), *ref, what="good frame")
 
 
-def test_pipeline_with_frame_planes(svb):
+@pytest.mark.parametrize("mode", ["tiled", "resident"])
+@pytest.mark.parametrize("step", [2, 1])
+def test_pipeline_with_frame_planes(svb, mode, step):
     """stereovision.py:84-113 per frame on the device: RANSAC's plane of each
     frame drives that frame's threshold / histogram / compaction. Each frame's
     output equals the oracle chain run with that frame's plane; a frame with
-    no plane keeps nothing (the reference's plane step raises)."""
+    no plane keeps nothing (the reference's plane step raises). Both kernel
+    families (the frame-resident one reads each frame's plane from memory)."""
     m = carmask()
     frames = 4
     sparse = _sparse_frame(300, 9)   # 300 points: fewer than 600 -> no plane
-    with svb.Batch(frames, H=H, W=W, step=2, with_bgr=True, with_points=True) as b:
+    with svb.Batch(frames, H=H, W=W, step=step, with_bgr=True, with_points=True) as b:
+        b.pipeline_mode(mode)
         b.synth(30)
         _, bgr3 = oracle.synth_frame(33)
         b.upload(3, sparse, bgr3)
@@ -205,7 +210,7 @@ def test_pipeline_with_frame_planes(svb):
             a, bb, c = res["abc"]
             assert np.array_equal(fp[:3], res["abc"])
             assert fp[3] == np.sqrt(a * a + bb * bb + c * c)       # device sqrt == the reference's math.sqrt
-            ref = oracle.pipeline_frame(disp, bgr, 2, abc=res["abc"])
+            ref = oracle.pipeline_frame(disp, bgr, step, abc=res["abc"])
             xyz, pts = b.read_points(f)
             assert tuple(int(v) for v in counts[f][:3]) == ref["counts"], f
             assert np.array_equal(b.read_hist(f)[:1000], ref["hist"][:1000]), f
