@@ -34,6 +34,7 @@ extern "C" {
 #define SV_E_STATE -4   /* not initialised / wrong object                  */
 #define SV_E_COMM -5    /* RCCL error                                      */
 #define SV_E_DEVICE -6  /* a kernel reported an internal failure (timeout) */
+#define SV_E_RANGE -7   /* input outside the supported value range          */
 
 /* functions.py:15,19,21,22 — focal length (px), baseline (m), image centre. */
 typedef struct { double f, B, cw, ch; } sv_camera;
@@ -139,6 +140,45 @@ int sv_ransac_draw(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld,
 int sv_ransac(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
               int32_t* tri, double* out_abc, double* out_err, uint8_t* out_flag, int* out_trials);
 
+/* ---- disparity stage, host images, synchronous ------ */
+
+/* cv2.StereoSGBM_create(minDisparity, numDisparities, blockSize, P1, P2,
+ * disp12MaxDiff, preFilterCap, uniquenessRatio) — functions.py:26 creates it
+ * as (0, 128, 21) with the other fields 0. OpenCV's substitutions for zero
+ * fields are applied (P1 -> 2, P2 -> max(5, P1 + 1), preFilterCap ->
+ * max(cap, 15) | 1, disp12MaxDiff -> 1, uniquenessRatio < 0 -> 10); mode is
+ * MODE_SGBM, speckleWindowSize 0. Supported: min_disp 0, num_disp 128, odd
+ * block <= 63, 128 + block/2 < W <= 2048. */
+typedef struct {
+    int min_disp, num_disp, block, P1, P2, disp12_max_diff, prefilter_cap, uniqueness;
+} sv_sgbm_params;
+
+/* cv2.LUT(image, table) of gammaChange (functions.py:61-67): out[i] = lut[in[i]]
+ * over n bytes (any channel count; the table is built by the caller, as the
+ * reference builds it in numpy). */
+int sv_lut_u8(const uint8_t* in, int64_t n, const uint8_t* lut, uint8_t* out);
+/* One image of greyscale (functions.py:89-97): cv2.cvtColor(BGR2GRAY)
+ * (fixed point, (B*1868 + G*9617 + R*4899 + 2^13) >> 14) then
+ * cv2.equalizeHist. bgr: H x W x 3 contiguous. */
+int sv_grey_equalize(const uint8_t* bgr, int H, int W, uint8_t* out);
+/* stereoProcessor.compute(grayL, grayR) (functions.py:108): H x W int16
+ * disparity x16, -16 where invalid. SV_E_RANGE when a path cost leaves int16
+ * (block cost sums above 32,763; OpenCV's int16 buffers would truncate). */
+int sv_sgbm_compute(const uint8_t* L, const uint8_t* R, int H, int W, const sv_sgbm_params* prm, int16_t* out);
+/* cv2.filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) on int16, in place
+ * (functions.py:111): 4-connected regions of pixels != newVal joined where
+ * neighbours differ by <= maxDiff; regions of <= maxSpeckleSize pixels are set
+ * to newVal. */
+int sv_filter_speckles(int16_t* img, int H, int W, int new_val, int max_size, int max_diff);
+/* functions.py:104-128 disparity(grayL, grayR, max_disparity, crop_disparity):
+ * SGBM -> filterSpeckles(0, 4000, max_disparity - 5) -> threshold TOZERO at 0
+ * -> (d / 16.).astype(uint8) -> crop [0:390, 135:W] when crop != 0 ->
+ * (x * (256. / max_disparity)).astype(uint8). out: rows x cols u8 with rows =
+ * crop ? min(390, H) : H, cols = crop ? W - 135 : W. raw16 / filt16 (nullable,
+ * H x W): the SGBM result before / after filterSpeckles. */
+int sv_disparity(const uint8_t* L, const uint8_t* R, int H, int W, const sv_sgbm_params* prm, int max_disparity,
+                 int crop, uint8_t* out, int16_t* raw16, int16_t* filt16);
+
 /* ---- batched, device-resident API ------------- */
 typedef struct sv_batch sv_batch;
 
@@ -243,10 +283,23 @@ int sv_batch_read_maskpoints(sv_batch* b, int frame, double* xyz, int64_t cap, i
 int sv_batch_ransac_trace(sv_batch* b, int trials);
 int sv_batch_read_ransac_trace(sv_batch* b, int frame, int32_t* out, int64_t cap, int* out_trials, int* out_k);
 
+/* Stereo pairs resident in HBM (frames x H x W grey left / right) and the
+ * batched disparity stage: sv_batch_sgbm runs functions.py:104-128 (no crop)
+ * on every pair and writes the batch's disparity (frames x H x W u8), the
+ * input of the pre-pass, K1 and the pipeline. chunk = frames per cost-volume
+ * chunk (0 = 32; 4 x 125 MB of int16 volumes per 1024 x 544 frame).
+ * Synchronous per chunk (the int16 range flags are read back).
+ * sv_batch_synth_pair: synthetic rectified pairs for global frame ids
+ * first.., generated on the device (row y's true disparity is the synthetic
+ * road's, halved: clamp(floor(3(y - 200) / 10), 0, 127)). */
+int sv_batch_synth_pair(sv_batch* b, int64_t first_frame_id);
+int sv_batch_upload_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t* R);
+int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int chunk);
+
 int sv_batch_sync(sv_batch* b);
-/* ms of the last sv_batch_project / sv_batch_pipeline, from HIP events
- * recorded on the batch stream around the kernels. which: 0 = project,
- * 1 = pipeline. */
+/* ms of the last sv_batch_project / sv_batch_pipeline / sv_batch_sgbm, from
+ * HIP events recorded on the batch stream around the kernels. which: 0 =
+ * project, 1 = pipeline, 2 = sgbm. */
 int sv_batch_last_ms(sv_batch* b, int which, float* ms);
 /* Sum of the per-launch durations (HIP events on the batch stream around each
  * K1 launch / each pipeline call) since the last reset, and their count.

@@ -1,0 +1,609 @@
+// SGBM disparity stage: functions.py:104-128
+//   StereoSGBM(0, 128, 21).compute -> filterSpeckles(0, 4000, 123) -> TOZERO
+//   -> /16 -> u8 -> optional crop -> x(256/128) -> u8
+// plus the grey front end of functions.py:61-97 (gamma LUT, BGR2GRAY,
+// equalizeHist) and a synthetic rectified-pair generator for the batch.
+//
+// OpenCV computes SGBM as one sequential row loop carrying the path costs of
+// four directions in row buffers. Here every aggregation direction is a set of
+// independent 1-D paths, one wave per path, 128 disparities as 64 lanes x 2:
+//   hsum_kernel     one workgroup per row: BT pixel costs (LDS-staged row
+//                   features) and the 21-wide horizontal box sum -> Hvol
+//   vertical_kernel one wave per column: the vertical box sum (OpenCV's
+//                   update rules, int16 wrap) -> Cvol, and the (0,-1) path -> L2
+//   diag_kernel     one wave per diagonal: the (-1,-1) and (+1,-1) paths -> L1, L3
+//   row_kernel      one wave per row: the (-1,0) path summed with L1..L3
+//                   (P = sat16), then the (+1,0) path, S = sat16(P + L),
+//                   winner, subpixel, disp2 and the left-right check -> int16
+//   cc_* kernels    filterSpeckles as union-find connected components
+//   out_kernel      speckle decision + TOZERO + scaling -> u8 (and int16)
+// Volumes are [frame][y][x][d] int16 (one 256-byte line per cell, lane l
+// holding d = 2l, 2l+1), so every path step is one coalesced 4-byte load or
+// store per lane. Exactness rules: see oracle/sgbm_oracle.c (same semantics).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../svx_device.h"
+#include "../svx_sgbm.h"
+
+namespace svx {
+namespace {
+
+constexpr int kMaxCost = 32767;
+constexpr int kInt16Min = -32768;
+
+__device__ __forceinline__ int lo16(uint32_t v) { return (int)(int16_t)(v & 0xFFFF); }
+__device__ __forceinline__ int hi16(uint32_t v) { return (int)(int16_t)(v >> 16); }
+__device__ __forceinline__ uint32_t pack16(int a, int b) { return (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)b << 16); }
+__device__ __forceinline__ int sat16(int v) { return v < kInt16Min ? kInt16Min : (v > kMaxCost ? kMaxCost : v); }
+__device__ __forceinline__ bool out16(int v) { return v < kInt16Min || v > kMaxCost; }
+// Lane hand-offs through LDS inside one wave: the hardware keeps a wave's LDS
+// operations in order; this keeps the compiler from moving loads above them.
+__device__ __forceinline__ void wave_lds_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// min over the wave (signed), every lane active: inclusive DPP min-scan, lane 63.
+__device__ __forceinline__ int wave_min_i32(int v) {
+    v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// One step of a path (OpenCV formula 13): lane l holds d0 = 2l, d1 = 2l + 1.
+// p0/p1: the predecessor's stored (int16) L; pmin: its stored min. A path
+// start has p0 = p1 = pmin = 0; d = -1 and d = 128 read MAX_COST. Returns the
+// untruncated L values (for the sums) and updates the state with the int16
+// truncations OpenCV stores.
+struct PathState {
+    int p0 = 0, p1 = 0, pmin = 0;
+};
+
+__device__ __forceinline__ void path_step(int c0, int c1, PathState& s, int P1, int P2, int& L0, int& L1,
+                                          bool& ovf) {
+    const int delta = s.pmin + P2;
+    const int left = __builtin_amdgcn_update_dpp(kMaxCost, s.p1, 0x138, 0xf, 0xf, false);   // wave_shr:1, d0 - 1
+    const int right = __builtin_amdgcn_update_dpp(kMaxCost, s.p0, 0x130, 0xf, 0xf, false);  // wave_shl:1, d1 + 1
+    const int m0 = min(min(s.p0, delta), min(left, s.p1) + P1);
+    const int m1 = min(min(s.p1, delta), min(s.p0, right) + P1);
+    L0 = c0 + m0 - delta;
+    L1 = c1 + m1 - delta;
+    const int wm = wave_min_i32(min(L0, L1));
+    ovf = ovf || out16(L0) || out16(L1);
+    s.p0 = (int)(int16_t)L0;
+    s.p1 = (int)(int16_t)L1;
+    s.pmin = (int)(int16_t)wm;
+}
+
+// ---------------------------------------------------------------------------
+// Row features: for each image and channel (0: clipped x-derivative, 1: raw
+// intensity) value | half-neighbour min << 8 | max << 16 (calcPixelCostBT).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bt_pair(uint32_t fu, uint32_t fv) {
+    const int u = fu & 0xFF, u0 = (fu >> 8) & 0xFF, u1 = fu >> 16;
+    const int v = fv & 0xFF, v0 = (fv >> 8) & 0xFF, v1 = fv >> 16;
+    const int c0 = max(max(0, u - v1), v0 - u);
+    const int c1 = max(max(0, v - u1), u0 - v);
+    return (uint32_t)min(c0, c1);
+}
+
+__global__ __launch_bounds__(256) void sgbm_hsum_kernel(SgbmK k, const uint8_t* __restrict__ left,
+                                                          const uint8_t* __restrict__ right, uint32_t* __restrict__ hvol,
+                                                          int frames) {
+    extern __shared__ uint32_t smem[];
+    const int W = k.W, H = k.H;
+    const int f = blockIdx.x / H, y = blockIdx.x - f * H;
+    if (f >= frames) return;
+    uint32_t* feat = smem;                                   // [img][ch][W]
+    uint8_t* tmp = reinterpret_cast<uint8_t*>(smem + 4 * W);  // [img][ch][W] values
+    uint32_t* ring = smem + 5 * W;                           // per wave: RS x 64
+    const int tid = threadIdx.x;
+    const int yu = y > 0 ? y - 1 : y, yd = y < H - 1 ? y + 1 : y;
+    for (int i = tid; i < 2 * W; i += blockDim.x) {
+        const int img = i >= W, x = i - img * W;
+        const uint8_t* src = (img ? right : left) + (size_t)f * k.frame_px;
+        int pv = k.ftzero, rv = k.ftzero;
+        if (x > 0 && x < W - 1) {
+            const uint8_t* r = src + (size_t)y * W;
+            const uint8_t* u = src + (size_t)yu * W;
+            const uint8_t* d = src + (size_t)yd * W;
+            const int g = (r[x + 1] - r[x - 1]) * 2 + u[x + 1] - u[x - 1] + d[x + 1] - d[x - 1];
+            pv = min(max(g, -k.ftzero), k.ftzero) + k.ftzero;
+            rv = r[x];
+        }
+        tmp[(img * 2 + 0) * W + x] = (uint8_t)pv;
+        tmp[(img * 2 + 1) * W + x] = (uint8_t)rv;
+    }
+    __syncthreads();
+    for (int i = tid; i < 4 * W; i += blockDim.x) {
+        const int row = i / W, x = i - row * W;
+        const uint8_t* v = tmp + row * W;
+        const int c = v[x];
+        const int l = x > 0 ? (c + v[x - 1]) >> 1 : c;
+        const int r = x < W - 1 ? (c + v[x + 1]) >> 1 : c;
+        feat[i] = (uint32_t)c | (uint32_t)min(min(l, r), c) << 8 | (uint32_t)max(max(l, r), c) << 16;
+    }
+    __syncthreads();
+
+    const int lane = lane_id(), wave = tid >> 6, nwaves = blockDim.x >> 6;
+    const int RS = 2 * k.SW2 + 1;
+    uint32_t* myring = ring + wave * RS * 64 + lane;
+    const int seg = (k.width1 + nwaves - 1) / nwaves;
+    const int xs = wave * seg, xe = min(k.width1, xs + seg);
+    if (xs >= xe) return;
+    const uint32_t* fLp = feat;
+    const uint32_t* fLr = feat + W;
+    const uint32_t* fRp = feat + 2 * W;
+    const uint32_t* fRr = feat + 3 * W;
+    const int d0 = 2 * lane;
+    // pixel cost pair (d0, d0 + 1) at cost column j (image column j + D)
+    auto pix = [&](int j) -> uint32_t {
+        j = min(max(j, 0), k.width1 - 1);
+        const int x = j + kSgD;
+        const uint32_t lp = fLp[x], lr = fLr[x];
+        const int xr0 = x - d0, xr1 = xr0 - 1;
+        const uint32_t a = bt_pair(lp, fRp[xr0]) + (bt_pair(lr, fRr[xr0]) >> 2);
+        const uint32_t b = bt_pair(lp, fRp[xr1]) + (bt_pair(lr, fRr[xr1]) >> 2);
+        return a | b << 16;
+    };
+    uint32_t sum = 0;
+    for (int j = xs - k.SW2, s = 0; j <= xs + k.SW2; ++j, ++s) {
+        const uint32_t v = pix(j);
+        myring[s * 64] = v;
+        sum += v;
+    }
+    uint32_t* out = hvol + ((size_t)f * H + y) * k.width1 * 64 + lane;
+    int slot = 0;   // ring slot of column xi - SW2
+    for (int xi = xs; xi < xe; ++xi) {
+        out[(size_t)xi * 64] = sum;
+        const uint32_t vn = pix(xi + 1 + k.SW2);
+        const uint32_t vo = myring[slot * 64];
+        myring[slot * 64] = vn;
+        sum = (sum + vn) - vo;   // both halves stay >= 0: no borrow between them
+        slot = slot + 1 == RS ? 0 : slot + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Vertical box sum with OpenCV's row rules, and the (0,-1) path.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint32_t* __restrict__ hvol,
+                                                              uint32_t* __restrict__ cvol, uint32_t* __restrict__ l2vol,
+                                                              uint32_t* __restrict__ flags, int frames) {
+    const int wpb = blockDim.x >> 6;
+    const int cols_blocks = (k.width1 + wpb - 1) / wpb;
+    const int f = blockIdx.x / cols_blocks;
+    const int xi = (blockIdx.x - f * cols_blocks) * wpb + (threadIdx.x >> 6);
+    if (f >= frames || xi >= k.width1) return;
+    const int lane = lane_id(), H = k.H;
+    const size_t rs = (size_t)k.width1 * 64;
+    const size_t base = (size_t)f * H * rs + (size_t)xi * 64 + lane;
+    const uint32_t* hb = hvol + base;
+    int c0 = 0, c1 = 0;
+    for (int kk = 0; kk <= k.SH2; ++kk) {
+        const uint32_t h = hb[(size_t)min(kk, H - 1) * rs];
+        const int sc = kk == 0 ? k.SH2 + 1 : 1;
+        c0 += lo16(h) * sc;
+        c1 += hi16(h) * sc;
+    }
+    PathState st;
+    bool ovf = false;
+    const bool upd_col = xi > 0;
+    for (int y = 0; y < H; ++y) {
+        if (y > 0 && upd_col && y + k.SH2 < H) {
+            const uint32_t a = hb[(size_t)(y + k.SH2) * rs];
+            const uint32_t s = hb[(size_t)max(y - k.SH2 - 1, 0) * rs];
+            c0 += lo16(a) - lo16(s);
+            c1 += hi16(a) - hi16(s);
+        }
+        const int cw0 = (int)(int16_t)c0, cw1 = (int)(int16_t)c1;
+        cvol[base + (size_t)y * rs] = pack16(cw0, cw1);
+        int L0, L1;
+        path_step(cw0, cw1, st, k.P1, k.P2, L0, L1, ovf);
+        l2vol[base + (size_t)y * rs] = pack16(L0, L1);
+    }
+    if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// Diagonal paths: dir 1 from (x-1, y-1), dir 3 from (x+1, y-1).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t* __restrict__ cvol,
+                                                          uint32_t* __restrict__ l1vol, uint32_t* __restrict__ l3vol,
+                                                          uint32_t* __restrict__ flags, int frames) {
+    const int wpb = blockDim.x >> 6;
+    const int npaths = k.width1 + k.H - 1;   // per direction
+    const int per_frame = 2 * npaths;
+    const int gw = blockIdx.x * wpb + (threadIdx.x >> 6);
+    const int f = gw / per_frame;
+    if (f >= frames) return;
+    int p = gw - f * per_frame;
+    const int dir = p >= npaths;   // 0: from x-1 (L1), 1: from x+1 (L3)
+    p -= dir * npaths;
+    int xi, y;
+    if (p < k.width1) {
+        xi = p;
+        y = 0;
+    } else {
+        xi = dir ? k.width1 - 1 : 0;
+        y = p - k.width1 + 1;
+    }
+    const int dx = dir ? -1 : 1;
+    const int lane = lane_id();
+    const size_t rs = (size_t)k.width1 * 64;
+    const size_t fb = (size_t)f * k.H * rs + lane;
+    uint32_t* out = dir ? l3vol : l1vol;
+    PathState st;
+    bool ovf = false;
+    uint32_t c = 0;
+    if (xi >= 0 && xi < k.width1 && y < k.H) c = cvol[fb + (size_t)y * rs + (size_t)xi * 64];
+    while (xi >= 0 && xi < k.width1 && y < k.H) {
+        const int nx = xi + dx, ny = y + 1;
+        uint32_t cn = 0;
+        if (nx >= 0 && nx < k.width1 && ny < k.H) cn = cvol[fb + (size_t)ny * rs + (size_t)nx * 64];
+        int L0, L1;
+        path_step(lo16(c), hi16(c), st, k.P1, k.P2, L0, L1, ovf);
+        out[fb + (size_t)y * rs + (size_t)xi * 64] = pack16(L0, L1);
+        c = cn;
+        xi = nx;
+        y = ny;
+    }
+    if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// Row kernel: (-1,0) path + sum, (+1,0) path + selection, left-right check.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* __restrict__ cvol,
+                                                         uint32_t* __restrict__ l1p, const uint32_t* __restrict__ l2vol,
+                                                         const uint32_t* __restrict__ l3vol, int16_t* __restrict__ d16,
+                                                         uint32_t* __restrict__ flags, int frames) {
+    extern __shared__ int16_t rsm[];
+    const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
+    const int gw = blockIdx.x * wpb + wave;
+    const int f = gw / k.H, y = gw - f * k.H;
+    if (f >= frames) return;
+    const int W = k.W, lane = lane_id();
+    int16_t* disp1 = rsm + wave * 3 * W;
+    int16_t* disp2 = disp1 + W;
+    int16_t* d2cost = disp2 + W;
+    const int INVALID = -kSgScale;   // (minD - 1) * 16, minD = 0
+    for (int x = lane; x < W; x += 64) {
+        disp1[x] = (int16_t)INVALID;
+        disp2[x] = (int16_t)INVALID;
+        d2cost[x] = (int16_t)kMaxCost;
+    }
+    wave_lds_sync();
+    const size_t rs = (size_t)k.width1 * 64;
+    const size_t rb = ((size_t)f * k.H + y) * rs + lane;
+    bool ovf = false;
+    // pass A: x ascending, direction (-1, 0); P = sat16(L0 + L1 + L2 + L3) replaces L1
+    {
+        PathState st;
+        for (int xi = 0; xi < k.width1; ++xi) {
+            const size_t o = rb + (size_t)xi * 64;
+            const uint32_t c = cvol[o], a = l1p[o], b = l2vol[o], e = l3vol[o];
+            int L0, L1;
+            path_step(lo16(c), hi16(c), st, k.P1, k.P2, L0, L1, ovf);
+            l1p[o] = pack16(sat16(L0 + lo16(a) + lo16(b) + lo16(e)), sat16(L1 + hi16(a) + hi16(b) + hi16(e)));
+        }
+    }
+    // pass B: x descending, direction (+1, 0), S = sat16(P + L), winner per pixel
+    {
+        PathState st;
+        const int d0 = 2 * lane;
+        for (int xi = k.width1 - 1; xi >= 0; --xi) {
+            const size_t o = rb + (size_t)xi * 64;
+            const uint32_t c = cvol[o], pp = l1p[o];
+            int L0, L1;
+            path_step(lo16(c), hi16(c), st, k.P1, k.P2, L0, L1, ovf);
+            const int S0 = sat16(lo16(pp) + L0), S1 = sat16(hi16(pp) + L1);
+            const int key = min(((S0 + 32768) << 7) | d0, ((S1 + 32768) << 7) | (d0 + 1));
+            const int kmin = wave_min_i32(key);
+            const int minS = (kmin >> 7) - 32768, best = kmin & 127;
+            if (k.uniq > 0) {
+                const bool bad = (S0 * (100 - k.uniq) < minS * 100 && abs(best - d0) > 1) ||
+                                 (S1 * (100 - k.uniq) < minS * 100 && abs(best - d0 - 1) > 1);
+                if (__any(bad)) continue;
+            }
+            if (minS == kMaxCost) {
+                // every S saturated: OpenCV's strict "<" never fires, bestDisp stays -1 and the
+                // pixel gets (-1) * 16 = INVALID; disp2 is not touched (its cost test is strict too)
+                continue;
+            }
+            const uint32_t spk = pack16(S0, S1);
+            int dd = best * kSgScale;
+            if (best > 0 && best < kSgD - 1) {
+                const uint32_t wm = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best - 1) >> 1);
+                const uint32_t wp = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best + 1) >> 1);
+                const int Sm = (best - 1) & 1 ? hi16(wm) : lo16(wm);
+                const int Sp = (best + 1) & 1 ? hi16(wp) : lo16(wp);
+                const int den = max(Sm + Sp - 2 * minS, 1);
+                dd = best * kSgScale + ((Sm - Sp) * kSgScale + den) / (den * 2);
+            }
+            if (lane == 0) {
+                const int x2 = xi + k.minX1 - best;
+                if (d2cost[x2] > minS) {
+                    d2cost[x2] = (int16_t)minS;
+                    disp2[x2] = (int16_t)best;
+                }
+                disp1[xi + k.minX1] = (int16_t)dd;
+            }
+        }
+    }
+    wave_lds_sync();   // lane 0's LDS writes before the check reads them
+    // left-right check -> the int16 result row
+    int16_t* orow = d16 + (size_t)f * k.frame_px + (size_t)y * W;
+    for (int x = lane; x < W; x += 64) {
+        int v = disp1[x];
+        if (v != INVALID) {
+            const int _d = v >> 4, d_ = (v + kSgScale - 1) >> 4;
+            const int _x = x - _d, x_ = x - d_;
+            if (0 <= _x && _x < W && disp2[_x] >= 0 && abs(disp2[_x] - _d) > k.d12 && 0 <= x_ && x_ < W &&
+                disp2[x_] >= 0 && abs(disp2[x_] - d_) > k.d12)
+                v = INVALID;
+        }
+        orow[x] = (int16_t)v;
+    }
+    if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// filterSpeckles: 4-connected components of pixels != newVal joined where
+// |difference| <= maxDiff (union-find, hooking the larger root under the
+// smaller), component sizes, then the speckle decision.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int cc_find(int32_t* par, int x) {
+    int p = __atomic_load_n(par + x, __ATOMIC_RELAXED);
+    while (p != x) {
+        const int gp = __atomic_load_n(par + p, __ATOMIC_RELAXED);
+        if (gp != p) __atomic_store_n(par + x, gp, __ATOMIC_RELAXED);   // path halving
+        x = p;
+        p = gp;
+    }
+    return x;
+}
+
+// Read-only find for the counting pass: that pass stores every pixel's root
+// into par[p], and a halving write from another thread's find could replace
+// such a root with a mere ancestor after it was stored.
+__device__ __forceinline__ int cc_root(const int32_t* par, int x) {
+    int p = __atomic_load_n(par + x, __ATOMIC_RELAXED);
+    while (p != x) {
+        x = p;
+        p = __atomic_load_n(par + x, __ATOMIC_RELAXED);
+    }
+    return x;
+}
+
+__device__ __forceinline__ void cc_unite(int32_t* par, int a, int b) {
+    a = cc_find(par, a);
+    b = cc_find(par, b);
+    while (a != b) {
+        if (a > b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        const int old = atomicCAS(par + b, b, a);
+        if (old == b) break;
+        b = old;   // b was hooked meanwhile: climb from its new parent
+        a = cc_find(par, a);
+        b = cc_find(par, b);
+    }
+}
+
+// parent[p] = p (frame-local index)
+__global__ __launch_bounds__(256) void sgbm_cc_init_kernel(int32_t* __restrict__ parent, int64_t n, int64_t px) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) parent[i] = (int32_t)(i % px);
+}
+
+__global__ __launch_bounds__(256) void sgbm_cc_union_kernel(SgbmK k, const int16_t* __restrict__ d16,
+                                                              int32_t* __restrict__ parent, int frames) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t f = i / k.frame_px;
+    if (f >= frames) return;
+    const int p = (int)(i - f * k.frame_px);
+    const int16_t* d = d16 + f * k.frame_px;
+    int32_t* par = parent + f * k.frame_px;
+    const int v = d[p];
+    if (v == k.new_val) return;
+    const int y = p / k.W, x = p - y * k.W;
+    if (x + 1 < k.W) {
+        const int q = d[p + 1];
+        if (q != k.new_val && abs(v - q) <= k.max_diff) cc_unite(par, p, p + 1);
+    }
+    if (y + 1 < k.H) {
+        const int q = d[p + k.W];
+        if (q != k.new_val && abs(v - q) <= k.max_diff) cc_unite(par, p, p + k.W);
+    }
+}
+
+__global__ __launch_bounds__(256) void sgbm_cc_count_kernel(SgbmK k, const int16_t* __restrict__ d16,
+                                                              int32_t* __restrict__ parent, int32_t* __restrict__ size,
+                                                              int frames) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t f = i / k.frame_px;
+    const bool in = f < frames;
+    int root = -1;
+    int32_t* par = parent + (in ? f : 0) * k.frame_px;
+    if (in) {
+        const int p = (int)(i - f * k.frame_px);
+        if (d16[f * k.frame_px + p] != k.new_val) {
+            root = cc_root(par, p);
+            __atomic_store_n(par + p, root, __ATOMIC_RELAXED);
+        }
+    }
+    // one atomic for the lanes sharing the first active lane's (frame, root)
+    const int64_t key = root < 0 ? -1 : f * k.frame_px + root;
+    const int64_t k0 = __shfl(key, __builtin_ctzll(__ballot(key >= 0) | (1ull << 63)));
+    const bool same = key >= 0 && key == k0;
+    const uint64_t m = __ballot(same);
+    if (same) {
+        if ((int)__builtin_ctzll(m) == lane_id()) atomicAdd(size + k0, (int)__builtin_popcountll(m));
+    } else if (key >= 0) {
+        atomicAdd(size + key, 1);
+    }
+}
+
+__global__ __launch_bounds__(256) void sgbm_out_kernel(SgbmK k, const int16_t* __restrict__ d16,
+                                                         const int32_t* __restrict__ parent,
+                                                         const int32_t* __restrict__ size, uint8_t* __restrict__ out,
+                                                         int16_t* __restrict__ filt, int frames) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t f = i / k.frame_px;
+    if (f >= frames) return;
+    const int p = (int)(i - f * k.frame_px);
+    int v = d16[f * k.frame_px + p];
+    if (v != k.new_val && size[f * k.frame_px + parent[f * k.frame_px + p]] <= k.max_size) v = k.new_val;
+    if (filt) filt[f * k.frame_px + p] = (int16_t)v;
+    const int y = p / k.W, x = p - y * k.W;
+    const int oy = y, ox = x - k.out_c0;
+    if (oy >= k.out_rows || ox < 0 || ox >= k.out_cols) return;
+    const int q = v > 0 ? v >> 4 : 0;   // TOZERO, then (d / 16.).astype(uint8)
+    out[f * (int64_t)k.out_rows * k.out_cols + (int64_t)oy * k.out_cols + ox] = (uint8_t)(int)((double)q * k.scale);
+}
+
+// ---------------------------------------------------------------------------
+// Front end: cv2.LUT, BGR2GRAY + equalizeHist, synthetic pairs.
+// ---------------------------------------------------------------------------
+__global__ void lut_kernel(const uint8_t* __restrict__ in, int64_t n, const uint8_t* __restrict__ lut,
+                           uint8_t* __restrict__ out) {
+    __shared__ uint8_t t[256];
+    if (threadIdx.x < 256) t[threadIdx.x] = lut[threadIdx.x];
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = t[in[i]];
+}
+
+__global__ __launch_bounds__(256) void grey_hist_kernel(const uint8_t* __restrict__ bgr, int64_t px, int frames,
+                                                          uint8_t* __restrict__ grey, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t per = (px + gridDim.x - 1) / gridDim.x;   // gridDim.x blocks per frame in y
+    const int f = blockIdx.y;
+    const int64_t p0 = blockIdx.x * per, p1 = min(px, p0 + per);
+    const uint8_t* src = bgr + (size_t)f * px * 3;
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        const uint8_t* c = src + 3 * p;
+        const int g = (c[0] * 1868 + c[1] * 9617 + c[2] * 4899 + (1 << 13)) >> 14;
+        grey[(size_t)f * px + p] = (uint8_t)g;
+        atomicAdd(&h[g], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(hist + f * 256 + threadIdx.x, h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void equalize_kernel(uint8_t* __restrict__ grey, int64_t px,
+                                                         const uint32_t* __restrict__ hist) {
+    __shared__ uint8_t lut[256];
+    const int f = blockIdx.y;
+    const uint32_t* h = hist + f * 256;
+    if (threadIdx.x == 0) {
+        int i = 0;
+        while (i < 255 && !h[i]) ++i;
+        if ((int64_t)h[i] == px) {
+            for (int j = 0; j < 256; ++j) lut[j] = (uint8_t)i;   // a constant image keeps its value
+        } else {
+            const float scale = 255.f / (float)(px - (int64_t)h[i]);
+            int64_t sum = 0;
+            lut[i] = 0;
+            for (int j = i + 1; j < 256; ++j) {
+                sum += h[j];
+                const float v = __fmul_rn((float)sum, scale);
+                const int r = (int)rintf(v);
+                lut[j] = (uint8_t)(r < 0 ? 0 : r > 255 ? 255 : r);
+            }
+            for (int j = 0; j < i; ++j) lut[j] = 0;
+        }
+    }
+    __syncthreads();
+    uint8_t* g = grey + (size_t)f * px;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < px; p += (int64_t)gridDim.x * blockDim.x)
+        g[p] = lut[g[p]];
+}
+
+__global__ void synth_pair_kernel(uint8_t* __restrict__ left, uint8_t* __restrict__ right, int H, int W, int frames,
+                                  int64_t first) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t px = (int64_t)H * W;
+    const int64_t f = i / px;
+    if (f >= frames) return;
+    const int p = (int)(i - f * px);
+    const int y = p / W, x = p - y * W;
+    const int D = sgbm_pair_disparity(y);
+    left[i] = sgbm_pair_texture(first + f, H, y, x);
+    right[i] = sgbm_pair_texture(first + f, H, y, x + D);
+}
+
+}  // namespace
+
+bool sgbm_supported(const SgbmK& k) {
+    return k.width1 > k.SW2 && k.W <= 2048 && k.H >= 1 && k.SW2 >= 0 && k.SW2 <= 31;
+}
+
+size_t sgbm_volume_bytes(const SgbmK& k) { return (size_t)k.H * k.width1 * kSgD * sizeof(int16_t); }
+
+hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_t* right, int frames,
+                               const SgbmScratch& s, hipStream_t st) {
+    const int H = k.H;
+    hipError_t e = hipMemsetAsync(s.flags, 0, sizeof(uint32_t) * frames, st);
+    if (e != hipSuccess) return e;
+    // hsum: features (4 W words) + byte values (W words) + 4 waves' rings
+    const size_t lds1 = sizeof(uint32_t) * (5 * (size_t)k.W + 4 * (2 * k.SW2 + 1) * 64);
+    hipLaunchKernelGGL(sgbm_hsum_kernel, dim3(frames * H), dim3(256), lds1, st, k, left, right, s.hl1, frames);
+    const int cb = (k.width1 + 3) / 4;
+    hipLaunchKernelGGL(sgbm_vertical_kernel, dim3(frames * cb), dim3(256), 0, st, k, s.hl1, s.c, s.l2, s.flags, frames);
+    const int paths = 2 * (k.width1 + H - 1) * frames;
+    hipLaunchKernelGGL(sgbm_diag_kernel, dim3((paths + 3) / 4), dim3(256), 0, st, k, s.c, s.hl1, s.l3, s.flags,
+                       frames);
+    const size_t lds4 = sizeof(int16_t) * 3 * (size_t)k.W * 4;
+    hipLaunchKernelGGL(sgbm_row_kernel, dim3((frames * H + 3) / 4), dim3(256), lds4, st, k, s.c, s.hl1, s.l2, s.l3,
+                       s.d16, s.flags, frames);
+    return hipGetLastError();
+}
+
+hipError_t launch_speckle_scale(const SgbmK& k, int frames, const SgbmScratch& s, uint8_t* out, int16_t* filt,
+                                hipStream_t st) {
+    const int64_t n = (int64_t)frames * k.frame_px;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(sgbm_cc_init_kernel, dim3(g), dim3(256), 0, st, s.parent, n, k.frame_px);
+    hipLaunchKernelGGL(sgbm_cc_union_kernel, dim3(g), dim3(256), 0, st, k, s.d16, s.parent, frames);
+    hipError_t e = hipMemsetAsync(s.size, 0, sizeof(int32_t) * n, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(sgbm_cc_count_kernel, dim3(g), dim3(256), 0, st, k, s.d16, s.parent, s.size, frames);
+    hipLaunchKernelGGL(sgbm_out_kernel, dim3(g), dim3(256), 0, st, k, s.d16, s.parent, s.size, out, filt, frames);
+    return hipGetLastError();
+}
+
+hipError_t launch_lut(const uint8_t* in, int64_t n, const uint8_t* lut, uint8_t* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((n + 1023) / 1024, 8192);
+    hipLaunchKernelGGL(lut_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, n, lut, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_grey_equalize(const uint8_t* bgr, int64_t px, int frames, uint8_t* grey, uint32_t* hist,
+                                hipStream_t s) {
+    hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * 256 * frames, s);
+    if (e != hipSuccess) return e;
+    const unsigned bx = (unsigned)std::min<int64_t>((px + 4095) / 4096, 256);
+    hipLaunchKernelGGL(grey_hist_kernel, dim3(bx, frames), dim3(256), 0, s, bgr, px, frames, grey, hist);
+    hipLaunchKernelGGL(equalize_kernel, dim3(bx, frames), dim3(256), 0, s, grey, px, hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_pair(uint8_t* left, uint8_t* right, int H, int W, int frames, int64_t first, hipStream_t s) {
+    const int64_t n = (int64_t)frames * H * W;
+    hipLaunchKernelGGL(synth_pair_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, left, right, H, W,
+                       frames, first);
+    return hipGetLastError();
+}
+
+}  // namespace svx

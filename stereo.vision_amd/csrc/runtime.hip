@@ -15,6 +15,7 @@
 
 #include "../../include/svx.h"
 #include "svx_launch.h"
+#include "svx_sgbm.h"
 
 using namespace svx;
 
@@ -63,6 +64,35 @@ struct DevBuf {
     T* as() const { return static_cast<T*>(p); }
 };
 
+// SGBM scratch for a chunk of frames (kernels/sgbm.hip): four int16 cost
+// volumes, the int16 disparity, union-find parents / sizes, overflow flags.
+struct SgbmBufs {
+    DevBuf vol[4], d16, par, size, flags;
+    int frames = 0;
+    hipError_t ensure(const SgbmK& k, int n) {
+        const size_t vb = sgbm_volume_bytes(k) * n, px = (size_t)k.frame_px * n;
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < 4 && e == hipSuccess; ++i) e = vol[i].ensure(vb);
+        if (e == hipSuccess) e = d16.ensure(px * sizeof(int16_t));
+        if (e == hipSuccess) e = par.ensure(px * sizeof(int32_t));
+        if (e == hipSuccess) e = size.ensure(px * sizeof(int32_t));
+        if (e == hipSuccess) e = flags.ensure(sizeof(uint32_t) * n);
+        if (e == hipSuccess) frames = n;
+        return e;
+    }
+    SgbmScratch scratch() const {
+        return SgbmScratch{vol[0].as<uint32_t>(), vol[1].as<uint32_t>(), vol[2].as<uint32_t>(), vol[3].as<uint32_t>(),
+                           d16.as<int16_t>(), par.as<int32_t>(), size.as<int32_t>(), flags.as<uint32_t>()};
+    }
+    void release() {
+        for (DevBuf* x : {&vol[0], &vol[1], &vol[2], &vol[3], &d16, &par, &size, &flags}) {
+            if (x->p) (void)hipFree(x->p);
+            x->p = nullptr;
+            x->bytes = 0;
+        }
+    }
+};
+
 struct Tables {
     bool valid = false;
     int H = 0, W = 0;
@@ -76,6 +106,8 @@ struct Device {
     std::mutex mu;
     // drop-in scratch
     DevBuf disp, bgr, xyz, rgb, ctrl, xy, aux, aux2;
+    DevBuf sg_l, sg_r, sg_out, sg_filt, sg_hist;   // host-frame SGBM / grey drop-ins
+    SgbmBufs sg;
     Tables tables;
     sv_batch* frame_batch = nullptr;  // cached 1-frame batch for sv_pipeline_frame
 };
@@ -196,6 +228,8 @@ struct sv_batch {
     DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
     DevBuf fplanes;             // per-frame keep1 plane fields (FramePlane) for sv_batch_pipeline_planes
     DevBuf dplane;              // the FramePlane of a device plane (sv_batch_pipeline_dev)
+    DevBuf pairL, pairR;        // rectified grey stereo pairs (frames x H x W each), SGBM input
+    SgbmBufs sg;                // SGBM scratch for one chunk of frames
     int64_t mcap = 0;
     int trace_trials = 0, trace_k = 0, traced_trials = 0;   // requested; k and trials of the recorded trace
     bool have_mask = false;
@@ -204,16 +238,16 @@ struct sv_batch {
     int64_t* counts = nullptr;
     uint32_t* err = nullptr;
     size_t ctrl_bytes = 0;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    float last_ms[2] = {0, 0};
-    bool have_ms[2] = {false, false};
+    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    float last_ms[3] = {0, 0, 0};
+    bool have_ms[3] = {false, false, false};
     int qpl = 1;               // K1 quads per lane (1, 2 or 4)
     int nontemporal = 1;       // K1 store flavour (non-temporal: measured faster)
     int pipe_mode = 0;         // 0 auto, 1 tiled (pipeline.hip), 2 frame-resident (resident.hip, both
                                // passes prefetch the next chunk), 3 same without prefetch, 4 pass-2 prefetch only
     // per-launch timing accumulator: event pairs recorded on the batch stream
     std::vector<hipEvent_t> pool;
-    std::vector<std::pair<int, int>> pending[2];  // (start idx, end idx) per op kind
+    std::vector<std::pair<int, int>> pending[3];  // (start idx, end idx) per op kind: project, pipeline, sgbm
     size_t pool_next = 0;
     hipError_t timed_event(int* idx) {
         if (pool_next == pool.size()) {
@@ -381,7 +415,7 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking);
-    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
+    for (int i = 0; i < 6 && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
     if (e != hipSuccess) {
         sv_batch_destroy(b);
         return fail(SV_E_HIP, "sv_batch_create: %s", hipGetErrorString(e));
@@ -395,8 +429,10 @@ int sv_batch_destroy(sv_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks,
-                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane})
+                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane,
+                      &b->pairL, &b->pairR})
         if (x->p) (void)hipFree(x->p);
+    b->sg.release();
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : b->pool) (void)hipEventDestroy(ev);
@@ -635,7 +671,7 @@ int sv_batch_sync(sv_batch* b) {
 }
 
 int sv_batch_last_ms(sv_batch* b, int which, float* ms) {
-    if (!b || !ms || which < 0 || which > 1) return fail(SV_E_ARG, "bad args");
+    if (!b || !ms || which < 0 || which > 2) return fail(SV_E_ARG, "bad args");
     if (!b->have_ms[which]) return fail(SV_E_STATE, "no timing recorded");
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipEventSynchronize(b->ev[2 * which + 1]));
@@ -644,7 +680,7 @@ int sv_batch_last_ms(sv_batch* b, int which, float* ms) {
 }
 
 int sv_batch_timing(sv_batch* b, int which, double* total_ms, int64_t* count) {
-    if (!b || which < 0 || which > 1 || !total_ms || !count) return fail(SV_E_ARG, "bad args");
+    if (!b || which < 0 || which > 2 || !total_ms || !count) return fail(SV_E_ARG, "bad args");
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
     double tot = 0;
@@ -662,8 +698,7 @@ int sv_batch_timing_reset(sv_batch* b) {
     if (!b) return fail(SV_E_ARG, "null");
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
-    b->pending[0].clear();
-    b->pending[1].clear();
+    for (auto& p : b->pending) p.clear();
     b->pool_next = 0;
     return SV_OK;
 }
@@ -1323,6 +1358,233 @@ int sv_synth_frame(int device, int64_t frame_id, int H, int W, uint8_t* disp, ui
     (void)hipFree(bd.p);
     (void)hipFree(bc.p);
     HIP_TRY(e);
+    return SV_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// disparity stage (functions.py:61-128)
+// ---------------------------------------------------------------------------
+namespace {
+// StereoSGBM parameters with OpenCV's substitutions for zero / negative values
+// (computeDisparitySGBM): P1 -> 2, P2 -> max(5, P1 + 1), preFilterCap ->
+// max(cap, 15) | 1, uniquenessRatio < 0 -> 10, disp12MaxDiff <= 0 -> 1.
+int make_sgbm(int H, int W, const sv_sgbm_params* prm, int max_disparity, int crop, SgbmK* k) {
+    if (!prm) return fail(SV_E_ARG, "null sgbm params");
+    if (prm->min_disp != 0) return fail(SV_E_ARG, "minDisparity must be 0 (got %d)", prm->min_disp);
+    if (prm->num_disp != kSgD) return fail(SV_E_ARG, "numDisparities must be %d (got %d)", kSgD, prm->num_disp);
+    const int SW = prm->block > 0 ? prm->block : 5;
+    if (SW % 2 == 0 || SW > 63) return fail(SV_E_ARG, "blockSize must be odd and <= 63 (got %d)", SW);
+    if (max_disparity < 1) return fail(SV_E_ARG, "max_disparity must be >= 1");
+    std::memset(k, 0, sizeof *k);
+    k->H = H;
+    k->W = W;
+    k->minX1 = kSgD;
+    k->width1 = W - kSgD;
+    k->SW2 = k->SH2 = SW / 2;
+    k->P1 = prm->P1 > 0 ? prm->P1 : 2;
+    k->P2 = std::max(prm->P2 > 0 ? prm->P2 : 5, k->P1 + 1);
+    k->ftzero = std::max(prm->prefilter_cap, 15) | 1;
+    k->uniq = prm->uniqueness >= 0 ? prm->uniqueness : 10;
+    k->d12 = prm->disp12_max_diff > 0 ? prm->disp12_max_diff : 1;
+    k->frame_px = (int64_t)H * W;
+    // functions.py:111 filterSpeckles(disparity, 0, 4000, max_disparity - 5)
+    k->new_val = 0;
+    k->max_size = 4000;
+    k->max_diff = max_disparity - 5;
+    k->out_rows = crop ? std::min(390, H) : H;
+    k->out_cols = crop ? std::max(W - 135, 0) : W;
+    k->out_c0 = crop ? 135 : 0;
+    k->scale = 256. / max_disparity;
+    if (H < 1 || W <= kSgD || !sgbm_supported(*k))
+        return fail(SV_E_ARG, "SGBM needs 1 <= H, %d + blockSize/2 < W <= 2048 (H=%d W=%d)", kSgD, H, W);
+    return SV_OK;
+}
+
+int sgbm_check_flags(const SgbmBufs& sg, int n, hipStream_t s) {
+    std::vector<uint32_t> fl(n);
+    HIP_TRY(hipMemcpyAsync(fl.data(), sg.flags.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int i = 0; i < n; ++i)
+        if (fl[i])
+            return fail(SV_E_RANGE, "SGBM frame %d: a path cost left the int16 range (block cost sums above "
+                                    "32,763: unsupported)", i);
+    return SV_OK;
+}
+
+// upload a grey pair (or take the device's copies) and run StereoSGBM.compute into d->sg.d16
+int sgbm_frame(Device* d, const uint8_t* L, const uint8_t* R, const SgbmK& k) {
+    const size_t px = (size_t)k.frame_px;
+    hipStream_t s = d->stream;
+    HIP_TRY(d->sg_l.ensure(px));
+    HIP_TRY(d->sg_r.ensure(px));
+    HIP_TRY(d->sg.ensure(k, 1));
+    HIP_TRY(hipMemcpyAsync(d->sg_l.p, L, px, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d->sg_r.p, R, px, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_sgbm_compute(k, d->sg_l.as<uint8_t>(), d->sg_r.as<uint8_t>(), 1, d->sg.scratch(), s));
+    return sgbm_check_flags(d->sg, 1, s);
+}
+}  // namespace
+
+int sv_lut_u8(const uint8_t* in, int64_t n, const uint8_t* lut, uint8_t* out) {
+    if (n < 0 || (n > 0 && (!in || !out)) || !lut) return fail(SV_E_ARG, "sv_lut_u8: bad arguments");
+    if (n == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    HIP_TRY(d->sg_l.ensure((size_t)n));
+    HIP_TRY(d->sg_hist.ensure(256));
+    HIP_TRY(hipMemcpyAsync(d->sg_l.p, in, (size_t)n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d->sg_hist.p, lut, 256, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_lut(d->sg_l.as<uint8_t>(), n, d->sg_hist.as<uint8_t>(), d->sg_l.as<uint8_t>(), s));
+    HIP_TRY(hipMemcpyAsync(out, d->sg_l.p, (size_t)n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SV_OK;
+}
+
+int sv_grey_equalize(const uint8_t* bgr, int H, int W, uint8_t* out) {
+    if (!bgr || !out || H < 0 || W < 0) return fail(SV_E_ARG, "sv_grey_equalize: bad arguments");
+    const int64_t px = (int64_t)H * W;
+    if (px == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    HIP_TRY(d->sg_l.ensure((size_t)px * 3));
+    HIP_TRY(d->sg_r.ensure((size_t)px));
+    HIP_TRY(d->sg_hist.ensure(sizeof(uint32_t) * 256));
+    HIP_TRY(hipMemcpyAsync(d->sg_l.p, bgr, (size_t)px * 3, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_grey_equalize(d->sg_l.as<uint8_t>(), px, 1, d->sg_r.as<uint8_t>(), d->sg_hist.as<uint32_t>(), s));
+    HIP_TRY(hipMemcpyAsync(out, d->sg_r.p, (size_t)px, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SV_OK;
+}
+
+int sv_sgbm_compute(const uint8_t* L, const uint8_t* R, int H, int W, const sv_sgbm_params* prm, int16_t* out) {
+    if (!L || !R || !out) return fail(SV_E_ARG, "sv_sgbm_compute: null buffer");
+    SgbmK k;
+    if (int rc = make_sgbm(H, W, prm, kSgD, 0, &k)) return rc;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    if (int rc = sgbm_frame(d, L, R, k)) return rc;
+    HIP_TRY(hipMemcpyAsync(out, d->sg.d16.p, sizeof(int16_t) * k.frame_px, hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    return SV_OK;
+}
+
+int sv_filter_speckles(int16_t* img, int H, int W, int new_val, int max_size, int max_diff) {
+    if (!img || H < 0 || W < 0) return fail(SV_E_ARG, "sv_filter_speckles: bad arguments");
+    const int64_t px = (int64_t)H * W;
+    if (px == 0) return SV_OK;
+    if (px > INT32_MAX) return fail(SV_E_ARG, "sv_filter_speckles: image too large");
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    SgbmK k;
+    std::memset(&k, 0, sizeof k);
+    k.H = H;
+    k.W = W;
+    k.frame_px = px;
+    k.new_val = new_val;
+    k.max_size = max_size;
+    k.max_diff = max_diff;
+    k.out_rows = 0;   // no scaled output
+    k.scale = 1;
+    HIP_TRY(d->sg.d16.ensure(sizeof(int16_t) * px));
+    HIP_TRY(d->sg.par.ensure(sizeof(int32_t) * px));
+    HIP_TRY(d->sg.size.ensure(sizeof(int32_t) * px));
+    HIP_TRY(d->sg_filt.ensure(sizeof(int16_t) * px));
+    HIP_TRY(hipMemcpyAsync(d->sg.d16.p, img, sizeof(int16_t) * px, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_speckle_scale(k, 1, d->sg.scratch(), nullptr, d->sg_filt.as<int16_t>(), s));
+    HIP_TRY(hipMemcpyAsync(img, d->sg_filt.p, sizeof(int16_t) * px, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SV_OK;
+}
+
+int sv_disparity(const uint8_t* L, const uint8_t* R, int H, int W, const sv_sgbm_params* prm, int max_disparity,
+                 int crop, uint8_t* out, int16_t* raw16, int16_t* filt16) {
+    if (!L || !R || !out) return fail(SV_E_ARG, "sv_disparity: null buffer");
+    SgbmK k;
+    if (int rc = make_sgbm(H, W, prm, max_disparity, crop, &k)) return rc;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    if (int rc = sgbm_frame(d, L, R, k)) return rc;
+    if (raw16) HIP_TRY(hipMemcpyAsync(raw16, d->sg.d16.p, sizeof(int16_t) * k.frame_px, hipMemcpyDeviceToHost, s));
+    const size_t ob = (size_t)k.out_rows * k.out_cols;
+    HIP_TRY(d->sg_out.ensure(ob ? ob : 1));
+    if (filt16) HIP_TRY(d->sg_filt.ensure(sizeof(int16_t) * k.frame_px));
+    HIP_TRY(launch_speckle_scale(k, 1, d->sg.scratch(), d->sg_out.as<uint8_t>(),
+                                 filt16 ? d->sg_filt.as<int16_t>() : nullptr, s));
+    if (ob) HIP_TRY(hipMemcpyAsync(out, d->sg_out.p, ob, hipMemcpyDeviceToHost, s));
+    if (filt16) HIP_TRY(hipMemcpyAsync(filt16, d->sg_filt.p, sizeof(int16_t) * k.frame_px, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SV_OK;
+}
+
+int sv_batch_synth_pair(sv_batch* b, int64_t first_frame_id) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    if (b->W + kSgD > 4096) return fail(SV_E_ARG, "synthetic pairs need W <= %d", 4096 - kSgD);
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t px = (size_t)b->H * b->W * b->frames;
+    HIP_TRY(b->pairL.ensure(px));
+    HIP_TRY(b->pairR.ensure(px));
+    HIP_TRY(launch_synth_pair(b->pairL.as<uint8_t>(), b->pairR.as<uint8_t>(), b->H, b->W, b->frames, first_frame_id,
+                              b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_upload_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t* R) {
+    if (!b || !L || !R || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "sv_batch_upload_pair: bad args");
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t px = (size_t)b->H * b->W;
+    HIP_TRY(b->pairL.ensure(px * b->frames));
+    HIP_TRY(b->pairR.ensure(px * b->frames));
+    HIP_TRY(hipMemcpyAsync(b->pairL.as<uint8_t>() + px * frame, L, px, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemcpyAsync(b->pairR.as<uint8_t>() + px * frame, R, px, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int chunk) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    if (!b->pairL.p || !b->pairR.p) return fail(SV_E_STATE, "no stereo pairs (sv_batch_synth_pair / upload_pair)");
+    SgbmK k;
+    if (int rc = make_sgbm(b->H, b->W, prm, max_disparity, 0, &k)) return rc;
+    HIP_TRY(hipSetDevice(b->device));
+    if (chunk <= 0) chunk = 32;
+    chunk = std::min(chunk, b->frames);
+    HIP_TRY(b->sg.ensure(k, chunk));
+    const size_t px = (size_t)k.frame_px;
+    int t0, t1;
+    HIP_TRY(hipEventRecord(b->ev[4], b->stream));
+    HIP_TRY(b->timed_event(&t0));
+    for (int f0 = 0; f0 < b->frames; f0 += chunk) {
+        const int n = std::min(chunk, b->frames - f0);
+        HIP_TRY(launch_sgbm_compute(k, b->pairL.as<uint8_t>() + px * f0, b->pairR.as<uint8_t>() + px * f0, n,
+                                    b->sg.scratch(), b->stream));
+        HIP_TRY(launch_speckle_scale(k, n, b->sg.scratch(), b->disp.as<uint8_t>() + px * f0, nullptr, b->stream));
+        if (int rc = sgbm_check_flags(b->sg, n, b->stream)) return rc;
+    }
+    HIP_TRY(b->timed_event(&t1));
+    HIP_TRY(hipEventRecord(b->ev[5], b->stream));
+    b->pending[2].push_back({t0, t1});
+    b->have_ms[2] = true;
     return SV_OK;
 }
 

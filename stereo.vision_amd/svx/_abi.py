@@ -77,6 +77,14 @@ SIGNATURES = {
     "sv_batch_pipeline_planes": [P, ctypes.POINTER(Camera), D, I, I, I],
     "sv_batch_pipeline_dev": [P, ctypes.POINTER(Camera), P, D, I, I, I],
     "sv_batch_read_frame_plane": [P, I, P],
+    "sv_lut_u8": [P, I64, P, P],
+    "sv_grey_equalize": [P, I, I, P],
+    "sv_sgbm_compute": [P, P, I, I, P, P],
+    "sv_filter_speckles": [P, I, I, I, I, I],
+    "sv_disparity": [P, P, I, I, P, I, I, P, P, P],
+    "sv_batch_synth_pair": [P, I64],
+    "sv_batch_upload_pair": [P, I, P, P],
+    "sv_batch_sgbm": [P, P, I, I],
     "sv_batch_sync": [P],
     "sv_batch_last_ms": [P, I, PF],
     "sv_batch_timing": [P, I, ctypes.POINTER(D), PI64],

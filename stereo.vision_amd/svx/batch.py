@@ -21,6 +21,9 @@ def synthetic_plane(f=DEFAULT_CAMERA[0], B=DEFAULT_CAMERA[1], ch=DEFAULT_CAMERA[
     return (0.0, k / B, -k * (horizon - ch) / (f * B))
 
 
+_WHICH = {"project": 0, "pipeline": 1, "sgbm": 2}
+
+
 class Batch:
     """`frames` x H x W disparity (+BGR) frames resident on one GPU."""
 
@@ -130,17 +133,34 @@ class Batch:
     def sync(self):
         _abi.call("sv_batch_sync", self._h)
 
+    # -- disparity stage (functions.py:104-128) ------------------------------------
+    def synth_pair(self, first_frame_id=0):
+        """Synthetic rectified grey pairs for global frame ids first.. (device)."""
+        _abi.call("sv_batch_synth_pair", self._h, int(first_frame_id))
+
+    def upload_pair(self, frame, left, right):
+        L = np.ascontiguousarray(left, np.uint8)
+        R = np.ascontiguousarray(right, np.uint8)
+        if L.shape != (self.H, self.W) or R.shape != (self.H, self.W):
+            raise ValueError(f"pair must be {self.H}x{self.W}")
+        _abi.call("sv_batch_upload_pair", self._h, frame, _abi.ptr(L), _abi.ptr(R))
+
+    def sgbm(self, max_disparity=128, chunk=0, **params):
+        """functions.disparity (no crop) of every pair -> the batch's disparity."""
+        from .disparity import sgbm_params
+        prm = sgbm_params(**params)
+        _abi.call("sv_batch_sgbm", self._h, ctypes.byref(prm), int(max_disparity), int(chunk))
+
     def last_ms(self, which="project"):
         ms = ctypes.c_float(0)
-        _abi.call("sv_batch_last_ms", self._h, 0 if which == "project" else 1, ctypes.byref(ms))
+        _abi.call("sv_batch_last_ms", self._h, _WHICH[which], ctypes.byref(ms))
         return float(ms.value)
 
     def timing(self, which="project"):
         """(total_ms, launches) of the per-launch event timings since reset_timing()."""
         tot = ctypes.c_double(0)
         cnt = ctypes.c_int64(0)
-        _abi.call("sv_batch_timing", self._h, 0 if which == "project" else 1, ctypes.byref(tot),
-                  ctypes.byref(cnt))
+        _abi.call("sv_batch_timing", self._h, _WHICH[which], ctypes.byref(tot), ctypes.byref(cnt))
         return float(tot.value), int(cnt.value)
 
     def reset_timing(self):

@@ -29,6 +29,9 @@ reference:
   ``calculateColourHistogram``, ``filterPointsByHistogram`` (functions.py:
   212-230, :300-323): see svx/stages.py — one device call each, same return
   types, dict order and errors as the reference.
+* disparity stage (functions.py:61-128): ``gammaChange``, ``preProcessImages``,
+  ``greyscale`` and ``disparity`` (StereoSGBM + filterSpeckles + scaling) —
+  see svx/disparity.py.
 * disparity pre-pass (functions.py:141-172): ``fillDisparity`` (new array, or
   the input itself when there is no previous frame), ``fillAltDisparity`` (in
   place, returns its argument), ``maskDisparity`` (new array; the mask is the
@@ -224,10 +227,12 @@ project_3D_points_to_2D = project3DPointsTo2DImagePoints
 from .ransac import RANSAC  # noqa: E402  (functions.py:278-298)
 from .stages import (calculateColourHistogram, calculatePointErrors, computePlanarThreshold,  # noqa: E402,F401
                      filterPointsByHistogram)
+from .disparity import disparity, gammaChange, greyscale, preProcessImages  # noqa: E402,F401 (functions.py:61-128)
 
 PATCHED = ("projectDisparityTo3d", "project3DPointsTo2DImagePoints", "fillDisparity", "fillAltDisparity",
            "maskDisparity", "capDisparity", "generatePointsAsImage", "RANSAC", "calculatePointErrors",
-           "computePlanarThreshold", "calculateColourHistogram", "filterPointsByHistogram")
+           "computePlanarThreshold", "calculateColourHistogram", "filterPointsByHistogram", "gammaChange",
+           "preProcessImages", "greyscale", "disparity")
 ALIASES = {"project_disparity_to_3d": "projectDisparityTo3d",
            "project_3D_points_to_2D": "project3DPointsTo2DImagePoints"}
 _saved = {}

@@ -1,0 +1,172 @@
+"""Disparity stage on the GPU (functions.py:61-128) against
+the oracle (oracle/sgbm_oracle.c, bit-exact: every output is integer) and the
+reference-run fixtures of tests/golden/sgbm.json.
+
+PARITY UNPINNED for the OpenCV calls themselves (StereoSGBM, filterSpeckles,
+cvtColor, equalizeHist): cv2 is absent, so the oracle restates OpenCV's
+published algorithm (tests/test_sgbm_cv2.py pins it wherever cv2 imports).
+"""
+import json
+import os
+import types
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN
+from oracle import sgbm as osg
+
+pytestmark = pytest.mark.gpu
+META = json.load(open(os.path.join(GOLDEN, "sgbm.json")))
+
+
+@pytest.fixture(scope="module")
+def sv():
+    import svx
+    from svx import batch, disparity, dropin
+    assert svx.device_count() >= 1
+    return types.SimpleNamespace(svx=svx, batch=batch, disp=disparity, dropin=dropin)
+
+
+def test_gamma_lut_matches_reference_tables(sv):
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, (61, 77, 3), dtype=np.uint8)
+    for g, table in META["gamma"].items():
+        assert np.array_equal(sv.disp.gammaChange(img, float(g)), np.asarray(table, np.uint8)[img])
+    a, b = sv.disp.preProcessImages(img, img[::-1])
+    t14 = np.asarray(META["gamma"]["1.4"], np.uint8)
+    assert np.array_equal(a, t14[img]) and np.array_equal(b, t14[img[::-1]])
+
+
+def test_grey_equalize_matches_oracle(sv):
+    rng = np.random.default_rng(1)
+    _, bgr0 = oracle.synth_frame(0)
+    cases = [bgr0, rng.integers(0, 256, (37, 53, 3), dtype=np.uint8),
+             rng.integers(100, 104, (544, 1024, 3), dtype=np.uint8), np.full((9, 5, 3), 77, np.uint8),
+             np.zeros((1, 1, 3), np.uint8)]
+    for bgr in cases:
+        assert np.array_equal(sv.disp.grey_equalize(bgr), osg.grey_equalize(bgr)), bgr.shape
+    gl, gr = sv.disp.greyscale(bgr0, bgr0[:, ::-1])
+    assert np.array_equal(gl, osg.grey_equalize(bgr0)) and np.array_equal(gr, osg.grey_equalize(bgr0[:, ::-1]))
+
+
+SMALL = [(96, 320, "pair"), (3, 139, "rand"), (5, 256, "rand"), (21, 200, "rand"), (64, 512, "pair"),
+         (33, 300, "rand")]
+
+
+def _pair(H, W, kind, seed):
+    if kind == "pair":
+        return osg.synth_pair(seed, H, W)
+    rng = np.random.default_rng(seed)
+    return (rng.integers(0, 256, (H, W), dtype=np.uint8), rng.integers(0, 256, (H, W), dtype=np.uint8))
+
+
+@pytest.mark.parametrize("H,W,kind", SMALL)
+def test_sgbm_compute_small(sv, H, W, kind):
+    L, R = _pair(H, W, kind, H + W)
+    assert np.array_equal(sv.disp.sgbm_compute(L, R), osg.sgbm(L, R))
+
+
+@pytest.mark.parametrize("kw", [dict(block=5), dict(block=9, P1=8, P2=32), dict(uniqueness=10),
+                                dict(disp12_max_diff=3, prefilter_cap=31), dict(block=1), dict(block=35)])
+def test_sgbm_parameters(sv, kw):
+    L, R = osg.synth_pair(7, 80, 400)
+    L = L.copy()
+    L[20:40, 200:260] = 90   # a textureless patch: ambiguous matches, uniqueness and LR rejections
+    prm = sv.disp.sgbm_params(**kw)
+    assert np.array_equal(sv.disp.sgbm_compute(L, R, prm), osg.sgbm(L, R, **kw)), kw
+
+
+def test_sgbm_full_frame_whole_stage(sv):
+    L, R = osg.synth_pair(0)
+    out, raw, filt = sv.disp.stereo_disparity(L, R, 128, False, with_raw=True)
+    ro, rr, rf = osg.disparity(L, R, with_raw=True)
+    assert np.array_equal(raw, rr)
+    assert np.array_equal(filt, rf)
+    assert np.array_equal(out, ro)
+    assert (raw != filt).sum() > 0            # speckles were removed
+    crop = sv.disp.disparity(L, R, 128, True)
+    assert crop.shape == (390, 889) and np.array_equal(crop, osg.scale(rf, 128, True))
+    rec = META["scaled"]["pair0"]
+    assert oracle.digest(filt) == rec["in"] and oracle.digest(out) == rec["md128_crop0"]["digest"]
+    assert oracle.digest(crop) == rec["md128_crop1"]["digest"]
+
+
+def test_filter_speckles_matches_oracle(sv):
+    rng = np.random.default_rng(3)
+    for H, W in [(1, 1), (7, 3), (40, 57), (544, 1024)]:
+        img = (rng.integers(-2, 6, (H, W)) * rng.integers(1, 40)).astype(np.int16)
+        for nv, ms, md in ((0, 5, 30), (0, 4000, 123), (-16, 12, 0)):
+            got = img.copy()
+            ret, _ = sv.disp.filterSpeckles(got, nv, ms, md)
+            assert ret is got
+            assert np.array_equal(got, osg.filter_speckles(img, nv, ms, md)), (H, W, nv, ms, md)
+
+
+def test_int16_cost_wrap_and_range(sv):
+    """A flat black left image against a white right one: every BT cost is 63,
+    so a 23 x 23 block sums to 33,327 and the int16 C wraps (as in OpenCV's
+    CostType buffers): the GPU reproduces the wrap. With P2 = 1000 a path
+    start's L = C - P2 leaves int16: SV_E_RANGE instead of a silent mismatch."""
+    L = np.zeros((40, 300), np.uint8)
+    R = np.full((40, 300), 255, np.uint8)
+    prm = sv.disp.sgbm_params(block=23)
+    assert np.array_equal(sv.disp.sgbm_compute(L, R, prm), osg.sgbm(L, R, block=23))
+    with pytest.raises(sv.svx.SvxError, match="int16"):
+        sv.disp.sgbm_compute(L, R, sv.disp.sgbm_params(block=23, P2=1000))
+
+
+def test_sgbm_rejects_unsupported(sv):
+    z = np.zeros((10, 300), np.uint8)
+    for kw in (dict(num_disp=64), dict(min_disp=1), dict(block=4)):
+        with pytest.raises(sv.svx.SvxError):
+            sv.disp.sgbm_compute(z, z, sv.disp.sgbm_params(**kw))
+    with pytest.raises(sv.svx.SvxError):
+        sv.disp.sgbm_compute(np.zeros((10, 128), np.uint8), np.zeros((10, 128), np.uint8))
+    with pytest.raises(ValueError):
+        sv.disp.sgbm_compute(z, z[:, :200])
+
+
+def test_batch_sgbm_matches_oracle(sv):
+    H, W, n, first = 544, 1024, 5, 11
+    with sv.batch.Batch(n, H, W, step=1, with_bgr=False) as b:
+        b.synth_pair(first)
+        b.sgbm(chunk=2)                       # 3 chunks, the last partial
+        for f in range(n):
+            L, R = osg.synth_pair(first + f, H, W)
+            assert np.array_equal(b.read_disp(f), osg.disparity(L, R)), f
+        ms, cnt = b.timing("sgbm")
+        assert cnt == 1 and ms > 0
+        rng = np.random.default_rng(9)
+        L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+        R = np.roll(L, -20, axis=1)
+        b.upload_pair(3, L, R)
+        b.sgbm()
+        assert np.array_equal(b.read_disp(3), osg.disparity(L, R))
+
+
+def test_dropin_installed_module(sv):
+    """functions.disparity / greyscale / preProcessImages patched into a module
+    object; a stereoProcessor with OpenCV's getters is honoured."""
+    mod = types.SimpleNamespace(camera_focal_length_px=399.9745178222656, stereo_camera_baseline_m=0.2090607502,
+                                image_centre_w=474.5, image_centre_h=262.0)
+    sv.dropin.install(mod)
+    try:
+        L, R = osg.synth_pair(2, 128, 384)
+        assert np.array_equal(mod.disparity(L, R, 128, False), osg.disparity(L, R))
+
+        class Proc:
+            def __getattr__(self, name):
+                vals = dict(getMinDisparity=0, getNumDisparities=128, getBlockSize=7, getP1=4, getP2=40,
+                            getDisp12MaxDiff=2, getPreFilterCap=20, getUniquenessRatio=5, getSpeckleWindowSize=0,
+                            getMode=0)
+                return lambda: vals[name]
+        mod.stereoProcessor = Proc()
+        exp = osg.scale(osg.filter_speckles(osg.sgbm(L, R, block=7, P1=4, P2=40, disp12_max_diff=2, prefilter_cap=20,
+                                                     uniqueness=5)), 128, False)
+        assert np.array_equal(mod.disparity(L, R, 128, False), exp)
+        gl, gr = mod.greyscale(*mod.preProcessImages(np.dstack([L] * 3), np.dstack([R] * 3)))
+        assert gl.shape == L.shape and gl.dtype == np.uint8
+    finally:
+        sv.dropin.uninstall()
