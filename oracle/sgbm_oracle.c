@@ -194,8 +194,11 @@ int svo_sgbm(const uint8_t* img1, const uint8_t* img2, int H, int W, const svo_s
         LrBuf[k] = calloc((width1 + 2) * lrcell, sizeof(cost_t));
         minLrBuf[k] = calloc((size_t)(width1 + 2) * NR2, sizeof(cost_t));
     }
-    int16_t* disp2 = malloc(sizeof(int16_t) * W);
-    int* disp2cost = malloc(sizeof(int) * W);
+    /* one slot of slack: with every S saturated bestDisp stays -1 and x2 = x + minX1 + 1 can be W
+     * (OpenCV reads past its row there too; a short cost can never exceed minS = MAX_COST, so it
+     * never writes) */
+    int16_t* disp2 = malloc(sizeof(int16_t) * (W + 1));
+    cost_t* disp2cost = malloc(sizeof(cost_t) * (W + 1));
     bt_rows t;
     uint8_t* rows = malloc((size_t)W * 12);
     for (int i = 0, k = 0; i < 2; ++i)
@@ -280,8 +283,8 @@ int svo_sgbm(const uint8_t* img1, const uint8_t* img2, int H, int W, const svo_s
         }
 
         /* ---- final loop: direction (+1, 0), selection, disp2 ---- */
-        for (int x = 0; x < W; ++x) {
-            d1row[x] = (int16_t)INVALID;
+        for (int x = 0; x <= W; ++x) {
+            if (x < W) d1row[x] = (int16_t)INVALID;
             disp2[x] = (int16_t)INVALID;
             disp2cost[x] = MAX_COST;
         }
@@ -312,7 +315,7 @@ int svo_sgbm(const uint8_t* img1, const uint8_t* img2, int H, int W, const svo_s
             d = bestDisp;
             int x2 = x + minX1 - d - minD;
             if (disp2cost[x2] > minS) {
-                disp2cost[x2] = minS;
+                disp2cost[x2] = (cost_t)minS;
                 disp2[x2] = (int16_t)(d + minD);
             }
             if (0 < d && d < D - 1) {

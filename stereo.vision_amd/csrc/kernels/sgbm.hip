@@ -397,58 +397,110 @@ __device__ __forceinline__ void cc_unite(int32_t* par, int a, int b) {
     }
 }
 
-// parent[p] = p (frame-local index)
-__global__ __launch_bounds__(256) void sgbm_cc_init_kernel(int32_t* __restrict__ parent, int64_t n, int64_t px) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) parent[i] = (int32_t)(i % px);
+// Row runs: maximal horizontal runs of pixels != newVal whose neighbours differ
+// by <= maxDiff. A run never needs a union inside it: every pixel's parent is
+// its run's first pixel (one wave per row, a segmented max-scan of run starts).
+__device__ __forceinline__ bool cc_link(int a, int b, const SgbmK& k) {
+    return a != k.new_val && b != k.new_val && abs(a - b) <= k.max_diff;
 }
 
+// run start of lane's pixel x (x < W) given carry = start of the previous chunk's last pixel
+__device__ __forceinline__ int cc_run_start(bool start, int x, int carry) {
+    int v = start ? x + 1 : 0;   // 0 = "no start here"
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
+    return v > 0 ? v - 1 : carry;
+}
+
+__global__ __launch_bounds__(256) void sgbm_cc_rows_kernel(SgbmK k, const int16_t* __restrict__ d16,
+                                                             int32_t* __restrict__ parent, int frames) {
+    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int f = gw / k.H, y = gw - f * k.H;
+    if (f >= frames) return;
+    const int lane = lane_id(), W = k.W;
+    const int16_t* d = d16 + (size_t)f * k.frame_px + (size_t)y * W;
+    int32_t* par = parent + (size_t)f * k.frame_px + (size_t)y * W;
+    int carry = 0;
+    for (int x0 = 0; x0 < W; x0 += 64) {
+        const int x = x0 + lane;
+        const bool in = x < W;
+        const int v = in ? d[x] : k.new_val;
+        const int vl = in && x > 0 ? d[x - 1] : k.new_val;
+        const int s = cc_run_start(in && !(x > 0 && cc_link(v, vl, k)), x, carry);
+        if (in) par[x] = y * W + s;
+        carry = __builtin_amdgcn_readlane(s, 63);
+    }
+}
+
+// Vertical unions: pixel p with its lower neighbour q, skipped when p-1 / q-1
+// are in the same runs as p / q and linked themselves (that union covered it).
 __global__ __launch_bounds__(256) void sgbm_cc_union_kernel(SgbmK k, const int16_t* __restrict__ d16,
                                                               int32_t* __restrict__ parent, int frames) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t f = i / k.frame_px;
     if (f >= frames) return;
     const int p = (int)(i - f * k.frame_px);
-    const int16_t* d = d16 + f * k.frame_px;
-    int32_t* par = parent + f * k.frame_px;
-    const int v = d[p];
-    if (v == k.new_val) return;
     const int y = p / k.W, x = p - y * k.W;
-    if (x + 1 < k.W) {
-        const int q = d[p + 1];
-        if (q != k.new_val && abs(v - q) <= k.max_diff) cc_unite(par, p, p + 1);
+    if (y + 1 >= k.H) return;
+    const int16_t* d = d16 + f * k.frame_px;
+    const int v = d[p], w = d[p + k.W];
+    if (!cc_link(v, w, k)) return;
+    if (x > 0) {
+        const int vl = d[p - 1], wl = d[p + k.W - 1];
+        if (cc_link(v, vl, k) && cc_link(w, wl, k) && cc_link(vl, wl, k)) return;
     }
-    if (y + 1 < k.H) {
-        const int q = d[p + k.W];
-        if (q != k.new_val && abs(v - q) <= k.max_diff) cc_unite(par, p, p + k.W);
-    }
+    cc_unite(parent + f * k.frame_px, p, p + k.W);
 }
 
+// Component sizes: one wave per row; each run adds its length at its root,
+// lanes sharing the wave's running root are summed first (large regions touch
+// one address once per row, not once per run).
 __global__ __launch_bounds__(256) void sgbm_cc_count_kernel(SgbmK k, const int16_t* __restrict__ d16,
-                                                              int32_t* __restrict__ parent, int32_t* __restrict__ size,
-                                                              int frames) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t f = i / k.frame_px;
-    const bool in = f < frames;
-    int root = -1;
-    int32_t* par = parent + (in ? f : 0) * k.frame_px;
-    if (in) {
-        const int p = (int)(i - f * k.frame_px);
-        if (d16[f * k.frame_px + p] != k.new_val) {
-            root = cc_root(par, p);
-            __atomic_store_n(par + p, root, __ATOMIC_RELAXED);
+                                                              const int32_t* __restrict__ parent,
+                                                              int32_t* __restrict__ size, int frames) {
+    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int f = gw / k.H, y = gw - f * k.H;
+    if (f >= frames) return;
+    const int lane = lane_id(), W = k.W;
+    const int16_t* d = d16 + (size_t)f * k.frame_px + (size_t)y * W;
+    const int32_t* par = parent + (size_t)f * k.frame_px;
+    int32_t* sz = size + (size_t)f * k.frame_px;
+    int carry = 0, acc_root = -1, acc = 0;
+    for (int x0 = 0; x0 < W; x0 += 64) {
+        const int x = x0 + lane;
+        const bool in = x < W;
+        const int v = in ? d[x] : k.new_val;
+        const int vl = in && x > 0 ? d[x - 1] : k.new_val;
+        const int vr = x + 1 < W ? d[x + 1] : k.new_val;
+        const int s = cc_run_start(in && !(x > 0 && cc_link(v, vl, k)), x, carry);
+        carry = __builtin_amdgcn_readlane(s, 63);
+        const bool end = in && v != k.new_val && !cc_link(v, vr, k);
+        const int root = end ? cc_root(par, y * W + s) : -1;
+        const int len = x - s + 1;
+        const bool mine = end && root == acc_root;
+        int add = mine ? len : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o, 64);
+        acc += add;
+        const uint64_t rest = __ballot(end && !mine);
+        if (rest) {
+            // the first remaining run's root becomes the running root (flush the old one)
+            const int r1 = __shfl(root, (int)__builtin_ctzll(rest), 64);
+            const bool take = end && !mine && root == r1;
+            int add1 = take ? len : 0;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) add1 += __shfl_xor(add1, o, 64);
+            if (lane == 0 && acc_root >= 0 && acc) atomicAdd(sz + acc_root, acc);
+            acc_root = r1;
+            acc = add1;
+            if (end && !mine && !take) atomicAdd(sz + root, len);
         }
     }
-    // one atomic for the lanes sharing the first active lane's (frame, root)
-    const int64_t key = root < 0 ? -1 : f * k.frame_px + root;
-    const int64_t k0 = __shfl(key, __builtin_ctzll(__ballot(key >= 0) | (1ull << 63)));
-    const bool same = key >= 0 && key == k0;
-    const uint64_t m = __ballot(same);
-    if (same) {
-        if ((int)__builtin_ctzll(m) == lane_id()) atomicAdd(size + k0, (int)__builtin_popcountll(m));
-    } else if (key >= 0) {
-        atomicAdd(size + key, 1);
-    }
+    if (lane == 0 && acc_root >= 0 && acc) atomicAdd(sz + acc_root, acc);
 }
 
 __global__ __launch_bounds__(256) void sgbm_out_kernel(SgbmK k, const int16_t* __restrict__ d16,
@@ -460,8 +512,9 @@ __global__ __launch_bounds__(256) void sgbm_out_kernel(SgbmK k, const int16_t* _
     if (f >= frames) return;
     const int p = (int)(i - f * k.frame_px);
     int v = d16[f * k.frame_px + p];
-    if (v != k.new_val && size[f * k.frame_px + parent[f * k.frame_px + p]] <= k.max_size) v = k.new_val;
+    if (v != k.new_val && size[f * k.frame_px + cc_root(parent + f * k.frame_px, p)] <= k.max_size) v = k.new_val;
     if (filt) filt[f * k.frame_px + p] = (int16_t)v;
+    if (!out) return;
     const int y = p / k.W, x = p - y * k.W;
     const int oy = y, ox = x - k.out_c0;
     if (oy >= k.out_rows || ox < 0 || ox >= k.out_cols) return;
@@ -573,11 +626,12 @@ hipError_t launch_speckle_scale(const SgbmK& k, int frames, const SgbmScratch& s
                                 hipStream_t st) {
     const int64_t n = (int64_t)frames * k.frame_px;
     const unsigned g = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(sgbm_cc_init_kernel, dim3(g), dim3(256), 0, st, s.parent, n, k.frame_px);
+    const unsigned rows = (unsigned)((frames * k.H + 3) / 4);   // one wave per row
+    hipLaunchKernelGGL(sgbm_cc_rows_kernel, dim3(rows), dim3(256), 0, st, k, s.d16, s.parent, frames);
     hipLaunchKernelGGL(sgbm_cc_union_kernel, dim3(g), dim3(256), 0, st, k, s.d16, s.parent, frames);
     hipError_t e = hipMemsetAsync(s.size, 0, sizeof(int32_t) * n, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(sgbm_cc_count_kernel, dim3(g), dim3(256), 0, st, k, s.d16, s.parent, s.size, frames);
+    hipLaunchKernelGGL(sgbm_cc_count_kernel, dim3(rows), dim3(256), 0, st, k, s.d16, s.parent, s.size, frames);
     hipLaunchKernelGGL(sgbm_out_kernel, dim3(g), dim3(256), 0, st, k, s.d16, s.parent, s.size, out, filt, frames);
     return hipGetLastError();
 }
