@@ -26,6 +26,10 @@ Also reported (same JSON line):
                 on the device against tests/golden/frame_digests.npz (the
                 pinned C oracle's per-frame digests, global frame ids).
   latency_1frame_us  configs[1]: one frame, step 1, K1 kernel time.
+  extras        SURVEY §8f components (N = 1): road raster + walk, pre-pass,
+                RANSAC (drop-in and batched), the per-frame-plane pipeline,
+                the drop-in chain, the SGBM disparity stage on 64 resident
+                stereo pairs and the whole device frame loop from the pairs.
   cpu_baseline  configs[0]: the nested-loop CPU port (oracle/cpu_loop.py, the
                 numpy-scalar semantics of functions.py:178-323) on one pinned
                 host core: stereovision.py:84-113 for frame 0 at step 2, per
@@ -342,6 +346,49 @@ def extras(b, args, with_cpu):
     return ex
 
 
+def sgbm_extra(sb, device, with_cpu, frames=64, chunk=32):
+    """§8f rank 4: the disparity stage (functions.py:104-128: StereoSGBM(0,128,21) + filterSpeckles
+    + scaling) on a resident batch of synthetic rectified pairs, frame 0 checked against the C
+    oracle; then the whole per-frame loop from the stereo pair on the device."""
+    from oracle import sgbm as osg
+    out = {}
+    with sb.Batch(frames, H, W, 1, with_bgr=True, with_points=True, device=device) as b:
+        b.synth(0)                 # BGR (the pipeline's colours); the disparity comes from SGBM
+        b.synth_pair(0)
+        b.sgbm(chunk=chunk)
+        b.reset_timing()
+        ms = _timed(b, lambda: b.sgbm(chunk=chunk), 3)
+        k_ms, k_n = b.timing("sgbm")
+        L, R = osg.synth_pair(0)
+        t0 = time.perf_counter()
+        ref = osg.disparity(L, R)
+        cpu_ms = (time.perf_counter() - t0) * 1e3
+        r = {"frames": frames, "chunk": chunk, "ms_per_batch": round(ms, 2),
+             "us_per_frame": round(k_ms / max(k_n, 1) / frames * 1e3, 1),
+             "frame0_matches_oracle": bool(np.array_equal(b.read_disp(0), ref)),
+             "kernels": "sgbm_hsum + sgbm_vertical + sgbm_diag + sgbm_row + cc_rows/union/count + out",
+             "parity": "unpinned vs OpenCV (absent); bit-exact vs oracle/sgbm_oracle.c"}
+        if with_cpu:
+            r["cpu_restatement_ms_per_frame"] = round(cpu_ms, 1)
+            r["cpu_note"] = "oracle/sgbm_oracle.c, 1 thread, scalar C (not OpenCV's SIMD build)"
+        out["sgbm_disparity"] = r
+        b.set_mask(carmask())
+
+        def loop():
+            b.sgbm(chunk=chunk)
+            b.prepass("previous", sync=False)
+            b.ransac(seed_base=0, trials=600, sync=False)
+            b.pipeline_planes(sync=False)
+            b.road_raster(sync=False)
+            b.nonzero(sync=False)
+        ms = _timed(b, loop, 2)
+        out["device_frame_loop_from_pairs"] = {
+            "ms_per_batch": round(ms, 2), "frames": frames, "frames_per_s": round(frames / ms * 1e3, 1),
+            "stages": "SGBM disparity -> prepass(previous+mask) -> maskpoints+RANSAC(600) -> pipeline(per-frame "
+                      "planes) -> road raster -> non-zero walk (stereovision.py:40-136 minus cv2 drawing)"}
+    return out
+
+
 def latency_1frame(sb, first, device):
     """configs[1]: one 1024x544 frame, step 1: K1 kernel time (HIP events), us."""
     with sb.Batch(1, H, W, 1, with_bgr=False, device=device) as one:
@@ -546,6 +593,7 @@ def main(argv=None):
     single = pl["n_gpus"] == 1
     if want_pipe and not args.no_extras and single:   # §8f component timings: the N=1 run only
         out["extras"] = extras(batches[0], args, not args.no_cpu)
+        out["extras"].update(sgbm_extra(sb, shards[0][0], not args.no_cpu))
 
     if pl["rank"] == 0 and single and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

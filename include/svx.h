@@ -71,7 +71,7 @@ int sv_backproject(const double* xyz, int64_t n, int64_t ld, const sv_camera* ca
  * out_counts[3] = N_valid, N_kept, N_kept2; out_hist[1024] = hue-bin counts of
  * the plane-kept points (bin k <-> key str(k/1000)); out_xyz (cap x 3, fp32,
  * NULL ok) and out_pts (cap x 2 int32) hold the N_kept2 surviving points in
- * reference order. Requires W % 8 == 0. */
+ * reference order. Any W >= 2 (rows are staged at a stride rounded up to 8). */
 int sv_pipeline_frame(const uint8_t* disp, const uint8_t* bgr, int H, int W, int step,
                       const sv_camera* cam, const sv_plane* plane, double point_thr, int hist_thr,
                       int64_t* out_counts, uint32_t* out_hist, float* out_xyz, int32_t* out_pts,
@@ -183,7 +183,10 @@ int sv_disparity(const uint8_t* L, const uint8_t* R, int H, int W, const sv_sgbm
 typedef struct sv_batch sv_batch;
 
 /* frames x H x W uint8 disparity (+ frames x H x W x 3 BGR if with_bgr) in
- * HBM. W % 8 == 0. Dense outputs: 3 fp32 planes (X, Y, Z) of
+ * HBM. Any W >= 2: rows are stored at a stride of round_up(W, 8) bytes (the
+ * pad columns lie outside every grid; uploads and read-backs use W), so the
+ * 390 x 889 frames of crop_disparity=True (functions.py:122-124) run fused;
+ * sv_batch_synth / the batched SGBM need W % 8 == 0. Dense outputs: 3 fp32 planes (X, Y, Z) of
  * frames x Hg x pitch, pitch = round_up(Wg, 4); Z == 0 marks d == 0 / pad. */
 int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr,
                     int with_points, sv_batch** out);

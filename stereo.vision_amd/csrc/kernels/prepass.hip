@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void fill_prev_kernel(const uint32_t* raw, uin
 
 // One wave per row of W bytes (W % 4 == 0); rows = frames * H.
 __global__ __launch_bounds__(256) void fill_mean_kernel(uint8_t* disp, uint8_t* masked, const uint8_t* __restrict__ mask,
-                                                        int64_t rows, int H, int W) {
+                                                        int64_t rows, int H, int W, int Wrow) {
     const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);
     if (row >= rows) return;
     const int lane = lane_id();
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void fill_mean_kernel(uint8_t* disp, uint8_t* 
         const uint32_t v = rp[w];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t b = (v >> (8 * k)) & 0xFF;
+            const uint32_t b = 4 * w + k < Wrow ? (v >> (8 * k)) & 0xFF : 0u;   // stride padding: not the row's
             sum += b;
             cnt += b != 0;
         }
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void fill_mean_kernel(uint8_t* disp, uint8_t* 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t b = (v >> (8 * k)) & 0xFF;
-            o |= (b < 2 ? mean : b) << (8 * k);
+            o |= (b < 2 && 4 * w + k < Wrow ? mean : b) << (8 * k);
         }
         rp[w] = o;
         if (mp) mp[w] = o & kp[w];
@@ -130,12 +130,12 @@ hipError_t launch_fill_prev(const uint8_t* raw, uint8_t* out, uint8_t* masked, c
 }
 
 hipError_t launch_fill_mean(uint8_t* disp, uint8_t* masked, const uint8_t* mask_ff, int frames, int H, int W,
-                            hipStream_t s) {
+                            int Wrow, hipStream_t s) {
     const int64_t rows = (int64_t)frames * H;
     if (rows <= 0) return hipSuccess;
     if (W % 4) return hipErrorInvalidValue;
     hipLaunchKernelGGL(fill_mean_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, disp, masked, mask_ff,
-                       rows, H, W);
+                       rows, H, W, Wrow);
     return hipGetLastError();
 }
 

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void maskpoints_kernel(const uint8_t* __restri
     const uint8_t* fd = disp + (int64_t)frame * frame_px;
     double* fo = out + (int64_t)frame * cap * 3;
     uint32_t* fpk = packed + (int64_t)frame * cap;
-    const int Hg = H / 2, Wg = W / 2;   // range(0, H-1, 2) x range(0, W-1, 2)
+    const int Hg = p.Hg, Wg = p.Wg;   // range(0, H-1, 2) x range(0, Wu-1, 2); W is the row stride
     const int Wq = (Wg + 3) / 4;
     const int64_t nq = (int64_t)Hg * Wq;
     const bool wide = (W % 4) == 0 && (reinterpret_cast<uintptr_t>(fd) & 7) == 0 &&

@@ -124,14 +124,17 @@ bool same_cam(const sv_camera& a, const sv_camera& b) {
 
 int grid_len(int n, int step) { return n > 1 ? (n - 1 + step - 1) / step : 0; }
 
-KParams make_params(int H, int W, int step, const sv_camera& cam) {
+// W: the row stride of the frames in memory; Wu: the frame's own width (the
+// grid range(0, Wu-1, step) of functions.py:185-186), 0 = W. A batch of any
+// width stores its rows at a stride rounded up to 8 bytes (aligned quad loads).
+KParams make_params(int H, int W, int step, const sv_camera& cam, int Wu = 0) {
     KParams p;
     std::memset(&p, 0, sizeof p);
     p.H = H;
     p.W = W;
     p.step = step;
     p.Hg = grid_len(H, step);
-    p.Wg = grid_len(W, step);
+    p.Wg = grid_len(Wu > 0 ? Wu : W, step);
     p.pitch = (p.Wg + 3) / 4 * 4;
     p.Q = p.pitch / 4;
     p.frame_quads = p.Hg * p.Q;
@@ -212,6 +215,7 @@ int ensure_tables(Device& d, int H, int W, const sv_camera& cam, hipStream_t s) 
 struct sv_batch {
     int device = 0;
     int frames = 0, H = 0, W = 0, step = 1;
+    int Wu = 0;                // the frames' own width; W = row stride = round_up(Wu, 8)
     bool with_bgr = false;
     KParams kp{};
     int64_t Ng = 0;            // grid points per frame
@@ -377,9 +381,11 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
                     sv_batch** out) {
     if (!out) return fail(SV_E_ARG, "null out");
     *out = nullptr;
-    if (frames < 1 || H < 2 || W < 8 || (W % 8) != 0 || (step != 1 && step != 2))
-        return fail(SV_E_ARG, "sv_batch_create: need frames>=1, H>=2, W%%8==0, step in {1,2} "
+    if (frames < 1 || H < 2 || W < 2 || W > 65536 || (step != 1 && step != 2))
+        return fail(SV_E_ARG, "sv_batch_create: need frames>=1, H>=2, 2<=W<=65536, step in {1,2} "
                               "(frames=%d H=%d W=%d step=%d)", frames, H, W, step);
+    const int Wu = W;
+    W = (W + 7) / 8 * 8;
     Device* d;
     if (int rc = dev_get(device, &d)) return rc;
     sv_batch* b = new sv_batch;
@@ -387,10 +393,11 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
     b->frames = frames;
     b->H = H;
     b->W = W;
+    b->Wu = Wu;
     b->step = step;
     b->with_bgr = with_bgr != 0;
     sv_camera cam0{1, 1, 0, 0};
-    b->kp = make_params(H, W, step, cam0);
+    b->kp = make_params(H, W, step, cam0, Wu);
     b->Ng = (int64_t)b->kp.Hg * b->kp.Wg;
     b->cap = ((size_t)b->Ng + 63) / 64 * 64;
     b->dense_per_frame = (int64_t)b->kp.Hg * b->kp.pitch;
@@ -455,7 +462,7 @@ int sv_batch_info(const sv_batch* b, int64_t* o) {
     o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->pts.bytes + b->ctrl.bytes);
     o[5] = b->frames;
     o[6] = b->H;
-    o[7] = b->W;
+    o[7] = b->Wu;
     return SV_OK;
 }
 
@@ -471,6 +478,7 @@ int sv_batch_tune(sv_batch* b, int qpl, int nontemporal) {
 
 int sv_batch_synth(sv_batch* b, int64_t first_frame_id) {
     if (!b) return fail(SV_E_ARG, "null batch");
+    if (b->Wu != b->W) return fail(SV_E_ARG, "synthetic frames need W %% 8 == 0 (W=%d)", b->Wu);
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(launch_synth(b->kp, b->disp.as<uint8_t>(), b->with_bgr ? b->bgr.as<uint8_t>() : nullptr,
                          b->frames, first_frame_id, b->stream));
@@ -483,9 +491,16 @@ int sv_batch_upload(sv_batch* b, int frame, const uint8_t* disp, const uint8_t* 
     if (bgr && !b->with_bgr) return fail(SV_E_ARG, "batch created without bgr");
     HIP_TRY(hipSetDevice(b->device));
     const size_t px = (size_t)b->H * b->W;
-    HIP_TRY(hipMemcpyAsync(b->disp.as<uint8_t>() + px * frame, disp, px, hipMemcpyHostToDevice, b->stream));
+    uint8_t* dd = b->disp.as<uint8_t>() + px * frame;
+    if (b->Wu == b->W) {
+        HIP_TRY(hipMemcpyAsync(dd, disp, px, hipMemcpyHostToDevice, b->stream));
+    } else {   // rows at the padded stride, pad columns zero (outside every grid)
+        HIP_TRY(hipMemcpy2DAsync(dd, b->W, disp, b->Wu, b->Wu, b->H, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemset2DAsync(dd + b->Wu, b->W, 0, b->W - b->Wu, b->H, b->stream));
+    }
     if (bgr)
-        HIP_TRY(hipMemcpyAsync(b->bgr.as<uint8_t>() + 3 * px * frame, bgr, 3 * px, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpy2DAsync(b->bgr.as<uint8_t>() + 3 * px * frame, 3 * (size_t)b->W, bgr, 3 * (size_t)b->Wu,
+                                 3 * (size_t)b->Wu, b->H, hipMemcpyHostToDevice, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }
@@ -497,7 +512,7 @@ int sv_batch_project(sv_batch* b, const sv_camera* cam, int sync) {
     HIP_TRY(b->X.ensure(plane));
     HIP_TRY(b->Y.ensure(plane));
     HIP_TRY(b->Z.ensure(plane));
-    KParams p = make_params(b->H, b->W, b->step, *cam);
+    KParams p = make_params(b->H, b->W, b->step, *cam, b->Wu);
     int t0, t1;
     HIP_TRY(hipEventRecord(b->ev[0], b->stream));
     HIP_TRY(b->timed_event(&t0));
@@ -536,7 +551,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
                                int hist_thr, int chunk, int sync, Device* d, const FramePlane* planes = nullptr,
                                int plane_stride = 1) {
     if (!b->with_bgr) return fail(SV_E_ARG, "pipeline needs a batch created with bgr");
-    KParams p = make_params(b->H, b->W, b->step, *cam);
+    KParams p = make_params(b->H, b->W, b->step, *cam, b->Wu);
     if (p.Wg > 4096 || p.Hg > 4096) return fail(SV_E_ARG, "pipeline supports grids up to 4096 x 4096");
     set_plane(p, *plane, point_thr, hist_thr);
     if (chunk <= 0) chunk = 1024;
@@ -617,7 +632,7 @@ int sv_batch_pipeline_planes(sv_batch* b, const sv_camera* cam, double point_thr
     if (int rc = dev_get(b->device, &d)) return rc;
     HIP_TRY(b->fplanes.ensure(sizeof(FramePlane) * (size_t)b->frames));
     const RansacRes r = ransac_res(b);
-    const KParams kp = make_params(b->H, b->W, b->step, *cam);
+    const KParams kp = make_params(b->H, b->W, b->step, *cam, b->Wu);
     HIP_TRY(launch_frame_planes(r.abc, r.trial, b->frames, kp, point_thr, b->fplanes.as<FramePlane>(), b->stream));
     const sv_plane none{0.0, 0.0, 0.0};   // per-frame planes replace it
     return batch_pipeline_impl(b, cam, &none, point_thr, hist_thr, chunk, sync, d, b->fplanes.as<FramePlane>());
@@ -629,7 +644,7 @@ int sv_batch_pipeline_dev(sv_batch* b, const sv_camera* cam, const double* dplan
     Device* d;
     if (int rc = dev_get(b->device, &d)) return rc;
     HIP_TRY(b->dplane.ensure(sizeof(FramePlane)));
-    const KParams kp = make_params(b->H, b->W, b->step, *cam);
+    const KParams kp = make_params(b->H, b->W, b->step, *cam, b->Wu);
     HIP_TRY(launch_frame_planes(dplane, nullptr, 1, kp, point_thr, b->dplane.as<FramePlane>(), b->stream));
     const sv_plane none{0.0, 0.0, 0.0};   // the device plane replaces it
     return batch_pipeline_impl(b, cam, &none, point_thr, hist_thr, chunk, sync, d, b->dplane.as<FramePlane>(), 0);
@@ -763,7 +778,7 @@ int sv_batch_digest(sv_batch* b, const sv_camera* cam, int which, uint64_t* out)
     if (which == 1 && !b->pts.p) return fail(SV_E_STATE, "sv_batch_digest: no pipeline outputs");
     if ((b->kp.frame_px % 4) != 0) return fail(SV_E_ARG, "sv_batch_digest: H * W must be a multiple of 4");
     HIP_TRY(hipSetDevice(b->device));
-    KParams p = make_params(b->H, b->W, b->step, *cam);
+    KParams p = make_params(b->H, b->W, b->step, *cam, b->Wu);
     DevBuf buf;
     HIP_TRY(buf.ensure(sizeof(uint64_t) * 8 * (size_t)b->frames));
     hipError_t e;
@@ -858,7 +873,7 @@ int sv_fill_mean(uint8_t* disp, int H, int W) {
     std::lock_guard<std::mutex> lk(d->mu);
     const int pitch = (W + 3) / 4 * 4;
     if (int rc = upload_u8(d->disp, disp, H, W, pitch, d->stream)) return rc;
-    HIP_TRY(launch_fill_mean(d->disp.as<uint8_t>(), nullptr, nullptr, 1, H, pitch, d->stream));
+    HIP_TRY(launch_fill_mean(d->disp.as<uint8_t>(), nullptr, nullptr, 1, H, pitch, W, d->stream));
     return download_u8(disp, d->disp, H, W, pitch, d->stream);
 }
 
@@ -890,7 +905,8 @@ int sv_batch_set_mask(sv_batch* b, const uint8_t* mask) {
     const int64_t px = (int64_t)b->H * b->W;
     HIP_TRY(b->carmask.ensure((size_t)px * 2));
     uint8_t* grey = b->carmask.as<uint8_t>() + px;
-    HIP_TRY(hipMemcpyAsync(grey, mask, (size_t)px, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemsetAsync(grey, 0, (size_t)px, b->stream));
+    HIP_TRY(hipMemcpy2DAsync(grey, b->W, mask, b->Wu, b->Wu, b->H, hipMemcpyHostToDevice, b->stream));
     HIP_TRY(launch_mask_bytes(grey, b->carmask.as<uint8_t>(), px, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     b->have_mask = true;
@@ -915,12 +931,13 @@ int sv_batch_prepass(sv_batch* b, int option, const uint8_t* prev0, int sync) {
             Device* d;
             if (int rc = dev_get(b->device, &d)) return rc;
             HIP_TRY(d->aux.ensure((size_t)px));
-            HIP_TRY(hipMemcpyAsync(d->aux.p, prev0, (size_t)px, hipMemcpyHostToDevice, b->stream));
+            HIP_TRY(hipMemsetAsync(d->aux.p, 0, (size_t)px, b->stream));
+            HIP_TRY(hipMemcpy2DAsync(d->aux.p, b->W, prev0, b->Wu, b->Wu, b->H, hipMemcpyHostToDevice, b->stream));
             p0 = d->aux.as<uint8_t>();
         }
         HIP_TRY(launch_fill_prev(disp, disp, masked, mff, p0, b->frames, px, b->stream));
     } else if (option == 2) {
-        HIP_TRY(launch_fill_mean(disp, masked, mff, b->frames, b->H, b->W, b->stream));
+        HIP_TRY(launch_fill_mean(disp, masked, mff, b->frames, b->H, b->W, b->Wu, b->stream));
     } else if (masked) {
         HIP_TRY(launch_mask(disp, masked, mff, b->frames, px, b->stream));
     }
@@ -934,8 +951,11 @@ int sv_batch_read_disp(sv_batch* b, int frame, uint8_t* disp, uint8_t* masked) {
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
     const size_t px = (size_t)b->H * b->W;
-    if (disp) HIP_TRY(hipMemcpy(disp, b->disp.as<uint8_t>() + px * frame, px, hipMemcpyDeviceToHost));
-    if (masked) HIP_TRY(hipMemcpy(masked, b->mdisp.as<uint8_t>() + px * frame, px, hipMemcpyDeviceToHost));
+    if (disp)
+        HIP_TRY(hipMemcpy2D(disp, b->Wu, b->disp.as<uint8_t>() + px * frame, b->W, b->Wu, b->H, hipMemcpyDeviceToHost));
+    if (masked)
+        HIP_TRY(hipMemcpy2D(masked, b->Wu, b->mdisp.as<uint8_t>() + px * frame, b->W, b->Wu, b->H,
+                            hipMemcpyDeviceToHost));
     return SV_OK;
 }
 
@@ -959,7 +979,7 @@ int sv_road_raster(const int32_t* pts, int64_t n, int H, int W, uint8_t* out_img
     HIP_TRY(d->aux.ensure((size_t)H * W));
     HIP_TRY(d->xy.ensure(sizeof(int32_t) * 2 * (size_t)(n > 0 ? n : 1)));
     if (n) HIP_TRY(hipMemcpyAsync(d->xy.p, pts, sizeof(int32_t) * 2 * n, hipMemcpyHostToDevice, s));
-    HIP_TRY(launch_raster(d->xy.as<int32_t>(), nullptr, 0, 0, n, d->aux.as<uint8_t>(), 1, H, W, s));
+    HIP_TRY(launch_raster(d->xy.as<int32_t>(), nullptr, 0, 0, n, d->aux.as<uint8_t>(), 1, H, W, W, s));
     HIP_TRY(hipMemcpyAsync(out_img, d->aux.p, (size_t)H * W, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return SV_OK;
@@ -1003,7 +1023,7 @@ int sv_batch_road_raster(sv_batch* b, int sync) {
     const size_t px = (size_t)b->H * b->W;
     HIP_TRY(b->road.ensure(px * b->frames));
     HIP_TRY(launch_raster(b->pts.as<int32_t>(), b->counts, 4, 2, (int64_t)b->cap, b->road.as<uint8_t>(), b->frames, b->H,
-                          b->W, b->stream));
+                          b->W, b->Wu, b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }
@@ -1027,7 +1047,7 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
     const size_t px = (size_t)b->H * b->W;
     if (img) {
         if (!b->road.p) return fail(SV_E_STATE, "no road images");
-        HIP_TRY(hipMemcpy(img, b->road.as<uint8_t>() + px * frame, px, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy2D(img, b->Wu, b->road.as<uint8_t>() + px * frame, b->W, b->Wu, b->H, hipMemcpyDeviceToHost));
     }
     if (n) {
         if (!b->nz.p) return fail(SV_E_STATE, "no non-zero walk (sv_batch_nonzero first)");
@@ -1071,7 +1091,7 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
     HIP_TRY(b->rres.ensure(F * (sizeof(double) * 4 + sizeof(int64_t) + sizeof(int32_t) + sizeof(uint32_t))));
     b->mcap = mcap;
     const RansacRes r = ransac_res(b);
-    const KParams p = make_params(b->H, b->W, 2, *cam);
+    const KParams p = make_params(b->H, b->W, 2, *cam, b->Wu);
     const uint8_t* mff = b->have_mask ? b->carmask.as<uint8_t>() : nullptr;
     HIP_TRY(launch_maskpoints(b->disp.as<uint8_t>(), mff, b->frames, b->H, b->W, p, b->mpts.as<double>(),
                               b->mpk.as<uint32_t>(), mcap, r.mcount, b->stream));
@@ -1538,6 +1558,7 @@ int sv_disparity(const uint8_t* L, const uint8_t* R, int H, int W, const sv_sgbm
 
 int sv_batch_synth_pair(sv_batch* b, int64_t first_frame_id) {
     if (!b) return fail(SV_E_ARG, "null batch");
+    if (b->Wu != b->W) return fail(SV_E_ARG, "batched SGBM needs W %% 8 == 0 (W=%d)", b->Wu);
     if (b->W + kSgD > 4096) return fail(SV_E_ARG, "synthetic pairs need W <= %d", 4096 - kSgD);
     HIP_TRY(hipSetDevice(b->device));
     const size_t px = (size_t)b->H * b->W * b->frames;
@@ -1551,6 +1572,7 @@ int sv_batch_synth_pair(sv_batch* b, int64_t first_frame_id) {
 
 int sv_batch_upload_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t* R) {
     if (!b || !L || !R || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "sv_batch_upload_pair: bad args");
+    if (b->Wu != b->W) return fail(SV_E_ARG, "batched SGBM needs W %% 8 == 0 (W=%d)", b->Wu);
     HIP_TRY(hipSetDevice(b->device));
     const size_t px = (size_t)b->H * b->W;
     HIP_TRY(b->pairL.ensure(px * b->frames));

@@ -72,16 +72,18 @@ hipError_t launch_store_plane(const FramePlane& v, FramePlane* dst, hipStream_t 
 hipError_t launch_mask_bytes(const uint8_t* m, uint8_t* out, int64_t n, hipStream_t s);
 hipError_t launch_fill_prev(const uint8_t* raw, uint8_t* out, uint8_t* masked, const uint8_t* mask_ff,
                             const uint8_t* prev0, int frames, int64_t frame_px, hipStream_t s);
+// rows of Wrow pixels stored at stride W (W % 4 == 0, Wrow <= W; the padding is left alone)
 hipError_t launch_fill_mean(uint8_t* disp, uint8_t* masked, const uint8_t* mask_ff, int frames, int H, int W,
-                            hipStream_t s);
+                            int Wrow, hipStream_t s);
 hipError_t launch_mask(const uint8_t* disp, uint8_t* out, const uint8_t* mask_ff, int frames, int64_t frame_px,
                        hipStream_t s);
 
 // kernels/raster.hip -------------------------------------------------------
 // Road raster (points -> 255 on a zeroed image) and the raster-order non-zero walk.
 // counts: NULL -> cap points per frame, else counts[frame * cstride + cidx].
+// images of H rows at stride W; Wu = the image width (numpy's negative-index wrap)
 hipError_t launch_raster(const int32_t* pts, const int64_t* counts, int cstride, int cidx, int64_t cap, uint8_t* img,
-                         int frames, int H, int W, hipStream_t s);
+                         int frames, int H, int W, int Wu, hipStream_t s);
 // img frames x px (px % 4 == 0, rows of W <= 4096 pixels)
 hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
                           hipStream_t s);

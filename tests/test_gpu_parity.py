@@ -389,6 +389,8 @@ def test_batch_baseline_size_properties(svx_mod):
 def test_errors_are_raised(svx_mod):
     from svx import SvxError
     with pytest.raises(SvxError):
-        svx_mod.batch.Batch(1, H=544, W=1020)       # W % 8 != 0
+        svx_mod.batch.Batch(1, H=544, W=1)          # no grid column (any W >= 2 is accepted)
+    with pytest.raises(SvxError):
+        svx_mod.batch.Batch(1, H=544, W=1024, step=3)
     with pytest.raises(TypeError):
         svx_mod.dropin.projectDisparityTo3d(np.zeros((4, 4), np.float32), 128)
