@@ -24,6 +24,6 @@ else
   rc=$?; echo "bench rc=$rc"; tail -2 "$OUT/bench.log"; stop_if_fatal $rc bench
 fi
 if [ -n "${SWEEP:-}" ]; then
-  timeout -k 10 600 python tools/sweep.py $SWEEP > "$OUT/sweep.log" 2>&1
+  timeout -k 10 600 python tools/prof.py sweep $SWEEP > "$OUT/sweep.log" 2>&1
   rc=$?; echo "sweep rc=$rc"; cat "$OUT/sweep.log" | tail -20
 fi
