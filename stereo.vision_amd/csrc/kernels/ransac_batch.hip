@@ -6,24 +6,31 @@
 //      grid (functions.py:185-193), in raster order, same arithmetic as the
 //      drop-in (bit-identical). One workgroup per frame, running offset,
 //      LDS-staged coalesced output.
-//  * ransac_batch_kernel — functions.py:278-298 for every frame, with the
-//      batch RNG contract: frame F draws CPython's stream after
-//      random.seed(seed_base + F). One workgroup per frame:
-//        wave 0 replays the stream: init_by_array seeding (one lane), the
-//          MT19937 twist in ascending 64-word steps (reads before writes, so
-//          the in-place recurrence holds), tempering, and _randbelow /
-//          random.sample consumed 64 draws at a time: a ballot finds the
-//          accepted draws, an LDS bitmap the already-selected indices, and
-//          draws repeated inside one batch are resolved in lane (= stream)
-//          order; then the three sample(points, 1) draws and numpy's
-//          cross-product test (functions.py:240-260), redrawn while collinear;
-//        waves 1-3 evaluate the previous trial meanwhile (abc from the
-//          adjugate in fp64, mean |P.abc - 1| / |abc| over the sample) and
-//          keep the first strict minimum (functions.py:289-293).
+//  * ransac_draw_kernel — the draws of functions.py:278-298 for every frame,
+//      with the batch RNG contract: frame F draws CPython's stream after
+//      random.seed(seed_base + F). One wave per frame replays the stream:
+//      init_by_array seeding (one lane), the MT19937 state advanced one
+//      dependency level of the next twist at a time as the stream moves
+//      (no copy of the outputs: tempered on read), _randbelow /
+//      random.sample consumed 64 draws at a time (a ballot finds the
+//      accepted draws, an LDS bitmap the already-selected indices, draws
+//      repeated inside one round resolved in lane = stream order), then the
+//      three sample(points, 1) draws and numpy's cross-product test
+//      (functions.py:240-260), redrawn while collinear, and abc from the
+//      adjugate in fp64. Writes every trial's sample and plane to memory.
+//  * ransac_eval_kernel — one workgroup per frame: the frame's packed points
+//      staged in LDS; every trial screened in fp32 from LDS (one wave per
+//      trial, a rigorous bound to the fp64 mean), then the trials in order:
+//      those the screen cannot rule out evaluated in fp64 exactly (mean
+//      |P.abc - 1| / |abc| over the sample) and the first strict minimum
+//      kept (functions.py:289-293).
 //      The plane is the GPU's fp64 solve of the winning 3x3 system (within
 //      ~1e-15 relative of numpy's LAPACK solve, not bit-identical); frames
 //      whose decision could hinge on that (a singular system, an
 //      ill-conditioned winner, a near-tie) are flagged.
+//   (One kernel doing both, wave 0 drawing beside wave 1 evaluating, was
+//   bound by the screen's random 4-byte gathers: ~94 GB of sector traffic per
+//   4096 frames, the points of the ~4096 frames in flight not fitting L2.)
 #include "../svx_launch.h"
 
 namespace svx {
@@ -142,6 +149,7 @@ hipError_t launch_maskpoints(const uint8_t* disp, const uint8_t* mask_ff, int fr
 // RANSAC, one workgroup per frame
 // ---------------------------------------------------------------------------
 constexpr int kRBMaxK = 1024;          // sample size limit
+constexpr int kRBMaxTrials = 4096;     // the eval kernel keeps two doubles per trial in LDS
 constexpr int kRBBitmapWords = 5120;   // 20 KB: the set branch for n <= 163,840 points
 // randomNonCollinearPoints loops for ever on degenerate input (every triple
 // collinear); the kernel gives up after this many attempts in one trial and
@@ -157,29 +165,13 @@ constexpr uint32_t kRBMaxDraws = 1u << 28;
 // launch for the batch's largest frame, the sample bitmap (set branch) or the
 // pool list (pool branch) and the two trial samples. RansacShared is the view
 // (pointers into LDS, kept in registers) the device functions take.
-struct RansacFixed {
-    uint32_t mt[624];
-    uint32_t tout[3][624];                    // tempered outputs of twists t (slot t % 3)
-    double tri[2][12];                        // abc[3], d, flag, then padding
-    double red[2];
-    double bnd[2];
-    uint32_t misc[8];
-    uint32_t dummy[64];                       // claims of rejected draws (one word a lane)
-};
-
+template <class IdxT>
 struct RansacShared {
     uint32_t* mt;
-    uint32_t (*tout)[624];
     uint32_t* bitmap;                         // set branch: selected indices of the current sample
     int32_t* pool;                            // pool branch: the shrinking list (same words)
-    int32_t* idx0;                            // per trial (double-buffered): the samples, k apart
     int k;
-    __device__ int32_t* idx(int b) const { return idx0 + b * k; }
-    double (*tri)[12];
-    double* red;
-    double* bnd;
-    uint32_t* misc;
-    uint32_t* dummy;
+    uint32_t* dummy;                          // claims of rejected draws (one word a lane)
 };
 
 // CPython's init_genrand + init_by_array (Modules/_randommodule.c) for a
@@ -233,7 +225,7 @@ __device__ __forceinline__ uint32_t rb_temper(uint32_t y) {
 // 1, [454, 624) from level 2 (word 623 also reads new[0]). Within a level every
 // lane reads all its inputs (up to 4 words a lane) before any lane writes, so
 // no read sees a word of its own level already replaced.
-__device__ __forceinline__ void rb_twist_level(uint32_t* mt, uint32_t* out, int lo, int hi) {
+__device__ __forceinline__ void rb_twist_level(uint32_t* mt, int lo, int hi) {
     constexpr uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, A = 0x9908b0dfu;
     const int lane = lane_id();
     uint32_t nv[4];
@@ -252,35 +244,43 @@ __device__ __forceinline__ void rb_twist_level(uint32_t* mt, uint32_t* out, int 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int kk = lo + lane + 64 * j;
-        if (kk < hi) {
-            mt[kk] = nv[j];
-            out[kk] = rb_temper(nv[j]);
-        }
+        if (kk < hi) mt[kk] = nv[j];
     }
     rb_wave_lds_sync();   // the next level reads this one's words
 }
 
-__device__ void rb_twist(uint32_t* mt, uint32_t* out) {
-    rb_twist_level(mt, out, 0, 227);
-    rb_twist_level(mt, out, 227, 454);
-    rb_twist_level(mt, out, 454, 624);
-}
-
-struct RbStream {   // wave 0's view of the frame's output stream
+// The stream without a copy of the outputs: the state words are advanced one
+// dependency level of the next twist at a time, as the stream moves. With T
+// whole twists and `lev` levels of twist T + 1 done, word w holds twist T + 1
+// for w below the level boundary B[lev] (0, 227, 454) and twist T above, i.e.
+// the state is exactly stream positions [G - 624, G), G = 624 T + B[lev]
+// (position q = 624 (twist - 1) + word), and output q = temper(mt[q % 624]).
+// A request [pos, pos + span) with span <= 192 advances levels while
+// pos + span > G; a level moves G by at most 227, so the positions it drops
+// (below the new G - 624 < pos + span - 397) were consumed already.
+struct RbStream {   // wave 0's view of the frame's output stream (uniform)
     uint32_t pos;     // next unconsumed output
-    uint32_t twists;  // twists generated (outputs [0, 624 * twists) exist)
+    uint32_t T;       // whole twists done
+    int lev;          // levels of twist T + 1 done (0..2)
+    __device__ uint32_t G() const { return 624u * T + (lev == 0 ? 0u : lev == 1 ? 227u : 454u); }
 };
 
-// make outputs [pos, pos + 64) available (at most one new twist per call)
-__device__ __forceinline__ void rb_ensure(RansacShared& sh, RbStream& st) {
-    while (st.pos + 64 > 624 * st.twists) {
-        rb_twist(sh.mt, sh.tout[st.twists % 3]);
-        ++st.twists;
+template <class IdxT>
+__device__ __forceinline__ void rb_advance(RansacShared<IdxT>& sh, RbStream& st, uint32_t span) {
+    while (st.pos + span > st.G()) {
+        const int lo = st.lev == 0 ? 0 : st.lev == 1 ? 227 : 454;
+        const int hi = st.lev == 0 ? 227 : st.lev == 1 ? 454 : 624;
+        rb_twist_level(sh.mt, lo, hi);
+        if (++st.lev == 3) {
+            st.lev = 0;
+            ++st.T;
+        }
     }
 }
 
-__device__ __forceinline__ uint32_t rb_word(const RansacShared& sh, uint32_t q) {
-    return sh.tout[(q / 624) % 3][q % 624];
+template <class IdxT>
+__device__ __forceinline__ uint32_t rb_word(const RansacShared<IdxT>& sh, uint32_t q) {
+    return rb_temper(sh.mt[q % 624]);
 }
 
 // numpy.cross(P1 - P2, P2 - P3) all zero (functions.py:255-258); products rounded first
@@ -292,11 +292,12 @@ __device__ __forceinline__ bool rb_collinear(const double* p1, const double* p2,
 }
 
 // wave 0: k accepted draws of randbelow(n) in stream order -> out[0..m) (m <= 3)
-__device__ void rb_draw_below(RansacShared& sh, RbStream& st, uint32_t n, int kb, int m, uint32_t* out) {
+template <class IdxT>
+__device__ void rb_draw_below(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, int kb, int m, uint32_t* out) {
     const int lane = lane_id();
     int got = 0;
     while (got < m && st.pos < kRBMaxDraws) {
-        rb_ensure(sh, st);
+        rb_advance(sh, st, 64u);
         const uint32_t r = rb_word(sh, st.pos + lane) >> (32 - kb);
         uint64_t acc = __ballot(r < n);
         int last = 63;
@@ -310,14 +311,6 @@ __device__ void rb_draw_below(RansacShared& sh, RbStream& st, uint32_t n, int kb
     }
 }
 
-// outputs [pos, pos + span) available, span <= 1024 (three twist slots suffice)
-__device__ __forceinline__ void rb_ensure_span(RansacShared& sh, RbStream& st, uint32_t span) {
-    while (st.pos + span > 624 * st.twists) {
-        rb_twist(sh.mt, sh.tout[st.twists % 3]);
-        ++st.twists;
-    }
-}
-
 // wave 0: random.sample(range(n), k) into idx (set branch), then clear the bits.
 // A round takes kRBWin windows of 64 draws (stream positions pos + 64 w + lane):
 // every accepted draw claims its index bit with atomicOr, whose return says
@@ -328,25 +321,23 @@ __device__ __forceinline__ void rb_ensure_span(RansacShared& sh, RbStream& st, u
 // and its lowest lane (earliest draw) wins, otherwise every lane drawing it is
 // rejected. The k-th selection in stream order ends the sample; bits claimed
 // past it are released and the stream resumes right after it.
-constexpr int kRBWin = 12;   // 768 draws a round: two rounds for a 600-point sample at n ~ 65k points
+constexpr int kRBWin = 3;   // 192 draws a round (the state holds 624 positions: a round must fit, RbStream)
 
-__device__ void rb_sample_set(RansacShared& sh, RbStream& st, uint32_t n, int kb, int k, int32_t* idx) {
+template <class IdxT>
+__device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, int kb, int k, IdxT* idx,
+                              int32_t* tr) {
     const int lane = lane_id();
-    int have = 0, round0 = 0;   // round0: picks made before the current round
-    uint32_t keptm = 0;         // this lane's picks of the current round (bit w: window w)
+    int have = 0;
     uint32_t r[kRBWin];
     while (have < k && st.pos < kRBMaxDraws) {
-        round0 = have;
-        keptm = 0;
-        rb_ensure_span(sh, st, 64 * kRBWin);
-        const uint32_t* ring = &sh.tout[0][0];    // outputs q at ring[q mod 3 * 624]
-        const uint32_t base = st.pos % (3 * 624);
+        rb_advance(sh, st, 64u * kRBWin);
+        const uint32_t base = st.pos % 624;
         uint32_t old[kRBWin];
 #pragma unroll
         for (int w = 0; w < kRBWin; ++w) {
             uint32_t i = base + 64 * w + lane;
-            i -= i >= 3 * 624 ? 3 * 624 : 0;
-            r[w] = ring[i] >> (32 - kb);
+            i -= i >= 624 ? 624 : 0;
+            r[w] = rb_temper(sh.mt[i]) >> (32 - kb);
         }
 #pragma unroll
         for (int w = 0; w < kRBWin; ++w) {   // claims issued in window order; rejected draws or a lane's dummy word
@@ -377,11 +368,13 @@ __device__ void rb_sample_set(RansacShared& sh, RbStream& st, uint32_t n, int kb
             const uint64_t sm = __ballot(sel);
             const int q = q0 + (int)__builtin_popcountll(sm & ((1ull << lane) - 1));
             if (sel) {
-                if (q < k) idx[q] = (int32_t)r[w];
+                if (q < k) {
+                    idx[q] = (IdxT)r[w];
+                    if (tr) tr[q] = (int32_t)r[w];
+                }
                 else atomicAnd(&sh.bitmap[r[w] >> 5], ~bit);
             }
-            keptm |= (uint32_t)(sel && q < k) << w;
-            const uint64_t lastm = __ballot(sel && q == k - 1);
+                const uint64_t lastm = __ballot(sel && q == k - 1);
             if (lastm) consumed = 64u * w + (uint32_t)__builtin_ctzll(lastm) + 1u;
             q0 += (int)__builtin_popcountll(sm);
         }
@@ -389,19 +382,14 @@ __device__ void rb_sample_set(RansacShared& sh, RbStream& st, uint32_t n, int kb
         st.pos += consumed;
         rb_wave_lds_sync();   // the next round reads bits set/cleared by other lanes
     }
-    // clear the sample's bits: the last round's picks from registers, earlier ones from idx
-#pragma unroll
-    for (int w = 0; w < kRBWin; ++w)
-        if ((keptm >> w) & 1u) atomicAnd(&sh.bitmap[r[w] >> 5], ~(1u << (r[w] & 31)));
-    for (int q = lane; q < round0; q += kWave) {
-        const uint32_t v = (uint32_t)idx[q];
-        atomicAnd(&sh.bitmap[v >> 5], ~(1u << (v & 31)));
-    }
+    // clear the sample's bits (the whole bitmap: a few words a lane)
+    for (uint32_t q = lane; q < (n + 31) / 32; q += kWave) sh.bitmap[q] = 0;
     rb_wave_lds_sync();
 }
 
 // wave 0, lane 0 drives: random.sample(range(n), k), pool branch (n <= setsize)
-__device__ void rb_sample_pool(RansacShared& sh, RbStream& st, uint32_t n, int k, int32_t* idx) {
+template <class IdxT>
+__device__ void rb_sample_pool(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, int k, IdxT* idx, int32_t* tr) {
     const int lane = lane_id();
     for (uint32_t q = lane; q < n; q += kWave) sh.pool[q] = (int32_t)q;
     rb_wave_lds_sync();
@@ -411,46 +399,133 @@ __device__ void rb_sample_pool(RansacShared& sh, RbStream& st, uint32_t n, int k
         uint32_t j = 0;
         rb_draw_below(sh, st, bound, kb, 1, &j);
         if (lane == 0) {
-            idx[i] = sh.pool[j];
+            idx[i] = (IdxT)sh.pool[j];
+            if (tr) tr[i] = sh.pool[j];
             sh.pool[j] = sh.pool[n - i - 1];
         }
     }
     rb_wave_lds_sync();   // idx (and the trace) read by every lane next
 }
 
-constexpr int kRBThreads = 128;   // wave 0 replays the stream, wave 1 evaluates
 constexpr int kRBGather = 10;     // screen gathers a lane keeps in flight
+constexpr int kRBEvalThreads = 1024;   // eval: 16 waves screen 16 trials at a time
 
-__global__ __launch_bounds__(kRBThreads) void ransac_batch_kernel(const double* __restrict__ pts,
-                                                           const uint32_t* __restrict__ packed, int64_t cap,
-                                                           KParams cp, const int64_t* __restrict__ counts,
-                                                           uint64_t seed_base,
-                                                           int64_t first_frame, int trials, int k,
-                                                           double* __restrict__ out_abc, double* __restrict__ out_err,
-                                                           int32_t* __restrict__ out_trial,
-                                                           uint32_t* __restrict__ out_flags,
-                                                           int32_t* __restrict__ trace, int trace_trials,
-                                                           int ablate, int bitmap_words) {
-    __shared__ RansacFixed fx;
-    extern __shared__ uint32_t rb_dyn[];   // [bitmap_words] bitmap / pool, then idx[2][k]
-    RansacShared sh;
-    sh.mt = fx.mt;
-    sh.tout = fx.tout;
+// One trial's record written by the draw kernel: a, b, c, |abc|, flag
+// (0 ok, 1 singular: numpy's LinAlgError, skipped; 2 ill-conditioned).
+constexpr int kRBTri = 5;
+
+template <class IdxT>
+__global__ __launch_bounds__(64) void ransac_draw_kernel(const double* __restrict__ pts, int64_t cap,
+                                                         const int64_t* __restrict__ counts, uint64_t seed_base,
+                                                         int64_t first_frame, int trials, int k,
+                                                         IdxT* __restrict__ sidx, double* __restrict__ tri,
+                                                         int32_t* __restrict__ fstat, int32_t* __restrict__ trace,
+                                                         int trace_trials, int bitmap_words) {
+    __shared__ uint32_t mt[624];
+    __shared__ uint32_t dummy[64];
+    extern __shared__ uint32_t rb_dyn[];   // [bitmap_words] bitmap / pool list
+    RansacShared<IdxT> sh;
+    sh.mt = mt;
     sh.bitmap = rb_dyn;
     sh.pool = reinterpret_cast<int32_t*>(rb_dyn);
-    sh.idx0 = reinterpret_cast<int32_t*>(rb_dyn + bitmap_words);
     sh.k = k;
-    sh.tri = fx.tri;
-    sh.red = fx.red;
-    sh.bnd = fx.bnd;
-    sh.misc = fx.misc;
-    sh.dummy = fx.dummy;
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    sh.dummy = dummy;
+    const int lane = lane_id();
     const int frame = blockIdx.x;
     const int64_t n64 = counts[frame];
     const double* fp = pts + (int64_t)frame * cap * 3;
-    const uint32_t* fpk = packed + (int64_t)frame * cap;
     if (n64 < k || trials <= 0) {   // every trial's random.sample raises: (None, None)
+        if (lane == 0) {
+            fstat[2 * frame] = 0;
+            fstat[2 * frame + 1] = 0;
+        }
+        return;
+    }
+    const uint32_t n = (uint32_t)n64;
+    const int kb = 32 - __builtin_clz(n);
+    const bool pool = (int64_t)n <= ransac_setsize(k);
+    for (int q = lane; q < bitmap_words; q += 64) sh.bitmap[q] = 0;
+    if (lane == 0) rb_seed(sh.mt, seed_base + (uint64_t)(first_frame + frame));
+    __syncthreads();   // one wave: orders lane 0's seeding before every lane's reads
+    RbStream st{0, 0, 0};
+    int status = 0, s = 0;
+    for (; s < trials; ++s) {
+        IdxT* idx = sidx + ((int64_t)frame * trials + s) * k;
+        int32_t* tr = s < trace_trials ? trace + ((int64_t)frame * trace_trials + s) * (k + 3) : nullptr;
+        if (pool) rb_sample_pool(sh, st, n, k, idx, tr);
+        else rb_sample_set(sh, st, n, kb, k, idx, tr);
+        uint32_t t3[3] = {0, 0, 0};
+        const double *p1 = fp, *p2 = fp, *p3 = fp;
+        int attempts = 0;
+        bool degenerate = false;
+        do {   // randomNonCollinearPoints
+            if (++attempts > kRBMaxAttempts) {
+                degenerate = true;
+                break;
+            }
+            rb_draw_below(sh, st, n, kb, 3, t3);
+            p1 = fp + 3 * (int64_t)t3[0];
+            p2 = fp + 3 * (int64_t)t3[1];
+            p3 = fp + 3 * (int64_t)t3[2];
+        } while (st.pos < kRBMaxDraws && rb_collinear(p1, p2, p3));
+        if (st.pos >= kRBMaxDraws) {
+            status = 2;
+            break;
+        }
+        if (degenerate) {
+            status = 1;
+            break;
+        }
+        if (tr && lane < 3) tr[k + lane] = (int32_t)(lane == 0 ? t3[0] : lane == 1 ? t3[1] : t3[2]);
+        if (lane == 0) {
+            // inv([P1;P2;P3]) 1 = (r2 x r3 + r3 x r1 + r1 x r2) / det
+            const double* r1 = p1;
+            const double* r2 = p2;
+            const double* r3 = p3;
+            const double c23[3] = {r2[1] * r3[2] - r2[2] * r3[1], r2[2] * r3[0] - r2[0] * r3[2],
+                                   r2[0] * r3[1] - r2[1] * r3[0]};
+            const double c31[3] = {r3[1] * r1[2] - r3[2] * r1[1], r3[2] * r1[0] - r3[0] * r1[2],
+                                   r3[0] * r1[1] - r3[1] * r1[0]};
+            const double c12[3] = {r1[1] * r2[2] - r1[2] * r2[1], r1[2] * r2[0] - r1[0] * r2[2],
+                                   r1[0] * r2[1] - r1[1] * r2[0]};
+            const double det = r1[0] * c23[0] + r1[1] * c23[1] + r1[2] * c23[2];
+            const double a = (c23[0] + c31[0] + c12[0]) / det;
+            const double b = (c23[1] + c31[1] + c12[1]) / det;
+            const double c = (c23[2] + c31[2] + c12[2]) / det;
+            const double n1 = sqrt(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
+            const double n2 = sqrt(r2[0] * r2[0] + r2[1] * r2[1] + r2[2] * r2[2]);
+            const double n3 = sqrt(r3[0] * r3[0] + r3[1] * r3[1] + r3[2] * r3[2]);
+            double fl = 0.0;
+            if (det == 0.0) fl = 1.0;                                 // numpy: LinAlgError, trial skipped
+            else if (!(fabs(det) >= 1e-6 * n1 * n2 * n3)) fl = 2.0;   // ill-conditioned
+            double* o = tri + ((int64_t)frame * trials + s) * kRBTri;
+            o[0] = a;
+            o[1] = b;
+            o[2] = c;
+            o[3] = sqrt(a * a + b * b + c * c);
+            o[4] = fl;
+        }
+    }
+    if (lane == 0) {
+        fstat[2 * frame] = status;   // 1: the reference would never return; 2: draw budget
+        fstat[2 * frame + 1] = s;    // trials drawn (the failing one excluded)
+    }
+}
+
+// Screen + decision. LDS: the frame's packed points (LDS_PTS) or none, then
+// per trial the screened mean and its bound (2 doubles).
+template <class IdxT, bool LDS_PTS>
+__global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
+    const double* __restrict__ pts, const uint32_t* __restrict__ packed, int64_t cap, KParams cp,
+    const int64_t* __restrict__ counts, int trials, int k, const IdxT* __restrict__ sidx,
+    const double* __restrict__ tri, const int32_t* __restrict__ fstat, double* __restrict__ out_abc,
+    double* __restrict__ out_err, int32_t* __restrict__ out_trial, uint32_t* __restrict__ out_flags, int ablate,
+    int lds_pts_words) {
+    extern __shared__ uint32_t ev_dyn[];
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int frame = blockIdx.x;
+    const int64_t n64 = counts[frame];
+    if (n64 < k || trials <= 0) {
         if (tid == 0) {
             out_trial[frame] = -1;
             out_flags[frame] = 0;
@@ -459,105 +534,63 @@ __global__ __launch_bounds__(kRBThreads) void ransac_batch_kernel(const double* 
         }
         return;
     }
-    const uint32_t n = (uint32_t)n64;
-    const int kb = 32 - __builtin_clz(n);
-    const bool pool = (int64_t)n <= ransac_setsize(k);
-    for (int q = tid; q < bitmap_words; q += kRBThreads) sh.bitmap[q] = 0;
-    if (tid == 0) {
-        sh.misc[0] = 0;
-        rb_seed(sh.mt, seed_base + (uint64_t)(first_frame + frame));
+    const int status = fstat[2 * frame], T = fstat[2 * frame + 1];
+    const double* fp = pts + (int64_t)frame * cap * 3;
+    const uint32_t* fpk = packed + (int64_t)frame * cap;
+    const uint32_t* P = fpk;
+    if constexpr (LDS_PTS) {
+        for (int64_t q = tid; q < n64; q += kRBEvalThreads) ev_dyn[q] = fpk[q];
+        P = ev_dyn;
     }
+    double* scr = reinterpret_cast<double*>(ev_dyn + (LDS_PTS ? lds_pts_words : 0));   // [T][2]
+    const double* ftri = tri + (int64_t)frame * trials * kRBTri;
+    const IdxT* fidx = sidx + (int64_t)frame * trials * k;
     __syncthreads();
-    RbStream st{0, 0};
-    double best = __builtin_huge_val(), second = __builtin_huge_val();
-    int best_t = -1;
-    uint32_t flags = 0;
-    double babc[3] = {0, 0, 0};
-    // step s: wave 0 draws trial s (s < trials), wave 1 evaluates trial s - 1
-    for (int s = 0; s <= trials; ++s) {
-        const int buf = s & 1;
-        if (wave == 0 && s < trials && !((ablate & 2) && s >= 2)) {   // DIAGNOSTIC 2: draw 2 trials only
-            int32_t* idx = sh.idx(buf);
-            if (pool) rb_sample_pool(sh, st, n, k, idx);
-            else rb_sample_set(sh, st, n, kb, k, idx);
-
-            uint32_t t3[3] = {0, 0, 0};
-            const double *p1, *p2, *p3;
-            int attempts = 0;
-            bool degenerate = false;
-            do {   // randomNonCollinearPoints
-                if (++attempts > kRBMaxAttempts) {
-                    degenerate = true;
-                    break;
-                }
-                rb_draw_below(sh, st, n, kb, 3, t3);
-                p1 = fp + 3 * (int64_t)t3[0];
-                p2 = fp + 3 * (int64_t)t3[1];
-                p3 = fp + 3 * (int64_t)t3[2];
-            } while (st.pos < kRBMaxDraws && rb_collinear(p1, p2, p3));
-            if (st.pos >= kRBMaxDraws) {
-                if (lane == 0) {
-                    sh.misc[0] = 2;
-                    sh.tri[buf][4] = 1.0;
-                }
-            } else if (degenerate) {
-                if (lane == 0) {
-                    sh.misc[0] = 1;
-                    sh.tri[buf][4] = 1.0;   // nothing to evaluate
-                }
-            } else if (s < trace_trials) {   // the draws themselves, for draw-level parity tests
-                int32_t* tr = trace + ((int64_t)frame * trace_trials + s) * (k + 3);
-                for (int q = lane; q < k; q += kWave) tr[q] = idx[q];
-                if (lane < 3) tr[k + lane] = (int32_t)(lane == 0 ? t3[0] : lane == 1 ? t3[1] : t3[2]);
-            }
-            if (!degenerate && st.pos < kRBMaxDraws && lane == 0) {
-                // inv([P1;P2;P3]) 1 = (r2 x r3 + r3 x r1 + r1 x r2) / det
-                const double* r1 = p1;
-                const double* r2 = p2;
-                const double* r3 = p3;
-                const double c23[3] = {r2[1] * r3[2] - r2[2] * r3[1], r2[2] * r3[0] - r2[0] * r3[2],
-                                       r2[0] * r3[1] - r2[1] * r3[0]};
-                const double c31[3] = {r3[1] * r1[2] - r3[2] * r1[1], r3[2] * r1[0] - r3[0] * r1[2],
-                                       r3[0] * r1[1] - r3[1] * r1[0]};
-                const double c12[3] = {r1[1] * r2[2] - r1[2] * r2[1], r1[2] * r2[0] - r1[0] * r2[2],
-                                       r1[0] * r2[1] - r1[1] * r2[0]};
-                const double det = r1[0] * c23[0] + r1[1] * c23[1] + r1[2] * c23[2];
-                const double a = (c23[0] + c31[0] + c12[0]) / det;
-                const double b = (c23[1] + c31[1] + c12[1]) / det;
-                const double c = (c23[2] + c31[2] + c12[2]) / det;
-                const double n1 = sqrt(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
-                const double n2 = sqrt(r2[0] * r2[0] + r2[1] * r2[1] + r2[2] * r2[2]);
-                const double n3 = sqrt(r3[0] * r3[0] + r3[1] * r3[1] + r3[2] * r3[2]);
-                double fl = 0.0;
-                if (det == 0.0) fl = 1.0;                                 // numpy: LinAlgError, trial skipped
-                else if (!(fabs(det) >= 1e-6 * n1 * n2 * n3)) fl = 2.0;   // ill-conditioned
-                sh.tri[buf][0] = a;
-                sh.tri[buf][1] = b;
-                sh.tri[buf][2] = c;
-                sh.tri[buf][3] = sqrt(a * a + b * b + c * c);
-                sh.tri[buf][4] = fl;
-            }
-        }
-        // Wave 1 screens trial s - 1 in fp32 from the packed points (one 4-byte
-        // gather a point), with a rigorous bound on the difference to the fp64
-        // mean; only a trial that could beat (or tie within 1e-9) the best so
-        // far is then evaluated in fp64 exactly as before (functions.py:289-293).
-        // A random sequence sets a new minimum ~ln(trials) times, so nearly
-        // every trial is decided by the screen.
-        if (wave != 0 && s > 0 && !(ablate & 1)) {   // DIAGNOSTIC 1: no evaluation
-            const int pb = buf ^ 1;
-            const double fl = sh.tri[pb][4];
-            double sum = 0.0, bnd = 0.0;
-            if (fl != 1.0) {
-                const float a = (float)sh.tri[pb][0], b = (float)sh.tri[pb][1], c = (float)sh.tri[pb][2];
-                const float fa = __builtin_fabsf(a), fb = __builtin_fabsf(b), fc = __builtin_fabsf(c);
-                for (int j0 = lane; j0 < k; j0 += kRBGather * kWave) {   // one batch for k <= 640
-                    uint32_t u[kRBGather];
+    // screen every trial in fp32 (one wave a trial): the mean distance from the
+    // packed points and, per point, the bound (|Xa| + |Yb| + |Zc| + 1) 2^-18 / |abc|
+    // on its difference to the fp64 distance (fp32 X, Y, Z within 2^-21 relative,
+    // fp32 a, b, c and two fmas); sums in fp64
+    if (!(ablate & 1)) {
+        // software-pipelined over the wave's trials: the next trial's indices and
+        // record are loaded (global, just written by the draw kernel) while this
+        // trial's points are gathered from LDS
+        constexpr int NW = kRBEvalThreads / 64;
+        auto load = [&](int t, uint32_t (&ix)[kRBGather], double (&rec)[kRBTri]) {
+            const IdxT* idx = fidx + (int64_t)t * k;
 #pragma unroll
-                    for (int v = 0; v < kRBGather; ++v) {
-                        const int j = j0 + kWave * v;
-                        u[v] = fpk[j < k ? sh.idx(pb)[j] : 0];
+            for (int v = 0; v < kRBGather; ++v) {
+                const int j = lane + kWave * v;
+                ix[v] = j < k ? (uint32_t)idx[j] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < kRBTri; ++q) rec[q] = ftri[(int64_t)t * kRBTri + q];
+        };
+        uint32_t nix[kRBGather];
+        double nrec[kRBTri];
+        if (wave < T) load(wave, nix, nrec);
+        for (int t = wave; t < T; t += NW) {
+            uint32_t ix[kRBGather];
+            double rec[kRBTri];
+#pragma unroll
+            for (int v = 0; v < kRBGather; ++v) ix[v] = nix[v];
+#pragma unroll
+            for (int q = 0; q < kRBTri; ++q) rec[q] = nrec[q];
+            if (t + NW < T) load(t + NW, nix, nrec);
+            double sum = 0.0, bnd = 0.0;
+            if (rec[4] != 1.0) {
+                const float a = (float)rec[0], b = (float)rec[1], c = (float)rec[2];
+                const float fa = __builtin_fabsf(a), fb = __builtin_fabsf(b), fc = __builtin_fabsf(c);
+                for (int j0 = lane, g = 0; j0 < k; j0 += kRBGather * kWave, ++g) {
+                    uint32_t u[kRBGather];
+                    if (g > 0) {   // k > 640: the rest of the sample (same order as the first batch)
+#pragma unroll
+                        for (int v = 0; v < kRBGather; ++v) {
+                            const int j = j0 + kWave * v;
+                            ix[v] = j < k ? (uint32_t)fidx[(int64_t)t * k + j] : 0u;
+                        }
                     }
+#pragma unroll
+                    for (int v = 0; v < kRBGather; ++v) u[v] = P[ix[v]];
 #pragma unroll
                     for (int v = 0; v < kRBGather; ++v) {
                         if (j0 + kWave * v >= k) continue;
@@ -579,77 +612,75 @@ __global__ __launch_bounds__(kRBThreads) void ransac_batch_kernel(const double* 
                 sum += __shfl_xor(sum, o, kWave);
                 bnd += __shfl_xor(bnd, o, kWave);
             }
-            if (lane == 0) {
-                sh.red[wave] = sum;
-                sh.bnd[wave] = bnd;
+            if (lane == 0) {   // the screened mean and its bound; bound -1 marks a singular trial
+                const double d = rec[3];
+                scr[2 * t] = sum / (d * k);
+                scr[2 * t + 1] = rec[4] == 1.0 ? -1.0 : bnd * 0x1p-18 / (d * k);
             }
         }
-        __syncthreads();
-        if (tid == 64 && s > 0) {   // the screen: can trial s - 1 matter?
-            const int pb = buf ^ 1;
-            const double fl = sh.tri[pb][4];
-            uint32_t full = 0;
-            if (fl == 1.0) {
-                flags |= 1u;
-            } else {
-                // |dist32 - dist64| <= (|Xa| + |Yb| + |Zc| + 1) 2^-18 / |abc| a point (fp32 X, Y, Z within
-                // 2^-21 relative, fp32 a, b, c and the two fmas, |abc| in fp32); sums in fp64
-                const double d = sh.tri[pb][3];
-                const double e32 = sh.red[1] / (d * k);
-                const double eb = sh.bnd[1] * 0x1p-18 / (d * k);
-                full = (ablate & 4) || !(e32 - eb > best * (1.0 + 1e-9));   // NaN / inf: evaluate in fp64
-                if (ablate & 1) full = 0;   // DIAGNOSTIC 1: no evaluation at all
-            }
-            sh.misc[1] = full;
-        }
-        __syncthreads();
-        if (s > 0 && sh.misc[1]) {   // uniform: the fp64 evaluation of trial s - 1 (rare)
-            const int pb = buf ^ 1;
-            if (wave != 0) {
-                const double a = sh.tri[pb][0], b = sh.tri[pb][1], c = sh.tri[pb][2], d = sh.tri[pb][3];
-                double sum = 0.0;
-                for (int j0 = lane; j0 < k; j0 += 4 * kWave) {   // every gather in flight before the arithmetic
-                    double qx[4], qy[4], qz[4];
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        const int j = j0 + kWave * v;
-                        const double* q = fp + 3 * (int64_t)(j < k ? sh.idx(pb)[j] : 0);
-                        qx[v] = q[0];
-                        qy[v] = q[1];
-                        qz[v] = q[2];
-                    }
-#pragma unroll
-                    for (int v = 0; v < 4; ++v)
-                        if (j0 + kWave * v < k) sum += fabs((qx[v] * a + qy[v] * b + qz[v] * c - 1.0) / d);
-                }
-#pragma unroll
-                for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
-                if (lane == 0) sh.red[wave] = sum;
-            }
-            __syncthreads();
-            if (tid == 64) {   // one lane keeps the decision (trial order, strict <)
-                const double fl = sh.tri[pb][4];
-                const double e = sh.red[1] / k;
-                if (e < best) {
-                    second = best;
-                    best = e;
-                    best_t = s - 1;
-                    babc[0] = sh.tri[pb][0];
-                    babc[1] = sh.tri[pb][1];
-                    babc[2] = sh.tri[pb][2];
-                    flags = (flags & ~2u) | (fl == 2.0 ? 2u : 0u);
-                } else if (e < second) {
-                    second = e;
-                }
-            }
-        }
-        __syncthreads();   // sh.idx / sh.tri of this step are reused two steps later
-        if (sh.misc[0]) break;   // uniform: read after the barrier
+    } else {
+        for (int t = tid; t < T; t += kRBEvalThreads) scr[2 * t + 1] = ftri[(int64_t)t * kRBTri + 4] == 1.0 ? -1.0 : 0.0;
     }
-    if (tid == 64) {
-        if (sh.misc[0]) {   // 1: the reference would never return; 2: draw budget
+    __syncthreads();
+    // the trials in order (uniform: every thread keeps the same decision state);
+    // those the screen cannot rule out are evaluated in fp64 by wave 0
+    double* red = scr + 2 * (int64_t)T;   // one double: wave 0's fp64 sum
+    double best = __builtin_huge_val(), second = __builtin_huge_val();
+    int best_t = -1;
+    uint32_t flags = 0;
+    double babc[3] = {0, 0, 0};
+    for (int t = 0; t < T; ++t) {   // LDS only, except for the (rare) fp64 evaluations
+        const double e32 = scr[2 * t], eb = scr[2 * t + 1];
+        if (eb < 0.0) {   // singular
+            flags |= 1u;
+            continue;
+        }
+        bool full = (ablate & 4) || !(e32 - eb > best * (1.0 + 1e-9));   // NaN / inf: evaluate in fp64
+        if (ablate & 1) full = false;   // DIAGNOSTIC 1: no evaluation at all
+        if (!full) continue;
+        const double* tr = ftri + (int64_t)t * kRBTri;
+        const double a = tr[0], b = tr[1], c = tr[2], d = tr[3], fl = tr[4];
+        if (wave == 0) {
+            const IdxT* idx = fidx + (int64_t)t * k;
+            double sum = 0.0;
+            (void)e32;
+            for (int j0 = lane; j0 < k; j0 += 4 * kWave) {   // every gather in flight before the arithmetic
+                double qx[4], qy[4], qz[4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int j = j0 + kWave * v;
+                    const double* q = fp + 3 * (int64_t)(j < k ? (uint32_t)idx[j] : 0u);
+                    qx[v] = q[0];
+                    qy[v] = q[1];
+                    qz[v] = q[2];
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    if (j0 + kWave * v < k) sum += fabs((qx[v] * a + qy[v] * b + qz[v] * c - 1.0) / d);
+            }
+#pragma unroll
+            for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
+            if (lane == 0) red[0] = sum;
+        }
+        __syncthreads();
+        const double e = red[0] / k;
+        __syncthreads();   // red is rewritten by the next evaluation
+        if (e < best) {   // trial order, strict <
+            second = best;
+            best = e;
+            best_t = t;
+            babc[0] = a;
+            babc[1] = b;
+            babc[2] = c;
+            flags = (flags & ~2u) | (fl == 2.0 ? 2u : 0u);
+        } else if (e < second) {
+            second = e;
+        }
+    }
+    if (tid == 0) {
+        if (status) {   // 1: the reference would never return; 2: draw budget
             best_t = -1;
-            flags |= sh.misc[0] == 1 ? 8u : 16u;
+            flags |= status == 1 ? 8u : 16u;
         }
         if (best_t >= 0 && second <= best * (1.0 + 1e-9)) flags |= 4u;   // near-tie
         out_trial[frame] = best_t;
@@ -661,22 +692,62 @@ __global__ __launch_bounds__(kRBThreads) void ransac_batch_kernel(const double* 
     }
 }
 
+template <class IdxT>
+static hipError_t launch_ransac_typed(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
+                                      const int64_t* counts, int64_t max_n, int64_t words, uint64_t seed_base,
+                                      int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs,
+                                      double* abc, double* err, int32_t* trial, uint32_t* flags, int32_t* trace,
+                                      int trace_trials, int ablate, hipStream_t s) {
+    IdxT* sidx = reinterpret_cast<IdxT*>(rs.sidx);
+    hipLaunchKernelGGL(ransac_draw_kernel<IdxT>, dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words, s, pts, cap,
+                       counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace,
+                       trace ? trace_trials : 0, (int)words);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // eval LDS: the points when they fit beside the screen results (160 KiB per workgroup)
+    const size_t scr = sizeof(double) * (2 * (size_t)trials + 1);
+    const int64_t pts_words = (max_n + 1) & ~1ll;   // the doubles after the points stay 8-byte aligned
+    const size_t pts_b = sizeof(uint32_t) * (size_t)pts_words;
+    const bool lds_pts = pts_b + scr <= 150 * 1024;
+    const size_t dyn = (lds_pts ? pts_b : 0) + scr;
+    if (lds_pts) {
+        // dynamic LDS above 64 KiB needs the per-kernel opt-in (on the current device)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ransac_eval_kernel<IdxT, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((ransac_eval_kernel<IdxT, true>), dim3(frames), dim3(kRBEvalThreads), dyn, s, pts, packed,
+                           cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags, ablate,
+                           (int)pts_words);
+    } else {
+        hipLaunchKernelGGL((ransac_eval_kernel<IdxT, false>), dim3(frames), dim3(kRBEvalThreads), dyn, s, pts, packed,
+                           cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags, ablate, 0);
+    }
+    return hipGetLastError();
+}
+
+size_t ransac_sidx_bytes(int64_t max_n, int frames, int trials, int k) {
+    return (max_n <= 65535 ? 2 : 4) * (size_t)frames * (size_t)trials * (size_t)k;
+}
+
 hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
                                const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
-                               int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
-                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, int ablate,
-                               hipStream_t s) {
+                               int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs, double* abc,
+                               double* err, int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials,
+                               int ablate, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
-    if (k < 1 || k > kRBMaxK || cap > (int64_t)kRBBitmapWords * 32 || max_n > cap) return hipErrorInvalidValue;
-    // dynamic LDS: the set branch's bitmap (n bits) or the pool branch's list (n words), for the largest frame
+    if (k < 1 || k > kRBMaxK || trials > kRBMaxTrials || cap > (int64_t)kRBBitmapWords * 32 || max_n > cap)
+        return hipErrorInvalidValue;
+    // draw-kernel LDS: the set branch's bitmap (n bits) or the pool branch's list (n words), for the largest frame
     int64_t words = (max_n + 31) / 32;
     if (max_pool_n > words) words = max_pool_n;
     if (words < 1) words = 1;
-    const size_t dyn = sizeof(uint32_t) * ((size_t)words + 2 * (size_t)k);
-    hipLaunchKernelGGL(ransac_batch_kernel, dim3(frames), dim3(kRBThreads), dyn, s, pts, packed, cap, cp, counts,
-                       seed_base, first_frame, trials, k, abc, err, trial, flags, trace, trace ? trace_trials : 0, ablate,
-                       (int)words);
-    return hipGetLastError();
+    // the samples as u16 indices when every frame has < 65536 points
+    if (max_n <= 65535)
+        return launch_ransac_typed<uint16_t>(pts, packed, cap, cp, counts, max_n, words, seed_base, first_frame,
+                                             frames, trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate,
+                                             s);
+    return launch_ransac_typed<int32_t>(pts, packed, cap, cp, counts, max_n, words, seed_base, first_frame, frames,
+                                        trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate, s);
 }
 
 // keep1 plane fields of every frame (plane_fields, as the host's set_plane)

@@ -230,6 +230,7 @@ struct sv_batch {
     DevBuf mpts, rres;          // maskpoints (frames x mcap x 3 fp64) + counts; batched RANSAC results
     DevBuf mpk;                 // maskpoints packed (frames x mcap words x | y << 12 | d << 24): RANSAC's fp32 screen
     DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
+    DevBuf rsidx, rtri;         // batched RANSAC scratch: every trial's sample; trial records + frame status
     DevBuf fplanes;             // per-frame keep1 plane fields (FramePlane) for sv_batch_pipeline_planes
     DevBuf dplane;              // the FramePlane of a device plane (sv_batch_pipeline_dev)
     DevBuf pairL, pairR;        // rectified grey stereo pairs (frames x H x W each), SGBM input
@@ -437,7 +438,7 @@ int sv_batch_destroy(sv_batch* b) {
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks,
                       &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane,
-                      &b->pairL, &b->pairR})
+                      &b->pairL, &b->pairR, &b->rsidx, &b->rtri})
         if (x->p) (void)hipFree(x->p);
     b->sg.release();
     for (auto& ev : b->ev)
@@ -1113,8 +1114,13 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
         max_n = std::max(max_n, c);
         if (c >= k && c <= setsize) max_pool_n = std::max(max_pool_n, c);
     }
+    if (trials > 4096) return fail(SV_E_ARG, "sv_batch_ransac: trials <= 4096");
+    HIP_TRY(b->rsidx.ensure(std::max<size_t>(ransac_sidx_bytes(max_n, b->frames, trials, k), 4)));
+    HIP_TRY(b->rtri.ensure(sizeof(double) * 5 * F * (size_t)std::max(trials, 1) + sizeof(int32_t) * 2 * F));
+    const RansacScratch rs{b->rsidx.p, b->rtri.as<double>(),
+                           reinterpret_cast<int32_t*>(b->rtri.as<double>() + 5 * F * (size_t)std::max(trials, 1))};
     HIP_TRY(launch_ransac_batch(b->mpts.as<double>(), b->mpk.as<uint32_t>(), mcap, p, r.mcount, max_n, max_pool_n,
-                                seed_base, first_frame, b->frames, trials, k, r.abc, r.err, r.trial, r.flags, trace,
+                                seed_base, first_frame, b->frames, trials, k, rs, r.abc, r.err, r.trial, r.flags, trace,
                                 b->trace_trials, ransac_ablate(), b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;

@@ -120,13 +120,23 @@ __host__ __device__ inline int64_t ransac_setsize(int k) {
     }
     return setsize;
 }
+// Per-trial scratch of the two RANSAC kernels: every trial's sample (u16 when
+// every frame has < 65536 points, else int32: ransac_sidx_bytes), its record
+// (a, b, c, |abc|, flag: frames x trials x 5 doubles) and per frame the status
+// and the number of trials drawn (frames x 2 int32).
+struct RansacScratch {
+    void* sidx;
+    double* tri;
+    int32_t* fstat;
+};
+size_t ransac_sidx_bytes(int64_t max_n, int frames, int trials, int k);
 // max_n: the largest frame's point count; max_pool_n: the largest count that takes random.sample's pool
-// branch (n <= setsize(k)), 0 if none (both size the dynamic LDS).
+// branch (n <= setsize(k)), 0 if none (both size the draw kernel's LDS). trials <= 4096.
 hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
                                const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
-                               int64_t first_frame, int frames, int trials, int k, double* abc, double* err,
-                               int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials, int ablate,
-                               hipStream_t s);
+                               int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs, double* abc,
+                               double* err, int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials,
+                               int ablate, hipStream_t s);
 // out[i] = plane_fields of abc[3i..3i+2] (trial[i] < 0, or trial NULL and a NaN plane: valid = 0);
 // trial may be NULL (a device plane, e.g. the RCCL broadcast buffer).
 hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, const KParams& p, double thr,
