@@ -713,7 +713,7 @@ static hipError_t launch_ransac_typed(const double* pts, const uint32_t* packed,
     if (lds_pts) {
         // dynamic LDS above 64 KiB needs the per-kernel opt-in (on the current device)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ransac_eval_kernel<IdxT, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((ransac_eval_kernel<IdxT, true>), dim3(frames), dim3(kRBEvalThreads), dyn, s, pts, packed,
                            cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags, ablate,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The repo's one profiling entry point (GPU box; diagnostic, not product).
 
-  prof.py workload  --what k1,pipe,planes,ransac,sgbm [--frames N --reps R --mode M --chunk C]
+  prof.py workload  --what k1,pipe,planes,ransac,sgbm,prepass,raster [--frames N --reps R --mode M --chunk C]
         a fixed workload to run under rocprofv3 (nothing else on the GPU)
   prof.py time      --what ... [--sizes 1280,3840,4096] [--mode M]
         per-launch kernel ms (HIP events on the batch stream), one JSON line per size
@@ -42,14 +42,16 @@ WHAT_TIMING = {"k1": "project", "pipe": "pipeline", "planes": "pipeline", "sgbm"
 
 def _batch(frames, what, mode="auto"):
     from svx import batch as sb
-    pipe = any(w in what for w in ("pipe", "planes", "ransac", "sgbm"))
+    pipe = any(w in what for w in ("pipe", "planes", "ransac", "sgbm", "raster"))
     b = sb.Batch(frames, step=1, with_bgr=pipe, with_points=pipe)
     b.synth(0)
     if pipe:
         b.pipeline_mode(mode)
     if "sgbm" in what:
         b.synth_pair(0)
-    if "planes" in what or "ransac" in what:
+    if "raster" in what:
+        b.pipeline(sync=True)   # the points the raster draws
+    if any(w in what for w in ("planes", "ransac", "prepass")):
         sys.path.insert(0, os.path.join(REPO, "tests"))
         from test_prepass_cpu import carmask
         b.set_mask(carmask())
@@ -67,6 +69,11 @@ def _run(b, w, chunk=0, sync=False):
         b.ransac(seed_base=0, trials=600, sync=sync)
     elif w == "sgbm":
         b.sgbm(chunk=chunk or 32)
+    elif w == "prepass":
+        b.prepass("previous", sync=sync)
+    elif w == "raster":
+        b.road_raster(sync=False)
+        b.nonzero(sync=sync)
     else:
         raise SystemExit(f"unknown workload {w}")
 
