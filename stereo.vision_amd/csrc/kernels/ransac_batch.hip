@@ -622,59 +622,98 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
         for (int t = tid; t < T; t += kRBEvalThreads) scr[2 * t + 1] = ftri[(int64_t)t * kRBTri + 4] == 1.0 ? -1.0 : 0.0;
     }
     __syncthreads();
-    // the trials in order (uniform: every thread keeps the same decision state);
-    // those the screen cannot rule out are evaluated in fp64 by wave 0
-    double* red = scr + 2 * (int64_t)T;   // one double: wave 0's fp64 sum
-    double best = __builtin_huge_val(), second = __builtin_huge_val();
-    int best_t = -1;
-    uint32_t flags = 0;
-    double babc[3] = {0, 0, 0};
-    for (int t = 0; t < T; ++t) {   // LDS only, except for the (rare) fp64 evaluations
-        const double e32 = scr[2 * t], eb = scr[2 * t + 1];
-        if (eb < 0.0) {   // singular
-            flags |= 1u;
-            continue;
+    // Which trials can matter? The running best before trial t is exactly
+    // min_{j<t} e_j (a trial the sequential screen skips has e_j >= LB_j >
+    // best_{j-1}), and e_j <= UB_j = e32_j + eb_j, so every trial the
+    // sequential procedure evaluates has LB_t <= min_{j<t} UB_j (1 + 1e-9): the
+    // candidates below are a superset. Evaluating a superset cannot change the
+    // winner (the first strict minimum), the error or the near-tie flag (a
+    // trial the sequential procedure skips has e > best (1 + 1e-9)).
+    // Wave 0: exclusive prefix-min of UB in trial order, the candidates
+    // compacted in order into cand[]; then every wave evaluates candidates in
+    // fp64 (the same per-lane order as before: bit-identical errors), and one
+    // lane decides over them in trial order.
+    int32_t* cand = reinterpret_cast<int32_t*>(scr + 2 * (int64_t)T);
+    double* ce = reinterpret_cast<double*>(cand + ((T + 1) & ~1));
+    __shared__ uint32_t ncand_s, any_singular_s;
+    if (wave == 0) {
+        double carry = __builtin_huge_val();
+        uint32_t nc = 0, sing = 0;
+        for (int t0 = 0; t0 < T; t0 += kWave) {
+            const int t = t0 + lane;
+            const bool in = t < T;
+            const double e32 = in ? scr[2 * t] : 0.0, eb = in ? scr[2 * t + 1] : -1.0;
+            const bool singular = in && eb < 0.0;
+            const double ub = (in && !singular) ? e32 + eb : __builtin_huge_val();
+            double inc = ub;   // inclusive min-scan over the wave
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const double v = __shfl_up(inc, o, kWave);
+                if (lane >= o) inc = fmin(inc, v);
+            }
+            double ex = __shfl_up(inc, 1, kWave);
+            ex = lane == 0 ? carry : fmin(ex, carry);   // min over j < t
+            bool c = in && !singular && !(e32 - eb > ex * (1.0 + 2e-9));   // NaN / inf: a candidate
+            if (ablate & 4) c = in && !singular;
+            if (ablate & 1) c = false;                                     // DIAGNOSTIC 1: no evaluation
+            const uint64_t m = __ballot(c);
+            if (c) cand[nc + __builtin_popcountll(m & ((1ull << lane) - 1))] = t;
+            nc += (uint32_t)__builtin_popcountll(m);
+            sing |= __ballot(singular) != 0 ? 1u : 0u;
+            carry = fmin(carry, __shfl(inc, kWave - 1, kWave));
         }
-        bool full = (ablate & 4) || !(e32 - eb > best * (1.0 + 1e-9));   // NaN / inf: evaluate in fp64
-        if (ablate & 1) full = false;   // DIAGNOSTIC 1: no evaluation at all
-        if (!full) continue;
+        if (lane == 0) {
+            ncand_s = nc;
+            any_singular_s = sing;
+        }
+    }
+    __syncthreads();
+    const uint32_t nc = ncand_s;
+    for (uint32_t ci = wave; ci < nc; ci += kRBEvalThreads / 64) {
+        const int t = cand[ci];
         const double* tr = ftri + (int64_t)t * kRBTri;
-        const double a = tr[0], b = tr[1], c = tr[2], d = tr[3], fl = tr[4];
-        if (wave == 0) {
-            const IdxT* idx = fidx + (int64_t)t * k;
-            double sum = 0.0;
-            (void)e32;
-            for (int j0 = lane; j0 < k; j0 += 4 * kWave) {   // every gather in flight before the arithmetic
-                double qx[4], qy[4], qz[4];
+        const double a = tr[0], b = tr[1], c = tr[2], d = tr[3];
+        const IdxT* idx = fidx + (int64_t)t * k;
+        double sum = 0.0;
+        for (int j0 = lane; j0 < k; j0 += 4 * kWave) {   // every gather in flight before the arithmetic
+            double qx[4], qy[4], qz[4];
 #pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int j = j0 + kWave * v;
-                    const double* q = fp + 3 * (int64_t)(j < k ? (uint32_t)idx[j] : 0u);
-                    qx[v] = q[0];
-                    qy[v] = q[1];
-                    qz[v] = q[2];
-                }
-#pragma unroll
-                for (int v = 0; v < 4; ++v)
-                    if (j0 + kWave * v < k) sum += fabs((qx[v] * a + qy[v] * b + qz[v] * c - 1.0) / d);
+            for (int v = 0; v < 4; ++v) {
+                const int j = j0 + kWave * v;
+                const double* q = fp + 3 * (int64_t)(j < k ? (uint32_t)idx[j] : 0u);
+                qx[v] = q[0];
+                qy[v] = q[1];
+                qz[v] = q[2];
             }
 #pragma unroll
-            for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
-            if (lane == 0) red[0] = sum;
+            for (int v = 0; v < 4; ++v)
+                if (j0 + kWave * v < k) sum += fabs((qx[v] * a + qy[v] * b + qz[v] * c - 1.0) / d);
         }
-        __syncthreads();
-        const double e = red[0] / k;
-        __syncthreads();   // red is rewritten by the next evaluation
-        if (e < best) {   // trial order, strict <
-            second = best;
-            best = e;
-            best_t = t;
-            babc[0] = a;
-            babc[1] = b;
-            babc[2] = c;
-            flags = (flags & ~2u) | (fl == 2.0 ? 2u : 0u);
-        } else if (e < second) {
-            second = e;
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
+        if (lane == 0) ce[ci] = sum / k;
+    }
+    __syncthreads();
+    double best = __builtin_huge_val(), second = __builtin_huge_val();
+    int best_t = -1;
+    uint32_t flags = any_singular_s ? 1u : 0u;
+    double babc[3] = {0, 0, 0};
+    if (tid == 0) {
+        for (uint32_t ci = 0; ci < nc; ++ci) {   // trial order, strict <
+            const double e = ce[ci];
+            if (e < best) {
+                const int t = cand[ci];
+                const double* tr = ftri + (int64_t)t * kRBTri;
+                second = best;
+                best = e;
+                best_t = t;
+                babc[0] = tr[0];
+                babc[1] = tr[1];
+                babc[2] = tr[2];
+                flags = (flags & ~2u) | (tr[4] == 2.0 ? 2u : 0u);
+            } else if (e < second) {
+                second = e;
+            }
         }
     }
     if (tid == 0) {
@@ -705,7 +744,9 @@ static hipError_t launch_ransac_typed(const double* pts, const uint32_t* packed,
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // eval LDS: the points when they fit beside the screen results (160 KiB per workgroup)
-    const size_t scr = sizeof(double) * (2 * (size_t)trials + 1);
+    // per trial: screened mean + bound (2 doubles), candidate index and its fp64 error
+    const size_t scr = sizeof(double) * 2 * (size_t)trials + sizeof(int32_t) * ((size_t)trials + 1) +
+                       sizeof(double) * ((size_t)trials + 1);
     const int64_t pts_words = (max_n + 1) & ~1ll;   // the doubles after the points stay 8-byte aligned
     const size_t pts_b = sizeof(uint32_t) * (size_t)pts_words;
     const bool lds_pts = pts_b + scr <= 150 * 1024;
