@@ -809,7 +809,7 @@ __device__ __forceinline__ void fused_body(const PipeBuffers& bf, const RParams&
 }
 
 template <int STEP, int QP, bool PF, bool PF1 = false>
-__global__ __launch_bounds__(256) void resident_fused_kernel(PipeBuffers bf, RParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void resident_fused_kernel(PipeBuffers bf, RParams p) {
     __shared__ FusedShared<QP> sh;
     fused_body<STEP, QP, PF, PF1>(bf, p, sh);
 }

@@ -55,6 +55,8 @@ def _batch(frames, what, mode="auto"):
         sys.path.insert(0, os.path.join(REPO, "tests"))
         from test_prepass_cpu import carmask
         b.set_mask(carmask())
+    if "planes" in what:   # as bench.py: RANSAC planes of the cleaned frames (fill previous + mask)
+        b.prepass("previous", sync=True)
     return b
 
 
