@@ -8,8 +8,8 @@
   prof.py sweep     K1 launch shapes (--k1 qpl:nt,...) and pipeline chunk sizes (--modes, --chunks)
   prof.py ab        --modes resident,tiled --ablate 0,256 [--with-k1]
         in-process A/B of pipeline variants (SVX_ABLATE diagnostics give INVALID results: times only)
-  prof.py ab-lib    --libs a.so,b.so --what pipe,planes
-        A/B of two libsvx builds, one child process per build, alternating (SVX_LIB)
+  prof.py ab-lib    --libs a.so,b.so | --envs "K=V;K=V" --what pipe,planes
+        A/B of libsvx builds (SVX_LIB) or environment settings, one child process per variant, alternating
   prof.py pmc       --groups "SQ_INSTS_VALU SQ_WAVE_CYCLES;FETCH_SIZE;WRITE_SIZE" [--ablate 0,256]
                     [--out gpurun_out/pmc] [--traffic FRAMES] -- <workload args>
         one `rocprofv3 --pmc` pass per group (never combined with tracing), then the summary
@@ -173,22 +173,26 @@ def cmd_ab(a):
 
 
 def cmd_ab_lib(a):
-    libs = [os.path.join(REPO, x) for x in a.libs.split(",")]
-    res = {x: [] for x in libs}
+    """variants = libsvx builds (--libs) or environment settings (--envs "K=V,K=V;K=V"), one child each"""
+    if a.envs:
+        variants = [(v, dict(kv.split("=", 1) for kv in v.split(",") if kv)) for v in a.envs.split(";")]
+    else:
+        variants = [(os.path.relpath(os.path.join(REPO, x), REPO), {"SVX_LIB": os.path.join(REPO, x)})
+                    for x in a.libs.split(",")]
+    res = {name: [] for name, _ in variants}
     for r in range(a.rounds):
-        for lib in (libs if r % 2 == 0 else libs[::-1]):
-            env = dict(os.environ, SVX_LIB=lib)
+        for name, extra in (variants if r % 2 == 0 else variants[::-1]):
+            env = dict(os.environ, **extra)
             p = subprocess.run([sys.executable, __file__, "time", "--what", a.what, "--sizes", str(a.frames),
                                 "--reps", str(a.reps)], env=env, capture_output=True, text=True, timeout=600)
             if p.returncode != 0:
                 print(p.stderr[-2000:], file=sys.stderr)
                 sys.exit(p.returncode)
-            res[lib].append(json.loads(p.stdout.strip().splitlines()[-1]))
-            print(os.path.basename(lib), res[lib][-1], flush=True)
-    for lib in libs:
-        keys = [k for k in res[lib][0] if k.endswith("_ms")]
-        print(json.dumps({"lib": os.path.relpath(lib, REPO),
-                          **{k: round(statistics.median(x[k] for x in res[lib]), 4) for k in keys}}))
+            res[name].append(json.loads(p.stdout.strip().splitlines()[-1]))
+            print(name, res[name][-1], flush=True)
+    for name, _ in variants:
+        keys = [k for k in res[name][0] if k.endswith("_ms")]
+        print(json.dumps({"variant": name, **{k: round(statistics.median(x[k] for x in res[name]), 4) for k in keys}}))
 
 
 def _load_pmc(root):
@@ -348,7 +352,8 @@ def main():
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--with-k1", action="store_true")
     p = sp.add_parser("ab-lib")
-    p.add_argument("--libs", required=True)
+    p.add_argument("--libs", default="")
+    p.add_argument("--envs", default="")
     p.add_argument("--what", default="pipe")
     p.add_argument("--frames", type=int, default=4096)
     p.add_argument("--reps", type=int, default=5)
