@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../svx_device.h"
 #include "../svx_sgbm.h"
@@ -171,6 +172,10 @@ __global__ __launch_bounds__(256) void sgbm_hsum_kernel(SgbmK k, const uint8_t* 
 // ---------------------------------------------------------------------------
 // Vertical box sum with OpenCV's row rules, and the (0,-1) path.
 // ---------------------------------------------------------------------------
+// The operands of a path step never depend on the recurrence, so every walk
+// below keeps the next U steps' loads in flight (registers, clamped addresses:
+// the loads past a path's end are redundant) while it runs the current U steps.
+template <int U>
 __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint32_t* __restrict__ hvol,
                                                               uint32_t* __restrict__ cvol, uint32_t* __restrict__ l2vol,
                                                               uint32_t* __restrict__ flags, int frames) {
@@ -179,32 +184,51 @@ __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint3
     const int f = blockIdx.x / cols_blocks;
     const int xi = (blockIdx.x - f * cols_blocks) * wpb + (threadIdx.x >> 6);
     if (f >= frames || xi >= k.width1) return;
-    const int lane = lane_id(), H = k.H;
+    const int lane = lane_id(), H = k.H, SH2 = k.SH2;
     const size_t rs = (size_t)k.width1 * 64;
     const size_t base = (size_t)f * H * rs + (size_t)xi * 64 + lane;
     const uint32_t* hb = hvol + base;
     int c0 = 0, c1 = 0;
-    for (int kk = 0; kk <= k.SH2; ++kk) {
+    for (int kk = 0; kk <= SH2; ++kk) {
         const uint32_t h = hb[(size_t)min(kk, H - 1) * rs];
-        const int sc = kk == 0 ? k.SH2 + 1 : 1;
+        const int sc = kk == 0 ? SH2 + 1 : 1;
         c0 += lo16(h) * sc;
         c1 += hi16(h) * sc;
     }
     PathState st;
     bool ovf = false;
     const bool upd_col = xi > 0;
-    for (int y = 0; y < H; ++y) {
-        if (y > 0 && upd_col && y + k.SH2 < H) {
-            const uint32_t a = hb[(size_t)(y + k.SH2) * rs];
-            const uint32_t s = hb[(size_t)max(y - k.SH2 - 1, 0) * rs];
-            c0 += lo16(a) - lo16(s);
-            c1 += hi16(a) - hi16(s);
+    // step y adds row y + SH2 and drops row y - SH2 - 1 (OpenCV's rules, below)
+    const auto load = [&](int y, uint32_t& a, uint32_t& r) {
+        a = hb[(size_t)min(y + SH2, H - 1) * rs];
+        r = hb[(size_t)min(max(y - SH2 - 1, 0), H - 1) * rs];
+    };
+    uint32_t ca[U], cr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load(u, ca[u], cr[u]);
+    for (int y0 = 0; y0 < H; y0 += U) {
+        uint32_t na[U], nr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) load(y0 + U + u, na[u], nr[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int y = y0 + u;
+            if (y >= H) break;
+            if (y > 0 && upd_col && y + SH2 < H) {
+                c0 += lo16(ca[u]) - lo16(cr[u]);
+                c1 += hi16(ca[u]) - hi16(cr[u]);
+            }
+            const int cw0 = (int)(int16_t)c0, cw1 = (int)(int16_t)c1;
+            cvol[base + (size_t)y * rs] = pack16(cw0, cw1);
+            int L0, L1;
+            path_step(cw0, cw1, st, k.P1, k.P2, L0, L1, ovf);
+            l2vol[base + (size_t)y * rs] = pack16(L0, L1);
         }
-        const int cw0 = (int)(int16_t)c0, cw1 = (int)(int16_t)c1;
-        cvol[base + (size_t)y * rs] = pack16(cw0, cw1);
-        int L0, L1;
-        path_step(cw0, cw1, st, k.P1, k.P2, L0, L1, ovf);
-        l2vol[base + (size_t)y * rs] = pack16(L0, L1);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ca[u] = na[u];
+            cr[u] = nr[u];
+        }
     }
     if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
 }
@@ -212,6 +236,7 @@ __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint3
 // ---------------------------------------------------------------------------
 // Diagonal paths: dir 1 from (x-1, y-1), dir 3 from (x+1, y-1).
 // ---------------------------------------------------------------------------
+template <int U>
 __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t* __restrict__ cvol,
                                                           uint32_t* __restrict__ l1vol, uint32_t* __restrict__ l3vol,
                                                           uint32_t* __restrict__ flags, int frames) {
@@ -232,25 +257,32 @@ __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t*
         xi = dir ? k.width1 - 1 : 0;
         y = p - k.width1 + 1;
     }
-    const int dx = dir ? -1 : 1;
+    // the path: cells (xi + t * dx, y + t), t < len
+    const int len = min(k.H - y, dir ? xi + 1 : k.width1 - xi);
     const int lane = lane_id();
     const size_t rs = (size_t)k.width1 * 64;
-    const size_t fb = (size_t)f * k.H * rs + lane;
+    const size_t a0 = (size_t)f * k.H * rs + (size_t)y * rs + (size_t)xi * 64 + lane;
+    const size_t step = dir ? rs - 64 : rs + 64;
     uint32_t* out = dir ? l3vol : l1vol;
     PathState st;
     bool ovf = false;
-    uint32_t c = 0;
-    if (xi >= 0 && xi < k.width1 && y < k.H) c = cvol[fb + (size_t)y * rs + (size_t)xi * 64];
-    while (xi >= 0 && xi < k.width1 && y < k.H) {
-        const int nx = xi + dx, ny = y + 1;
-        uint32_t cn = 0;
-        if (nx >= 0 && nx < k.width1 && ny < k.H) cn = cvol[fb + (size_t)ny * rs + (size_t)nx * 64];
-        int L0, L1;
-        path_step(lo16(c), hi16(c), st, k.P1, k.P2, L0, L1, ovf);
-        out[fb + (size_t)y * rs + (size_t)xi * 64] = pack16(L0, L1);
-        c = cn;
-        xi = nx;
-        y = ny;
+    uint32_t cc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cc[u] = cvol[a0 + (size_t)min(u, len - 1) * step];
+    for (int t0 = 0; t0 < len; t0 += U) {
+        uint32_t nc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) nc[u] = cvol[a0 + (size_t)min(t0 + U + u, len - 1) * step];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = t0 + u;
+            if (t >= len) break;
+            int L0, L1;
+            path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1, ovf);
+            out[a0 + (size_t)t * step] = pack16(L0, L1);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) cc[u] = nc[u];
     }
     if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
 }
@@ -258,6 +290,7 @@ __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t*
 // ---------------------------------------------------------------------------
 // Row kernel: (-1,0) path + sum, (+1,0) path + selection, left-right check.
 // ---------------------------------------------------------------------------
+template <int U>
 __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* __restrict__ cvol,
                                                          uint32_t* __restrict__ l1p, const uint32_t* __restrict__ l2vol,
                                                          const uint32_t* __restrict__ l3vol, int16_t* __restrict__ d16,
@@ -281,57 +314,102 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
     const size_t rs = (size_t)k.width1 * 64;
     const size_t rb = ((size_t)f * k.H + y) * rs + lane;
     bool ovf = false;
+    const int n = k.width1;
     // pass A: x ascending, direction (-1, 0); P = sat16(L0 + L1 + L2 + L3) replaces L1
     {
         PathState st;
-        for (int xi = 0; xi < k.width1; ++xi) {
-            const size_t o = rb + (size_t)xi * 64;
-            const uint32_t c = cvol[o], a = l1p[o], b = l2vol[o], e = l3vol[o];
-            int L0, L1;
-            path_step(lo16(c), hi16(c), st, k.P1, k.P2, L0, L1, ovf);
-            l1p[o] = pack16(sat16(L0 + lo16(a) + lo16(b) + lo16(e)), sat16(L1 + hi16(a) + hi16(b) + hi16(e)));
+        uint32_t cc[U], ca[U], cb[U], ce[U];
+        const auto load = [&](int xi, uint32_t& c, uint32_t& a, uint32_t& b, uint32_t& e) {
+            const size_t o = rb + (size_t)min(xi, n - 1) * 64;
+            c = cvol[o];
+            a = l1p[o];
+            b = l2vol[o];
+            e = l3vol[o];
+        };
+#pragma unroll
+        for (int u = 0; u < U; ++u) load(u, cc[u], ca[u], cb[u], ce[u]);
+        for (int x0 = 0; x0 < n; x0 += U) {
+            uint32_t nc[U], na[U], nb[U], ne[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) load(x0 + U + u, nc[u], na[u], nb[u], ne[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int xi = x0 + u;
+                if (xi >= n) break;
+                int L0, L1;
+                path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1, ovf);
+                l1p[rb + (size_t)xi * 64] = pack16(sat16(L0 + lo16(ca[u]) + lo16(cb[u]) + lo16(ce[u])),
+                                                   sat16(L1 + hi16(ca[u]) + hi16(cb[u]) + hi16(ce[u])));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                cc[u] = nc[u];
+                ca[u] = na[u];
+                cb[u] = nb[u];
+                ce[u] = ne[u];
+            }
         }
     }
     // pass B: x descending, direction (+1, 0), S = sat16(P + L), winner per pixel
     {
         PathState st;
         const int d0 = 2 * lane;
-        for (int xi = k.width1 - 1; xi >= 0; --xi) {
-            const size_t o = rb + (size_t)xi * 64;
-            const uint32_t c = cvol[o], pp = l1p[o];
-            int L0, L1;
-            path_step(lo16(c), hi16(c), st, k.P1, k.P2, L0, L1, ovf);
-            const int S0 = sat16(lo16(pp) + L0), S1 = sat16(hi16(pp) + L1);
-            const int key = min(((S0 + 32768) << 7) | d0, ((S1 + 32768) << 7) | (d0 + 1));
-            const int kmin = wave_min_i32(key);
-            const int minS = (kmin >> 7) - 32768, best = kmin & 127;
-            if (k.uniq > 0) {
-                const bool bad = (S0 * (100 - k.uniq) < minS * 100 && abs(best - d0) > 1) ||
-                                 (S1 * (100 - k.uniq) < minS * 100 && abs(best - d0 - 1) > 1);
-                if (__any(bad)) continue;
-            }
-            if (minS == kMaxCost) {
-                // every S saturated: OpenCV's strict "<" never fires, bestDisp stays -1 and the
-                // pixel gets (-1) * 16 = INVALID; disp2 is not touched (its cost test is strict too)
-                continue;
-            }
-            const uint32_t spk = pack16(S0, S1);
-            int dd = best * kSgScale;
-            if (best > 0 && best < kSgD - 1) {
-                const uint32_t wm = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best - 1) >> 1);
-                const uint32_t wp = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best + 1) >> 1);
-                const int Sm = (best - 1) & 1 ? hi16(wm) : lo16(wm);
-                const int Sp = (best + 1) & 1 ? hi16(wp) : lo16(wp);
-                const int den = max(Sm + Sp - 2 * minS, 1);
-                dd = best * kSgScale + ((Sm - Sp) * kSgScale + den) / (den * 2);
-            }
-            if (lane == 0) {
-                const int x2 = xi + k.minX1 - best;
-                if (d2cost[x2] > minS) {
-                    d2cost[x2] = (int16_t)minS;
-                    disp2[x2] = (int16_t)best;
+        uint32_t cc[U], cp[U];
+        // step j visits xi = n - 1 - j (pass A's P of every cell is stored before these loads)
+        const auto load = [&](int j, uint32_t& c, uint32_t& pp) {
+            const size_t o = rb + (size_t)max(n - 1 - j, 0) * 64;
+            c = cvol[o];
+            pp = l1p[o];
+        };
+#pragma unroll
+        for (int u = 0; u < U; ++u) load(u, cc[u], cp[u]);
+        for (int j0 = 0; j0 < n; j0 += U) {
+            uint32_t nc[U], np[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) load(j0 + U + u, nc[u], np[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int xi = n - 1 - (j0 + u);
+                if (xi < 0) break;
+                int L0, L1;
+                path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1, ovf);
+                const int S0 = sat16(lo16(cp[u]) + L0), S1 = sat16(hi16(cp[u]) + L1);
+                const int key = min(((S0 + 32768) << 7) | d0, ((S1 + 32768) << 7) | (d0 + 1));
+                const int kmin = wave_min_i32(key);
+                const int minS = (kmin >> 7) - 32768, best = kmin & 127;
+                if (k.uniq > 0) {
+                    const bool bad = (S0 * (100 - k.uniq) < minS * 100 && abs(best - d0) > 1) ||
+                                     (S1 * (100 - k.uniq) < minS * 100 && abs(best - d0 - 1) > 1);
+                    if (__any(bad)) continue;
                 }
-                disp1[xi + k.minX1] = (int16_t)dd;
+                if (minS == kMaxCost) {
+                    // every S saturated: OpenCV's strict "<" never fires, bestDisp stays -1 and the
+                    // pixel gets (-1) * 16 = INVALID; disp2 is not touched (its cost test is strict too)
+                    continue;
+                }
+                const uint32_t spk = pack16(S0, S1);
+                int dd = best * kSgScale;
+                if (best > 0 && best < kSgD - 1) {
+                    const uint32_t wm = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best - 1) >> 1);
+                    const uint32_t wp = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best + 1) >> 1);
+                    const int Sm = (best - 1) & 1 ? hi16(wm) : lo16(wm);
+                    const int Sp = (best + 1) & 1 ? hi16(wp) : lo16(wp);
+                    const int den = max(Sm + Sp - 2 * minS, 1);
+                    dd = best * kSgScale + ((Sm - Sp) * kSgScale + den) / (den * 2);
+                }
+                if (lane == 0) {
+                    const int x2 = xi + k.minX1 - best;
+                    if (d2cost[x2] > minS) {
+                        d2cost[x2] = (int16_t)minS;
+                        disp2[x2] = (int16_t)best;
+                    }
+                    disp1[xi + k.minX1] = (int16_t)dd;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                cc[u] = nc[u];
+                cp[u] = np[u];
             }
         }
     }
@@ -597,6 +675,12 @@ __global__ void synth_pair_kernel(uint8_t* __restrict__ left, uint8_t* __restric
 
 }  // namespace
 
+// steps each path walk keeps in flight (SVX_SGBM_PF: 1, 4 or 8; A/B only; 16 measured no faster)
+static int sgbm_prefetch() {
+    const char* e = std::getenv("SVX_SGBM_PF");
+    return e && *e ? std::atoi(e) : 8;
+}
+
 bool sgbm_supported(const SgbmK& k) {
     return k.width1 > k.SW2 && k.W <= 2048 && k.H >= 1 && k.SW2 >= 0 && k.SW2 <= 31;
 }
@@ -612,13 +696,24 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
     const size_t lds1 = sizeof(uint32_t) * (5 * (size_t)k.W + 4 * (2 * k.SW2 + 1) * 64);
     hipLaunchKernelGGL(sgbm_hsum_kernel, dim3(frames * H), dim3(256), lds1, st, k, left, right, s.hl1, frames);
     const int cb = (k.width1 + 3) / 4;
-    hipLaunchKernelGGL(sgbm_vertical_kernel, dim3(frames * cb), dim3(256), 0, st, k, s.hl1, s.c, s.l2, s.flags, frames);
     const int paths = 2 * (k.width1 + H - 1) * frames;
-    hipLaunchKernelGGL(sgbm_diag_kernel, dim3((paths + 3) / 4), dim3(256), 0, st, k, s.c, s.hl1, s.l3, s.flags,
-                       frames);
     const size_t lds4 = sizeof(int16_t) * 3 * (size_t)k.W * 4;
-    hipLaunchKernelGGL(sgbm_row_kernel, dim3((frames * H + 3) / 4), dim3(256), lds4, st, k, s.c, s.hl1, s.l2, s.l3,
-                       s.d16, s.flags, frames);
+    const int pf = sgbm_prefetch();
+#define SVX_SGBM_WALKS(U)                                                                                         \
+    hipLaunchKernelGGL(sgbm_vertical_kernel<U>, dim3(frames * cb), dim3(256), 0, st, k, s.hl1, s.c, s.l2, s.flags, \
+                       frames);                                                                                    \
+    hipLaunchKernelGGL(sgbm_diag_kernel<U>, dim3((paths + 3) / 4), dim3(256), 0, st, k, s.c, s.hl1, s.l3, s.flags, \
+                       frames);                                                                                    \
+    hipLaunchKernelGGL(sgbm_row_kernel<U>, dim3((frames * H + 3) / 4), dim3(256), lds4, st, k, s.c, s.hl1, s.l2,   \
+                       s.l3, s.d16, s.flags, frames)
+    if (pf == 1) {
+        SVX_SGBM_WALKS(1);
+    } else if (pf == 4) {
+        SVX_SGBM_WALKS(4);
+    } else {
+        SVX_SGBM_WALKS(8);
+    }
+#undef SVX_SGBM_WALKS
     return hipGetLastError();
 }
 
