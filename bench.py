@@ -316,8 +316,15 @@ def extras(b, args, with_cpu):
     b.reset_timing()
     ms = _timed(b, lambda: b.pipeline_planes(sync=False), 3)
     k_ms, k_n = b.timing("pipeline")
-    ex["pipeline_frame_planes"] = {"ms_per_batch": round(ms, 3), "gpu_ms_per_call": round(k_ms / max(k_n, 1), 4),
-                                   "frames": b.frames, "kept_points": int(b.read_counts()[:, 2].sum()),
+    kept = int(b.read_counts()[:, 2].sum())
+    fp_bytes = 4 * b.Ng * b.frames + 20 * kept + 4096 * b.frames   # the config-4 accounting, this call's points
+    fp_s = k_ms / max(k_n, 1) / 1e3
+    ex["pipeline_frame_planes"] = {"ms_per_batch": round(ms, 3), "gpu_ms_per_call": round(fp_s * 1e3, 4),
+                                   "frames": b.frames, "kept_points": kept,
+                                   "algorithmic_bytes_per_call": fp_bytes,
+                                   "frac": round(fp_bytes / fp_s / 1e9 / PEAK_HBM_GBS, 4) if fp_s > 0 else None,
+                                   "workload": "the prepass-cleaned frames (fill previous + carmask), each with its "
+                                               "own RANSAC plane (threshold 0.05, hist thr 10)",
                                    "kernels": "frame_planes_kernel + resident_fused_kernel (each frame's plane)"
                                    if b.frames >= 512 else "frame_planes_kernel + tiled kernels"}
 
