@@ -6,7 +6,7 @@
   prof.py time      --what ... [--sizes 1280,3840,4096] [--mode M]
         per-launch kernel ms (HIP events on the batch stream), one JSON line per size
   prof.py sweep     K1 launch shapes (--k1 qpl:nt,...) and pipeline chunk sizes (--modes, --chunks)
-  prof.py ab        --modes resident,tiled --ablate 0,256 [--with-k1]
+  prof.py ab        --modes resident,tiled --ablate 0,256 [--env NAME=v1,v2] [--what pipe|planes] [--with-k1]
         in-process A/B of pipeline variants (SVX_ABLATE diagnostics give INVALID results: times only)
   prof.py ab-lib    --libs a.so,b.so | --envs "K=V;K=V" --what pipe,planes
         A/B of libsvx builds (SVX_LIB) or environment settings, one child process per variant, alternating
@@ -147,28 +147,37 @@ def cmd_sweep(a):
 
 
 def cmd_ab(a):
-    b = _batch(a.frames, "k1,pipe")
-    variants = [(m, int(x)) for m in a.modes.split(",") for x in a.ablate.split(",")]
+    b = _batch(a.frames, "k1,pipe,planes" if a.what == "planes" else "k1,pipe")
+    if a.what == "planes":
+        b.ransac(seed_base=0, trials=600)
+    ev = a.env.split("=", 1) if a.env else None   # NAME=v1,v2,... : one variant per value (in-process A/B)
+    vals = ev[1].split(",") if ev else [""]
+    variants = [(m, int(x), v) for m in a.modes.split(",") for x in a.ablate.split(",") for v in vals]
     if a.with_k1:   # the box's HBM speed beside the variants, to compare runs across boxes
-        variants.append(("k1", 0))
+        variants.append(("k1", 0, ""))
     res = {v: [] for v in variants}
     for _ in range(a.rounds):
-        for mode, abl in variants:
+        for mode, abl, v in variants:
             os.environ["SVX_ABLATE"] = str(abl)
+            if ev and v:
+                os.environ[ev[0]] = v
             k1 = mode == "k1"
             if not k1:
                 b.pipeline_mode(mode)
-            w = "k1" if k1 else "pipe"
+            w = "k1" if k1 else a.what
             _run(b, w, sync=True)
             b.reset_timing()
             for _ in range(a.reps):
                 _run(b, w)
             ms, n = b.timing(WHAT_TIMING[w])
-            res[(mode, abl)].append(ms / n)
+            res[(mode, abl, v)].append(ms / n)
     os.environ["SVX_ABLATE"] = "0"
-    for (mode, abl), v in res.items():
-        print(json.dumps({"mode": mode, "ablate": abl, "median_ms": round(statistics.median(v), 4),
-                          "min_ms": round(min(v), 4), "max_ms": round(max(v), 4)}), flush=True)
+    if ev:
+        os.environ.pop(ev[0], None)
+    for (mode, abl, v), t in res.items():
+        print(json.dumps({"mode": mode, "ablate": abl, "env": f"{ev[0]}={v}" if ev and v else "",
+                          "median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
+                          "max_ms": round(max(t), 4)}), flush=True)
     b.close()
 
 
@@ -348,6 +357,8 @@ def main():
     p.add_argument("--frames", type=int, default=4096)
     p.add_argument("--modes", default="resident")
     p.add_argument("--ablate", default="0")
+    p.add_argument("--env", default="", help="NAME=v1,v2: an environment knob read per call, one variant per value")
+    p.add_argument("--what", default="pipe", choices=["pipe", "planes"])
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--with-k1", action="store_true")
