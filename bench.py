@@ -79,6 +79,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--traffic-pipeline", default=os.path.join(REPO, "profiles", "traffic_pipeline.json"))
+    ap.add_argument("--traffic-planes", default=os.path.join(REPO, "profiles", "traffic_planes.json"))
     return ap.parse_args(argv)
 
 
@@ -325,6 +326,7 @@ def extras(b, args, with_cpu):
                                    "frac": round(fp_bytes / fp_s / 1e9 / PEAK_HBM_GBS, 4) if fp_s > 0 else None,
                                    "workload": "the prepass-cleaned frames (fill previous + carmask), each with its "
                                                "own RANSAC plane (threshold 0.05, hist thr 10)",
+                                   "traffic": pipeline_traffic(args.traffic_planes, b.frames, args.step),
                                    "kernels": "frame_planes_kernel + resident_fused_kernel (each frame's plane)"
                                    if b.frames >= 512 else "frame_planes_kernel + tiled kernels"}
 
