@@ -286,15 +286,19 @@ int sv_batch_read_maskpoints(sv_batch* b, int frame, double* xyz, int64_t cap, i
 int sv_batch_ransac_trace(sv_batch* b, int trials);
 int sv_batch_read_ransac_trace(sv_batch* b, int frame, int32_t* out, int64_t cap, int* out_trials, int* out_k);
 
-/* Stereo pairs resident in HBM (frames x H x W grey left / right) and the
- * batched disparity stage: sv_batch_sgbm runs functions.py:104-128 (no crop)
- * on every pair and writes the batch's disparity (frames x H x W u8), the
- * input of the pre-pass, K1 and the pipeline. chunk = frames per cost-volume
- * chunk (0 = 32; 4 x 125 MB of int16 volumes per 1024 x 544 frame).
- * Synchronous per chunk (the int16 range flags are read back).
+/* Stereo pairs resident in HBM (frames x Hp x Wp grey left / right) and the
+ * batched disparity stage: sv_batch_sgbm runs functions.py:104-128 on every
+ * pair and writes the batch's disparity (frames x H x W u8), the input of the
+ * pre-pass, K1 and the pipeline. The pairs have the batch's shape (no crop)
+ * unless sv_batch_pair_shape(b, Hp, Wp) sets the uncropped one: then the batch
+ * (H = min(390, Hp), W = Wp - 135) receives disparity_scaled[0:390, 135:Wp],
+ * crop_disparity=True (functions.py:122-124). Wp % 8 == 0. chunk = frames per
+ * cost-volume chunk (0 = 32; 4 x 125 MB of int16 volumes per 1024 x 544
+ * frame). Synchronous per chunk (the int16 range flags are read back).
  * sv_batch_synth_pair: synthetic rectified pairs for global frame ids
  * first.., generated on the device (row y's true disparity is the synthetic
  * road's, halved: clamp(floor(3(y - 200) / 10), 0, 127)). */
+int sv_batch_pair_shape(sv_batch* b, int H, int W);
 int sv_batch_synth_pair(sv_batch* b, int64_t first_frame_id);
 int sv_batch_upload_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t* R);
 int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int chunk);

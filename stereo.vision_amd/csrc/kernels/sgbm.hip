@@ -597,7 +597,7 @@ __global__ __launch_bounds__(256) void sgbm_out_kernel(SgbmK k, const int16_t* _
     const int oy = y, ox = x - k.out_c0;
     if (oy >= k.out_rows || ox < 0 || ox >= k.out_cols) return;
     const int q = v > 0 ? v >> 4 : 0;   // TOZERO, then (d / 16.).astype(uint8)
-    out[f * (int64_t)k.out_rows * k.out_cols + (int64_t)oy * k.out_cols + ox] = (uint8_t)(int)((double)q * k.scale);
+    out[f * (int64_t)k.out_rows * k.out_stride + (int64_t)oy * k.out_stride + ox] = (uint8_t)(int)((double)q * k.scale);
 }
 
 // ---------------------------------------------------------------------------

@@ -233,7 +233,8 @@ struct sv_batch {
     DevBuf rsidx, rtri;         // batched RANSAC scratch: every trial's sample; trial records + frame status
     DevBuf fplanes;             // per-frame keep1 plane fields (FramePlane) for sv_batch_pipeline_planes
     DevBuf dplane;              // the FramePlane of a device plane (sv_batch_pipeline_dev)
-    DevBuf pairL, pairR;        // rectified grey stereo pairs (frames x H x W each), SGBM input
+    DevBuf pairL, pairR;        // rectified grey stereo pairs (frames x pairH x pairW each), SGBM input
+    int pairH = 0, pairW = 0;   // the pairs' shape: the batch's (H, W), or (Hp, Wp) whose crop is the batch
     SgbmBufs sg;                // SGBM scratch for one chunk of frames
     int64_t mcap = 0;
     int trace_trials = 0, trace_k = 0, traced_trials = 0;   // requested; k and trials of the recorded trace
@@ -1421,6 +1422,7 @@ int make_sgbm(int H, int W, const sv_sgbm_params* prm, int max_disparity, int cr
     k->out_rows = crop ? std::min(390, H) : H;
     k->out_cols = crop ? std::max(W - 135, 0) : W;
     k->out_c0 = crop ? 135 : 0;
+    k->out_stride = k->out_cols;
     k->scale = 256. / max_disparity;
     if (H < 1 || W <= kSgD || !sgbm_supported(*k))
         return fail(SV_E_ARG, "SGBM needs 1 <= H, %d + blockSize/2 < W <= 2048 (H=%d W=%d)", kSgD, H, W);
@@ -1562,15 +1564,45 @@ int sv_disparity(const uint8_t* L, const uint8_t* R, int H, int W, const sv_sgbm
     return SV_OK;
 }
 
+// the pairs' shape: the batch's own, unless sv_batch_pair_shape chose the uncropped one
+static void pair_shape(const sv_batch* b, int* H, int* W) {
+    *H = b->pairH ? b->pairH : b->H;
+    *W = b->pairW ? b->pairW : b->Wu;
+}
+
+int sv_batch_pair_shape(sv_batch* b, int H, int W) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    const bool own = H == b->H && W == b->Wu;
+    // functions.py:122-124: disparity_scaled[0:390, 135:W] of an H x W pair
+    if (!own && !(W > 135 && W - 135 == b->Wu && std::min(390, H) == b->H))
+        return fail(SV_E_ARG, "pair shape %d x %d: the batch (%d x %d) must be the pair's shape or its crop "
+                              "[0:390, 135:W]", H, W, b->H, b->Wu);
+    if (!own && W % 8) return fail(SV_E_ARG, "batched SGBM needs the pair width %% 8 == 0 (W=%d)", W);
+    int h0, w0;
+    pair_shape(b, &h0, &w0);
+    if (h0 != H || w0 != W) {   // a new shape: the pairs are uploaded again
+        for (DevBuf* x : {&b->pairL, &b->pairR}) {
+            if (x->p) (void)hipFree(x->p);
+            x->p = nullptr;
+            x->bytes = 0;
+        }
+    }
+    b->pairH = own ? 0 : H;
+    b->pairW = own ? 0 : W;
+    return SV_OK;
+}
+
 int sv_batch_synth_pair(sv_batch* b, int64_t first_frame_id) {
     if (!b) return fail(SV_E_ARG, "null batch");
-    if (b->Wu != b->W) return fail(SV_E_ARG, "batched SGBM needs W %% 8 == 0 (W=%d)", b->Wu);
-    if (b->W + kSgD > 4096) return fail(SV_E_ARG, "synthetic pairs need W <= %d", 4096 - kSgD);
+    int H, W;
+    pair_shape(b, &H, &W);
+    if (W % 8) return fail(SV_E_ARG, "batched SGBM needs W %% 8 == 0 (W=%d)", W);
+    if (W + kSgD > 4096) return fail(SV_E_ARG, "synthetic pairs need W <= %d", 4096 - kSgD);
     HIP_TRY(hipSetDevice(b->device));
-    const size_t px = (size_t)b->H * b->W * b->frames;
+    const size_t px = (size_t)H * W * b->frames;
     HIP_TRY(b->pairL.ensure(px));
     HIP_TRY(b->pairR.ensure(px));
-    HIP_TRY(launch_synth_pair(b->pairL.as<uint8_t>(), b->pairR.as<uint8_t>(), b->H, b->W, b->frames, first_frame_id,
+    HIP_TRY(launch_synth_pair(b->pairL.as<uint8_t>(), b->pairR.as<uint8_t>(), H, W, b->frames, first_frame_id,
                               b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
@@ -1578,9 +1610,11 @@ int sv_batch_synth_pair(sv_batch* b, int64_t first_frame_id) {
 
 int sv_batch_upload_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t* R) {
     if (!b || !L || !R || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "sv_batch_upload_pair: bad args");
-    if (b->Wu != b->W) return fail(SV_E_ARG, "batched SGBM needs W %% 8 == 0 (W=%d)", b->Wu);
+    int H, W;
+    pair_shape(b, &H, &W);
+    if (W % 8) return fail(SV_E_ARG, "batched SGBM needs W %% 8 == 0 (W=%d)", W);
     HIP_TRY(hipSetDevice(b->device));
-    const size_t px = (size_t)b->H * b->W;
+    const size_t px = (size_t)H * W;
     HIP_TRY(b->pairL.ensure(px * b->frames));
     HIP_TRY(b->pairR.ensure(px * b->frames));
     HIP_TRY(hipMemcpyAsync(b->pairL.as<uint8_t>() + px * frame, L, px, hipMemcpyHostToDevice, b->stream));
@@ -1592,13 +1626,17 @@ int sv_batch_upload_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t
 int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int chunk) {
     if (!b) return fail(SV_E_ARG, "null batch");
     if (!b->pairL.p || !b->pairR.p) return fail(SV_E_STATE, "no stereo pairs (sv_batch_synth_pair / upload_pair)");
+    int H, W;
+    pair_shape(b, &H, &W);
+    const int crop = b->pairW ? 1 : 0;   // the batch is the pair's [0:390, 135:W] (sv_batch_pair_shape)
     SgbmK k;
-    if (int rc = make_sgbm(b->H, b->W, prm, max_disparity, 0, &k)) return rc;
+    if (int rc = make_sgbm(H, W, prm, max_disparity, crop, &k)) return rc;
+    k.out_stride = b->W;   // the batch's row stride (a cropped 889-wide row is stored in 896 bytes)
     HIP_TRY(hipSetDevice(b->device));
     if (chunk <= 0) chunk = 32;
     chunk = std::min(chunk, b->frames);
     HIP_TRY(b->sg.ensure(k, chunk));
-    const size_t px = (size_t)k.frame_px;
+    const size_t px = (size_t)k.frame_px, opx = (size_t)b->H * b->W;
     int t0, t1;
     HIP_TRY(hipEventRecord(b->ev[4], b->stream));
     HIP_TRY(b->timed_event(&t0));
@@ -1606,7 +1644,7 @@ int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int
         const int n = std::min(chunk, b->frames - f0);
         HIP_TRY(launch_sgbm_compute(k, b->pairL.as<uint8_t>() + px * f0, b->pairR.as<uint8_t>() + px * f0, n,
                                     b->sg.scratch(), b->stream));
-        HIP_TRY(launch_speckle_scale(k, n, b->sg.scratch(), b->disp.as<uint8_t>() + px * f0, nullptr, b->stream));
+        HIP_TRY(launch_speckle_scale(k, n, b->sg.scratch(), b->disp.as<uint8_t>() + opx * f0, nullptr, b->stream));
         if (int rc = sgbm_check_flags(b->sg, n, b->stream)) return rc;
     }
     HIP_TRY(b->timed_event(&t1));

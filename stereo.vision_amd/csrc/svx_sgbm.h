@@ -17,6 +17,7 @@ struct SgbmK {
     int64_t frame_px;
     int new_val, max_size, max_diff;  // filterSpeckles
     int out_rows, out_cols, out_c0;   // scaled output geometry (crop: 390 x (W - 135) at column 135)
+    int out_stride;                   // bytes between output rows (>= out_cols); a frame is out_rows of them
     double scale;                     // 256. / max_disparity
 };
 

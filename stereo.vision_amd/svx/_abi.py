@@ -82,6 +82,7 @@ SIGNATURES = {
     "sv_sgbm_compute": [P, P, I, I, P, P],
     "sv_filter_speckles": [P, I, I, I, I, I],
     "sv_disparity": [P, P, I, I, P, I, I, P, P, P],
+    "sv_batch_pair_shape": [P, I, I],
     "sv_batch_synth_pair": [P, I64],
     "sv_batch_upload_pair": [P, I, P, P],
     "sv_batch_sgbm": [P, P, I, I],

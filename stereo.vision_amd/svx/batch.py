@@ -134,6 +134,13 @@ class Batch:
         _abi.call("sv_batch_sync", self._h)
 
     # -- disparity stage (functions.py:104-128) ------------------------------------
+    def pair_shape(self, H, W):
+        """The stereo pairs' shape: the batch's own (default), or an H x W pair
+        whose crop_disparity=True output [0:390, 135:W] is the batch
+        (functions.py:122-124)."""
+        _abi.call("sv_batch_pair_shape", self._h, int(H), int(W))
+        self._pair = (int(H), int(W))
+
     def synth_pair(self, first_frame_id=0):
         """Synthetic rectified grey pairs for global frame ids first.. (device)."""
         _abi.call("sv_batch_synth_pair", self._h, int(first_frame_id))
@@ -141,12 +148,14 @@ class Batch:
     def upload_pair(self, frame, left, right):
         L = np.ascontiguousarray(left, np.uint8)
         R = np.ascontiguousarray(right, np.uint8)
-        if L.shape != (self.H, self.W) or R.shape != (self.H, self.W):
-            raise ValueError(f"pair must be {self.H}x{self.W}")
+        shape = getattr(self, "_pair", (self.H, self.W))
+        if L.shape != shape or R.shape != shape:
+            raise ValueError(f"pair must be {shape[0]}x{shape[1]}")
         _abi.call("sv_batch_upload_pair", self._h, frame, _abi.ptr(L), _abi.ptr(R))
 
     def sgbm(self, max_disparity=128, chunk=0, **params):
-        """functions.disparity (no crop) of every pair -> the batch's disparity."""
+        """functions.disparity of every pair -> the batch's disparity (cropped
+        when pair_shape() set the uncropped pair shape)."""
         from .disparity import sgbm_params
         prm = sgbm_params(**params)
         _abi.call("sv_batch_sgbm", self._h, ctypes.byref(prm), int(max_disparity), int(chunk))

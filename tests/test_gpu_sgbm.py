@@ -146,6 +146,34 @@ def test_batch_sgbm_matches_oracle(sv):
         assert np.array_equal(b.read_disp(3), osg.disparity(L, R))
 
 
+def test_batch_sgbm_crop(sv):
+    """crop_disparity=True (functions.py:122-124) in the batch: 544 x 1024 pairs,
+    a 390 x 889 batch (rows stored at a stride of 896) receiving
+    disparity_scaled[0:390, 135:1024]; then the pre-pass and the pipeline of
+    the cropped frames run fused (tests/test_gpu_anywidth.py)."""
+    Hp, Wp, n, first = 544, 1024, 3, 40
+    with sv.batch.Batch(n, 390, 889, step=1, with_bgr=False) as b:
+        b.pair_shape(Hp, Wp)
+        b.synth_pair(first)
+        b.sgbm(chunk=2)
+        for f in range(n):
+            L, R = osg.synth_pair(first + f, Hp, Wp)
+            assert np.array_equal(b.read_disp(f), osg.disparity(L, R, crop=True)), f
+        rng = np.random.default_rng(4)
+        L = rng.integers(0, 256, (Hp, Wp), dtype=np.uint8)
+        R = np.roll(L, -30, axis=1)
+        b.upload_pair(1, L, R)
+        b.sgbm()
+        assert np.array_equal(b.read_disp(1), osg.disparity(L, R, crop=True))
+        with pytest.raises(ValueError):
+            b.upload_pair(0, L[:390, :889], R[:390, :889])
+        with pytest.raises(sv.svx.SvxError):
+            b.pair_shape(544, 1000)            # 1000 - 135 != 889
+        b.pair_shape(390, 889)                 # back to the batch's own shape: 889 % 8 != 0 for SGBM
+        with pytest.raises(sv.svx.SvxError):
+            b.synth_pair(0)
+
+
 def test_dropin_installed_module(sv):
     """functions.disparity / greyscale / preProcessImages patched into a module
     object; a stereoProcessor with OpenCV's getters is honoured."""
