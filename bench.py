@@ -382,8 +382,10 @@ def sgbm_extra(sb, device, with_cpu, frames=64, chunk=32):
             r["cpu_note"] = "oracle/sgbm_oracle.c, 1 thread, scalar C (not OpenCV's SIMD build)"
         out["sgbm_disparity"] = r
         b.set_mask(carmask())
+        b.synth_bgr_pair(0)        # BGR stereo pairs: the loop starts at stereovision.py:44
 
         def loop():
+            b.preprocess(1.4, sync=False)   # gamma (in place: re-applied to the resident pairs each time), grey
             b.sgbm(chunk=chunk)
             b.prepass("previous", sync=False)
             b.ransac(seed_base=0, trials=600, sync=False)
@@ -393,8 +395,9 @@ def sgbm_extra(sb, device, with_cpu, frames=64, chunk=32):
         ms = _timed(b, loop, 2)
         out["device_frame_loop_from_pairs"] = {
             "ms_per_batch": round(ms, 2), "frames": frames, "frames_per_s": round(frames / ms * 1e3, 1),
-            "stages": "SGBM disparity -> prepass(previous+mask) -> maskpoints+RANSAC(600) -> pipeline(per-frame "
-                      "planes) -> road raster -> non-zero walk (stereovision.py:40-136 minus cv2 drawing)"}
+            "stages": "BGR pairs: gamma 1.4 + grey/equalizeHist -> SGBM disparity -> prepass(previous+mask) -> "
+                      "maskpoints+RANSAC(600) -> pipeline(per-frame planes, the corrected left image's colours) -> "
+                      "road raster -> non-zero walk (stereovision.py:40-136 minus cv2 drawing)"}
     return out
 
 

@@ -299,6 +299,18 @@ int sv_batch_read_ransac_trace(sv_batch* b, int frame, int32_t* out, int64_t cap
  * first.., generated on the device (row y's true disparity is the synthetic
  * road's, halved: clamp(floor(3(y - 200) / 10), 0, 127)). */
 int sv_batch_pair_shape(sv_batch* b, int H, int W);
+/* The front end of performStereoVision (stereovision.py:44-46) for the batch:
+ * BGR stereo pairs (frames x Hp x Wp x 3, the pair shape above) uploaded or
+ * generated on the device, then sv_batch_preprocess applies the gamma table
+ * `lut` (256 bytes: functions.py:61-67's table for gamma 1.4, built by the
+ * caller) to both images in place (preProcessImages, :81-87), writes
+ * BGR2GRAY + equalizeHist of both (greyscale, :89-97) as the SGBM pairs, and,
+ * for a batch with BGR, copies the corrected left image's top-left H x W into
+ * the batch's BGR (the colours projectDisparityTo3d reads at the disparity's
+ * own (y, x), cropped or not). */
+int sv_batch_upload_bgr_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t* R);
+int sv_batch_synth_bgr_pair(sv_batch* b, int64_t first_frame_id);
+int sv_batch_preprocess(sv_batch* b, const uint8_t* lut, int sync);
 int sv_batch_synth_pair(sv_batch* b, int64_t first_frame_id);
 int sv_batch_upload_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t* R);
 int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int chunk);

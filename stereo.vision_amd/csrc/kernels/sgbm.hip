@@ -673,7 +673,54 @@ __global__ void synth_pair_kernel(uint8_t* __restrict__ left, uint8_t* __restric
     right[i] = sgbm_pair_texture(first + f, H, y, x + D);
 }
 
+__global__ void synth_bgr_pair_kernel(uint8_t* __restrict__ left, uint8_t* __restrict__ right, int H, int W,
+                                      int frames, int64_t first) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t px = (int64_t)H * W;
+    const int64_t f = i / px;
+    if (f >= frames) return;
+    const int p = (int)(i - f * px);
+    const int y = p / W, x = p - y * W;
+    const int D = sgbm_pair_disparity(y);
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        const int u = side ? x + D : x;   // the scene column this pixel sees
+        const int t = sgbm_pair_texture(first + f, H, y, u);
+        // channel jitter of the scene point (a second texture draw), same in both views
+        const int j = sgbm_pair_texture(first + f + 0x4000000000ll, H, y, u);
+        uint8_t* o = (side ? right : left) + 3 * i;
+        o[0] = (uint8_t)t;
+        o[1] = (uint8_t)min(255, t + (j & 31));
+        o[2] = (uint8_t)max(0, t - ((j >> 3) & 31));
+    }
+}
+
+__global__ __launch_bounds__(256) void copy_bgr_region_kernel(const uint8_t* __restrict__ src, int Hp, int Wp,
+                                                              uint8_t* __restrict__ dst, int H, int W, int Wu) {
+    const int row = blockIdx.x, f = blockIdx.y;   // row < H <= Hp
+    const uint8_t* s = src + ((int64_t)f * Hp + row) * Wp * 3;
+    uint8_t* d = dst + ((int64_t)f * H + row) * W * 3;
+    for (int b = threadIdx.x; b < 3 * Wu; b += blockDim.x) d[b] = s[b];
+}
+
 }  // namespace
+
+hipError_t launch_synth_bgr_pair(uint8_t* left, uint8_t* right, int H, int W, int frames, int64_t first,
+                                 hipStream_t s) {
+    const int64_t n = (int64_t)frames * H * W;
+    hipLaunchKernelGGL(synth_bgr_pair_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, left, right, H, W,
+                       frames, first);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_bgr_region(const uint8_t* src, int Hp, int Wp, uint8_t* dst, int H, int W, int Wu, int frames,
+                                  hipStream_t s) {
+    if (frames <= 0 || H <= 0) return hipSuccess;
+    if (H > Hp || Wu > Wp || Wu > W) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(copy_bgr_region_kernel, dim3((unsigned)H, (unsigned)frames), dim3(256), 0, s, src, Hp, Wp, dst,
+                       H, W, Wu);
+    return hipGetLastError();
+}
 
 // steps each path walk keeps in flight (SVX_SGBM_PF: 1, 4 or 8; A/B only; 16 measured no faster)
 static int sgbm_prefetch() {

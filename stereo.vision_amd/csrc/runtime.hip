@@ -235,6 +235,7 @@ struct sv_batch {
     DevBuf dplane;              // the FramePlane of a device plane (sv_batch_pipeline_dev)
     DevBuf pairL, pairR;        // rectified grey stereo pairs (frames x pairH x pairW each), SGBM input
     int pairH = 0, pairW = 0;   // the pairs' shape: the batch's (H, W), or (Hp, Wp) whose crop is the batch
+    DevBuf bgrL, bgrR, glut, ghist;   // BGR stereo pairs (frames x pairH x pairW x 3), gamma table, hist scratch
     SgbmBufs sg;                // SGBM scratch for one chunk of frames
     int64_t mcap = 0;
     int trace_trials = 0, trace_k = 0, traced_trials = 0;   // requested; k and trials of the recorded trace
@@ -439,7 +440,8 @@ int sv_batch_destroy(sv_batch* b) {
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks,
                       &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane,
-                      &b->pairL, &b->pairR, &b->rsidx, &b->rtri})
+                      &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
+                      &b->glut, &b->ghist})
         if (x->p) (void)hipFree(x->p);
     b->sg.release();
     for (auto& ev : b->ev)
@@ -1620,6 +1622,67 @@ int sv_batch_upload_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t
     HIP_TRY(hipMemcpyAsync(b->pairL.as<uint8_t>() + px * frame, L, px, hipMemcpyHostToDevice, b->stream));
     HIP_TRY(hipMemcpyAsync(b->pairR.as<uint8_t>() + px * frame, R, px, hipMemcpyHostToDevice, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_upload_bgr_pair(sv_batch* b, int frame, const uint8_t* L, const uint8_t* R) {
+    if (!b || !L || !R || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "sv_batch_upload_bgr_pair: bad args");
+    int H, W;
+    pair_shape(b, &H, &W);
+    if (W % 8) return fail(SV_E_ARG, "batched SGBM needs W %% 8 == 0 (W=%d)", W);
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t px3 = (size_t)H * W * 3;
+    HIP_TRY(b->bgrL.ensure(px3 * b->frames));
+    HIP_TRY(b->bgrR.ensure(px3 * b->frames));
+    HIP_TRY(hipMemcpyAsync(b->bgrL.as<uint8_t>() + px3 * frame, L, px3, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemcpyAsync(b->bgrR.as<uint8_t>() + px3 * frame, R, px3, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_synth_bgr_pair(sv_batch* b, int64_t first_frame_id) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    int H, W;
+    pair_shape(b, &H, &W);
+    if (W % 8) return fail(SV_E_ARG, "batched SGBM needs W %% 8 == 0 (W=%d)", W);
+    if (W + kSgD > 4096) return fail(SV_E_ARG, "synthetic pairs need W <= %d", 4096 - kSgD);
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t px3 = (size_t)H * W * 3 * b->frames;
+    HIP_TRY(b->bgrL.ensure(px3));
+    HIP_TRY(b->bgrR.ensure(px3));
+    HIP_TRY(launch_synth_bgr_pair(b->bgrL.as<uint8_t>(), b->bgrR.as<uint8_t>(), H, W, b->frames, first_frame_id,
+                                  b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_preprocess(sv_batch* b, const uint8_t* lut, int sync) {
+    if (!b || !lut) return fail(SV_E_ARG, "sv_batch_preprocess: bad args");
+    if (!b->bgrL.p || !b->bgrR.p) return fail(SV_E_STATE, "no BGR pairs (sv_batch_synth_bgr_pair / upload_bgr_pair)");
+    int H, W;
+    pair_shape(b, &H, &W);
+    HIP_TRY(hipSetDevice(b->device));
+    const int64_t px = (int64_t)H * W;
+    HIP_TRY(b->glut.ensure(256));
+    HIP_TRY(b->ghist.ensure(sizeof(uint32_t) * 256 * b->frames));
+    HIP_TRY(b->pairL.ensure((size_t)px * b->frames));
+    HIP_TRY(b->pairR.ensure((size_t)px * b->frames));
+    HIP_TRY(hipMemcpyAsync(b->glut.p, lut, 256, hipMemcpyHostToDevice, b->stream));
+    const int64_t n3 = px * 3 * b->frames;
+    // preProcessImages: the gamma table on both images (in place), functions.py:81-87
+    HIP_TRY(launch_lut(b->bgrL.as<uint8_t>(), n3, b->glut.as<uint8_t>(), b->bgrL.as<uint8_t>(), b->stream));
+    HIP_TRY(launch_lut(b->bgrR.as<uint8_t>(), n3, b->glut.as<uint8_t>(), b->bgrR.as<uint8_t>(), b->stream));
+    // greyscale: BGR2GRAY + equalizeHist of both, functions.py:89-97 -> the SGBM pairs
+    HIP_TRY(launch_grey_equalize(b->bgrL.as<uint8_t>(), px, b->frames, b->pairL.as<uint8_t>(),
+                                 b->ghist.as<uint32_t>(), b->stream));
+    HIP_TRY(launch_grey_equalize(b->bgrR.as<uint8_t>(), px, b->frames, b->pairR.as<uint8_t>(),
+                                 b->ghist.as<uint32_t>(), b->stream));
+    // the pipeline's colours: projectDisparityTo3d(disparity, 128, imgL) reads the gamma-corrected left image at
+    // the disparity's own (y, x) (stereovision.py:44, :84), the top-left H x W of it when the disparity is cropped
+    if (b->with_bgr)
+        HIP_TRY(launch_copy_bgr_region(b->bgrL.as<uint8_t>(), H, W, b->bgr.as<uint8_t>(), b->H, b->W, b->Wu, b->frames,
+                                       b->stream));
+    if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }
 

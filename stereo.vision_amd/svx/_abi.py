@@ -83,6 +83,9 @@ SIGNATURES = {
     "sv_filter_speckles": [P, I, I, I, I, I],
     "sv_disparity": [P, P, I, I, P, I, I, P, P, P],
     "sv_batch_pair_shape": [P, I, I],
+    "sv_batch_upload_bgr_pair": [P, I, P, P],
+    "sv_batch_synth_bgr_pair": [P, I64],
+    "sv_batch_preprocess": [P, P, I],
     "sv_batch_synth_pair": [P, I64],
     "sv_batch_upload_pair": [P, I, P, P],
     "sv_batch_sgbm": [P, P, I, I],

@@ -141,6 +141,27 @@ class Batch:
         _abi.call("sv_batch_pair_shape", self._h, int(H), int(W))
         self._pair = (int(H), int(W))
 
+    def upload_bgr_pair(self, frame, left, right):
+        """One host BGR stereo pair (the pair shape x 3), for preprocess()."""
+        shape = getattr(self, "_pair", (self.H, self.W)) + (3,)
+        L = np.ascontiguousarray(left, np.uint8)
+        R = np.ascontiguousarray(right, np.uint8)
+        if L.shape != shape or R.shape != shape:
+            raise ValueError(f"BGR pair must be {shape}")
+        _abi.call("sv_batch_upload_bgr_pair", self._h, frame, _abi.ptr(L), _abi.ptr(R))
+
+    def synth_bgr_pair(self, first_frame_id=0):
+        """Synthetic BGR stereo pairs for global frame ids first.. (device)."""
+        _abi.call("sv_batch_synth_bgr_pair", self._h, int(first_frame_id))
+
+    def preprocess(self, gamma=1.4, sync=True):
+        """stereovision.py:44-46 on the BGR pairs: preProcessImages (gamma, in
+        place), greyscale (-> the SGBM pairs) and the corrected left image's
+        colours into the batch (with_bgr)."""
+        from .disparity import gamma_table
+        lut = np.ascontiguousarray(gamma_table(gamma), np.uint8)
+        _abi.call("sv_batch_preprocess", self._h, _abi.ptr(lut), int(bool(sync)))
+
     def synth_pair(self, first_frame_id=0):
         """Synthetic rectified grey pairs for global frame ids first.. (device)."""
         _abi.call("sv_batch_synth_pair", self._h, int(first_frame_id))

@@ -174,6 +174,55 @@ def test_batch_sgbm_crop(sv):
             b.synth_pair(0)
 
 
+def _front_end(L, R):
+    """oracle chain of stereovision.py:44-46: gamma 1.4 (functions.py:61-87), greyscale (:89-97)."""
+    t = osg.gamma_table(1.4)
+    gl, gr = t[L], t[R]
+    return gl, osg.grey_equalize(gl), osg.grey_equalize(gr)
+
+
+@pytest.mark.parametrize("crop", [False, True])
+def test_batch_bgr_front_end(sv, crop):
+    """The batch from BGR stereo pairs: preprocess() (gamma on both images,
+    grey + equalizeHist -> the SGBM pairs, the corrected left image's colours
+    into the batch), sgbm(), then the pipeline, whose hue histogram reads those
+    colours at the disparity's own (y, x) — the top-left of the uncropped image
+    when the disparity is cropped (functions.py:178-196)."""
+    Hp, Wp, n = (544, 1024, 1) if crop else (96, 320, 3)
+    H, W = (390, 889) if crop else (Hp, Wp)
+    rng = np.random.default_rng(31 + crop)
+    pairs = []
+    for f in range(n):
+        L = rng.integers(0, 256, (Hp, Wp, 3), dtype=np.uint8)
+        pairs.append((L, np.roll(L, -(12 + 5 * f), axis=1)))
+    plane = (0.0, 0.0, 0.01)
+    with sv.batch.Batch(n, H, W, step=1, with_bgr=True, with_points=True) as b:
+        if crop:
+            b.pair_shape(Hp, Wp)
+        for f, (L, R) in enumerate(pairs):
+            b.upload_bgr_pair(f, L, R)
+        b.preprocess(1.4)
+        b.sgbm()
+        b.pipeline(plane=plane, point_thr=1e9, hist_thr=2)
+        counts = b.read_counts()
+        for f, (L, R) in enumerate(pairs):
+            gl, grey_l, grey_r = _front_end(L, R)
+            d = osg.disparity(grey_l, grey_r, crop=crop)
+            assert np.array_equal(b.read_disp(f), d), f
+            ref = oracle.pipeline_frame(d, np.ascontiguousarray(gl[:H, :W]), 1, abc=np.array(plane), point_thr=1e9,
+                                        hist_thr=2)
+            assert tuple(int(v) for v in counts[f]) == ref["counts"], f
+            assert np.array_equal(b.read_hist(f), ref["hist"]), f
+            assert np.array_equal(b.read_points(f)[1], ref["pts"]), f
+    with sv.batch.Batch(1, 544, 320, with_bgr=False) as b:
+        with pytest.raises(sv.svx.SvxError):
+            b.preprocess()                         # no BGR pairs
+        b.synth_bgr_pair(5)                        # rows below 200 see the synthetic road's disparity
+        b.preprocess()
+        b.sgbm()
+        assert b.read_disp(0)[300:].any()
+
+
 def test_dropin_installed_module(sv):
     """functions.disparity / greyscale / preProcessImages patched into a module
     object; a stereoProcessor with OpenCV's getters is honoured."""
