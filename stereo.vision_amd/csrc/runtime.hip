@@ -54,7 +54,7 @@ struct DevBuf {
     // hipMalloc's pages, where K1's planes land decides how its three store streams spread over the HBM
     // channels: K1 took 4.35-5.0 ms from one allocation to the next, 4.23-4.34 ms contiguous.
     // SVX_CONTIG: 0 = never, 2 = every large buffer (A/B).
-    hipError_t ensure(size_t n, bool contiguous = false) {
+    hipError_t ensure(size_t n, bool contiguous = false, int tag = 0) {
         if (n <= bytes) return hipSuccess;
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -65,7 +65,8 @@ struct DevBuf {
             const char* v = std::getenv("SVX_CONTIG");
             return v && *v ? std::atoi(v) : 1;
         }();
-        if (mode != 0 && (contiguous || mode == 2) && want >= (256u << 20)) {
+        // A/B: SVX_CONTIG bit 4 also the pipeline outputs (tag 4), 8 the inputs (tag 8), 16 the masks (tag 16)
+        if (mode != 0 && (contiguous || mode == 2 || (mode & tag)) && want >= (256u << 20)) {
             e = hipExtMallocWithFlags(&p, want, hipDeviceMallocContiguous);
             if (e != hipSuccess) {
                 (void)hipGetLastError();
@@ -422,11 +423,11 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
     if (const char* e = std::getenv("SVX_CAP_PAD")) b->cap += (size_t)std::atoi(e) / 64 * 64;   // A/B: frame stride
     b->dense_per_frame = (int64_t)b->kp.Hg * b->kp.pitch;
     const size_t px = (size_t)frames * H * W;
-    hipError_t e = b->disp.ensure(px);
-    if (e == hipSuccess && b->with_bgr) e = b->bgr.ensure(px * 3);
+    hipError_t e = b->disp.ensure(px, false, 8);
+    if (e == hipSuccess && b->with_bgr) e = b->bgr.ensure(px * 3, false, 8);
     if (e == hipSuccess && with_points) {
-        e = b->xyz.ensure(sizeof(float) * 3 * b->cap * frames);
-        if (e == hipSuccess) e = b->pts.ensure(sizeof(int32_t) * 2 * b->cap * frames);
+        e = b->xyz.ensure(sizeof(float) * 3 * b->cap * frames, false, 4);
+        if (e == hipSuccess) e = b->pts.ensure(sizeof(int32_t) * 2 * b->cap * frames, false, 4);
     }
     if (e == hipSuccess) {
         const size_t hist_b = sizeof(uint32_t) * kBins * frames, cnt_b = sizeof(int64_t) * 4 * frames;
@@ -578,13 +579,13 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     if (chunk <= 0) chunk = 1024;
     if (chunk > b->frames) chunk = b->frames;
     const size_t cap = b->cap;   // Ng rounded up to 64: 256-byte aligned SoA planes
-    HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames));
-    HIP_TRY(b->pts.ensure(sizeof(int32_t) * 2 * cap * b->frames));
+    HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames, false, 4));
+    HIP_TRY(b->pts.ensure(sizeof(int32_t) * 2 * cap * b->frames, false, 4));
     const size_t tiles = (size_t)pipeline_tiles_per_frame(p);
     const size_t kb_bytes = sizeof(uint16_t) * 256 * tiles * b->frames;
     const size_t pres_bytes = sizeof(uint32_t) * (kBins / 32) * tiles * b->frames;
     const size_t tc_bytes = sizeof(uint32_t) * tiles * b->frames;
-    HIP_TRY(b->masks.ensure(kb_bytes + pres_bytes + 2 * tc_bytes));
+    HIP_TRY(b->masks.ensure(kb_bytes + pres_bytes + 2 * tc_bytes, false, 16));
     if (int rc = ensure_tables(*d, b->H, b->W, *cam, b->stream)) return rc;
     PipeBuffers bf;
     bf.disp = b->disp.as<uint8_t>();
