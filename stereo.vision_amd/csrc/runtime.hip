@@ -68,6 +68,8 @@ struct DevBuf {
         // A/B: SVX_CONTIG bit 4 also the pipeline outputs (tag 4), 8 the inputs (tag 8), 16 the masks (tag 16)
         if (mode != 0 && (contiguous || mode == 2 || (mode & tag)) && want >= (256u << 20)) {
             e = hipExtMallocWithFlags(&p, want, hipDeviceMallocContiguous);
+            if (std::getenv("SVX_CONTIG_LOG"))
+                std::fprintf(stderr, "svx: contiguous %zu bytes: %s\n", want, hipGetErrorString(e));
             if (e != hipSuccess) {
                 (void)hipGetLastError();
                 p = nullptr;
