@@ -67,16 +67,18 @@ __device__ __forceinline__ uint64_t disp_hash_part(const uint32_t* fd, int64_t w
 __global__ __launch_bounds__(256) void digest_pipe_kernel(const uint8_t* __restrict__ disp,
                                                           const uint32_t* __restrict__ hist,
                                                           const int64_t* __restrict__ counts,
-                                                          const float* __restrict__ xyz,
+                                                          const float* __restrict__ ox,
+                                                          const float* __restrict__ oy,
+                                                          const float* __restrict__ oz, int64_t ofs,
                                                           const int32_t* __restrict__ pts, int64_t cap, KParams p,
                                                           uint64_t* __restrict__ out) {
     __shared__ uint64_t red[4][4];
     const int frame = blockIdx.x, tid = threadIdx.x;
     const uint8_t* fd = disp + (int64_t)frame * p.frame_px;
     const int64_t n2 = counts[4 * (int64_t)frame + 2];
-    const float* oX = xyz + (int64_t)frame * 3 * cap;
-    const float* oY = oX + cap;
-    const float* oZ = oY + cap;
+    const float* oX = ox + (int64_t)frame * ofs;
+    const float* oY = oy + (int64_t)frame * ofs;
+    const float* oZ = oz + (int64_t)frame * ofs;
     const int32_t* oP = pts + (int64_t)frame * 2 * cap;
     uint64_t acc[4] = {disp_hash_part(reinterpret_cast<const uint32_t*>(fd), p.frame_px / 4), 0, 0, 0};
     for (int k = tid; k < 1000; k += 256)
@@ -167,10 +169,10 @@ __global__ __launch_bounds__(256) void digest_dense_kernel(const uint8_t* __rest
 }  // namespace
 
 hipError_t launch_digest_pipe(const KParams& p, const uint8_t* disp, const uint32_t* hist, const int64_t* counts,
-                              const float* xyz, const int32_t* pts, int64_t cap, int frames, uint64_t* out,
-                              hipStream_t s) {
+                              const PipeBuffers& bf, int frames, uint64_t* out, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
-    hipLaunchKernelGGL(digest_pipe_kernel, dim3(frames), dim3(256), 0, s, disp, hist, counts, xyz, pts, cap, p, out);
+    hipLaunchKernelGGL(digest_pipe_kernel, dim3(frames), dim3(256), 0, s, disp, hist, counts, bf.ox, bf.oy, bf.oz,
+                       bf.ofs, bf.pts, bf.cap, p, out);
     return hipGetLastError();
 }
 

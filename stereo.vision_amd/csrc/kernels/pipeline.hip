@@ -378,9 +378,9 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
     const uint32_t end = rowbase;            // one past the last valid LDS slot
     __syncthreads();
     const uint32_t g0 = toff - lead;
-    float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap + g0;
-    float* oY = oX + bf.cap;
-    float* oZ = oY + bf.cap;
+    float* oX = bf.ox + (int64_t)frame * bf.ofs + g0;
+    float* oY = bf.oy + (int64_t)frame * bf.ofs + g0;
+    float* oZ = bf.oz + (int64_t)frame * bf.ofs + g0;
     int32_t* oP = bf.pts + ((int64_t)frame * bf.cap + g0) * 2;
     // Groups of 4 outputs at 16-byte-aligned slots: lane l of a wave stores the
     // X, Y, Z of group m0 + l, and the (x, y) pairs of slots 4 m0 + 2l, +1 and

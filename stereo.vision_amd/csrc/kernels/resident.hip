@@ -543,7 +543,8 @@ template <int STEP, int QP, bool PF, class SH>
 __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, const uint32_t* hist,
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
                                          const uint8_t* fdisp, const uint8_t* fbgr, const RLean& L,
-                                         const FramePlane* Lp, const PipeBuffers& bf, float* oX, int32_t* oP,
+                                         const FramePlane* Lp, const PipeBuffers& bf, float* oX, float* oY,
+                                         float* oZ, int32_t* oP,
                                          uint32_t& running, uint32_t& flushed, bool next_run, const uint16_t* fkb,
                                          const RParams& p) {
     constexpr int QPL = RCfg<STEP, QP>::QPL;
@@ -600,8 +601,6 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     // written first as a partial group (uniform, rare).
     const uint32_t T = (uint32_t)((tot >> 0) & 0xFFFF) + (uint32_t)((tot >> 16) & 0xFFFF) +
                        (uint32_t)((tot >> 32) & 0xFFFF) + (uint32_t)((tot >> 48) & 0xFFFF);
-    float* oY = oX + bf.cap;
-    float* oZ = oY + bf.cap;
     if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (stage_of<QP>() - 1)] = sh.red[tid];   // the tail
     if (T > (uint32_t)stage_of<QP>() - (running - flushed)) {
         p2_write<STEP, QP>(sh.stage, flushed, running, oX, oY, oZ, oP, p);
@@ -760,7 +759,9 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     const uint8_t* fdisp = bf.disp + (int64_t)frame * p.frame_px;
     const uint8_t* fbgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
     uint32_t* wstage = sh.stage + wave * WREGION;
-    float* oX = bf.xyz + (int64_t)frame * 3 * bf.cap;
+    float* oX = bf.ox + (int64_t)frame * bf.ofs;
+    float* oY = bf.oy + (int64_t)frame * bf.ofs;
+    float* oZ = bf.oz + (int64_t)frame * bf.ofs;
     int32_t* oP = bf.pts + (int64_t)frame * bf.cap * 2;
     uint32_t running = 0, flushed = 0;
     const int n2 = (p.ablate & 256) ? 0 : p.nchunks;
@@ -780,7 +781,7 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
             if (PF) p2_load<STEP, QP>(r2, c + 1, tid, fdisp, sh.crange, bf, p, true, run(c + 1), fkb);
             continue;
         }
-        p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oP,
+        p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oY, oZ, oP,
                                running, flushed, c + 1 < n2 && run(c + 1), fkb, p);
     }
     if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;

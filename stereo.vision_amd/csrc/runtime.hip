@@ -244,6 +244,8 @@ struct sv_batch {
     hipStream_t stream2 = nullptr;   // pipeline offsets kernels (stream B), beside the stage launches
     std::vector<hipEvent_t> sync_ev; // pipeline hand-offs between A and B (timing disabled)
     DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks;
+    DevBuf oxb, oyb, ozb;       // pipeline X, Y, Z: three planes of frames x cap (default; SoA in xyz: A/B)
+    bool out_planes = false;
     DevBuf mdisp, carmask;      // pre-pass: masked disparity (frames x H x W), 0x00/0xFF mask (H x W)
     DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
     DevBuf mpts, rres;          // maskpoints (frames x mcap x 3 fp64) + counts; batched RANSAC results
@@ -288,6 +290,40 @@ struct sv_batch {
 };
 
 extern "C" {
+
+// The pipeline's fp32 outputs: three planes of frames x cap in separate allocations (frame f's X at
+// X + f cap), or, with SVX_PIPE_PLANES=0 (A/B), SoA per frame (X[cap] Y[cap] Z[cap] of frame f at 3 cap f).
+// The planes were faster and steadier: 5.94-6.06 vs 5.98-6.23 ms for the pipeline, 6.66-6.87 vs 6.63-7.70
+// with per-frame planes (five alternating processes each).
+static hipError_t ensure_points(sv_batch* b) {
+    const size_t plane = sizeof(float) * b->cap * (size_t)b->frames;
+    hipError_t e;
+    if (b->out_planes) {
+        e = b->oxb.ensure(plane, false, 4);
+        if (e == hipSuccess) e = b->oyb.ensure(plane, false, 4);
+        if (e == hipSuccess) e = b->ozb.ensure(plane, false, 4);
+    } else {
+        e = b->xyz.ensure(3 * plane, false, 4);
+    }
+    if (e == hipSuccess) e = b->pts.ensure(2 * plane, false, 4);
+    return e;
+}
+
+static void point_planes(const sv_batch* b, PipeBuffers& bf) {
+    if (b->out_planes) {
+        bf.ox = b->oxb.as<float>();
+        bf.oy = b->oyb.as<float>();
+        bf.oz = b->ozb.as<float>();
+        bf.ofs = (int64_t)b->cap;
+    } else {
+        bf.ox = b->xyz.as<float>();
+        bf.oy = bf.ox + b->cap;
+        bf.oz = bf.oy + b->cap;
+        bf.ofs = 3 * (int64_t)b->cap;
+    }
+    bf.pts = b->pts.as<int32_t>();
+    bf.cap = (int64_t)b->cap;
+}
 
 const char* sv_version(void) { return "svx 0.1.0 (gfx950)"; }
 
@@ -427,10 +463,9 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
     const size_t px = (size_t)frames * H * W;
     hipError_t e = b->disp.ensure(px, false, 8);
     if (e == hipSuccess && b->with_bgr) e = b->bgr.ensure(px * 3, false, 8);
-    if (e == hipSuccess && with_points) {
-        e = b->xyz.ensure(sizeof(float) * 3 * b->cap * frames, false, 4);
-        if (e == hipSuccess) e = b->pts.ensure(sizeof(int32_t) * 2 * b->cap * frames, false, 4);
-    }
+    b->out_planes = true;   // three planes (A/B: SVX_PIPE_PLANES=0 for SoA per frame)
+    if (const char* e2 = std::getenv("SVX_PIPE_PLANES")) b->out_planes = *e2 != '0';
+    if (e == hipSuccess && with_points) e = ensure_points(b);
     if (e == hipSuccess) {
         const size_t hist_b = sizeof(uint32_t) * kBins * frames, cnt_b = sizeof(int64_t) * 4 * frames;
         e = b->ctrl.ensure(hist_b + cnt_b + 64);
@@ -458,7 +493,7 @@ int sv_batch_destroy(sv_batch* b) {
     if (!b) return SV_OK;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
-    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->xyz, &b->pts, &b->ctrl, &b->masks,
+    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->pts, &b->ctrl, &b->masks,
                       &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
                       &b->glut, &b->ghist})
@@ -483,7 +518,8 @@ int sv_batch_info(const sv_batch* b, int64_t* o) {
     o[1] = b->kp.Wg;
     o[2] = b->kp.pitch;
     o[3] = b->Ng;
-    o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->pts.bytes + b->ctrl.bytes);
+    o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->oxb.bytes * 3 + b->pts.bytes +
+                     b->ctrl.bytes);
     o[5] = b->frames;
     o[6] = b->H;
     o[7] = b->Wu;
@@ -580,9 +616,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     set_plane(p, *plane, point_thr, hist_thr);
     if (chunk <= 0) chunk = 1024;
     if (chunk > b->frames) chunk = b->frames;
-    const size_t cap = b->cap;   // Ng rounded up to 64: 256-byte aligned SoA planes
-    HIP_TRY(b->xyz.ensure(sizeof(float) * 3 * cap * b->frames, false, 4));
-    HIP_TRY(b->pts.ensure(sizeof(int32_t) * 2 * cap * b->frames, false, 4));
+    HIP_TRY(ensure_points(b));
     const size_t tiles = (size_t)pipeline_tiles_per_frame(p);
     const size_t kb_bytes = sizeof(uint16_t) * 256 * tiles * b->frames;
     const size_t pres_bytes = sizeof(uint32_t) * (kBins / 32) * tiles * b->frames;
@@ -598,11 +632,9 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     bf.pres = reinterpret_cast<uint32_t*>(b->masks.as<char>() + kb_bytes);
     bf.tcount = reinterpret_cast<uint32_t*>(b->masks.as<char>() + kb_bytes + pres_bytes);
     bf.toff = bf.tcount + tiles * b->frames;
-    bf.xyz = b->xyz.as<float>();
-    bf.pts = b->pts.as<int32_t>();
+    point_planes(b, bf);
     bf.dxbits = d->tables.dx.as<uint32_t>();
     bf.dybits = d->tables.dy.as<uint32_t>();
-    bf.cap = (int64_t)cap;
     bf.planes = planes;
     bf.plane_stride = plane_stride;
     int mode = b->pipe_mode;
@@ -784,11 +816,13 @@ int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64
     *n = c[2];
     if (c[2] > cap) return fail(SV_E_CAP, "capacity %lld < %lld", (long long)cap, (long long)c[2]);
     const size_t np = (size_t)c[2], cap_f = b->cap;
-    if (xyz && np) {   // device layout is SoA per frame: X[cap] Y[cap] Z[cap]
+    if (xyz && np) {   // device layout: X, Y, Z planes of the frame (point_planes)
         std::vector<float> soa(3 * np);
-        const float* src = b->xyz.as<float>() + 3 * cap_f * frame;
+        PipeBuffers bf;
+        point_planes(b, bf);
+        const float* src[3] = {bf.ox + bf.ofs * frame, bf.oy + bf.ofs * frame, bf.oz + bf.ofs * frame};
         for (int k = 0; k < 3; ++k)
-            HIP_TRY(hipMemcpy(soa.data() + k * np, src + k * cap_f, 4 * np, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(soa.data() + k * np, src[k], 4 * np, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < np; ++i)
             for (int k = 0; k < 3; ++k) xyz[3 * i + k] = soa[k * np + i];
     }
@@ -810,8 +844,12 @@ int sv_batch_digest(sv_batch* b, const sv_camera* cam, int which, uint64_t* out)
         e = launch_digest_dense(p, b->disp.as<uint8_t>(), b->X.as<float>(), b->Y.as<float>(), b->Z.as<float>(),
                                 b->frames, buf.as<uint64_t>(), b->stream);
     else
-        e = launch_digest_pipe(p, b->disp.as<uint8_t>(), b->hist, b->counts, b->xyz.as<float>(), b->pts.as<int32_t>(),
-                               (int64_t)b->cap, b->frames, buf.as<uint64_t>(), b->stream);
+    {
+        PipeBuffers bf;
+        point_planes(b, bf);
+        e = launch_digest_pipe(p, b->disp.as<uint8_t>(), b->hist, b->counts, bf, b->frames, buf.as<uint64_t>(),
+                               b->stream);
+    }
     if (e == hipSuccess) e = hipMemcpyAsync(out, buf.p, sizeof(uint64_t) * 8 * (size_t)b->frames, hipMemcpyDeviceToHost,
                                             b->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(b->stream);

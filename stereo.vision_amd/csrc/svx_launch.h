@@ -38,7 +38,10 @@ struct PipeBuffers {
     uint32_t* tcount;    // frames x tiles: keep1 count per tile (pass 1)
     uint32_t* toff;      // frames x tiles: output offset of each tile (offsets kernel)
     uint32_t* pres;      // frames x tiles x 32: hue bins present among the tile's keep1 points
-    float* xyz;          // frames x {X[cap], Y[cap], Z[cap]} (SoA per frame)
+    float* ox;           // frame f's X[cap] at ox + f * ofs (Y, Z likewise): three planes of frames x cap
+    float* oy;           //   (ofs = cap), or SoA per frame (ofs = 3 cap, oy = ox + cap, oz = ox + 2 cap)
+    float* oz;
+    int64_t ofs;
     int32_t* pts;        // frames x cap x (x, y) int32
     const uint32_t* dxbits;
     const uint32_t* dybits;
@@ -156,8 +159,7 @@ hipError_t launch_select(int mode, const double* vals, double thr, const int16_t
 // kernels/digest.hip -------------------------------------------------------
 // Per-frame verification digests (out: frames x 8 u64, see sv_batch_digest).
 hipError_t launch_digest_pipe(const KParams& p, const uint8_t* disp, const uint32_t* hist, const int64_t* counts,
-                              const float* xyz, const int32_t* pts, int64_t cap, int frames, uint64_t* out,
-                              hipStream_t s);
+                              const PipeBuffers& bf, int frames, uint64_t* out, hipStream_t s);
 hipError_t launch_digest_dense(const KParams& p, const uint8_t* disp, const float* X, const float* Y, const float* Z,
                                int frames, uint64_t* out, hipStream_t s);
 
