@@ -381,80 +381,59 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
     float* oX = bf.ox + (int64_t)frame * bf.ofs + g0;
     float* oY = bf.oy + (int64_t)frame * bf.ofs + g0;
     float* oZ = bf.oz + (int64_t)frame * bf.ofs + g0;
-    int32_t* oP = bf.pts + ((int64_t)frame * bf.cap + g0) * 2;
+    int32_t* oPx = bf.px + (int64_t)frame * bf.cap + g0;
+    int32_t* oPy = bf.py + (int64_t)frame * bf.cap + g0;
     // Groups of 4 outputs at 16-byte-aligned slots: lane l of a wave stores the
-    // X, Y, Z of group m0 + l, and the (x, y) pairs of slots 4 m0 + 2l, +1 and
-    // 4 m0 + 128 + 2l, +1, so every store instruction covers 1 KiB contiguous
-    // (one group per lane would leave each P store's lines half-filled).
+    // X, Y, Z, x, y of group m0 + l, so every store instruction covers 1 KiB
+    // contiguous of its plane.
     const uint32_t groups = (end + 3) >> 2;
     for (uint32_t m0 = tid & ~63u; m0 < groups; m0 += 256) {   // uniform per wave
         const uint32_t m = m0 + lane;
-        const uint32_t sp = 4 * m0 + 2 * lane;   // first P slot of this lane
-        uint32_t pu[4], wx[4], wy[4];
+        if (m >= groups) continue;
+        const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.desc[4 * m]);
+        uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w}, wx[4], wy[4];
+        bool ok[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {   // all table loads in flight together
-            const uint32_t se = sp + (e >> 1) * 128 + (e & 1);
-            const uint32_t uu = (se >= lead && se < end) ? sh.desc[se] : (1u << 24);
-            pu[e] = uu;
-            const uint32_t d = uu >> 24;
-            const int y = (int)((uu >> 12) & 0xFFF) * STEP;
-            const int x = (int)(uu & 0xFFF) * STEP;
+            const uint32_t s_ = 4 * m + e;
+            ok[e] = s_ >= lead && s_ < end;
+            u[e] = ok[e] ? u[e] : (1u << 24);
+            const uint32_t d = u[e] >> 24;
+            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(u[e] & 0xFFF) * STEP;
             wx[e] = bf.dxbits[d * p.dx_words + (x >> 5)];
             wy[e] = bf.dybits[d * p.dy_words + (y >> 5)];
         }
-        if (m < groups) {
-            const uint4 u4 = *reinterpret_cast<const uint4*>(&sh.desc[4 * m]);
-            const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
-            float X[4], Y[4], Z[4];
-            bool ok[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t s_ = 4 * m + e;
-                ok[e] = s_ >= lead && s_ < end;
-                const uint32_t uu = ok[e] ? u[e] : (1u << 24);
-                const uint32_t d = uu >> 24;
-                const int y = (int)((uu >> 12) & 0xFFF) * STEP;
-                const int x = (int)(uu & 0xFFF) * STEP;
-                const float r = __builtin_amdgcn_rcpf((float)d);
-                const float K = p.B32 * r;
-                X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
-                Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
-                Z[e] = p.fB32 * r;
-            }
-            if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
-                __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + 4 * m));
-                __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + 4 * m));
-                __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + 4 * m));
-            } else {                // the tile's first / last group
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (!ok[e]) continue;
-                    oX[4 * m + e] = X[e];
-                    oY[4 * m + e] = Y[e];
-                    oZ[4 * m + e] = Z[e];
-                }
-            }
-        }
+        float X[4], Y[4], Z[4];
         int PX[4], PY[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int y = (int)((pu[e] >> 12) & 0xFFF) * STEP;
-            const int x = (int)(pu[e] & 0xFFF) * STEP;
+            const uint32_t d = u[e] >> 24;
+            const int y = (int)((u[e] >> 12) & 0xFFF) * STEP;
+            const int x = (int)(u[e] & 0xFFF) * STEP;
+            const float r = __builtin_amdgcn_rcpf((float)d);
+            const float K = p.B32 * r;
+            X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
+            Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
+            Z[e] = p.fB32 * r;
             PX[e] = x - (int)((wx[e] >> (x & 31)) & 1);
             PY[e] = y - (int)((wy[e] >> (y & 31)) & 1);
         }
+        if (ok[0] && ok[3]) {   // full group: 16-byte non-temporal stores
+            __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + 4 * m));
+            __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + 4 * m));
+            __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + 4 * m));
+            __builtin_nontemporal_store((v4i){PX[0], PX[1], PX[2], PX[3]}, reinterpret_cast<v4i*>(oPx + 4 * m));
+            __builtin_nontemporal_store((v4i){PY[0], PY[1], PY[2], PY[3]}, reinterpret_cast<v4i*>(oPy + 4 * m));
+        } else {                // the tile's first / last group
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t sh_ = sp + 128 * h;
-            if (sh_ >= lead && sh_ + 1 < end) {
-                __builtin_nontemporal_store((v4i){PX[2 * h], PY[2 * h], PX[2 * h + 1], PY[2 * h + 1]},
-                                            reinterpret_cast<v4i*>(oP + 2 * (size_t)sh_));
-            } else {
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    if (sh_ + e >= lead && sh_ + e < end)
-                        *reinterpret_cast<int2*>(oP + 2 * (size_t)(sh_ + e)) = make_int2(PX[2 * h + e], PY[2 * h + e]);
-                }
+            for (int e = 0; e < 4; ++e) {
+                if (!ok[e]) continue;
+                oX[4 * m + e] = X[e];
+                oY[4 * m + e] = Y[e];
+                oZ[4 * m + e] = Z[e];
+                oPx[4 * m + e] = PX[e];
+                oPy[4 * m + e] = PY[e];
             }
         }
     }

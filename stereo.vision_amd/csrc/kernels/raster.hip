@@ -19,31 +19,32 @@ namespace svx {
 
 typedef int v2i __attribute__((ext_vector_type(2)));
 
-// points: frames x cap x 2 int32 (x, y); counts[frame * cstride + cidx] = points of the frame
-__global__ __launch_bounds__(256) void raster_kernel(const int32_t* __restrict__ pts, const int64_t* __restrict__ counts,
-                                                     int cstride, int cidx, int64_t cap, uint8_t* __restrict__ img,
-                                                     int H, int W, int Wu) {
+// point i of frame f: x = px[(f cap + i) * ps], y = py[(f cap + i) * ps] (ps = 1: the pipeline's two planes;
+// ps = 2: interleaved (x, y) pairs); counts[frame * cstride + cidx] = points of the frame
+__global__ __launch_bounds__(256) void raster_kernel(const int32_t* __restrict__ px, const int32_t* __restrict__ py,
+                                                     int ps, const int64_t* __restrict__ counts, int cstride, int cidx,
+                                                     int64_t cap, uint8_t* __restrict__ img, int H, int W, int Wu) {
     const int frame = blockIdx.y;
     const int64_t n = counts ? counts[(int64_t)frame * cstride + cidx] : cap;
-    const int2* fp = reinterpret_cast<const int2*>(pts) + (int64_t)frame * cap;
+    const int64_t f0 = (int64_t)frame * cap;
     uint8_t* fi = img + (int64_t)frame * H * W;
     for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const int2 p = fp[i];
-        const int x = p.x < 0 ? p.x + Wu : p.x, y = p.y < 0 ? p.y + H : p.y;
+        const int qx = px[(f0 + i) * ps], qy = py[(f0 + i) * ps];
+        const int x = qx < 0 ? qx + Wu : qx, y = qy < 0 ? qy + H : qy;
         fi[(int64_t)y * W + x] = 255;
     }
 }
 
-hipError_t launch_raster(const int32_t* pts, const int64_t* counts, int cstride, int cidx, int64_t cap, uint8_t* img,
-                         int frames, int H, int W, int Wu, hipStream_t s) {
+hipError_t launch_raster(const int32_t* px, const int32_t* py, int ps, const int64_t* counts, int cstride, int cidx,
+                         int64_t cap, uint8_t* img, int frames, int H, int W, int Wu, hipStream_t s) {
     if (frames <= 0 || (int64_t)H * W <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(img, 0, (size_t)frames * H * W, s);
     if (e != hipSuccess) return e;
     if (cap <= 0) return hipSuccess;
     int64_t bx = (cap + 256 * 8 - 1) / (256 * 8);
     if (bx > 1024) bx = 1024;
-    hipLaunchKernelGGL(raster_kernel, dim3((unsigned)bx, (unsigned)frames), dim3(256), 0, s, pts, counts, cstride, cidx,
-                       cap, img, H, W, Wu);
+    hipLaunchKernelGGL(raster_kernel, dim3((unsigned)bx, (unsigned)frames), dim3(256), 0, s, px, py, ps, counts,
+                       cstride, cidx, cap, img, H, W, Wu);
     return hipGetLastError();
 }
 

@@ -453,36 +453,26 @@ __device__ __forceinline__ uint32_t rdesc(uint32_t d, uint32_t gy, uint32_t gx, 
 }
 
 // Write outputs [a, b) of the frame from their LDS descriptors (slot = g mod
-// the stage size); groups of 4 outputs at 16-byte-aligned positions. The P
-// plane is written in whole lines: lane l's group (outputs
-// 4l..4l+3 of its wave's 256-output block) gives the X, Y, Z stores, and the
-// lane also produces the (x, y) pairs of outputs 2l, 2l+1 and 128+2l, 129+2l of
-// the block, so each of the two P stores covers 1 KiB contiguous (with one
-// group per lane, every P store would cover 2 KiB half-filled). The loop runs
-// over wave blocks, uniform per wave. No global loads: the next block's
-// descriptors are read from LDS before the stores.
+// the stage size); groups of 4 outputs at 16-byte-aligned positions: lane l
+// writes the X, Y, Z, x, y of outputs 4l..4l+3 of its wave's 256-output block,
+// one 16-byte non-temporal store per plane, so every store instruction covers
+// 1 KiB contiguous. The loop runs over wave blocks, uniform per wave; it reads
+// only LDS.
 template <int STEP, int QP>
 __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint32_t b, float* oX, float* oY,
-                                         float* oZ, int32_t* oP, const RParams& p) {
+                                         float* oZ, int32_t* oPx, int32_t* oPy, const RParams& p) {
     constexpr uint32_t SM = stage_of<QP>() - 1;
     const uint32_t first = a & ~3u;
     const uint32_t groups = (b - first + 3) >> 2;
     const int lane = lane_id();
-    uint32_t m0 = threadIdx.x & ~63u;   // this wave's first group
-    uint32_t pu[4];                     // P outputs 2l, 2l+1, 128+2l, 129+2l of the block
-    auto fetch = [&](uint32_t mm0) {
-        const uint32_t o = first + 4 * mm0 + 2 * lane;
-        const uint2 lo = *reinterpret_cast<const uint2*>(&stage[o & SM]);
-        const uint2 hi = *reinterpret_cast<const uint2*>(&stage[(o + 128) & SM]);
-        pu[0] = lo.x; pu[1] = lo.y; pu[2] = hi.x; pu[3] = hi.y;
-    };
-    if (m0 < groups) fetch(m0);
-    while (m0 < groups) {   // uniform per wave
+    for (uint32_t m0 = threadIdx.x & ~63u; m0 < groups; m0 += 256) {   // uniform per wave
         const uint32_t m = m0 + lane;
+        if (m >= groups) continue;
         const uint32_t g = first + 4 * m;
         const uint4 u4 = *reinterpret_cast<const uint4*>(&stage[g & SM]);
         const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
         float X[4], Y[4], Z[4];
+        int PX[4], PY[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const uint32_t d = u[e] >> 24;   // a stale slot past b may give rcp(0) = inf: never stored
@@ -493,46 +483,26 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
             X[e] = centred(x, p.cw_hi, p.cw_lo) * K;
             Y[e] = centred(y, p.ch_hi, p.ch_lo) * K;
             Z[e] = p.fB32 * rr;
+            PX[e] = x - (int)((u[e] >> 11) & 1);
+            PY[e] = y - (int)((u[e] >> 23) & 1);
         }
-        int PX[4], PY[4];
+        if (g >= a && g + 3 < b) {
+            __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + g));
+            __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + g));
+            __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + g));
+            __builtin_nontemporal_store((v4i){PX[0], PX[1], PX[2], PX[3]}, reinterpret_cast<v4i*>(oPx + g));
+            __builtin_nontemporal_store((v4i){PY[0], PY[1], PY[2], PY[3]}, reinterpret_cast<v4i*>(oPy + g));
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            PX[e] = (int)(pu[e] & 0x7FF) * STEP - (int)((pu[e] >> 11) & 1);
-            PY[e] = (int)((pu[e] >> 12) & 0x7FF) * STEP - (int)((pu[e] >> 23) & 1);
-        }
-        const uint32_t o = first + 4 * m0 + 2 * lane;
-        const uint32_t mn = m0 + 256;
-        if (mn < groups) fetch(mn);   // before the stores below
-        if (m < groups) {
-            if (g >= a && g + 3 < b) {
-                __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + g));
-                __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + g));
-                __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + g));
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (!(g + e >= a && g + e < b)) continue;
-                    oX[g + e] = X[e];
-                    oY[g + e] = Y[e];
-                    oZ[g + e] = Z[e];
-                }
+            for (int e = 0; e < 4; ++e) {
+                if (!(g + e >= a && g + e < b)) continue;
+                oX[g + e] = X[e];
+                oY[g + e] = Y[e];
+                oZ[g + e] = Z[e];
+                oPx[g + e] = PX[e];
+                oPy[g + e] = PY[e];
             }
         }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t oh = o + 128 * h;
-            if (oh >= a && oh + 1 < b) {
-                __builtin_nontemporal_store((v4i){PX[2 * h], PY[2 * h], PX[2 * h + 1], PY[2 * h + 1]},
-                                            reinterpret_cast<v4i*>(oP + 2 * (size_t)oh));
-            } else {
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    if (oh + e >= a && oh + e < b)
-                        *reinterpret_cast<int2*>(oP + 2 * (size_t)(oh + e)) = make_int2(PX[2 * h + e], PY[2 * h + e]);
-                }
-            }
-        }
-        m0 = mn;
     }
 }
 
@@ -544,7 +514,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
                                          const uint8_t* fdisp, const uint8_t* fbgr, const RLean& L,
                                          const FramePlane* Lp, const PipeBuffers& bf, float* oX, float* oY,
-                                         float* oZ, int32_t* oP,
+                                         float* oZ, int32_t* oPx, int32_t* oPy,
                                          uint32_t& running, uint32_t& flushed, bool next_run, const uint16_t* fkb,
                                          const RParams& p) {
     constexpr int QPL = RCfg<STEP, QP>::QPL;
@@ -603,7 +573,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
                        (uint32_t)((tot >> 32) & 0xFFFF) + (uint32_t)((tot >> 48) & 0xFFFF);
     if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (stage_of<QP>() - 1)] = sh.red[tid];   // the tail
     if (T > (uint32_t)stage_of<QP>() - (running - flushed)) {
-        p2_write<STEP, QP>(sh.stage, flushed, running, oX, oY, oZ, oP, p);
+        p2_write<STEP, QP>(sh.stage, flushed, running, oX, oY, oZ, oPx, oPy, p);
         flushed = running;
     }
     // descriptors (rdesc) with the back-projection delta bits of each point,
@@ -652,7 +622,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     // chunk's dirty path may reuse sh.stage before its scatter restores them
     if (tid < (int)(running - upto)) sh.red[tid] = sh.stage[(upto + tid) & (stage_of<QP>() - 1)];
     if (upto > flushed) {
-        p2_write<STEP, QP>(sh.stage, flushed, upto, oX, oY, oZ, oP, p);
+        p2_write<STEP, QP>(sh.stage, flushed, upto, oX, oY, oZ, oPx, oPy, p);
         flushed = upto;
     }
 }
@@ -762,7 +732,8 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     float* oX = bf.ox + (int64_t)frame * bf.ofs;
     float* oY = bf.oy + (int64_t)frame * bf.ofs;
     float* oZ = bf.oz + (int64_t)frame * bf.ofs;
-    int32_t* oP = bf.pts + (int64_t)frame * bf.cap * 2;
+    int32_t* oPx = bf.px + (int64_t)frame * bf.cap;
+    int32_t* oPy = bf.py + (int64_t)frame * bf.cap;
     uint32_t running = 0, flushed = 0;
     const int n2 = (p.ablate & 256) ? 0 : p.nchunks;
     // a chunk in which pass 1 kept no point (its keep1 range is 0 in every wave;
@@ -781,7 +752,8 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
             if (PF) p2_load<STEP, QP>(r2, c + 1, tid, fdisp, sh.crange, bf, p, true, run(c + 1), fkb);
             continue;
         }
-        p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oY, oZ, oP,
+        p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oY, oZ,
+                               oPx, oPy,
                                running, flushed, c + 1 < n2 && run(c + 1), fkb, p);
     }
     if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;

@@ -243,7 +243,8 @@ struct sv_batch {
     hipStream_t stream = nullptr;    // K1, pass 1 (stream A)
     hipStream_t stream2 = nullptr;   // pipeline offsets kernels (stream B), beside the stage launches
     std::vector<hipEvent_t> sync_ev; // pipeline hand-offs between A and B (timing disabled)
-    DevBuf disp, bgr, X, Y, Z, xyz, pts, ctrl, masks;
+    DevBuf disp, bgr, X, Y, Z, xyz, ctrl, masks;
+    DevBuf ppx, ppy;            // the pipeline's int32 (x, y): two planes of frames x cap
     DevBuf oxb, oyb, ozb;       // pipeline X, Y, Z: three planes of frames x cap (default; SoA in xyz: A/B)
     bool out_planes = false;
     DevBuf mdisp, carmask;      // pre-pass: masked disparity (frames x H x W), 0x00/0xFF mask (H x W)
@@ -305,7 +306,8 @@ static hipError_t ensure_points(sv_batch* b) {
     } else {
         e = b->xyz.ensure(3 * plane, false, 4);
     }
-    if (e == hipSuccess) e = b->pts.ensure(2 * plane, false, 4);
+    if (e == hipSuccess) e = b->ppx.ensure(plane, false, 4);
+    if (e == hipSuccess) e = b->ppy.ensure(plane, false, 4);
     return e;
 }
 
@@ -321,7 +323,8 @@ static void point_planes(const sv_batch* b, PipeBuffers& bf) {
         bf.oz = bf.oy + b->cap;
         bf.ofs = 3 * (int64_t)b->cap;
     }
-    bf.pts = b->pts.as<int32_t>();
+    bf.px = b->ppx.as<int32_t>();
+    bf.py = b->ppy.as<int32_t>();
     bf.cap = (int64_t)b->cap;
 }
 
@@ -493,7 +496,7 @@ int sv_batch_destroy(sv_batch* b) {
     if (!b) return SV_OK;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
-    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->pts, &b->ctrl, &b->masks,
+    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppx, &b->ppy, &b->ctrl, &b->masks,
                       &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
                       &b->glut, &b->ghist})
@@ -518,7 +521,7 @@ int sv_batch_info(const sv_batch* b, int64_t* o) {
     o[1] = b->kp.Wg;
     o[2] = b->kp.pitch;
     o[3] = b->Ng;
-    o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->oxb.bytes * 3 + b->pts.bytes +
+    o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->oxb.bytes * 3 + b->ppx.bytes * 2 +
                      b->ctrl.bytes);
     o[5] = b->frames;
     o[6] = b->H;
@@ -808,7 +811,7 @@ int sv_batch_read_hist(sv_batch* b, int frame, uint32_t* hist) {
 }
 
 int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64_t cap, int64_t* n) {
-    if (!b || !n || frame < 0 || frame >= b->frames || !b->pts.p) return fail(SV_E_ARG, "bad args");
+    if (!b || !n || frame < 0 || frame >= b->frames || !b->ppx.p) return fail(SV_E_ARG, "bad args");
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
     int64_t c[4];
@@ -826,14 +829,22 @@ int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64
         for (size_t i = 0; i < np; ++i)
             for (int k = 0; k < 3; ++k) xyz[3 * i + k] = soa[k * np + i];
     }
-    if (pts && np) HIP_TRY(hipMemcpy(pts, b->pts.as<int32_t>() + 2 * cap_f * frame, 8 * np, hipMemcpyDeviceToHost));
+    if (pts && np) {   // device layout: x and y planes; the caller gets (x, y) pairs
+        std::vector<int32_t> pl(2 * np);
+        HIP_TRY(hipMemcpy(pl.data(), b->ppx.as<int32_t>() + cap_f * frame, 4 * np, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(pl.data() + np, b->ppy.as<int32_t>() + cap_f * frame, 4 * np, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < np; ++i) {
+            pts[2 * i] = pl[i];
+            pts[2 * i + 1] = pl[np + i];
+        }
+    }
     return SV_OK;
 }
 
 int sv_batch_digest(sv_batch* b, const sv_camera* cam, int which, uint64_t* out) {
     if (!b || !cam || !out || which < 0 || which > 1) return fail(SV_E_ARG, "sv_batch_digest: bad args");
     if (which == 0 && !b->Z.p) return fail(SV_E_STATE, "sv_batch_digest: nothing projected");
-    if (which == 1 && !b->pts.p) return fail(SV_E_STATE, "sv_batch_digest: no pipeline outputs");
+    if (which == 1 && !b->ppx.p) return fail(SV_E_STATE, "sv_batch_digest: no pipeline outputs");
     if ((b->kp.frame_px % 4) != 0) return fail(SV_E_ARG, "sv_batch_digest: H * W must be a multiple of 4");
     HIP_TRY(hipSetDevice(b->device));
     KParams p = make_params(b->H, b->W, b->step, *cam, b->Wu);
@@ -1041,7 +1052,8 @@ int sv_road_raster(const int32_t* pts, int64_t n, int H, int W, uint8_t* out_img
     HIP_TRY(d->aux.ensure((size_t)H * W));
     HIP_TRY(d->xy.ensure(sizeof(int32_t) * 2 * (size_t)(n > 0 ? n : 1)));
     if (n) HIP_TRY(hipMemcpyAsync(d->xy.p, pts, sizeof(int32_t) * 2 * n, hipMemcpyHostToDevice, s));
-    HIP_TRY(launch_raster(d->xy.as<int32_t>(), nullptr, 0, 0, n, d->aux.as<uint8_t>(), 1, H, W, W, s));
+    HIP_TRY(launch_raster(d->xy.as<int32_t>(), d->xy.as<int32_t>() + 1, 2, nullptr, 0, 0, n, d->aux.as<uint8_t>(), 1, H,
+                          W, W, s));
     HIP_TRY(hipMemcpyAsync(out_img, d->aux.p, (size_t)H * W, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return SV_OK;
@@ -1080,11 +1092,12 @@ int sv_nonzero_points(const uint8_t* img, int H, int W, int32_t* out, int64_t ca
 
 int sv_batch_road_raster(sv_batch* b, int sync) {
     if (!b) return fail(SV_E_ARG, "null batch");
-    if (!b->pts.p) return fail(SV_E_STATE, "no pipeline points (create the batch with points and run the pipeline)");
+    if (!b->ppx.p) return fail(SV_E_STATE, "no pipeline points (create the batch with points and run the pipeline)");
     HIP_TRY(hipSetDevice(b->device));
     const size_t px = (size_t)b->H * b->W;
     HIP_TRY(b->road.ensure(px * b->frames));
-    HIP_TRY(launch_raster(b->pts.as<int32_t>(), b->counts, 4, 2, (int64_t)b->cap, b->road.as<uint8_t>(), b->frames, b->H,
+    HIP_TRY(launch_raster(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), 1, b->counts, 4, 2, (int64_t)b->cap,
+                          b->road.as<uint8_t>(), b->frames, b->H,
                           b->W, b->Wu, b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;

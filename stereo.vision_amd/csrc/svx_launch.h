@@ -42,7 +42,8 @@ struct PipeBuffers {
     float* oy;           //   (ofs = cap), or SoA per frame (ofs = 3 cap, oy = ox + cap, oz = ox + 2 cap)
     float* oz;
     int64_t ofs;
-    int32_t* pts;        // frames x cap x (x, y) int32
+    int32_t* px;         // the int32 back-projection (planePoints): x and y as two planes of frames x cap
+    int32_t* py;         //   (frame f's at f * cap)
     const uint32_t* dxbits;
     const uint32_t* dybits;
     int64_t cap;         // points per frame (Ng)
@@ -84,9 +85,10 @@ hipError_t launch_mask(const uint8_t* disp, uint8_t* out, const uint8_t* mask_ff
 // kernels/raster.hip -------------------------------------------------------
 // Road raster (points -> 255 on a zeroed image) and the raster-order non-zero walk.
 // counts: NULL -> cap points per frame, else counts[frame * cstride + cidx].
-// images of H rows at stride W; Wu = the image width (numpy's negative-index wrap)
-hipError_t launch_raster(const int32_t* pts, const int64_t* counts, int cstride, int cidx, int64_t cap, uint8_t* img,
-                         int frames, int H, int W, int Wu, hipStream_t s);
+// images of H rows at stride W; Wu = the image width (numpy's negative-index wrap). Point i of frame f:
+// (px[(f cap + i) ps], py[(f cap + i) ps]): ps = 1 for two planes, 2 for interleaved (x, y) pairs.
+hipError_t launch_raster(const int32_t* px, const int32_t* py, int ps, const int64_t* counts, int cstride, int cidx,
+                         int64_t cap, uint8_t* img, int frames, int H, int W, int Wu, hipStream_t s);
 // img frames x px (px % 4 == 0, rows of W <= 4096 pixels)
 hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
                           hipStream_t s);
