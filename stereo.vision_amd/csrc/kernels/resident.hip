@@ -55,7 +55,7 @@ __device__ __forceinline__ uint32_t pk_max16(uint32_t a, uint32_t b) {
 }
 
 
-template <int STEP, int QP>
+template <int STEP, int QP, bool LC>
 struct RCfg {
     static constexpr int QPL = QP;                 // quads per lane per chunk
     static constexpr int CW = 3 * STEP;            // BGR dwords per quad
@@ -85,18 +85,27 @@ struct RParams {      // what the streaming kernel needs (kept small: SGPR budge
     float B32, fB32, cw_hi, cw_lo, ch_hi, ch_lo;
 };
 
-template <int STEP, int QP>
+// quad slot i of lane tid in chunk c. Default: slot-major ((c * QPL + i) * 256
+// + tid: each load instruction covers 256 contiguous quads). LC (lane-contiguous;
+// step 1, Q % 4 == 0, W % 16 == 0, so a lane's QPL quads are one 16-byte-aligned
+// run of one row): c * QPL * 256 + tid * QPL + i, loaded with one wide load per plane.
+template <int QPL, bool LC>
+__device__ __forceinline__ int r_qi(int c, int tid, int i) {
+    return LC ? c * QPL * 256 + tid * QPL + i : (c * QPL + i) * 256 + tid;
+}
+
+template <int STEP, int QP, bool LC>
 struct RQuads {   // this lane's quads of one chunk
-    int gy[RCfg<STEP, QP>::QPL];   // grid row, -1 past the frame end
-    int q[RCfg<STEP, QP>::QPL];    // quad within the row
+    int gy[RCfg<STEP, QP, LC>::QPL];   // grid row, -1 past the frame end
+    int q[RCfg<STEP, QP, LC>::QPL];    // quad within the row
 };
 
-template <int STEP, int QP>
-__device__ __forceinline__ void r_geometry(int c, int tid, const RParams& p, RQuads<STEP, QP>& g) {
-    constexpr int QPL = RCfg<STEP, QP>::QPL;
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ void r_geometry(int c, int tid, const RParams& p, RQuads<STEP, QP, LC>& g) {
+    constexpr int QPL = RCfg<STEP, QP, LC>::QPL;
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
-        const int qi = (c * QPL + i) * 256 + tid;
+        const int qi = r_qi<QPL, LC>(c, tid, i);
         const bool ok = qi < p.frame_quads;
         const int qc = ok ? qi : p.frame_quads - 1;
         const int gy = fastdiv40(qc, p.Q_m40);
@@ -107,16 +116,16 @@ __device__ __forceinline__ void r_geometry(int c, int tid, const RParams& p, RQu
 
 // the geometry of chunk c from that of chunk c - 1 (all its quads inside the
 // frame): every quad slot advances by drow rows and dq quads, no division
-template <int STEP, int QP>
-__device__ __forceinline__ void r_geometry_next(int c, int tid, const RParams& p, RQuads<STEP, QP>& g) {
-    constexpr int QPL = RCfg<STEP, QP>::QPL;
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ void r_geometry_next(int c, int tid, const RParams& p, RQuads<STEP, QP, LC>& g) {
+    constexpr int QPL = RCfg<STEP, QP, LC>::QPL;
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
         int q = g.q[i] + p.dq, gy = g.gy[i] + p.drow;
         const bool wrap = q >= p.Q;
         q -= wrap ? p.Q : 0;
         gy += wrap ? 1 : 0;
-        const bool ok = (c * QPL + i) * 256 + tid < p.frame_quads;
+        const bool ok = r_qi<QPL, LC>(c, tid, i) < p.frame_quads;
         g.q[i] = ok ? q : p.Q - 1;   // past the end: an in-range load address (row 0), gy = -1
         g.gy[i] = ok ? gy : -1;
     }
@@ -124,18 +133,27 @@ __device__ __forceinline__ void r_geometry_next(int c, int tid, const RParams& p
 
 // byte offset of quad (gy, q) in a frame plane with `bpp` bytes per pixel
 // (24-bit multiplies: full-rate, operands < 2^24 for frames the resident kernel takes)
-template <int STEP, int QP>
+template <int STEP, int QP, bool LC>
 __device__ __forceinline__ uint32_t r_off(int gy, int q, int bpp, const RParams& p) {
     const uint32_t px = __umul24((uint32_t)(gy < 0 ? 0 : gy) * STEP, (uint32_t)p.W) + 4u * STEP * (uint32_t)q;
     return bpp == 3 ? 3u * px : px;
 }
 
-template <int STEP, int QP>
-__device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<STEP, QP>& g, const RParams& p,
-                                            uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP]) {
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<STEP, QP, LC>& g, const RParams& p,
+                                            uint32_t (&dw)[RCfg<STEP, QP, LC>::QPL][STEP]) {
+    if constexpr (LC) {   // the lane's QPL (= 4) quads: one 16-byte load
+        static_assert(STEP == 1 && RCfg<STEP, QP, LC>::QPL == 4, "lane-contiguous quads: step 1, 4 quads a lane");
+        const uint4 w = *reinterpret_cast<const uint4*>(fdisp + r_off<STEP, QP, LC>(g.gy[0], g.q[0], 1, p));
+        dw[0][0] = w.x;
+        dw[1][0] = w.y;
+        dw[2][0] = w.z;
+        dw[3][0] = w.w;
+        return;
+    }
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
-        const uint8_t* a = fdisp + r_off<STEP, QP>(g.gy[i], g.q[i], 1, p);
+    for (int i = 0; i < RCfg<STEP, QP, LC>::QPL; ++i) {
+        const uint8_t* a = fdisp + r_off<STEP, QP, LC>(g.gy[i], g.q[i], 1, p);
         if constexpr (STEP == 1) {
             dw[i][0] = *reinterpret_cast<const uint32_t*>(a);
         } else {
@@ -146,12 +164,24 @@ __device__ __forceinline__ void r_load_disp(const uint8_t* fdisp, const RQuads<S
     }
 }
 
-template <int STEP, int QP>
-__device__ __forceinline__ void r_load_bgr(const uint8_t* fbgr, const RQuads<STEP, QP>& g, const RParams& p,
-                                           uint32_t (&cw)[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW]) {
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ void r_load_bgr(const uint8_t* fbgr, const RQuads<STEP, QP, LC>& g, const RParams& p,
+                                           uint32_t (&cw)[RCfg<STEP, QP, LC>::QPL][RCfg<STEP, QP, LC>::CW]) {
+    if constexpr (LC) {   // 48 contiguous bytes: three 16-byte loads, quad i = dwords 3i .. 3i + 2
+        const uint4* cp = reinterpret_cast<const uint4*>(fbgr + r_off<STEP, QP, LC>(g.gy[0], g.q[0], 3, p));
+        const uint4 x = cp[0], y = cp[1], z = cp[2];
+        const uint32_t v[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w};
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
-        const uint8_t* a = fbgr + r_off<STEP, QP>(g.gy[i], g.q[i], 3, p);
+        for (int i = 0; i < 4; ++i) {
+            cw[i][0] = v[3 * i];
+            cw[i][1] = v[3 * i + 1];
+            cw[i][2] = v[3 * i + 2];
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < RCfg<STEP, QP, LC>::QPL; ++i) {
+        const uint8_t* a = fbgr + r_off<STEP, QP, LC>(g.gy[i], g.q[i], 3, p);
         if constexpr (STEP == 1) {
             const uint32_t* cp = reinterpret_cast<const uint32_t*>(a);
             cw[i][0] = cp[0];
@@ -166,17 +196,17 @@ __device__ __forceinline__ void r_load_bgr(const uint8_t* fbgr, const RQuads<STE
 }
 
 // disparity byte of point k of a quad
-template <int STEP, int QP>
+template <int STEP, int QP, bool LC>
 __device__ __forceinline__ uint32_t r_d(const uint32_t (&w)[STEP], int k) {
     if constexpr (STEP == 1) return (w[0] >> (8 * k)) & 0xFF;
     else return (w[k >> 1] >> (16 * (k & 1))) & 0xFF;
 }
 
 // colour (B | G<<8 | R<<16, top byte junk) of point k of a quad
-template <int STEP, int QP>
-__device__ __forceinline__ uint32_t r_col(const uint32_t (&c)[RCfg<STEP, QP>::CW], int k) {
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ uint32_t r_col(const uint32_t (&c)[RCfg<STEP, QP, LC>::CW], int k) {
     const int o = 3 * STEP * k, w = o >> 2, sh = o & 3;
-    const uint32_t hi = (w + 1 < RCfg<STEP, QP>::CW) ? c[w + 1] : 0u;
+    const uint32_t hi = (w + 1 < RCfg<STEP, QP, LC>::CW) ? c[w + 1] : 0u;
     return sh == 0 ? c[w] : __builtin_amdgcn_alignbyte(hi, c[w], sh);
 }
 
@@ -202,10 +232,10 @@ struct RLean {
 // frame's plane: keep1_lean in fp32 (the same fp32 operations as keep1_lean,
 // svx_device.h), the fp64 reference arithmetic for the points inside its guard
 // (rare; one fp64 evaluation site, looped over the lane's uncertain points).
-template <int STEP, int QP>
-__device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP], const RQuads<STEP, QP>& g,
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP, QP, LC>::QPL][STEP], const RQuads<STEP, QP, LC>& g,
                                             const RLean& L, const FramePlane* Lp, int Wg) {
-    constexpr int QPL = RCfg<STEP, QP>::QPL;
+    constexpr int QPL = RCfg<STEP, QP, LC>::QPL;
     uint32_t keep = 0, unc = 0;
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
@@ -213,7 +243,7 @@ __device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP, QP>:
         uint32_t k4 = 0, u4 = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t d = r_d<STEP, QP>(dw[i], k);
+            const uint32_t d = r_d<STEP, QP, LC>(dw[i], k);
             const float df = (float)d;
             const float u = __builtin_fmaf(L.al, (float)((4 * g.q[i] + k) * STEP), beta);
             const float s = u - df;
@@ -241,7 +271,7 @@ __device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP, QP>:
                     const bool hit = b == (uint32_t)(4 * i + k);
                     x = hit ? (4 * g.q[i] + k) * STEP : x;
                     y = hit ? g.gy[i] * STEP : y;
-                    d = hit ? r_d<STEP, QP>(dw[i], k) : d;
+                    d = hit ? r_d<STEP, QP, LC>(dw[i], k) : d;
                 }
             }
             keep = r_keep1_f64(x, y, d, Lp) ? (keep | (1u << b)) : (keep & ~(1u << b));
@@ -251,12 +281,12 @@ __device__ __forceinline__ uint32_t r_keep1(const uint32_t (&dw)[RCfg<STEP, QP>:
 }
 
 // grid points with d != 0 in this lane's chunk (pad columns and rows past the end excluded)
-template <int STEP, int QP>
-__device__ __forceinline__ uint32_t r_nvalid(const uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP], const RQuads<STEP, QP>& g,
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ uint32_t r_nvalid(const uint32_t (&dw)[RCfg<STEP, QP, LC>::QPL][STEP], const RQuads<STEP, QP, LC>& g,
                                              const RParams& p) {
     uint32_t n = 0;
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
+    for (int i = 0; i < RCfg<STEP, QP, LC>::QPL; ++i) {
         const int nin = g.gy[i] < 0 ? 0 : min(4, p.Wg - 4 * g.q[i]);
         uint32_t v;   // the quad's 4 disparity bytes, point k at byte k
         if constexpr (STEP == 1) v = dw[i][0];
@@ -291,20 +321,20 @@ __device__ __forceinline__ uint32_t r_bin_sel(uint32_t col) {
 // order, without branching on lane masks: a point that is not kept writes its
 // colour to this lane's private dump slot instead. Returns the wave's total
 // and this lane's first slot.
-template <int STEP, int QP>
+template <int STEP, int QP, bool LC>
 __device__ __forceinline__ uint32_t r_stage_colours_sel(uint32_t keep,
-                                                        const uint32_t (&cw)[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW],
+                                                        const uint32_t (&cw)[RCfg<STEP, QP, LC>::QPL][RCfg<STEP, QP, LC>::CW],
                                                         uint32_t* wstage, uint32_t* dump, uint32_t& pos0) {
     const uint32_t cnt = __builtin_popcount(keep);
     const uint32_t inc = wave_incl_scan(cnt);
     pos0 = inc - cnt;
     uint32_t pos = pos0;
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
+    for (int i = 0; i < RCfg<STEP, QP, LC>::QPL; ++i) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t bit = (keep >> (4 * i + k)) & 1u;
-            *(bit ? wstage + pos : dump) = r_col<STEP, QP>(cw[i], k);
+            *(bit ? wstage + pos : dump) = r_col<STEP, QP, LC>(cw[i], k);
             pos += bit;
         }
     }
@@ -314,40 +344,40 @@ __device__ __forceinline__ uint32_t r_stage_colours_sel(uint32_t keep,
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 
-template <int STEP, int QP>
+template <int STEP, int QP, bool LC>
 struct P1Regs {
-    RQuads<STEP, QP> g;
-    uint32_t dw[RCfg<STEP, QP>::QPL][STEP];
-    uint32_t cw[RCfg<STEP, QP>::QPL][RCfg<STEP, QP>::CW];
+    RQuads<STEP, QP, LC> g;
+    uint32_t dw[RCfg<STEP, QP, LC>::QPL][STEP];
+    uint32_t cw[RCfg<STEP, QP, LC>::QPL][RCfg<STEP, QP, LC>::CW];
 };
 
-template <int STEP, int QP>
+template <int STEP, int QP, bool LC>
 struct P2Regs {
-    RQuads<STEP, QP> g;
-    uint32_t dw[RCfg<STEP, QP>::QPL][STEP];
+    RQuads<STEP, QP, LC> g;
+    uint32_t dw[RCfg<STEP, QP, LC>::QPL][STEP];
     uint32_t kb;                 // step 1: the keep1 bits of pass 1 (step 2 evaluates keep1 again)
     uint32_t fx[kRDN / 8], fy;   // the chunk's staged delta words (this lane's share)
     int dlo, ywb;                // first staged disparity; the chunk's 32-row word
     bool narrow;                 // the chunk's keep1 range and rows fit the stage
 };
 
-template <int STEP, int QP>
-__device__ __forceinline__ void p1_load(P1Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ void p1_load(P1Regs<STEP, QP, LC>& r, int c, int tid, const uint8_t* fdisp, const uint8_t* fbgr,
                                         const RParams& p, bool next, bool any) {
-    if (next) r_geometry_next<STEP, QP>(c, tid, p, r.g);   // r.g holds chunk c - 1
-    else r_geometry<STEP, QP>(c, tid, p, r.g);
-    r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
-    if (any) r_load_bgr<STEP, QP>(fbgr, r.g, p, r.cw);   // uniform: a chunk the plane rules out needs only its valid count
+    if (next) r_geometry_next<STEP, QP, LC>(c, tid, p, r.g);   // r.g holds chunk c - 1
+    else r_geometry<STEP, QP, LC>(c, tid, p, r.g);
+    r_load_disp<STEP, QP, LC>(fdisp, r.g, p, r.dw);
+    if (any) r_load_bgr<STEP, QP, LC>(fbgr, r.g, p, r.cw);   // uniform: a chunk the plane rules out needs only its valid count
 }
 
-template <int STEP, int QP>
-__device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, const uint8_t* fdisp,
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ void p2_load(P2Regs<STEP, QP, LC>& r, int c, int tid, const uint8_t* fdisp,
                                         const uint32_t* crange, const PipeBuffers& bf, const RParams& p, bool next,
                                         bool run, const uint16_t* fkb) {
-    if (next) r_geometry_next<STEP, QP>(c, tid, p, r.g);   // r.g holds chunk c - 1
-    else r_geometry<STEP, QP>(c, tid, p, r.g);
+    if (next) r_geometry_next<STEP, QP, LC>(c, tid, p, r.g);   // r.g holds chunk c - 1
+    else r_geometry<STEP, QP, LC>(c, tid, p, r.g);
     if (!run) return;   // uniform: a chunk pass 2 skips (none of its grid points can be kept)
-    r_load_disp<STEP, QP>(fdisp, r.g, p, r.dw);
+    r_load_disp<STEP, QP, LC>(fdisp, r.g, p, r.dw);
     if constexpr (STEP == 1) r.kb = fkb[c * 256 + tid];   // pass 1's keep1 bits (this lane wrote them)
     // delta words of the chunk's keep1 disparities (pass 1's range), written to
     // LDS at the chunk's start; every index is clamped in range, so the loads
@@ -356,7 +386,7 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, con
     const uint32_t w = pk_max16(pk_max16(cr.x, cr.y), pk_max16(cr.z, cr.w));
     const int dmn = max(0, 255 - (int)(w >> 16)), dmx = (int)(w & 0xFFFFu);
     const int dlo = min(dmn, 256 - kRDN);
-    constexpr int per = RCfg<STEP, QP>::QPL * 256;   // quads per chunk
+    constexpr int per = RCfg<STEP, QP, LC>::QPL * 256;   // quads per chunk
     const int ywb = (fastdiv40(c * per, p.Q_m40) * STEP) >> 5;
     const int ywl = (fastdiv40(min((c + 1) * per, p.frame_quads) - 1, p.Q_m40) * STEP) >> 5;
     r.dlo = dlo;
@@ -370,8 +400,8 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP>& r, int c, int tid, con
 
 // stage the chunk's delta words (loaded by p2_load) into dl: dx word (d, xw) at
 // (d - dlo) * kRDxStride + xw, dy word of d at kRDyOff + d - dlo
-template <int STEP, int QP>
-__device__ __forceinline__ void p2_stage_deltas(const P2Regs<STEP, QP>& r, uint32_t* dl) {
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ void p2_stage_deltas(const P2Regs<STEP, QP, LC>& r, uint32_t* dl) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < kRDN / 8; ++j) dl[(8 * j + (tid >> 5)) * kRDxStride + (tid & 31)] = r.fx[j];
@@ -380,11 +410,11 @@ __device__ __forceinline__ void p2_stage_deltas(const P2Regs<STEP, QP>& r, uint3
 
 // this wave's keep1 disparity range of the chunk as (255 - dmin) << 16 | dmax
 // (0 when nothing is kept): byte masks from the keep nibbles, no per-point branch
-template <int STEP, int QP>
-__device__ __forceinline__ uint32_t r_keep_range(const uint32_t (&dw)[RCfg<STEP, QP>::QPL][STEP], uint32_t keep) {
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ uint32_t r_keep_range(const uint32_t (&dw)[RCfg<STEP, QP, LC>::QPL][STEP], uint32_t keep) {
     uint32_t dmn = 255, dmx = 0;
 #pragma unroll
-    for (int i = 0; i < RCfg<STEP, QP>::QPL; ++i) {
+    for (int i = 0; i < RCfg<STEP, QP, LC>::QPL; ++i) {
         uint32_t v;   // the quad's 4 disparity bytes, point k at byte k
         if constexpr (STEP == 1) v = dw[i][0];
         else v = __builtin_amdgcn_perm(dw[i][1], dw[i][0], 0x06040200u);
@@ -405,13 +435,13 @@ __device__ __forceinline__ uint32_t r_keep_range(const uint32_t (&dw)[RCfg<STEP,
 
 // pass 1 of one chunk: keep1, valid/kept counts, dense hue binning into hist,
 // candidate mark into dirty, keep1 disparity range into crange. Wave-local (no barrier).
-template <int STEP, int QP>
-__device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint32_t* hist, uint32_t* dirty,
+template <int STEP, int QP, bool LC>
+__device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP, LC>& r, int c, uint32_t* hist, uint32_t* dirty,
                                          uint32_t* crange, uint32_t* wstage, uint32_t* dump, const RParams& p,
                                          uint32_t& nvalid, uint32_t& nkept, bool any, uint16_t* fkb,
                                          uint32_t keep) {
     const int lane = lane_id();
-    nvalid += r_nvalid<STEP, QP>(r.dw, r.g, p);
+    nvalid += r_nvalid<STEP, QP, LC>(r.dw, r.g, p);
     if constexpr (STEP == 1) fkb[c * 256 + threadIdx.x] = (uint16_t)keep;   // for pass 2 (read back by this lane)
     if (!any) {   // uniform: the plane rules out every grid point of the chunk: nothing to bin
         if (lane == 0) crange[4 * c + (threadIdx.x >> 6)] = 0u;
@@ -419,13 +449,13 @@ __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP>& r, int c, uint3
     }
     nkept += __builtin_popcount(keep);
     {
-        const uint32_t w = r_keep_range<STEP, QP>(r.dw, keep);
+        const uint32_t w = r_keep_range<STEP, QP, LC>(r.dw, keep);
         if (lane == 0) crange[4 * c + (threadIdx.x >> 6)] = w;
     }
     uint32_t pos0;
     bool cand = false;
     {
-        const uint32_t wtotal = r_stage_colours_sel<STEP, QP>(keep, r.cw, wstage, dump, pos0);
+        const uint32_t wtotal = r_stage_colours_sel<STEP, QP, LC>(keep, r.cw, wstage, dump, pos0);
         // a point is a candidate while its bin holds fewer than hist_thr points (never for hist_thr < 0)
         const uint32_t lim = p.hist_thr < 0 ? 0u : (uint32_t)p.hist_thr;
         for (uint32_t j = lane; j < ((p.ablate & 512) ? 0u : wtotal); j += 2 * kWave) {   // two colours in flight
@@ -458,7 +488,7 @@ __device__ __forceinline__ uint32_t rdesc(uint32_t d, uint32_t gy, uint32_t gx, 
 // one 16-byte non-temporal store per plane, so every store instruction covers
 // 1 KiB contiguous. The loop runs over wave blocks, uniform per wave; it reads
 // only LDS.
-template <int STEP, int QP>
+template <int STEP, int QP, bool LC>
 __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint32_t b, float* oX, float* oY,
                                          float* oZ, int32_t* oPx, int32_t* oPy, const RParams& p) {
     constexpr uint32_t SM = stage_of<QP>() - 1;
@@ -509,31 +539,31 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
 // pass 2 of one chunk: keep2, block scan, descriptor scatter, then the
 // chunk's whole output groups. Two barriers. Loads chunk c + 1 into r before
 // the stores (PF).
-template <int STEP, int QP, bool PF, class SH>
-__device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, const uint32_t* hist,
+template <int STEP, int QP, bool LC, bool PF, class SH>
+__device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool more, const uint32_t* hist,
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
                                          const uint8_t* fdisp, const uint8_t* fbgr, const RLean& L,
                                          const FramePlane* Lp, const PipeBuffers& bf, float* oX, float* oY,
                                          float* oZ, int32_t* oPx, int32_t* oPy,
                                          uint32_t& running, uint32_t& flushed, bool next_run, const uint16_t* fkb,
                                          const RParams& p) {
-    constexpr int QPL = RCfg<STEP, QP>::QPL;
+    constexpr int QPL = RCfg<STEP, QP, LC>::QPL;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     uint32_t keep;
     if constexpr (STEP == 1) keep = r.kb;
-    else keep = r_keep1<STEP, QP>(r.dw, r.g, L, Lp, p.Wg);   // chunks pass 2 runs: not ruled out, or the last
+    else keep = r_keep1<STEP, QP, LC>(r.dw, r.g, L, Lp, p.Wg);   // chunks pass 2 runs: not ruled out, or the last
     // this chunk's delta words into LDS, read by its scatter after the next
     // barrier (every wave has finished chunk c - 1's scatter)
     uint32_t* dl = sh.dlt;
-    p2_stage_deltas<STEP, QP>(r, dl);
+    p2_stage_deltas<STEP, QP, LC>(r, dl);
     const int dlo = r.dlo;
     const bool narrow = r.narrow;
     if ((dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: candidate chunk (rare)
-        uint32_t cw[QPL][RCfg<STEP, QP>::CW];
-        r_load_bgr<STEP, QP>(fbgr, r.g, p, cw);
+        uint32_t cw[QPL][RCfg<STEP, QP, LC>::CW];
+        r_load_bgr<STEP, QP, LC>(fbgr, r.g, p, cw);
         __syncthreads();   // every wave is done writing the previous chunk: sh.stage is free
         uint32_t pos0;
-        const uint32_t wtotal = r_stage_colours_sel<STEP, QP>(keep, cw, wstage, sh.dump + tid, pos0);
+        const uint32_t wtotal = r_stage_colours_sel<STEP, QP, LC>(keep, cw, wstage, sh.dump + tid, pos0);
         for (uint32_t j = lane; j < wtotal; j += kWave) {
             const uint32_t bin = r_bin_sel(wstage[j]);
             wstage[j] = (int64_t)hist[bin] > (int64_t)p.hist_thr ? 1u : 0u;
@@ -547,13 +577,17 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
             }
         }
     }
-    uint64_t cnt = 0;
-#pragma unroll
-    for (int i = 0; i < QPL; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
-    // the four 16-bit row counts never carry (<= 256 each): two 32-bit DPP scans
+    uint64_t cnt = 0, inc;
     const auto add = [](uint32_t a, uint32_t b) { return a + b; };
-    const uint64_t inc = (uint64_t)wave_scan_dpp((uint32_t)cnt, add) |
-                         ((uint64_t)wave_scan_dpp((uint32_t)(cnt >> 32), add) << 32);
+    if constexpr (LC) {   // raster order is lane order: one 32-bit scan of the lane's count (in field 0)
+        cnt = (uint64_t)__builtin_popcount(keep);
+        inc = (uint64_t)wave_scan_dpp((uint32_t)cnt, add);
+    } else {
+#pragma unroll
+        for (int i = 0; i < QPL; ++i) cnt += (uint64_t)__builtin_popcount((keep >> (4 * i)) & 0xF) << (16 * i);
+        // the four 16-bit row counts never carry (<= 256 each): two 32-bit DPP scans
+        inc = (uint64_t)wave_scan_dpp((uint32_t)cnt, add) | ((uint64_t)wave_scan_dpp((uint32_t)(cnt >> 32), add) << 32);
+    }
     if (lane == 63) sh.wtot[wave] = inc;
     __syncthreads();
     uint64_t wbase = 0, tot = 0;
@@ -569,24 +603,26 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     // group of 4 written below is whole and the writes start on a 128-byte line. If this chunk's
     // points would wrap onto that tail (almost every point kept), the tail is
     // written first as a partial group (uniform, rare).
-    const uint32_t T = (uint32_t)((tot >> 0) & 0xFFFF) + (uint32_t)((tot >> 16) & 0xFFFF) +
-                       (uint32_t)((tot >> 32) & 0xFFFF) + (uint32_t)((tot >> 48) & 0xFFFF);
+    const uint32_t T = LC ? (uint32_t)tot
+                          : (uint32_t)((tot >> 0) & 0xFFFF) + (uint32_t)((tot >> 16) & 0xFFFF) +
+                                (uint32_t)((tot >> 32) & 0xFFFF) + (uint32_t)((tot >> 48) & 0xFFFF);
     if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (stage_of<QP>() - 1)] = sh.red[tid];   // the tail
     if (T > (uint32_t)stage_of<QP>() - (running - flushed)) {
-        p2_write<STEP, QP>(sh.stage, flushed, running, oX, oY, oZ, oPx, oPy, p);
+        p2_write<STEP, QP, LC>(sh.stage, flushed, running, oX, oY, oZ, oPx, oPy, p);
         flushed = running;
     }
     // descriptors (rdesc) with the back-projection delta bits of each point,
     // branch-free: a slot that is not kept writes to this lane's dump word
     uint32_t rowbase = running;
+    uint32_t olc = running + (uint32_t)excl;   // LC: the lane's outputs are one run
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
-        uint32_t o = rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
+        uint32_t o = LC ? olc : rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
         rowbase += (uint32_t)((tot >> (16 * i)) & 0xFFFF);
         const uint32_t gy = (uint32_t)max(r.g.gy[i], 0), y = gy * STEP;
         uint32_t dv[4], bx[4], by[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) dv[k] = r_d<STEP, QP>(r.dw[i], k);
+        for (int k = 0; k < 4; ++k) dv[k] = r_d<STEP, QP, LC>(r.dw[i], k);
         if (narrow) {   // uniform: every kept d in [dlo, dlo + kRDN), the chunk's rows in word ywb
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -611,8 +647,9 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
                 rdesc(dv[k], gy, (uint32_t)(4 * r.g.q[i] + k), bx[k], by[k]);
             o += bit;
         }
+        olc = o;
     }
-    if (PF && more) p2_load<STEP, QP>(r, c + 1, tid, fdisp, sh.crange, bf, p, true, next_run, fkb);   // in flight before the stores
+    if (PF && more) p2_load<STEP, QP, LC>(r, c + 1, tid, fdisp, sh.crange, bf, p, true, next_run, fkb);   // in flight before the stores
     __syncthreads();
     running += T;
     // write whole 128-byte lines: outputs up to a multiple of 32 (X, Y, Z: 32 floats a line; P: 16 pairs),
@@ -622,7 +659,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP>& r, int c, bool more, 
     // chunk's dirty path may reuse sh.stage before its scatter restores them
     if (tid < (int)(running - upto)) sh.red[tid] = sh.stage[(upto + tid) & (stage_of<QP>() - 1)];
     if (upto > flushed) {
-        p2_write<STEP, QP>(sh.stage, flushed, upto, oX, oY, oZ, oPx, oPy, p);
+        p2_write<STEP, QP, LC>(sh.stage, flushed, upto, oX, oY, oZ, oPx, oPy, p);
         flushed = upto;
     }
 }
@@ -649,9 +686,9 @@ static_assert(sizeof(FusedShared<4>) <= 32768, "5 workgroups per CU (160 KiB LDS
 
 // sh.cany bit c: can the plane keep some grid point of chunk c (rows_keepable
 // over the chunk's rows)? One lane per chunk (nchunks <= 256), one ballot per wave.
-template <int STEP, int QP>
+template <int STEP, int QP, bool LC>
 __device__ __forceinline__ void chunk_keepable_bits(FusedShared<QP>& sh, const FramePlane* Lp, const RParams& p) {
-    constexpr int per = RCfg<STEP, QP>::QPL * 256;   // quads per chunk
+    constexpr int per = RCfg<STEP, QP, LC>::QPL * 256;   // quads per chunk
     const int c = threadIdx.x;
     bool k = false;
     const FramePlane L = *Lp;
@@ -672,42 +709,42 @@ __device__ __forceinline__ bool chunk_any(const FusedShared<QP>& sh, int c) {   
     return __builtin_amdgcn_readfirstlane((sh.cany[c >> 5] >> (c & 31)) & 1u) != 0;
 }
 
-template <int STEP, int QP, bool PF1 = false>
+template <int STEP, int QP, bool LC, bool PF1 = false>
 __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, const PipeBuffers& bf,
                                             const RLean& L, const FramePlane* Lp,
                                             const RParams& p) {
-    constexpr int WREGION = 64 * RCfg<STEP, QP>::QPL * 4;
+    constexpr int WREGION = 64 * RCfg<STEP, QP, LC>::QPL * 4;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const uint8_t* fdisp = bf.disp + (int64_t)frame * p.frame_px;
     const uint8_t* fbgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
     uint32_t* wstage = sh.stage + wave * WREGION;
     for (int i = tid; i < kRBins; i += 256) sh.hist[i] = 0;
     if (tid < maxchunks_of<QP>() / 32) sh.dirty[tid] = 0;
-    chunk_keepable_bits<STEP, QP>(sh, Lp, p);
+    chunk_keepable_bits<STEP, QP, LC>(sh, Lp, p);
     __syncthreads();
     uint32_t nvalid = 0, nkept = 0;
     uint16_t* fkb = bf.kbits + (int64_t)frame * p.nchunks * 256;   // step 1: keep1 bits per chunk and lane
     const int n1 = (p.ablate & 128) ? 0 : p.nchunks;   // ablate: DIAGNOSTIC ONLY
     if constexpr (PF1) {   // chunk c + 1's loads in flight while chunk c is binned (pass 1 stores nothing)
-        P1Regs<STEP, QP> r1;
-        if (n1 > 0) p1_load<STEP, QP>(r1, 0, tid, fdisp, fbgr, p, false, chunk_any(sh, 0));
+        P1Regs<STEP, QP, LC> r1;
+        if (n1 > 0) p1_load<STEP, QP, LC>(r1, 0, tid, fdisp, fbgr, p, false, chunk_any(sh, 0));
         for (int c = 0; c < n1; ++c) {
-            P1Regs<STEP, QP> cur = r1;
+            P1Regs<STEP, QP, LC> cur = r1;
             // keep1 before chunk c + 1's loads are issued: its rare fp64 path then
             // runs with one chunk's registers live, not two
             const bool any = chunk_any(sh, c);
-            const uint32_t keep = any ? r_keep1<STEP, QP>(cur.dw, cur.g, L, Lp, p.Wg) : 0u;
-            if (c + 1 < n1) p1_load<STEP, QP>(r1, c + 1, tid, fdisp, fbgr, p, true, chunk_any(sh, c + 1));
-            p1_chunk<STEP, QP>(cur, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept,
+            const uint32_t keep = any ? r_keep1<STEP, QP, LC>(cur.dw, cur.g, L, Lp, p.Wg) : 0u;
+            if (c + 1 < n1) p1_load<STEP, QP, LC>(r1, c + 1, tid, fdisp, fbgr, p, true, chunk_any(sh, c + 1));
+            p1_chunk<STEP, QP, LC>(cur, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept,
                                any, fkb, keep);
         }
     } else {
         for (int c = 0; c < n1; ++c) {
-            P1Regs<STEP, QP> r1;
+            P1Regs<STEP, QP, LC> r1;
             const bool any = chunk_any(sh, c);
-            p1_load<STEP, QP>(r1, c, tid, fdisp, fbgr, p, false, any);
-            const uint32_t keep = any ? r_keep1<STEP, QP>(r1.dw, r1.g, L, Lp, p.Wg) : 0u;
-            p1_chunk<STEP, QP>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept, any, fkb,
+            p1_load<STEP, QP, LC>(r1, c, tid, fdisp, fbgr, p, false, any);
+            const uint32_t keep = any ? r_keep1<STEP, QP, LC>(r1.dw, r1.g, L, Lp, p.Wg) : 0u;
+            p1_chunk<STEP, QP, LC>(r1, c, sh.hist, sh.dirty, sh.crange, wstage, sh.dump + tid, p, nvalid, nkept, any, fkb,
                                keep);
         }
     }
@@ -720,11 +757,11 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
     __syncthreads();   // histogram, dirty bits, counts complete
 }
 
-template <int STEP, int QP, bool PF>
+template <int STEP, int QP, bool LC, bool PF>
 __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, const PipeBuffers& bf,
                                             const RLean& L, const FramePlane* Lp,
                                             const RParams& p) {
-    constexpr int WREGION = 64 * RCfg<STEP, QP>::QPL * 4;
+    constexpr int WREGION = 64 * RCfg<STEP, QP, LC>::QPL * 4;
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint8_t* fdisp = bf.disp + (int64_t)frame * p.frame_px;
     const uint8_t* fbgr = bf.bgr + (int64_t)frame * p.frame_px * 3;
@@ -744,15 +781,15 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
         return c + 1 == n2 || (cr.x | cr.y | cr.z | cr.w) != 0u;
     };
     const uint16_t* fkb = bf.kbits + (int64_t)frame * p.nchunks * 256;
-    P2Regs<STEP, QP> r2;
-    if (PF && n2 > 0) p2_load<STEP, QP>(r2, 0, tid, fdisp, sh.crange, bf, p, false, run(0), fkb);
+    P2Regs<STEP, QP, LC> r2;
+    if (PF && n2 > 0) p2_load<STEP, QP, LC>(r2, 0, tid, fdisp, sh.crange, bf, p, false, run(0), fkb);
     for (int c = 0; c < n2; ++c) {
-        if (!PF) p2_load<STEP, QP>(r2, c, tid, fdisp, sh.crange, bf, p, c > 0, run(c), fkb);
+        if (!PF) p2_load<STEP, QP, LC>(r2, c, tid, fdisp, sh.crange, bf, p, c > 0, run(c), fkb);
         if (!run(c)) {   // uniform; c + 1 < n2 here
-            if (PF) p2_load<STEP, QP>(r2, c + 1, tid, fdisp, sh.crange, bf, p, true, run(c + 1), fkb);
+            if (PF) p2_load<STEP, QP, LC>(r2, c + 1, tid, fdisp, sh.crange, bf, p, true, run(c + 1), fkb);
             continue;
         }
-        p2_chunk<STEP, QP, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oY, oZ,
+        p2_chunk<STEP, QP, LC, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oY, oZ,
                                oPx, oPy,
                                running, flushed, c + 1 < n2 && run(c + 1), fkb, p);
     }
@@ -763,14 +800,14 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
 // One workgroup = one frame: pass 1 over all chunks, then pass 2 (grid = frames).
 // The frame's plane: bf.planes[frame * bf.plane_stride] (device memory).
 // ---------------------------------------------------------------------------
-template <int STEP, int QP, bool PF, bool PF1>
+template <int STEP, int QP, bool LC, bool PF, bool PF1>
 __device__ __forceinline__ void fused_body(const PipeBuffers& bf, const RParams& p,
                                            FusedShared<QP>& sh) {
     const int tid = threadIdx.x;
     const int frame = blockIdx.x;
     const FramePlane* Lp = bf.planes + (int64_t)frame * bf.plane_stride;
     const RLean L{Lp->al32, Lp->bb32, Lp->b032, Lp->tn32, Lp->g32};
-    frame_pass1<STEP, QP, PF1>(frame, sh, bf, L, Lp, p);
+    frame_pass1<STEP, QP, LC, PF1>(frame, sh, bf, L, Lp, p);
     // pass 2 (store-bound) issues ahead of other workgroups' pass-1 waves on the SIMD: -0.2 to -0.4 %
     // (5.78 vs 5.80 ms, 6.81 vs 6.82 with per-frame planes; ten and eight in-process alternations)
     __builtin_amdgcn_s_setprio(2);
@@ -781,18 +818,26 @@ __device__ __forceinline__ void fused_body(const PipeBuffers& bf, const RParams&
         cn[0] = (int64_t)sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
         cn[1] = (int64_t)sh.red[4] + sh.red[5] + sh.red[6] + sh.red[7];
     }
-    frame_pass2<STEP, QP, PF>(frame, sh, bf, L, Lp, p);
+    frame_pass2<STEP, QP, LC, PF>(frame, sh, bf, L, Lp, p);
 }
 
-template <int STEP, int QP, bool PF, bool PF1 = false>
+template <int STEP, int QP, bool LC, bool PF, bool PF1 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void resident_fused_kernel(PipeBuffers bf, RParams p) {
     __shared__ FusedShared<QP> sh;
-    fused_body<STEP, QP, PF, PF1>(bf, p, sh);
+    fused_body<STEP, QP, LC, PF, PF1>(bf, p, sh);
 }
 
 bool resident_supported(const KParams& p) {   // frame_quads <= 2^20: every QP's chunk count fits its dirty bits
     return (p.step == 1 || p.step == 2) && p.pitch <= 2048 && p.Hg <= 2048 &&   // rdesc: 11-bit coordinates
            resident_chunks_per_frame(p, 4) <= kRMaxChunks && p.frame_px * 3 < (1ll << 31);
+}
+
+// lane-contiguous quads (r_qi) for step 1 when a lane's 4 quads are one aligned
+// 16-byte run of a row; SVX_RES_LC=0 keeps the slot-major order (A/B knob)
+static bool resident_lane_quads(const KParams& kp) {
+    const char* v = std::getenv("SVX_RES_LC");   // read per call (tools/prof.py ab --env)
+    const bool on = !(v && v[0] == '0');
+    return on && kp.step == 1 && kp.Q % 4 == 0 && kp.W % 16 == 0 && kp.frame_px % 16 == 0;
 }
 
 static RParams resident_params(const KParams& kp, int qpl) {
@@ -836,16 +881,21 @@ hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, int
     if (frames <= 0) return hipSuccess;
     if (!resident_supported(kp) || !b.planes) return hipErrorInvalidValue;
     const dim3 grid(frames), block(256);
-    if (kp.step == 1) {
+    if (kp.step == 1 && resident_lane_quads(kp)) {
         const RParams p = resident_params(kp, 4);
-        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true>), grid, block, 0, s, b, p);
-        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true>), grid, block, 0, s, b, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, false>), grid, block, 0, s, b, p);
+        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true, true>), grid, block, 0, s, b, p);
+        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true>), grid, block, 0, s, b, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, false>), grid, block, 0, s, b, p);
+    } else if (kp.step == 1) {
+        const RParams p = resident_params(kp, 4);
+        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, false, true, true>), grid, block, 0, s, b, p);
+        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, false, true>), grid, block, 0, s, b, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, false, false>), grid, block, 0, s, b, p);
     } else {
         const RParams p = resident_params(kp, 2);
-        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<2, 2, true, true>), grid, block, 0, s, b, p);
-        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<2, 2, true>), grid, block, 0, s, b, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<2, 2, false>), grid, block, 0, s, b, p);
+        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<2, 2, false, true, true>), grid, block, 0, s, b, p);
+        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<2, 2, false, true>), grid, block, 0, s, b, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<2, 2, false, false>), grid, block, 0, s, b, p);
     }
     return hipGetLastError();
 }
