@@ -4,6 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT="$PWD/gpurun_out"; mkdir -p "$OUT"
 SKIP_PROF=0 bash tools/gpu_check.sh || exit $?
+python3 tools/prof.py dispatches "$OUT/prof" --kernel resident_fused > "$OUT/resident_dispatches.json" || exit $?
 python3 tools/prof.py pmc --groups "FETCH_SIZE;WRITE_SIZE" --out "$OUT/pmc_k1" --traffic 4096 -- --what k1 --frames 4096 --reps 3 || exit $?
 python3 tools/prof.py pmc --groups "FETCH_SIZE;WRITE_SIZE" --out "$OUT/pmc_pipe" --traffic 4096 -- --what pipe --frames 4096 --reps 1 || exit $?
 python3 tools/prof.py pmc --groups "FETCH_SIZE;WRITE_SIZE" --out "$OUT/pmc_planes" --traffic 4096 -- --what planes --frames 4096 --reps 1 || exit $?

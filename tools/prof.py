@@ -297,6 +297,20 @@ def cmd_trace(a):
               f"  grid {r.get('Grid_Size_X', r.get('Grid_Size', '?'))}")
 
 
+def cmd_dispatches(a):
+    """Per-dispatch durations of the kernels matching a.kernel in a rocprofv3 kernel trace
+    (the bench process's rocprof average mixes placement probes, timed calls and other workloads)."""
+    rows = []
+    for f in glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True):
+        rows += [r for r in csv.DictReader(open(f)) if a.kernel in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    out = defaultdict(list)
+    for r in rows:
+        out[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(
+            round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6, 4))
+    print(json.dumps({"source": a.dir, "unit": "ms", "dispatches": out}, indent=1))
+
+
 def cmd_dropin(a):
     import random
     import types
@@ -390,12 +404,15 @@ def main():
     p.add_argument("step", type=int)
     p = sp.add_parser("dropin")
     p.add_argument("--reps", type=int, default=5)
+    p = sp.add_parser("dispatches")
+    p.add_argument("dir")
+    p.add_argument("--kernel", default="resident_fused")
     a = ap.parse_args()
     if getattr(a, "workload", None) is not None:
         a.workload = [w for w in a.workload if w != "--"]
     {"workload": cmd_workload, "time": cmd_time, "sweep": cmd_sweep, "ab": cmd_ab, "ab-lib": cmd_ab_lib,
      "pmc": cmd_pmc, "summary": cmd_summary, "traffic": cmd_traffic, "trace": cmd_trace,
-     "dropin": cmd_dropin}[a.cmd](a)
+     "dropin": cmd_dropin, "dispatches": cmd_dispatches}[a.cmd](a)
 
 
 if __name__ == "__main__":
