@@ -1,0 +1,224 @@
+// Speed-of-light probe for the pipeline's data movement (diagnostic, not product).
+//
+// The resident pipeline (kernels/resident.hip) moves, per 4096-frame call, the
+// disparity (1 B/px) and BGR (3 B/px) of every frame in, and 20 B per kept point
+// out, as five frame-strided planes (X, Y, Z f32; x, y i32) at frame * cap. This
+// program moves the same bytes with the same layout and no arithmetic, one
+// workgroup per frame, so its rate is the practical ceiling of that traffic mix:
+//   mode 0  read the frame (disparity + BGR), then write its outputs   (the pipeline's order)
+//   mode 1  reads and writes interleaved chunk by chunk
+//   mode 2  reads only
+//   mode 3  writes only
+//   mode 4  mode 0 with the reads done twice (pass 1 and pass 2 both read the disparity)
+// and, writes only, other output layouts of the same bytes:
+//   mode 5  five planes, frame stride = kept (dense frames)
+//   mode 6  one plane, 20 B per point (AoS), frame stride 5 x cap
+//   mode 7  five planes, frame stride cap + 64 (another channel phase per frame)
+//   mode 8  five dense planes swept in 4 KiB tiles across frames (K1's pattern: no per-frame streams)
+//   mode 9  five planes, frame stride cap, each lane writing 2 x 16 B contiguous per plane
+//   mode 10 read-then-write, each frame's output region taken from a global counter (atomicAdd) after its reads
+//   mode 11 five planes, frame stride cap, every frame writing all cap outputs (no gaps; more bytes)
+//   mode 12 mode 1 (chunk-interleaved reads and writes) into a region taken from the counter after the first chunk's reads
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/_sol_pipe tools/sol_pipe.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                                  \
+        }                                                                                  \
+    } while (0)
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+struct Args {
+    const uint4* disp;   // frames x px bytes
+    const uint4* bgr;    // frames x 3 px bytes
+    float* o[5];         // frames x cap
+    uint32_t* sink;
+    int64_t px16;        // 16-byte words of disparity per frame
+    int64_t cap;         // outputs per frame (multiple of 4)
+    int64_t kept;        // outputs written per frame (multiple of 4)
+    int mode;
+    int64_t stride;      // floats between frames in a plane (writes)
+    int nplanes;         // planes written
+    int64_t nper;        // floats per plane per frame
+    unsigned long long* counter;
+};
+
+__device__ __forceinline__ uint32_t read_range(const Args& a, int f, int64_t w0, int64_t w1) {
+    uint32_t acc = 0;
+    const uint4* d = a.disp + f * a.px16;
+    const uint4* c = a.bgr + f * a.px16 * 3;
+    for (int64_t w = w0 + threadIdx.x; w < w1; w += 256) {
+        const uint4 x = *(d + w);
+        const uint4 y0 = *(c + 3 * w), y1 = *(c + 3 * w + 1),
+                    y2 = *(c + 3 * w + 2);
+        acc ^= x.x ^ x.y ^ x.z ^ x.w ^ y0.x ^ y0.w ^ y1.y ^ y1.z ^ y2.x ^ y2.w;
+    }
+    return acc;
+}
+
+__device__ __forceinline__ void write_range(const Args& a, int f, int64_t g0, int64_t g1, float v) {
+    for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
+        const v4f q = {v, v, v, v};
+#pragma unroll
+        for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + f * a.cap + g));
+    }
+}
+
+__device__ __forceinline__ void write_layout(const Args& a, int f, float v) {
+    const v4f q = {v, v, v, v};
+    if (a.mode == 9) {
+        for (int64_t g = 8 * threadIdx.x; g < a.nper; g += 2048)
+            for (int k = 0; k < 5; ++k) {
+                __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + f * a.stride + g));
+                if (g + 8 <= a.nper) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + f * a.stride + g + 4));
+            }
+        return;
+    }
+    for (int64_t g = 4 * threadIdx.x; g < a.nper; g += 1024)
+        for (int k = 0; k < a.nplanes; ++k)
+            __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + f * a.stride + g));
+}
+
+__global__ __launch_bounds__(256) void sweep_kernel(Args a, int64_t total) {   // mode 8
+    const v4f q = {1.f, 1.f, 1.f, 1.f};
+    for (int64_t t = blockIdx.x; t * 1024 < total; t += gridDim.x) {
+        const int64_t g = t * 1024 + 4 * threadIdx.x;
+        if (g < total)
+            for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + g));
+    }
+}
+
+__global__ __launch_bounds__(256) void sol_kernel(Args a) {
+    const int f = blockIdx.x;
+    uint32_t acc = 0;
+    const float v = (float)f;
+    if (a.mode == 12) {
+        const int n = 64;   // chunks
+        __shared__ int64_t base12;
+        for (int c = 0; c < n; ++c) {
+            acc ^= read_range(a, f, a.px16 * c / n, a.px16 * (c + 1) / n);
+            if (c == 0) {
+                if (threadIdx.x == 0) base12 = (int64_t)atomicAdd(a.counter, (unsigned long long)a.kept);
+                __syncthreads();
+            }
+            const int64_t g0 = (a.kept / 4 * c / n) * 4, g1 = (a.kept / 4 * (c + 1) / n) * 4;
+            for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
+                const v4f q = {v, v, v, v};
+#pragma unroll
+                for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + base12 + g));
+            }
+        }
+    } else if (a.mode == 10) {
+        acc ^= read_range(a, f, 0, a.px16);
+        __shared__ int64_t base;
+        if (threadIdx.x == 0) base = (int64_t)atomicAdd(a.counter, (unsigned long long)a.kept);
+        __syncthreads();
+        for (int64_t g = 4 * threadIdx.x; g < a.kept; g += 1024) {
+            const v4f q = {v, v, v, v};
+#pragma unroll
+            for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + base + g));
+        }
+    } else if (a.mode >= 5) {
+        write_layout(a, f, v);
+    } else if (a.mode == 1) {
+        const int n = 64;   // chunks
+        for (int c = 0; c < n; ++c) {
+            acc ^= read_range(a, f, a.px16 * c / n, a.px16 * (c + 1) / n);
+            write_range(a, f, (a.kept / 4 * c / n) * 4, (a.kept / 4 * (c + 1) / n) * 4, v);
+        }
+    } else {
+        if (a.mode != 3) acc ^= read_range(a, f, 0, a.px16);
+        if (a.mode == 4) {   // pass 2 re-reads the disparity
+            const uint4* d = a.disp + f * a.px16;
+            for (int64_t w = threadIdx.x; w < a.px16; w += 256) {
+                const uint4 x = *(d + w);
+                acc ^= x.x ^ x.w;
+            }
+        }
+        if (a.mode != 2) write_range(a, f, 0, a.kept, v);
+    }
+    if (acc == 0x12345678u) a.sink[f] = acc;   // keeps the loads
+}
+
+int main(int argc, char** argv) {
+    const int frames = argc > 1 ? std::atoi(argv[1]) : 4096;
+    const int64_t px = 544 * 1024;
+    const int64_t kept = argc > 2 ? std::atoll(argv[2]) : 277200;   // 1.135 G kept points / 4096 frames (the bench pipeline)
+    const int64_t cap = (555489 + 3) / 4 * 4 + 64;   // room for mode 7's padding
+    Args a{};
+    void* p;
+    CK(hipMalloc(&p, frames * px));
+    CK(hipMemset(p, 1, frames * px));
+    a.disp = (const uint4*)p;
+    CK(hipMalloc(&p, frames * px * 3));
+    CK(hipMemset(p, 2, frames * px * 3));
+    a.bgr = (const uint4*)p;
+    for (int k = 0; k < 5; ++k) {
+        CK(hipMalloc(&p, frames * cap * 4 * (k == 0 ? 5 : 1)));   // plane 0 also holds mode 6's AoS
+        a.o[k] = (float*)p;
+    }
+    CK(hipMalloc(&p, frames * 4));
+    a.sink = (uint32_t*)p;
+    CK(hipMalloc(&p, 8));
+    a.counter = (unsigned long long*)p;
+    a.px16 = px / 16;
+    a.cap = cap;
+    a.kept = kept;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const char* names[] = {"read-then-write", "interleaved", "read only", "write only", "read, re-read disp, write",
+                           "write: dense frames", "write: one AoS plane", "write: stride cap+64", "write: dense sweep",
+                           "write: 32 B per lane", "read-then-write, atomic regions", "write: full frames, stride cap",
+                           "interleaved, atomic regions"};
+    const int64_t cap0 = cap - 64;
+    for (int round = 0; round < 2; ++round)
+        for (int mode = 0; mode < 13; ++mode) {
+            a.mode = mode;
+            a.nplanes = 5;
+            a.nper = kept;
+            a.stride = cap0;
+            if (mode == 5) a.stride = kept;
+            if (mode == 6) {
+                a.nplanes = 1;
+                a.nper = 5 * kept;
+                a.stride = 5 * cap0;
+            }
+            if (mode == 7) a.stride = cap;
+            if (mode == 11) a.nper = cap0;
+            auto launch = [&]() {
+                if (mode == 8) hipLaunchKernelGGL(sweep_kernel, dim3(4096), dim3(256), 0, 0, a, kept * frames);
+                else hipLaunchKernelGGL(sol_kernel, dim3(frames), dim3(256), 0, 0, a);
+            };
+            float best = 1e30f, tot = 0.f;
+            const int reps = 5;
+            CK(hipMemset(a.counter, 0, 8));
+            launch();
+            for (int r = 0; r < reps; ++r) {
+                CK(hipMemset(a.counter, 0, 8));
+                CK(hipEventRecord(e0, 0));
+                launch();
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                best = ms < best ? ms : best;
+                tot += ms;
+            }
+            const double rd = ((mode == 3 || mode >= 5) && mode != 10 && mode != 12 ? 0. : 4. * px * frames) + (mode == 4 ? 1. * px * frames : 0.);
+            const double wr = mode == 2 ? 0. : 20. * (mode == 11 ? cap0 : kept) * frames;
+            std::printf("{\"round\": %d, \"mode\": %d, \"what\": \"%s\", \"GB\": %.2f, \"best_ms\": %.3f, \"mean_ms\": %.3f, "
+                        "\"TBps_best\": %.2f}\n",
+                        round, mode, names[mode], (rd + wr) / 1e9, best, tot / reps, (rd + wr) / best / 1e9);
+            std::fflush(stdout);
+        }
+    return 0;
+}
