@@ -19,6 +19,7 @@
 //   mode 10 read-then-write, each frame's output region taken from a global counter (atomicAdd) after its reads
 //   mode 11 five planes, frame stride cap, every frame writing all cap outputs (no gaps; more bytes)
 //   mode 12 mode 1 (chunk-interleaved reads and writes) into a region taken from the counter after the first chunk's reads
+// argv: frames (4096), outputs per frame (277200), 1 = output planes physically contiguous (0)
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/_sol_pipe tools/sol_pipe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -161,8 +162,11 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&p, frames * px * 3));
     CK(hipMemset(p, 2, frames * px * 3));
     a.bgr = (const uint4*)p;
+    const bool contig = argc > 3 && std::atoi(argv[3]) != 0;   // outputs physically contiguous
     for (int k = 0; k < 5; ++k) {
-        CK(hipMalloc(&p, frames * cap * 4 * (k == 0 ? 5 : 1)));   // plane 0 also holds mode 6's AoS
+        const size_t bytes = frames * cap * 4 * (k == 0 ? 5 : 1);   // plane 0 also holds mode 6's AoS
+        if (contig) CK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous));
+        else CK(hipMalloc(&p, bytes));
         a.o[k] = (float*)p;
     }
     CK(hipMalloc(&p, frames * 4));
