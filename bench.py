@@ -281,9 +281,11 @@ def extras(b, args, with_cpu):
     px = b.frames * H * W
     n2 = int(b.read_counts()[:, 2].sum())
     ms = _timed(b, lambda: (b.road_raster(sync=False), b.nonzero(sync=False)), 3)
-    byts = px + 8 * n2 + px + 8 * n2          # raster: zero + point reads (+1 B each); walk: image + [j,i]
+    # one pass (road_kernel): the points in (8 B each), the images out once, 8 B per non-zero pixel out (at most
+    # one per point: counted as one per point, so approx_GBps is an upper bound)
+    byts = 8 * n2 + px + 8 * n2
     ex["road_raster_nonzero"] = {"ms_per_batch": round(ms, 3), "approx_GBps": round(byts / ms / 1e6, 1),
-                                 "points": n2, "kernels": "raster_kernel + nonzero_kernel"}
+                                 "points": n2, "kernels": "road_kernel (raster + non-zero walk in one pass)"}
     mask = carmask()
     b.set_mask(mask)
     ms = _timed(b, lambda: b.prepass("previous", sync=False), 3)

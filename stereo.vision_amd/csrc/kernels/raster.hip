@@ -117,6 +117,161 @@ __global__ __launch_bounds__(256) void nonzero_kernel(const uint8_t* __restrict_
     if (tid == 0) counts[frame] = running;
 }
 
+// ---------------------------------------------------------------------------
+// The batch's road images and their walks in one pass (road_kernel). The
+// pipeline's points come in raster order of their grid points, (x, y) = (gx -
+// dx, gy - dy) with deltas 0 or 1, so y never drops by more than one along the
+// list (y_j >= y_i - 1 for j > i). One workgroup per frame builds its image a
+// band of rows at a time in LDS: it zeroes the band, marks the points whose
+// row is in the band (scanning the list from a cursor; a chunk holding a row
+// >= r1 + 1 ends the band, the first chunk holding a row >= r1 starts the next
+// band's scan), writes the band's rows once (no memset, no read-modify-write
+// of scattered bytes) and walks the band's non-zero pixels from LDS with the
+// nonzero_kernel's scan and staging (no re-read of the image). A point with y
+// = -1 (numpy's img[-1], the last row) is kept in a bit row until the band
+// holding row H - 1. Bytes per frame: the points (8 B each) + the image once +
+// the walk (8 B per non-zero pixel), against + the image three more times
+// (zeroing, the scattered bytes' read-modify-write, the walk's read) before.
+// ---------------------------------------------------------------------------
+constexpr int kRoadBandBytes = 12288;   // LDS of one band (W = 1024: 12 rows): 29 KB in all, 5 workgroups per CU
+
+struct RoadShared {
+    uint32_t wtot[4];
+    uint32_t wrap[128];                   // bit x: row H - 1 has a point with y = -1 at x (W <= 4096)
+    uint32_t stage[256 * 16];             // a walk chunk's pixel indices, in output order
+};
+
+__global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ px, const int32_t* __restrict__ py,
+                                                   const int64_t* __restrict__ counts, int64_t cap,
+                                                   uint8_t* __restrict__ img, int H, int W, int Wu, int R,
+                                                   uint64_t W_m40, int32_t* __restrict__ nzout,
+                                                   int64_t* __restrict__ nzcount) {
+    __shared__ RoadShared sh;
+    extern __shared__ uint4 road_band[];   // the band: R rows of W bytes (dynamic LDS)
+    uint8_t* const band = reinterpret_cast<uint8_t*>(road_band);
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int frame = blockIdx.x;
+    int64_t n = counts[4 * (int64_t)frame + 2];
+    n = n < 0 ? 0 : (n > cap ? cap : n);
+    const int32_t* fx = px + (int64_t)frame * cap;
+    const int32_t* fy = py + (int64_t)frame * cap;
+    uint8_t* fimg = img + (int64_t)frame * H * W;
+    int2* fo = reinterpret_cast<int2*>(nzout) + (int64_t)frame * cap;
+    if (tid < 128) sh.wrap[tid] = 0;
+    // this lane's 4 points of the 1024-point chunk at i0 (qy = -2: past the list)
+    const auto load = [&](int64_t i0, int (&qx)[4], int (&qy)[4]) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t i = i0 + t * 256 + tid;
+            const bool ok = i < n;
+            qx[t] = ok ? fx[i] : 0;
+            qy[t] = ok ? fy[i] : -2;
+        }
+    };
+    int64_t cur = 0;
+    uint32_t running = 0;
+    for (int r0 = 0; r0 < H; r0 += R) {
+        const int r1 = min(r0 + R, H);
+        const int bpx = (r1 - r0) * W, bz = (bpx + 15) & ~15;
+        for (int o = 16 * tid; o < bz; o += 16 * 256) *reinterpret_cast<uint4*>(band + o) = make_uint4(0, 0, 0, 0);
+        __syncthreads();   // band zeroed (and the previous band's walk is done with sh.stage)
+        int64_t i = cur, next = -1;
+        int qx[4], qy[4], nx[4], ny[4];
+        if (i < n) load(i, qx, qy);
+        while (i < n) {
+            if (i + 1024 < n) load(i + 1024, nx, ny);   // in flight while this chunk is marked
+            bool ge1 = false, ge2 = false;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int y = qy[t];
+                if (y == -2) continue;
+                const int x = qx[t] < 0 ? qx[t] + Wu : qx[t];
+                if (y < 0) atomicOr(&sh.wrap[x >> 5], 1u << (x & 31));
+                else if (y >= r0 && y < r1) band[(y - r0) * W + x] = 255;
+                ge1 |= y >= r1;
+                ge2 |= y >= r1 + 1;
+            }
+            const bool any1 = __syncthreads_or(ge1) != 0;
+            const bool any2 = __syncthreads_or(ge2) != 0;
+            if (next < 0 && any1) next = i;   // the next band's rows start in this chunk at the earliest
+            i += 1024;
+            if (any2) break;                  // every later point lies at row r1 or below
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                qx[t] = nx[t];
+                qy[t] = ny[t];
+            }
+        }
+        cur = next >= 0 ? next : i;
+        if (r1 == H) {   // the wrapped points' marks on the last row
+            for (int x = tid; x < W; x += 256)
+                if ((sh.wrap[x >> 5] >> (x & 31)) & 1u) band[(H - 1 - r0) * W + x] = 255;
+        }
+        __syncthreads();   // the band is complete
+        for (int o = 8 * tid; o < bpx; o += 8 * 256)
+            *reinterpret_cast<uint2*>(fimg + (int64_t)r0 * W + o) = *reinterpret_cast<const uint2*>(band + o);
+        // the band's non-zero pixels in raster order (nonzero_kernel's chunk logic, from LDS)
+        const uint32_t* bw = reinterpret_cast<const uint32_t*>(band);
+        const int vecs = bz / 16;
+        for (int base = 0; base < vecs; base += 256) {
+            const int v = base + tid;
+            uint4 q = make_uint4(0, 0, 0, 0);
+            if (v < vecs) q = *reinterpret_cast<const uint4*>(bw + 4 * v);
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+            uint32_t bits = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t nz = (((w[k] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w[k]) & 0x80808080u;
+                bits |= ((nz >> 7) & 1u) << (4 * k) | ((nz >> 15) & 1u) << (4 * k + 1) |
+                        ((nz >> 23) & 1u) << (4 * k + 2) | ((nz >> 31) & 1u) << (4 * k + 3);
+            }
+            const uint32_t cnt = __builtin_popcount(bits);
+            const uint32_t inc = wave_incl_scan(cnt);
+            if (lane == 63) sh.wtot[wave] = inc;
+            __syncthreads();   // also: the previous chunk's writes have read sh.stage
+            uint32_t wbase = 0, tot = 0;
+#pragma unroll
+            for (int w4 = 0; w4 < 4; ++w4) {
+                const uint32_t t = sh.wtot[w4];
+                wbase += w4 < wave ? t : 0u;
+                tot += t;
+            }
+            uint32_t o = wbase + inc - cnt;
+            const uint32_t p0 = (uint32_t)r0 * (uint32_t)W + (uint32_t)(v * 16);
+            while (bits) {
+                const int b = __builtin_ctz(bits);
+                bits &= bits - 1;
+                sh.stage[o++] = p0 + (uint32_t)b;
+            }
+            __syncthreads();   // sh.wtot is rewritten next chunk; sh.stage is complete
+            v2i* dst = reinterpret_cast<v2i*>(fo + running);
+            for (uint32_t j = tid; j < tot; j += 256) {
+                const uint32_t p = sh.stage[j];
+                const int y = fastdiv40((int)p, W_m40);
+                __builtin_nontemporal_store((v2i){(int)(p - (uint32_t)y * (uint32_t)W), y}, dst + j);
+            }
+            running += tot;
+        }
+    }
+    if (tid == 0) nzcount[frame] = running;
+}
+
+hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* counts, int64_t cap, uint8_t* img,
+                       int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, hipStream_t s) {
+    if (frames <= 0) return hipSuccess;
+    if (W <= 0 || W > 4096 || W % 8 || H <= 0 || Wu <= 0 || Wu > W || (int64_t)H * W >= (1ll << 28))
+        return hipErrorInvalidValue;
+    int bytes = kRoadBandBytes;   // SVX_ROAD_BAND: A/B knob
+    if (const char* e = std::getenv("SVX_ROAD_BAND")) bytes = std::max(4096, std::min(65536, std::atoi(e)));
+    const int R = std::max(1, bytes / W);   // rows per band
+    const size_t dyn = ((size_t)R * W + 15) / 16 * 16;
+    if (dyn > 65536) return hipErrorInvalidValue;
+    const uint64_t m40 = (((uint64_t)1 << 40) + (uint64_t)W - 1) / (uint64_t)W;
+    hipLaunchKernelGGL(road_kernel, dim3(frames), dim3(256), dyn, s, px, py, counts, cap, img, H, W, Wu, R, m40, nzout,
+                       nzcount);
+    return hipGetLastError();
+}
+
 hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
                           hipStream_t s) {
     if (frames <= 0) return hipSuccess;

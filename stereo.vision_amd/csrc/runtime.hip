@@ -251,6 +251,7 @@ struct sv_batch {
     bool pipe_placed = false;   // the resident pipeline's outputs were placed (pipe_place)
     DevBuf mdisp, carmask;      // pre-pass: masked disparity (frames x H x W), 0x00/0xFF mask (H x W)
     DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
+    bool nz_fresh = false;      // nz holds the walk of the current road images (road_kernel wrote both)
     DevBuf mpts, rres;          // maskpoints (frames x mcap x 3 fp64) + counts; batched RANSAC results
     DevBuf mpk;                 // maskpoints packed (frames x mcap words x | y << 12 | d << 24): RANSAC's fp32 screen
     DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
@@ -1229,9 +1230,19 @@ int sv_batch_road_raster(sv_batch* b, int sync) {
     HIP_TRY(hipSetDevice(b->device));
     const size_t px = (size_t)b->H * b->W;
     HIP_TRY(b->road.ensure(px * b->frames));
-    HIP_TRY(launch_raster(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), 1, b->counts, 4, 2, (int64_t)b->cap,
-                          b->road.as<uint8_t>(), b->frames, b->H,
-                          b->W, b->Wu, b->stream));
+    HIP_TRY(b->nz.ensure(sizeof(int32_t) * 2 * b->cap * b->frames));
+    HIP_TRY(b->nzcount.ensure(sizeof(int64_t) * b->frames));
+    // the images and their non-zero walks in one pass (road_kernel); SVX_ROAD_FUSED=0: raster, then the walk
+    const char* v = std::getenv("SVX_ROAD_FUSED");
+    b->nz_fresh = !(v && v[0] == '0');
+    if (b->nz_fresh) {
+        HIP_TRY(launch_road(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), b->counts, (int64_t)b->cap,
+                            b->road.as<uint8_t>(), b->frames, b->H, b->W, b->Wu, b->nz.as<int32_t>(),
+                            b->nzcount.as<int64_t>(), b->stream));
+    } else {
+        HIP_TRY(launch_raster(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), 1, b->counts, 4, 2, (int64_t)b->cap,
+                              b->road.as<uint8_t>(), b->frames, b->H, b->W, b->Wu, b->stream));
+    }
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }
@@ -1240,6 +1251,10 @@ int sv_batch_nonzero(sv_batch* b, int sync) {
     if (!b) return fail(SV_E_ARG, "null batch");
     if (!b->road.p) return fail(SV_E_STATE, "no road images (sv_batch_road_raster first)");
     HIP_TRY(hipSetDevice(b->device));
+    if (b->nz_fresh) {   // sv_batch_road_raster walked the images it wrote
+        if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
+        return SV_OK;
+    }
     HIP_TRY(b->nz.ensure(sizeof(int32_t) * 2 * b->cap * b->frames));
     HIP_TRY(b->nzcount.ensure(sizeof(int64_t) * b->frames));
     HIP_TRY(launch_nonzero(b->road.as<uint8_t>(), b->frames, (int64_t)b->H * b->W, b->W, b->nz.as<int32_t>(),

@@ -89,6 +89,11 @@ hipError_t launch_mask(const uint8_t* disp, uint8_t* out, const uint8_t* mask_ff
 // (px[(f cap + i) ps], py[(f cap + i) ps]): ps = 1 for two planes, 2 for interleaved (x, y) pairs.
 hipError_t launch_raster(const int32_t* px, const int32_t* py, int ps, const int64_t* counts, int cstride, int cidx,
                          int64_t cap, uint8_t* img, int frames, int H, int W, int Wu, hipStream_t s);
+// The batch's road images and walks in one pass (road_kernel): the pipeline's points (two planes, frame f's
+// counts[4f + 2] points at f * cap, in the pipeline's raster order) -> img (frames x H x W, W % 8 == 0) and the
+// raster-order [j, i] of every non-zero pixel (frames x cap pairs) + nzcount[frame].
+hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* counts, int64_t cap, uint8_t* img,
+                       int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, hipStream_t s);
 // img frames x px (px % 4 == 0, rows of W <= 4096 pixels)
 hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
                           hipStream_t s);

@@ -131,3 +131,34 @@ def test_batch_road_raster_and_walk(svx_mod, step):
             img, walk = b.read_road(f, walk=True)
             assert np.array_equal(img, rimg)
             assert np.array_equal(walk, oracle.nonzero_points(rimg))
+
+
+@pytest.mark.parametrize("step", [1, 2])
+def test_batch_road_edge_frames(svx_mod, step):
+    """The fused road pass (bands of rows in LDS, a cursor over the raster-ordered points) on frames with no
+    point, every grid point, points on a few scattered rows only, and random disparity: image and walk equal
+    the oracle's generatePointsAsImage and its raster-order walk."""
+    rng = np.random.default_rng(7)
+    H, W = 544, 1024
+    frames = []
+    frames.append(np.zeros((H, W), np.uint8))
+    frames.append(np.full((H, W), 255, np.uint8))
+    sparse = np.zeros((H, W), np.uint8)
+    for r in (0, 1, 37, 38, 200, 411, 542, 543):
+        sparse[r, rng.integers(0, W, 40)] = rng.integers(1, 256, 40)
+    frames.append(sparse)
+    frames.append(rng.integers(0, 256, (H, W)).astype(np.uint8))
+    bgr = rng.integers(0, 256, (H, W, 3)).astype(np.uint8)
+    kw = dict(plane=(0.0, 0.0, 0.01), point_thr=1e9, hist_thr=0)
+    with svx_mod.batch.Batch(len(frames), H=H, W=W, step=step, with_bgr=True, with_points=True) as b:
+        for f, d in enumerate(frames):
+            b.upload(f, d, bgr)
+        b.pipeline(**kw)
+        b.road_raster()
+        b.nonzero()
+        for f, d in enumerate(frames):
+            ref = oracle.pipeline_frame(d, bgr, step, abc=np.array(kw["plane"]), point_thr=1e9, hist_thr=0)
+            rimg = oracle.road_raster(ref["pts"])
+            img, walk = b.read_road(f, walk=True)
+            assert np.array_equal(img, rimg), f
+            assert np.array_equal(walk, oracle.nonzero_points(rimg)), f
