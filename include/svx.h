@@ -252,7 +252,10 @@ int sv_batch_read_disp(sv_batch* b, int frame, uint8_t* disp, uint8_t* masked);
 
 /* Road images of the pipeline's int32 points (generatePointsAsImage per
  * frame), their raster-order non-zero walks, and read-back (img and/or the
- * walk; n receives the walk's length). */
+ * walk; n receives the walk's length). sv_batch_road_raster writes the images
+ * and their walks in one pass (the walks are then already current and
+ * sv_batch_nonzero only orders/syncs); with SVX_ROAD_FUSED=0 it writes the
+ * images only and sv_batch_nonzero walks them. */
 int sv_batch_road_raster(sv_batch* b, int sync);
 int sv_batch_nonzero(sv_batch* b, int sync);
 int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int64_t cap, int64_t* n);
