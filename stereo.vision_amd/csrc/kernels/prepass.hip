@@ -35,13 +35,13 @@ __device__ __forceinline__ uint32_t fill4(uint32_t raw, uint32_t prev) {
     return out;
 }
 
-constexpr int kFillUnroll = 8;
-
-// words = pixels / 4 per frame; disp may equal out (in place).
+// words = pixels / 4 per frame; disp may equal out (in place). U frames of loads in flight per lane.
+template <int U>
 __global__ __launch_bounds__(256) void fill_prev_kernel(const uint32_t* raw, uint32_t* out, uint32_t* masked,
                                                         const uint32_t* __restrict__ mask, const uint32_t* prev0,
                                                         int frames, int64_t words) {
-    const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+    constexpr int kFillUnroll = U;
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= words) return;
     uint32_t c = prev0 ? prev0[i] : 0u;
     bool have = prev0 != nullptr;
@@ -122,10 +122,21 @@ hipError_t launch_fill_prev(const uint8_t* raw, uint8_t* out, uint8_t* masked, c
     if (frames <= 0 || frame_px <= 0) return hipSuccess;
     if (frame_px % 4) return hipErrorInvalidValue;
     const int64_t words = frame_px / 4;
-    hipLaunchKernelGGL(fill_prev_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s,
-                       reinterpret_cast<const uint32_t*>(raw), reinterpret_cast<uint32_t*>(out),
-                       reinterpret_cast<uint32_t*>(masked), reinterpret_cast<const uint32_t*>(mask_ff),
-                       reinterpret_cast<const uint32_t*>(prev0), frames, words);
+    // A/B knob SVX_FILL="U,B": frames of loads in flight per lane (8, 16, 32) and the workgroup size. 64-lane
+    // workgroups spread a frame's 2,176 waves evenly over the 256 CUs (256-lane ones leave 32 CUs a third
+    // workgroup): 1.47 vs 1.53 ms per 4096 frames; 16 and 32 frames in flight are slower (1.58-1.63, 1.77 ms)
+    int U = 8, B = 64;
+    if (const char* e = std::getenv("SVX_FILL")) std::sscanf(e, "%d,%d", &U, &B);
+    if (B != 64 && B != 128 && B != 256) B = 256;
+    const dim3 grid((unsigned)((words + B - 1) / B)), block(B);
+    const auto* r = reinterpret_cast<const uint32_t*>(raw);
+    auto* o = reinterpret_cast<uint32_t*>(out);
+    auto* m = reinterpret_cast<uint32_t*>(masked);
+    const auto* k = reinterpret_cast<const uint32_t*>(mask_ff);
+    const auto* p = reinterpret_cast<const uint32_t*>(prev0);
+    if (U >= 32) hipLaunchKernelGGL(fill_prev_kernel<32>, grid, block, 0, s, r, o, m, k, p, frames, words);
+    else if (U >= 16) hipLaunchKernelGGL(fill_prev_kernel<16>, grid, block, 0, s, r, o, m, k, p, frames, words);
+    else hipLaunchKernelGGL(fill_prev_kernel<8>, grid, block, 0, s, r, o, m, k, p, frames, words);
     return hipGetLastError();
 }
 
