@@ -233,6 +233,72 @@ __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint3
     if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
 }
 
+// The same walk for a compile-time half window (the reference's block 21: SH2 = 10) with each horizontal sum
+// read once: the row a step drops (max(y - SH2 - 1, 0)) is the row added RS = 2 SH2 + 1 steps before it, or
+// one of rows 0 .. SH2 read for the first window, so the walk keeps the next RS drops in registers (a ring
+// indexed by the unrolled step) and loads only the added rows, the next block's in flight.
+template <int SH2C>
+__global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const uint32_t* __restrict__ hvol,
+                                                                   uint32_t* __restrict__ cvol,
+                                                                   uint32_t* __restrict__ l2vol,
+                                                                   uint32_t* __restrict__ flags, int frames) {
+    constexpr int RS = 2 * SH2C + 1;
+    const int wpb = blockDim.x >> 6;
+    const int cols_blocks = (k.width1 + wpb - 1) / wpb;
+    const int f = blockIdx.x / cols_blocks;
+    const int xi = (blockIdx.x - f * cols_blocks) * wpb + (threadIdx.x >> 6);
+    if (f >= frames || xi >= k.width1) return;
+    const int lane = lane_id(), H = k.H;
+    const size_t rs = (size_t)k.width1 * 64;
+    const size_t base = (size_t)f * H * rs + (size_t)xi * 64 + lane;
+    const uint32_t* hb = hvol + base;
+    // drop[u]: the row step y0 + u subtracts (block y0 = 0: rows max(u - SH2 - 1, 0), read with the first window)
+    uint32_t drop[RS];
+    int c0 = 0, c1 = 0;
+#pragma unroll
+    for (int kk = 0; kk <= SH2C; ++kk) {
+        const uint32_t h = hb[(size_t)min(kk, H - 1) * rs];
+        const int sc = kk == 0 ? SH2C + 1 : 1;
+        c0 += lo16(h) * sc;
+        c1 += hi16(h) * sc;
+        if (kk == 0) {
+#pragma unroll
+            for (int u = 0; u <= SH2C + 1; ++u) drop[u] = h;   // steps 1 .. SH2 + 1 drop row 0
+        } else if (kk < SH2C) {
+            drop[kk + SH2C + 1] = h;                           // step kk + SH2 + 1 drops row kk
+        }   // row SH2 is step RS's drop: step 0 stores it (drop[0] = its added row, SH2)
+    }
+    PathState st;
+    bool ovf = false;
+    const bool upd_col = xi > 0;
+    uint32_t add[RS];   // the rows steps y0 .. y0 + RS - 1 add (y + SH2, clamped)
+#pragma unroll
+    for (int u = 0; u < RS; ++u) add[u] = hb[(size_t)min(u + SH2C, H - 1) * rs];
+    for (int y0 = 0; y0 < H; y0 += RS) {
+        uint32_t nadd[RS];
+#pragma unroll
+        for (int u = 0; u < RS; ++u) nadd[u] = hb[(size_t)min(y0 + RS + u + SH2C, H - 1) * rs];
+#pragma unroll
+        for (int u = 0; u < RS; ++u) {
+            const int y = y0 + u;
+            if (y >= H) break;
+            if (y > 0 && upd_col && y + SH2C < H) {
+                c0 += lo16(add[u]) - lo16(drop[u]);
+                c1 += hi16(add[u]) - hi16(drop[u]);
+            }
+            drop[u] = add[u];   // step y + RS drops row y + SH2
+            const int cw0 = (int)(int16_t)c0, cw1 = (int)(int16_t)c1;
+            cvol[base + (size_t)y * rs] = pack16(cw0, cw1);
+            int L0, L1;
+            path_step(cw0, cw1, st, k.P1, k.P2, L0, L1, ovf);
+            l2vol[base + (size_t)y * rs] = pack16(L0, L1);
+        }
+#pragma unroll
+        for (int u = 0; u < RS; ++u) add[u] = nadd[u];
+    }
+    if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
+}
+
 // ---------------------------------------------------------------------------
 // Diagonal paths: dir 1 from (x-1, y-1), dir 3 from (x+1, y-1).
 // ---------------------------------------------------------------------------
@@ -746,9 +812,16 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
     const int paths = 2 * (k.width1 + H - 1) * frames;
     const size_t lds4 = sizeof(int16_t) * 3 * (size_t)k.W * 4;
     const int pf = sgbm_prefetch();
+    // the register-ring vertical walk for the reference's block 21 (SVX_SGBM_VRING=0: the generic walk)
+    const char* vr = std::getenv("SVX_SGBM_VRING");
+    const bool vring = k.SH2 == 10 && !(vr && vr[0] == '0');
 #define SVX_SGBM_WALKS(U)                                                                                         \
-    hipLaunchKernelGGL(sgbm_vertical_kernel<U>, dim3(frames * cb), dim3(256), 0, st, k, s.hl1, s.c, s.l2, s.flags, \
-                       frames);                                                                                    \
+    if (vring)                                                                                                    \
+        hipLaunchKernelGGL(sgbm_vertical_ring_kernel<10>, dim3(frames * cb), dim3(256), 0, st, k, s.hl1, s.c,     \
+                           s.l2, s.flags, frames);                                                                \
+    else                                                                                                          \
+        hipLaunchKernelGGL(sgbm_vertical_kernel<U>, dim3(frames * cb), dim3(256), 0, st, k, s.hl1, s.c, s.l2,     \
+                           s.flags, frames);                                                                      \
     hipLaunchKernelGGL(sgbm_diag_kernel<U>, dim3((paths + 3) / 4), dim3(256), 0, st, k, s.c, s.hl1, s.l3, s.flags, \
                        frames);                                                                                    \
     hipLaunchKernelGGL(sgbm_row_kernel<U>, dim3((frames * H + 3) / 4), dim3(256), lds4, st, k, s.c, s.hl1, s.l2,   \
