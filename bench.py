@@ -358,6 +358,37 @@ def extras(b, args, with_cpu):
                                "frames_per_s": round(b.frames / ms * 1e3, 1),
                                "stages": "prepass(previous+mask) -> maskpoints+RANSAC(600) -> pipeline(per-frame "
                                          "planes) -> road raster -> non-zero walk"}
+    # the same loop with two batches in flight, each on its own stream: the RANSAC draws (one wave's dependent
+    # chain per frame) leave the HBM idle, and the other batch's pre-pass, pipeline and road pass fill it
+    from svx import batch as sbm
+    with sbm.Batch(b.frames, H, W, args.step, with_bgr=True, with_points=True, device=b.device) as b2:
+        b2.synth(b.frames)
+        b2.set_mask(mask)
+        pair = (b, b2)
+
+        def two_loops():
+            for x in pair:
+                x.prepass("previous", sync=False)
+                x.ransac(seed_base=0, trials=600, sync=False)
+            for x in pair:
+                x.pipeline_planes(sync=False)
+                x.road_raster(sync=False)
+                x.nonzero(sync=False)
+        two_loops()
+        for x in pair:
+            x.sync()
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            two_loops()
+        for x in pair:
+            x.sync()
+        ms2 = (time.perf_counter() - t0) / reps / 2 * 1e3
+    ex["device_frame_loop_two_batches"] = {"ms_per_batch": round(ms2, 2), "frames": b.frames,
+                                           "frames_per_s": round(b.frames / ms2 * 1e3, 1),
+                                           "stages": "as device_frame_loop, two batches of frames in flight on two "
+                                                     "streams (each batch's pre-pass + RANSAC, then each batch's "
+                                                     "pipeline + road)"}
     return ex
 
 
