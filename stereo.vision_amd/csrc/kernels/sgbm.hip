@@ -169,6 +169,163 @@ __global__ __launch_bounds__(256) void sgbm_hsum_kernel(SgbmK k, const uint8_t* 
     }
 }
 
+// The same horizontal sums for a compile-time half window (the reference's block 21: SW2 = 10), with less work
+// per column. (1) Both BT channels in one packed 16-bit operation: a pixel's features are three words, value,
+// half-neighbour min and max, each holding channel 0 (x-derivative) in the low and channel 1 (raw) in the high
+// half, so a cost is 9 v_pk_* operations plus its channel sum. (2) Lane l's cost pair at column j reads the right
+// features A_j(l) = R[j + D - 2l] and A_{j-1}(l) (= R[j + D - 2l - 1]); since A_{j+1}(l) = A_{j-1}(l - 1), the
+// next column's right features are the previous-but-one's moved up a lane (DPP), lane 0 taking the new
+// R[j + 1 + D], so the main loop reads LDS only at one address for the whole wave. (3) The window's RS columns
+// are a register ring indexed by the unrolled step.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+struct BtFeat {
+    uint32_t v, lo, hi;   // value, half-neighbour min, max: channel 0 | channel 1 << 16
+};
+__device__ __forceinline__ uint32_t bt_cost2(const BtFeat& a, const BtFeat& b) {
+    const s16x2 z = {0, 0};
+    const s16x2 u = as_s16x2(a.v), u0 = as_s16x2(a.lo), u1 = as_s16x2(a.hi);
+    const s16x2 v = as_s16x2(b.v), v0 = as_s16x2(b.lo), v1 = as_s16x2(b.hi);
+    const s16x2 c0 = __builtin_elementwise_max(__builtin_elementwise_max(u - v1, z), v0 - u);
+    const s16x2 c1 = __builtin_elementwise_max(__builtin_elementwise_max(v - u1, z), u0 - v);
+    const uint32_t c = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(c0, c1));
+    return (c & 0xFFFF) + (c >> 18);   // channel 0 + (channel 1 >> 2); both in 0 .. 255
+}
+
+template <int SW2C>
+__global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint8_t* __restrict__ left,
+                                                               const uint8_t* __restrict__ right,
+                                                               uint32_t* __restrict__ hvol, int frames) {
+    constexpr int RS = 2 * SW2C + 1;
+    extern __shared__ uint32_t smem[];
+    const int W = k.W, H = k.H;
+    const int f = blockIdx.x / H, y = blockIdx.x - f * H;
+    if (f >= frames) return;
+    uint2* featA = reinterpret_cast<uint2*>(smem);             // [img][W] (value, min)
+    uint32_t* featB = reinterpret_cast<uint32_t*>(featA + 2 * W);   // [img][W] max
+    uint8_t* raw = reinterpret_cast<uint8_t*>(smem);           // [img][row above, row, row below][W], dead before
+                                                               // the features are written over it
+    uint8_t* tmp = reinterpret_cast<uint8_t*>(featB + 2 * W);  // [img][ch][W] values
+    const int tid = threadIdx.x;
+    const int yu = y > 0 ? y - 1 : y, yd = y < H - 1 ? y + 1 : y;
+    if (((W | (int)((uintptr_t)left | (uintptr_t)right)) & 3) == 0) {
+        // 4-byte words, every load of the thread issued before the first is waited for (W <= 2048: <= 12 each)
+        constexpr int kPer = 12;
+        const int wpr = W >> 2, nw = 6 * wpr;
+        uint32_t v[kPer];
+#pragma unroll
+        for (int t = 0; t < kPer; ++t) {
+            const int i = tid + t * 256;
+            if (i < nw) {
+                const int r = i / wpr, xw = i - r * wpr;
+                const int img = r >= 3, row = r - 3 * img;
+                const int yy = row == 0 ? yu : (row == 1 ? y : yd);
+                v[t] = reinterpret_cast<const uint32_t*>((img ? right : left) + (size_t)f * k.frame_px +
+                                                         (size_t)yy * W)[xw];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kPer; ++t) {
+            const int i = tid + t * 256;
+            if (i < nw) reinterpret_cast<uint32_t*>(raw)[i] = v[t];
+        }
+    } else {
+        for (int i = tid; i < 6 * W; i += 256) {
+            const int r = i / W, x = i - r * W;
+            const int img = r >= 3, row = r - 3 * img;
+            const int yy = row == 0 ? yu : (row == 1 ? y : yd);
+            raw[i] = (img ? right : left)[(size_t)f * k.frame_px + (size_t)yy * W + x];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * W; i += 256) {
+        const int img = i >= W, x = i - img * W;
+        const uint8_t* u = raw + img * 3 * W;
+        const uint8_t* r = u + W;
+        const uint8_t* d = r + W;
+        int pv = k.ftzero, rv = k.ftzero;
+        if (x > 0 && x < W - 1) {
+            const int g = (r[x + 1] - r[x - 1]) * 2 + u[x + 1] - u[x - 1] + d[x + 1] - d[x - 1];
+            pv = min(max(g, -k.ftzero), k.ftzero) + k.ftzero;
+            rv = r[x];
+        }
+        tmp[(img * 2 + 0) * W + x] = (uint8_t)pv;
+        tmp[(img * 2 + 1) * W + x] = (uint8_t)rv;
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * W; i += 256) {
+        const int img = i >= W, x = i - img * W;
+        uint32_t fv = 0, flo = 0, fhi = 0;
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch) {
+            const uint8_t* v = tmp + (img * 2 + ch) * W;
+            const int c = v[x];
+            const int l = x > 0 ? (c + v[x - 1]) >> 1 : c;
+            const int r = x < W - 1 ? (c + v[x + 1]) >> 1 : c;
+            fv |= (uint32_t)c << (16 * ch);
+            flo |= (uint32_t)min(min(l, r), c) << (16 * ch);
+            fhi |= (uint32_t)max(max(l, r), c) << (16 * ch);
+        }
+        featA[i] = make_uint2(fv, flo);
+        featB[i] = fhi;
+    }
+    __syncthreads();
+
+    const int lane = lane_id(), wave = tid >> 6;
+    const int n = k.width1;
+    const int seg = (n + 3) / 4;
+    const int xs = wave * seg, xe = min(n, xs + seg);
+    if (xs >= xe) return;
+    const int d0 = 2 * lane;
+    const auto feat = [&](int i) -> BtFeat {
+        const uint2 a = featA[i];
+        return BtFeat{a.x, a.y, featB[i]};
+    };
+    // cost pair (d0, d0 + 1) from the left features at x and the right ones at x - d0 (a) and x - d0 - 1 (b)
+    const auto cost = [](const BtFeat& l, const BtFeat& a, const BtFeat& b) -> uint32_t {
+        return bt_cost2(l, a) | bt_cost2(l, b) << 16;
+    };
+    const auto pix = [&](int j) -> uint32_t {
+        j = min(max(j, 0), n - 1);
+        const int x = j + kSgD;
+        return cost(feat(x), feat(W + x - d0), feat(W + x - d0 - 1));
+    };
+    uint32_t ring[RS];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int s = 0; s < RS; ++s) {
+        ring[s] = pix(xs - SW2C + s);
+        sum += ring[s];
+    }
+    int jn = min(xs + SW2C, n - 1);   // the last column computed; ring[RS - 1] holds its cost
+    uint32_t vlast = ring[RS - 1];
+    BtFeat acur = feat(W + jn + kSgD - d0), aprev = feat(W + jn + kSgD - d0 - 1);   // A_jn, A_{jn - 1}
+    uint32_t* out = hvol + ((size_t)f * H + y) * n * 64 + lane;
+    for (int x0 = xs; x0 < xe; x0 += RS) {
+#pragma unroll
+        for (int u = 0; u < RS; ++u) {
+            const int xi = x0 + u;
+            if (xi >= xe) break;
+            out[(size_t)xi * 64] = sum;   // (non-temporal stores: no faster)
+            // step xi adds column xi + 1 + SW2 (clamped: past the last column it is the last column again)
+            if (jn < n - 1) {
+                ++jn;
+                const int x = jn + kSgD;
+                const BtFeat rn = feat(W + x);   // lane 0's A_jn
+                BtFeat anew;                     // wave_shr:1 of A_{jn - 2}
+                anew.v = __builtin_amdgcn_update_dpp((int)rn.v, (int)aprev.v, 0x138, 0xf, 0xf, false);
+                anew.lo = __builtin_amdgcn_update_dpp((int)rn.lo, (int)aprev.lo, 0x138, 0xf, 0xf, false);
+                anew.hi = __builtin_amdgcn_update_dpp((int)rn.hi, (int)aprev.hi, 0x138, 0xf, 0xf, false);
+                vlast = cost(feat(x), anew, acur);
+                aprev = acur;
+                acur = anew;
+            }
+            sum = (sum + vlast) - ring[u];
+            ring[u] = vlast;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Vertical box sum with OpenCV's row rules, and the (0,-1) path.
 // ---------------------------------------------------------------------------
@@ -806,8 +963,16 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
     hipError_t e = hipMemsetAsync(s.flags, 0, sizeof(uint32_t) * frames, st);
     if (e != hipSuccess) return e;
     // hsum: features (4 W words) + byte values (W words) + 4 waves' rings
-    const size_t lds1 = sizeof(uint32_t) * (5 * (size_t)k.W + 4 * (2 * k.SW2 + 1) * 64);
-    hipLaunchKernelGGL(sgbm_hsum_kernel, dim3(frames * H), dim3(256), lds1, st, k, left, right, s.hl1, frames);
+    // (the register-ring walk for the reference's block 21: features (24 W bytes, the staged rows (6 W) under
+    // them) + byte values (4 W); SVX_SGBM_HRING=0: the generic kernel)
+    const char* hr = std::getenv("SVX_SGBM_HRING");
+    if (k.SW2 == 10 && !(hr && hr[0] == '0')) {
+        hipLaunchKernelGGL(sgbm_hsum_ring_kernel<10>, dim3(frames * H), dim3(256), 28 * (size_t)k.W, st, k, left,
+                           right, s.hl1, frames);
+    } else {
+        const size_t lds1 = sizeof(uint32_t) * (5 * (size_t)k.W + 4 * (2 * k.SW2 + 1) * 64);
+        hipLaunchKernelGGL(sgbm_hsum_kernel, dim3(frames * H), dim3(256), lds1, st, k, left, right, s.hl1, frames);
+    }
     const int cb = (k.width1 + 3) / 4;
     const int paths = 2 * (k.width1 + H - 1) * frames;
     const size_t lds4 = sizeof(int16_t) * 3 * (size_t)k.W * 4;
