@@ -392,7 +392,7 @@ def extras(b, args, with_cpu):
     return ex
 
 
-def sgbm_extra(sb, device, with_cpu, frames=64, chunk=32):
+def sgbm_extra(sb, device, with_cpu, frames=128, chunk=128):
     """§8f rank 4: the disparity stage (functions.py:104-128: StereoSGBM(0,128,21) + filterSpeckles
     + scaling) on a resident batch of synthetic rectified pairs, frame 0 checked against the C
     oracle; then the whole per-frame loop from the stereo pair on the device."""

@@ -70,7 +70,7 @@ def _run(b, w, chunk=0, sync=False):
     elif w == "ransac":
         b.ransac(seed_base=0, trials=600, sync=sync)
     elif w == "sgbm":
-        b.sgbm(chunk=chunk or 32)
+        b.sgbm(chunk=chunk)
     elif w == "prepass":
         b.prepass("previous", sync=sync)
     elif w == "raster":
