@@ -162,7 +162,9 @@ int sv_lut_u8(const uint8_t* in, int64_t n, const uint8_t* lut, uint8_t* out);
  * cv2.equalizeHist. bgr: H x W x 3 contiguous. */
 int sv_grey_equalize(const uint8_t* bgr, int H, int W, uint8_t* out);
 /* stereoProcessor.compute(grayL, grayR) (functions.py:108): H x W int16
- * disparity x16, -16 where invalid. SV_E_RANGE when a path cost leaves int16
+ * disparity x16, -16 where invalid — computeDisparitySGBM followed, as in
+ * OpenCV's StereoSGBM::compute, by medianBlur(disp, disp, 3) (exact 3 x 3
+ * median, replicated border). SV_E_RANGE when a path cost leaves int16
  * (block cost sums above 32,763; OpenCV's int16 buffers would truncate). */
 int sv_sgbm_compute(const uint8_t* L, const uint8_t* R, int H, int W, const sv_sgbm_params* prm, int16_t* out);
 /* cv2.filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) on int16, in place
@@ -175,7 +177,8 @@ int sv_filter_speckles(int16_t* img, int H, int W, int new_val, int max_size, in
  * -> (d / 16.).astype(uint8) -> crop [0:390, 135:W] when crop != 0 ->
  * (x * (256. / max_disparity)).astype(uint8). out: rows x cols u8 with rows =
  * crop ? min(390, H) : H, cols = crop ? W - 135 : W. raw16 / filt16 (nullable,
- * H x W): the SGBM result before / after filterSpeckles. */
+ * H x W): the compute() result (after its medianBlur) before / after
+ * filterSpeckles. */
 int sv_disparity(const uint8_t* L, const uint8_t* R, int H, int W, const sv_sgbm_params* prm, int max_disparity,
                  int crop, uint8_t* out, int16_t* raw16, int16_t* filt16);
 
@@ -376,8 +379,10 @@ int sv_comm_group_end(void);
 int sv_comm_broadcast_plane(sv_comm* c, sv_plane* inout, int root);
 /* Broadcast the plane from root into device memory, ordered on batch b's
  * stream (b on the comm's device): the root passes its host plane, the other
- * ranks NULL. *out_dplane = the comm's device buffer (3 doubles a, b, c),
- * valid for stream-ordered use on b's stream (sv_batch_pipeline_dev). No host
+ * ranks NULL. *out_dplane = batch b's own device slot (3 doubles a, b, c;
+ * one per batch, so batches in flight on other streams and the comm's
+ * synchronous calls never overwrite it), valid for stream-ordered use on b's
+ * stream (sv_batch_pipeline_dev) until b's next broadcast. No host
  * sync. Inside a group, the broadcast is enqueued at sv_comm_group_end: enqueue
  * the pipelines after it. */
 int sv_comm_broadcast_plane_dev(sv_comm* c, sv_batch* b, const sv_plane* plane, int root, const double** out_dplane);

@@ -4,7 +4,9 @@ Python side of ``oracle/sgbm_oracle.c`` (functions.py:61-128
 ``gamma_table`` / ``gamma_change`` restate functions.py:61-67 with the same
 numpy expression; ``grey_equalize`` = cv2.cvtColor(BGR2GRAY) + equalizeHist
 (functions.py:89-97); ``sgbm`` = StereoSGBM(0, 128, 21).compute;
-``filter_speckles``; ``disparity`` = functions.py:104-128 end to end.
+``sgbm_raw`` = computeDisparitySGBM alone, ``median3`` = the medianBlur(disp, disp, 3)
+StereoSGBM::compute runs after it; ``filter_speckles``; ``disparity`` =
+functions.py:104-128 end to end.
 ``synth_pair`` is the numpy twin of the device's synthetic rectified pair.
 
 PARITY UNPINNED for the cv2 calls (cv2 is absent here; see sgbm_oracle.c).
@@ -42,6 +44,10 @@ def _lib():
         lib.svo_grey_equalize.restype = None
         lib.svo_sgbm.argtypes = [P, P, ci, ci, P, P]
         lib.svo_sgbm.restype = ci
+        lib.svo_sgbm_compute.argtypes = [P, P, ci, ci, P, P]
+        lib.svo_sgbm_compute.restype = ci
+        lib.svo_median3_s16.argtypes = [P, ci, ci, P]
+        lib.svo_median3_s16.restype = None
         lib.svo_filter_speckles.argtypes = [P, ci, ci, ci, ci, ci]
         lib.svo_filter_speckles.restype = ci
         lib.svo_disparity_scale.argtypes = [P, ci, ci, ci, ci, P]
@@ -69,8 +75,7 @@ def grey_equalize(bgr):
     return out
 
 
-def sgbm(left, right, **kw):
-    """StereoSGBM.compute(left, right): (H, W) int16 disparity x16."""
+def _sgbm_call(fn, left, right, kw):
     left = np.ascontiguousarray(left, np.uint8)
     right = np.ascontiguousarray(right, np.uint8)
     if left.shape != right.shape or left.ndim != 2:
@@ -78,9 +83,29 @@ def sgbm(left, right, **kw):
     H, W = left.shape
     out = np.empty((H, W), np.int16)
     prm = params(**kw)
-    rc = _lib().svo_sgbm(_p(left), _p(right), H, W, ctypes.byref(prm), _p(out))
+    rc = fn(_p(left), _p(right), H, W, ctypes.byref(prm), _p(out))
     if rc:
         raise ValueError("svo_sgbm: unsupported geometry (rc=%d)" % rc)
+    return out
+
+
+def sgbm(left, right, **kw):
+    """StereoSGBM.compute(left, right): (H, W) int16 disparity x16
+    (computeDisparitySGBM, then medianBlur 3 as OpenCV's compute does)."""
+    return _sgbm_call(_lib().svo_sgbm_compute, left, right, kw)
+
+
+def sgbm_raw(left, right, **kw):
+    """computeDisparitySGBM alone (before compute's medianBlur)."""
+    return _sgbm_call(_lib().svo_sgbm, left, right, kw)
+
+
+def median3(d16):
+    """cv2.medianBlur(d16, 3) on int16: exact 3 x 3 median, replicated border."""
+    d16 = np.ascontiguousarray(d16, np.int16)
+    H, W = d16.shape
+    out = np.empty_like(d16)
+    _lib().svo_median3_s16(_p(d16), H, W, _p(out))
     return out
 
 

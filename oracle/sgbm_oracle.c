@@ -7,6 +7,7 @@
  *   preProcessImages / gammaChange (functions.py:61-67, :81-87)  — numpy table, see oracle/sgbm.py
  *   greyscale (functions.py:89-97)  = cv2.cvtColor(BGR2GRAY) + cv2.equalizeHist
  *   disparity (functions.py:104-128) = StereoSGBM(0, 128, 21).compute
+ *                                        (computeDisparitySGBM + medianBlur 3)
  *                                      + cv2.filterSpeckles(d, 0, 4000, 123)
  *                                      + cv2.threshold(TOZERO at 0) + /16 -> u8
  *                                      + optional crop + x(256/128) -> u8
@@ -16,7 +17,8 @@
  * no OpenCV sources). The reference pins no version (no requirements file;
  * readme.md asks for "opencv"), so this file restates the algorithm OpenCV
  * 4.x publishes for these calls (modules/calib3d/src/stereosgbm.cpp:
- * computeDisparitySGBM with mode MODE_SGBM, calcPixelCostBT, filterSpecklesImpl;
+ * StereoSGBMImpl::compute, computeDisparitySGBM with mode MODE_SGBM,
+ * calcPixelCostBT, filterSpecklesImpl; imgproc/median_blur medianBlur_SortNet;
  * modules/imgproc: RGB2Gray<uchar> fixed point, equalizeHist), structure for
  * structure: the same row-by-row loop, the same cyclic horizontal-sum buffer,
  * the same int16 (CostType) truncations and saturations, the same MAX_COST
@@ -356,6 +358,58 @@ int svo_sgbm(const uint8_t* img1, const uint8_t* img2, int H, int W, const svo_s
 }
 
 /* ------------------------------------------------------------------------
+ * cv2.medianBlur(disp, disp, 3) on the int16 disparity, the step
+ * StereoSGBM::compute runs right after computeDisparitySGBM (OpenCV 2.4's
+ * StereoSGBM::operator(), 3.x and 4.x StereoSGBMImpl::compute) and before its
+ * internal speckle filter (off here: speckleWindowSize 0). OpenCV's 3 x 3
+ * sorting network (medianBlur_SortNet) yields the exact median of the 9
+ * values; the border replicates (rows max(y-1, 0) / min(y+1, H-1), columns
+ * likewise); a 1-row or 1-column image takes the median of 3 along its length.
+ * In-place calls work on a copy (cv::medianBlur copies src when dst aliases it).
+ * --------------------------------------------------------------------- */
+static int med3i(int a, int b, int c) { return imax(imin(a, b), imin(imax(a, b), c)); }
+
+void svo_median3_s16(const int16_t* src, int H, int W, int16_t* dst) {
+    if (H <= 0 || W <= 0) return;
+    if (H == 1 || W == 1) {
+        const int n = H * W;
+        for (int i = 0; i < n; ++i)
+            dst[i] = (int16_t)med3i(src[i > 0 ? i - 1 : 0], src[i], src[i < n - 1 ? i + 1 : n - 1]);
+        return;
+    }
+    for (int y = 0; y < H; ++y) {
+        const int16_t* r[3] = {src + (size_t)imax(y - 1, 0) * W, src + (size_t)y * W, src + (size_t)imin(y + 1, H - 1) * W};
+        for (int x = 0; x < W; ++x) {
+            const int xs[3] = {imax(x - 1, 0), x, imin(x + 1, W - 1)};
+            int v[9], k = 0;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) v[k++] = r[i][xs[j]];
+            /* insertion sort of 9: the 5th smallest is the median */
+            for (int i = 1; i < 9; ++i) {
+                int t = v[i], j = i - 1;
+                while (j >= 0 && v[j] > t) {
+                    v[j + 1] = v[j];
+                    --j;
+                }
+                v[j + 1] = t;
+            }
+            dst[(size_t)y * W + x] = (int16_t)v[4];
+        }
+    }
+}
+
+/* StereoSGBM::compute (MODE_SGBM, speckleWindowSize 0) = computeDisparitySGBM + medianBlur 3 */
+int svo_sgbm_compute(const uint8_t* img1, const uint8_t* img2, int H, int W, const svo_sgbm_params* prm,
+                     int16_t* disp1) {
+    int16_t* raw = malloc(sizeof(int16_t) * (size_t)(H * W > 0 ? H * W : 1));
+    if (!raw) return -2;
+    int rc = svo_sgbm(img1, img2, H, W, prm, raw);
+    if (rc == 0) svo_median3_s16(raw, H, W, disp1);
+    free(raw);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------
  * cv2.filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) on int16, in
  * place (filterSpecklesImpl<short>): 4-connected regions of pixels != newVal
  * whose neighbours differ by <= maxDiff; a region of <= maxSpeckleSize pixels
@@ -430,7 +484,7 @@ void svo_disparity_scale(const int16_t* d16, int H, int W, int max_disparity, in
 /* functions.py:104-128 disparity(grayL, grayR, max_disparity, crop_disparity) */
 int svo_disparity(const uint8_t* L, const uint8_t* R, int H, int W, const svo_sgbm_params* prm, int max_disparity,
                   int crop, int16_t* work16, uint8_t* out) {
-    int rc = svo_sgbm(L, R, H, W, prm, work16);
+    int rc = svo_sgbm_compute(L, R, H, W, prm, work16);
     if (rc) return rc;
     rc = svo_filter_speckles(work16, H, W, 0, 4000, max_disparity - 5);
     if (rc) return rc;

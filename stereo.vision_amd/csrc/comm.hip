@@ -28,11 +28,12 @@ struct sv_comm {
     ncclComm_t comm = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
-    void* buf = nullptr;  // 4 KB device scratch
+    void* buf = nullptr;  // 4 KB device scratch of the synchronous host-plane / count calls (on c->stream)
 };
 
 extern "C" int sv_comm_set_error(const char* msg);                                  // runtime.hip
-extern "C" int sv_batch_stream_internal(sv_batch* b, int* device, hipStream_t* stream);  // runtime.hip
+extern "C" int sv_batch_stream_internal(sv_batch* b, int* device, hipStream_t* stream,
+                                        double** abc_slot);   // runtime.hip
 
 namespace {
 // The root's host plane into the comm's device buffer, on the batch stream.
@@ -165,13 +166,16 @@ int sv_comm_broadcast_plane_dev(sv_comm* c, sv_batch* b, const sv_plane* plane, 
     if (!c || !b || !out_dplane) return sv_comm_set_error("sv_comm_broadcast_plane_dev: null"), SV_E_ARG;
     int dev = -1;
     hipStream_t s = nullptr;
-    if (sv_batch_stream_internal(b, &dev, &s) != SV_OK || dev != c->device)
+    if (sv_batch_stream_internal(b, &dev, &s, nullptr) != SV_OK || dev != c->device)
         return sv_comm_set_error("sv_comm_broadcast_plane_dev: batch and comm are on different devices"), SV_E_ARG;
     int rank = -1;
     NCCL_TRY(ncclCommUserRank(c->comm, &rank));
     if (rank == root && !plane) return sv_comm_set_error("sv_comm_broadcast_plane_dev: the root needs the plane"), SV_E_ARG;
     HIPC_TRY(hipSetDevice(c->device));
-    double* buf = static_cast<double*>(c->buf);
+    // the plane lands in the batch's own slot, written and read on the batch's stream only
+    double* buf = nullptr;
+    if (sv_batch_stream_internal(b, &dev, &s, &buf) != SV_OK)
+        return sv_comm_set_error("sv_comm_broadcast_plane_dev: no device memory for the plane slot"), SV_E_HIP;
     if (rank == root) {
         hipLaunchKernelGGL(store_abc_kernel, dim3(1), dim3(64), 0, s, plane->a, plane->b, plane->c, buf);
         HIPC_TRY(hipGetLastError());

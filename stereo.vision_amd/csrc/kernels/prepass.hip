@@ -126,7 +126,7 @@ hipError_t launch_fill_prev(const uint8_t* raw, uint8_t* out, uint8_t* masked, c
     // workgroups spread a frame's 2,176 waves evenly over the 256 CUs (256-lane ones leave 32 CUs a third
     // workgroup): 1.47 vs 1.53 ms per 4096 frames; 16 and 32 frames in flight are slower (1.58-1.63, 1.77 ms)
     int U = 8, B = 64;
-    if (const char* e = std::getenv("SVX_FILL")) std::sscanf(e, "%d,%d", &U, &B);
+    if (const char* e = svx_knob("SVX_FILL")) std::sscanf(e, "%d,%d", &U, &B);
     if (B != 64 && B != 128 && B != 256) B = 256;
     const dim3 grid((unsigned)((words + B - 1) / B)), block(B);
     const auto* r = reinterpret_cast<const uint32_t*>(raw);

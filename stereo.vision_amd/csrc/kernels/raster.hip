@@ -273,7 +273,7 @@ hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* coun
     if (W <= 0 || W > 4096 || W % 8 || H <= 0 || Wu <= 0 || Wu > W || (int64_t)H * W >= (1ll << 28))
         return hipErrorInvalidValue;
     int bytes = kRoadBandBytes;   // SVX_ROAD_BAND: A/B knob
-    if (const char* e = std::getenv("SVX_ROAD_BAND")) bytes = std::max(4096, std::min(65536, std::atoi(e)));
+    if (const char* e = svx_knob("SVX_ROAD_BAND")) bytes = std::max(4096, std::min(65536, std::atoi(e)));
     const int R = std::max(1, bytes / W);   // rows per band
     const size_t dyn = ((size_t)R * W + 15) / 16 * 16;
     if (dyn > 65536) return hipErrorInvalidValue;

@@ -835,7 +835,7 @@ bool resident_supported(const KParams& p) {   // frame_quads <= 2^20: every QP's
 // lane-contiguous quads (r_qi) for step 1 when a lane's 4 quads are one aligned
 // 16-byte run of a row; SVX_RES_LC=0 keeps the slot-major order (A/B knob)
 static bool resident_lane_quads(const KParams& kp) {
-    const char* v = std::getenv("SVX_RES_LC");   // read per call (tools/prof.py ab --env)
+    const char* v = svx_knob("SVX_RES_LC");   // read per call (tools/prof.py ab --env)
     const bool on = !(v && v[0] == '0');
     return on && kp.step == 1 && kp.Q % 4 == 0 && kp.W % 16 == 0 && kp.frame_px % 16 == 0;
 }

@@ -705,6 +705,41 @@ __device__ __forceinline__ void cc_unite(int32_t* par, int a, int b) {
     }
 }
 
+// cv2.medianBlur(disp, disp, 3), which StereoSGBM::compute runs on the int16
+// disparity right after computeDisparitySGBM (OpenCV 2.4 operator(), 3.x / 4.x
+// StereoSGBMImpl::compute). OpenCV's sorting network gives the exact median of
+// the 3 x 3 window with replicated borders; here each of the three columns is
+// sorted (3 compare-exchanges) and median9 = med3(max of the column minima,
+// med3 of the column medians, min of the column maxima), which is exact. A
+// 1-row or 1-column image degenerates to OpenCV's 1-D median of 3 by itself
+// (replicated columns / rows make the three columns equal / constant).
+__device__ __forceinline__ int med3_i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+
+__global__ __launch_bounds__(256) void sgbm_median3_kernel(int H, int W, int64_t frame_px,
+                                                             const int16_t* __restrict__ raw,
+                                                             int16_t* __restrict__ out, int frames) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t f = i / frame_px;
+    if (f >= frames) return;
+    const int p = (int)(i - f * frame_px);
+    const int y = p / W, x = p - y * W;
+    const int16_t* d = raw + f * frame_px;
+    const int16_t* r0 = d + (size_t)max(y - 1, 0) * W;
+    const int16_t* r1 = d + (size_t)y * W;
+    const int16_t* r2 = d + (size_t)min(y + 1, H - 1) * W;
+    const int xs[3] = {max(x - 1, 0), x, min(x + 1, W - 1)};
+    int lo[3], md[3], hi[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int a = r0[xs[j]], b = r1[xs[j]], c = r2[xs[j]];
+        lo[j] = min(a, min(b, c));
+        hi[j] = max(a, max(b, c));
+        md[j] = med3_i(a, b, c);
+    }
+    const int v = med3_i(max(lo[0], max(lo[1], lo[2])), med3_i(md[0], md[1], md[2]), min(hi[0], min(hi[1], hi[2])));
+    out[i] = (int16_t)v;
+}
+
 // Row runs: maximal horizontal runs of pixels != newVal whose neighbours differ
 // by <= maxDiff. A run never needs a union inside it: every pixel's parent is
 // its run's first pixel (one wave per row, a segmented max-scan of run starts).
@@ -954,7 +989,7 @@ hipError_t launch_copy_bgr_region(const uint8_t* src, int Hp, int Wp, uint8_t* d
 
 // steps each path walk keeps in flight (SVX_SGBM_PF: 1, 4 or 8; A/B only; 16 measured no faster)
 static int sgbm_prefetch() {
-    const char* e = std::getenv("SVX_SGBM_PF");
+    const char* e = svx_knob("SVX_SGBM_PF");
     return e && *e ? std::atoi(e) : 8;
 }
 
@@ -972,7 +1007,7 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
     // hsum: features (4 W words) + byte values (W words) + 4 waves' rings
     // (the register-ring walk for the reference's block 21: features (24 W bytes, the staged rows (6 W) under
     // them) + byte values (4 W); SVX_SGBM_HRING=0: the generic kernel)
-    const char* hr = std::getenv("SVX_SGBM_HRING");
+    const char* hr = svx_knob("SVX_SGBM_HRING");
     if (k.SW2 == 10 && !(hr && hr[0] == '0')) {
         hipLaunchKernelGGL(sgbm_hsum_ring_kernel<10>, dim3(frames * H), dim3(256), 28 * (size_t)k.W, st, k, left,
                            right, s.hl1, frames);
@@ -985,11 +1020,11 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
     const size_t lds4 = sizeof(int16_t) * 3 * (size_t)k.W * 4;
     const int pf = sgbm_prefetch();
     // the register-ring vertical walk for the reference's block 21 (SVX_SGBM_VRING=0: the generic walk)
-    const char* vr = std::getenv("SVX_SGBM_VRING");
+    const char* vr = svx_knob("SVX_SGBM_VRING");
     const bool vring = k.SH2 == 10 && !(vr && vr[0] == '0');
     // non-temporal loads of the volumes the row walk reads for the last time, and of its P: 26.40 vs 26.48 ms per
     // 64 frames, faster in 4 of 5 alternations (SVX_SGBM_NT=0: plain accesses; A/B)
-    const char* ntv = std::getenv("SVX_SGBM_NT");
+    const char* ntv = svx_knob("SVX_SGBM_NT");
     const bool nt = !(ntv && ntv[0] == '0');
 #define SVX_SGBM_WALKS(U)                                                                                         \
     if (vring)                                                                                                    \
@@ -1002,10 +1037,10 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
                        frames);                                                                                    \
     if (nt)                                                                                                       \
         hipLaunchKernelGGL((sgbm_row_kernel<U, true>), dim3((frames * H + 3) / 4), dim3(256), lds4, st, k, s.c,   \
-                           s.hl1, s.l2, s.l3, s.d16, s.flags, frames);                                            \
+                           s.hl1, s.l2, s.l3, s.raw, s.flags, frames);                                            \
     else                                                                                                          \
         hipLaunchKernelGGL((sgbm_row_kernel<U, false>), dim3((frames * H + 3) / 4), dim3(256), lds4, st, k, s.c,  \
-                           s.hl1, s.l2, s.l3, s.d16, s.flags, frames)
+                           s.hl1, s.l2, s.l3, s.raw, s.flags, frames)
     if (pf == 1) {
         SVX_SGBM_WALKS(1);
     } else if (pf == 4) {
@@ -1014,6 +1049,10 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
         SVX_SGBM_WALKS(8);
     }
 #undef SVX_SGBM_WALKS
+    // StereoSGBM::compute's medianBlur(disp, disp, 3): raw -> d16
+    const int64_t n = (int64_t)frames * k.frame_px;
+    hipLaunchKernelGGL(sgbm_median3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, k.H, k.W,
+                       k.frame_px, s.raw, s.d16, frames);
     return hipGetLastError();
 }
 

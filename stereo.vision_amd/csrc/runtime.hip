@@ -63,13 +63,13 @@ struct DevBuf {
         size_t want = n < 4096 ? 4096 : n + n / 4;
         hipError_t e = hipErrorUnknown;
         static const int mode = [] {
-            const char* v = std::getenv("SVX_CONTIG");
+            const char* v = svx_knob("SVX_CONTIG");
             return v && *v ? std::atoi(v) : 1;
         }();
         // A/B: SVX_CONTIG bit 4 also the pipeline outputs (tag 4), 8 the inputs (tag 8), 16 the masks (tag 16)
         if (mode != 0 && (contiguous || mode == 2 || (mode & tag)) && want >= (256u << 20)) {
             e = hipExtMallocWithFlags(&p, want, hipDeviceMallocContiguous);
-            if (std::getenv("SVX_CONTIG_LOG"))
+            if (svx_knob("SVX_CONTIG_LOG"))
                 std::fprintf(stderr, "svx: contiguous %zu bytes: %s\n", want, hipGetErrorString(e));
             if (e != hipSuccess) {
                 (void)hipGetLastError();
@@ -87,12 +87,13 @@ struct DevBuf {
 // SGBM scratch for a chunk of frames (kernels/sgbm.hip): four int16 cost
 // volumes, the int16 disparity, union-find parents / sizes, overflow flags.
 struct SgbmBufs {
-    DevBuf vol[4], d16, par, size, flags;
+    DevBuf vol[4], raw, d16, par, size, flags;
     int frames = 0;
     hipError_t ensure(const SgbmK& k, int n) {
         const size_t vb = sgbm_volume_bytes(k) * n, px = (size_t)k.frame_px * n;
         hipError_t e = hipSuccess;
         for (int i = 0; i < 4 && e == hipSuccess; ++i) e = vol[i].ensure(vb);
+        if (e == hipSuccess) e = raw.ensure(px * sizeof(int16_t));
         if (e == hipSuccess) e = d16.ensure(px * sizeof(int16_t));
         if (e == hipSuccess) e = par.ensure(px * sizeof(int32_t));
         if (e == hipSuccess) e = size.ensure(px * sizeof(int32_t));
@@ -100,12 +101,18 @@ struct SgbmBufs {
         if (e == hipSuccess) frames = n;
         return e;
     }
+    size_t held_bytes() const {
+        size_t n = 0;
+        for (const DevBuf* x : {&vol[0], &vol[1], &vol[2], &vol[3], &raw, &d16, &par, &size}) n += x->bytes;
+        return n;
+    }
     SgbmScratch scratch() const {
         return SgbmScratch{vol[0].as<uint32_t>(), vol[1].as<uint32_t>(), vol[2].as<uint32_t>(), vol[3].as<uint32_t>(),
-                           d16.as<int16_t>(), par.as<int32_t>(), size.as<int32_t>(), flags.as<uint32_t>()};
+                           raw.as<int16_t>(), d16.as<int16_t>(), par.as<int32_t>(), size.as<int32_t>(),
+                           flags.as<uint32_t>()};
     }
     void release() {
-        for (DevBuf* x : {&vol[0], &vol[1], &vol[2], &vol[3], &d16, &par, &size, &flags}) {
+        for (DevBuf* x : {&vol[0], &vol[1], &vol[2], &vol[3], &raw, &d16, &par, &size, &flags}) {
             if (x->p) (void)hipFree(x->p);
             x->p = nullptr;
             x->bytes = 0;
@@ -185,7 +192,7 @@ void set_plane(KParams& p, const sv_plane& pl, double thr, int hist_thr) {
     p.hist_thr = hist_thr;
     // Diagnostic ablation for profiling only (documented in DESIGN.md): when set,
     // kernels skip parts of their work and the results are NOT valid.
-    const char* ab = std::getenv("SVX_ABLATE");
+    const char* ab = svx_knob("SVX_ABLATE");
     p.ablate = ab ? std::atoi(ab) : 0;
 }
 
@@ -258,6 +265,7 @@ struct sv_batch {
     DevBuf rsidx, rtri;         // batched RANSAC scratch: every trial's sample; trial records + frame status
     DevBuf fplanes;             // per-frame keep1 plane fields (FramePlane) for sv_batch_pipeline_planes
     DevBuf dplane;              // the FramePlane of a device plane (sv_batch_pipeline_dev)
+    DevBuf abc;                 // this batch's slot for a broadcast plane (sv_comm_broadcast_plane_dev)
     DevBuf pairL, pairR;        // rectified grey stereo pairs (frames x pairH x pairW each), SGBM input
     int pairH = 0, pairW = 0;   // the pairs' shape: the batch's (H, W), or (Hp, Wp) whose crop is the batch
     DevBuf bgrL, bgrR, glut, ghist;   // BGR stereo pairs (frames x pairH x pairW x 3), gamma table, hist scratch
@@ -342,11 +350,20 @@ int sv_comm_set_error(const char* msg) {
     return 0;
 }
 
-// comm.hip: a batch's device and stream (collectives are ordered on the batch's stream)
-int sv_batch_stream_internal(sv_batch* b, int* device, hipStream_t* stream) {
+// comm.hip: a batch's device, stream (collectives are ordered on the batch's stream) and its own device slot
+// for a broadcast plane (3 doubles), so that two batches — or a comm's other calls — never share the buffer
+// a pending pipeline reads the plane from
+int sv_batch_stream_internal(sv_batch* b, int* device, hipStream_t* stream, double** abc_slot) {
     if (!b) return SV_E_ARG;
     *device = b->device;
     *stream = b->stream;
+    if (abc_slot) {
+        if (hipSetDevice(b->device) != hipSuccess || b->abc.ensure(sizeof(double) * 3) != hipSuccess) {
+            (void)hipGetLastError();
+            return SV_E_HIP;
+        }
+        *abc_slot = b->abc.as<double>();
+    }
     return SV_OK;
 }
 
@@ -465,13 +482,13 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
     b->kp = make_params(H, W, step, cam0, Wu);
     b->Ng = (int64_t)b->kp.Hg * b->kp.Wg;
     b->cap = ((size_t)b->Ng + 63) / 64 * 64;
-    if (const char* e = std::getenv("SVX_CAP_PAD")) b->cap += (size_t)std::atoi(e) / 64 * 64;   // A/B: frame stride
+    if (const char* e = svx_knob("SVX_CAP_PAD")) b->cap += (size_t)std::atoi(e) / 64 * 64;   // A/B: frame stride
     b->dense_per_frame = (int64_t)b->kp.Hg * b->kp.pitch;
     const size_t px = (size_t)frames * H * W;
     hipError_t e = b->disp.ensure(px, false, 8);
     if (e == hipSuccess && b->with_bgr) e = b->bgr.ensure(px * 3, false, 8);
     b->out_planes = true;   // three planes (A/B: SVX_PIPE_PLANES=0 for SoA per frame)
-    if (const char* e2 = std::getenv("SVX_PIPE_PLANES")) b->out_planes = *e2 != '0';
+    if (const char* e2 = svx_knob("SVX_PIPE_PLANES")) b->out_planes = *e2 != '0';
     if (e == hipSuccess && with_points) e = ensure_points(b);
     if (e == hipSuccess) {
         const size_t hist_b = sizeof(uint32_t) * kBins * frames, cnt_b = sizeof(int64_t) * 4 * frames;
@@ -501,7 +518,7 @@ int sv_batch_destroy(sv_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppx, &b->ppy, &b->ctrl, &b->masks,
-                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane,
+                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
                       &b->glut, &b->ghist, &b->sgflags})
         if (x->p) (void)hipFree(x->p);
@@ -579,7 +596,7 @@ int sv_batch_upload(sv_batch* b, int frame, const uint8_t* disp, const uint8_t* 
 // held until the end, so each lands elsewhere; at most half the free memory), and keeps the fastest.
 static int k1_place(sv_batch* b, const KParams& p, size_t plane) {
     int tries = 3;
-    if (const char* e = std::getenv("SVX_K1_TRIES")) tries = std::max(1, std::atoi(e));
+    if (const char* e = svx_knob("SVX_K1_TRIES")) tries = std::max(1, std::atoi(e));
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     const size_t set_b = 3 * (plane + plane / 4);   // DevBuf::ensure's slack
@@ -613,7 +630,7 @@ static int k1_place(sv_batch* b, const KParams& p, size_t plane) {
                 if (e == hipSuccess) e = hipEventElapsedTime(&ms, b->ev[0], b->ev[1]);
             }
             if (e != hipSuccess) break;
-            if (std::getenv("SVX_CONTIG_LOG")) std::fprintf(stderr, "svx: K1 placement %d: %.3f ms\n", t, ms);
+            if (svx_knob("SVX_CONTIG_LOG")) std::fprintf(stderr, "svx: K1 placement %d: %.3f ms\n", t, ms);
             if (best < 0 || ms < best_ms) {
                 best = t;
                 best_ms = ms;
@@ -685,7 +702,7 @@ RansacRes ransac_res(sv_batch* b) {
 // on each (all held), and the fastest set is kept. SVX_PIPE_TRIES=1 turns it off.
 static hipError_t pipe_place(sv_batch* b, const KParams& p, PipeBuffers bf, hipStream_t s) {
     int tries = 3;
-    if (const char* e = std::getenv("SVX_PIPE_TRIES")) tries = std::max(1, std::atoi(e));
+    if (const char* e = svx_knob("SVX_PIPE_TRIES")) tries = std::max(1, std::atoi(e));
     const size_t plane = sizeof(float) * b->cap * (size_t)b->frames;
     const size_t set_b = 5 * (plane + plane / 4);
     size_t free_b = 0, total_b = 0;
@@ -720,7 +737,7 @@ static hipError_t pipe_place(sv_batch* b, const KParams& p, PipeBuffers bf, hipS
             if (e == hipSuccess) e = hipEventElapsedTime(&ms, b->ev[0], b->ev[1]);
         }
         if (e != hipSuccess) break;
-        if (std::getenv("SVX_CONTIG_LOG")) std::fprintf(stderr, "svx: pipeline placement %d: %.3f ms\n", t, ms);
+        if (svx_knob("SVX_CONTIG_LOG")) std::fprintf(stderr, "svx: pipeline placement %d: %.3f ms\n", t, ms);
         if (best < 0 || ms < best_ms) {
             best = t;
             best_ms = ms;
@@ -1234,7 +1251,7 @@ int sv_batch_road_raster(sv_batch* b, int sync) {
     HIP_TRY(b->nz.ensure(sizeof(int32_t) * 2 * b->cap * b->frames));
     HIP_TRY(b->nzcount.ensure(sizeof(int64_t) * b->frames));
     // the images and their non-zero walks in one pass (road_kernel); SVX_ROAD_FUSED=0: raster, then the walk
-    const char* v = std::getenv("SVX_ROAD_FUSED");
+    const char* v = svx_knob("SVX_ROAD_FUSED");
     b->nz_fresh = !(v && v[0] == '0');
     if (b->nz_fresh) {
         HIP_TRY(launch_road(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), b->counts, (int64_t)b->cap,
@@ -1294,7 +1311,7 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 // 2 draws only the first two trials (results invalid); 4 evaluates every trial in fp64 (no fp32
 // screen; results valid, for A/B).
 static int ransac_ablate() {
-    const char* e = std::getenv("SVX_RANSAC_ABLATE");
+    const char* e = svx_knob("SVX_RANSAC_ABLATE");
     return e ? std::atoi(e) : 0;
 }
 
@@ -1802,8 +1819,8 @@ int sv_batch_pair_shape(sv_batch* b, int H, int W) {
     if (!own && W % 8) return fail(SV_E_ARG, "batched SGBM needs the pair width %% 8 == 0 (W=%d)", W);
     int h0, w0;
     pair_shape(b, &h0, &w0);
-    if (h0 != H || w0 != W) {   // a new shape: the pairs are uploaded again
-        for (DevBuf* x : {&b->pairL, &b->pairR}) {
+    if (h0 != H || w0 != W) {   // a new shape: the grey and the BGR pairs are uploaded again
+        for (DevBuf* x : {&b->pairL, &b->pairR, &b->bgrL, &b->bgrR}) {
             if (x->p) (void)hipFree(x->p);
             x->p = nullptr;
             x->bytes = 0;
@@ -1881,8 +1898,12 @@ int sv_batch_preprocess(sv_batch* b, const uint8_t* lut, int sync) {
     if (!b->bgrL.p || !b->bgrR.p) return fail(SV_E_STATE, "no BGR pairs (sv_batch_synth_bgr_pair / upload_bgr_pair)");
     int H, W;
     pair_shape(b, &H, &W);
-    HIP_TRY(hipSetDevice(b->device));
     const int64_t px = (int64_t)H * W;
+    // the BGR pairs must hold every frame at the current pair shape (a partial upload after a shape change
+    // would otherwise be read past its allocation)
+    if (b->bgrL.bytes < (size_t)px * 3 * b->frames || b->bgrR.bytes < (size_t)px * 3 * b->frames)
+        return fail(SV_E_STATE, "BGR pairs hold fewer bytes than %d frames of %d x %d x 3", b->frames, H, W);
+    HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(b->glut.ensure(256));
     HIP_TRY(b->ghist.ensure(sizeof(uint32_t) * 256 * b->frames));
     HIP_TRY(b->pairL.ensure((size_t)px * b->frames));
@@ -1915,10 +1936,23 @@ int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int
     SgbmK k;
     if (int rc = make_sgbm(H, W, prm, max_disparity, crop, &k)) return rc;
     k.out_stride = b->W;   // the batch's row stride (a cropped 889-wide row is stored in 896 bytes)
+    if (b->pairL.bytes < (size_t)k.frame_px * b->frames || b->pairR.bytes < (size_t)k.frame_px * b->frames)
+        return fail(SV_E_STATE, "stereo pairs hold fewer bytes than %d frames of %d x %d", b->frames, H, W);
     HIP_TRY(hipSetDevice(b->device));
-    // 128 frames a chunk (64 GB of volumes): the walks' last round of workgroups is a smaller share of a larger
-    // launch — 388 vs 401-424 us per frame at 32 and 403 at 64 (128 frames, alternating runs)
-    if (chunk <= 0) chunk = 128;
+    // 128 frames a chunk (64 GB of volumes at 544 x 1024): the walks' last round of workgroups is a smaller share
+    // of a larger launch — 388 vs 401-424 us per frame at 32 and 403 at 64 (128 frames, alternating runs). The
+    // default is capped by the device's free memory: the largest chunk whose scratch (what the batch does not
+    // hold already, with DevBuf's 1/4 slack) fits in 3/4 of it, at least 1 frame.
+    if (chunk <= 0) {
+        chunk = std::min(128, b->frames);
+        size_t fr = 0, tot = 0;
+        HIP_TRY(hipMemGetInfo(&fr, &tot));
+        const size_t per = (4 * sgbm_volume_bytes(k) + (size_t)k.frame_px * (2 * sizeof(int16_t) + 2 * sizeof(int32_t))) *
+                           5 / 4;
+        const size_t held = b->sg.held_bytes();
+        const size_t budget = (fr + held) / 4 * 3;
+        while (chunk > 1 && (size_t)chunk * per > budget) chunk = chunk * 3 / 4;
+    }
     chunk = std::min(chunk, b->frames);
     HIP_TRY(b->sg.ensure(k, chunk));
     // the range flags of every frame of the batch, checked once after the last chunk (no host sync between chunks)

@@ -13,6 +13,19 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
+// Measurement knobs (A/B selectors, placement probes, ablations
+// whose results are invalid) exist only in the diagnostic build, libsvx_diag.so
+// (`make diag`, -DSVX_DIAG; tools/prof.py selects it through SVX_LIB). The
+// release libsvx.so reads no SVX_* environment variable: the argument is not
+// even compiled, so no knob name is in its string table (tests/test_abi_cpu.py).
+#ifdef SVX_DIAG
+#define svx_knob(name) std::getenv(name)
+#else
+#define svx_knob(name) ((const char*)nullptr)
+#endif
+
 namespace svx {
 
 constexpr int kWave = 64;

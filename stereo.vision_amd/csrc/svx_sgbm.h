@@ -23,17 +23,19 @@ struct SgbmK {
 
 // Device scratch for a chunk of frames: four int16 cost volumes (frames x H x
 // width1 x 128) — hl1 holds the horizontal sums, then L1, then P — plus the
-// int16 disparity, union-find parents, component sizes and overflow flags.
+// int16 disparity (raw: computeDisparitySGBM's; d16: after compute's medianBlur),
+// union-find parents, component sizes and overflow flags.
 struct SgbmScratch {
     uint32_t *hl1, *c, *l2, *l3;
-    int16_t* d16;
+    int16_t *raw, *d16;
     int32_t *parent, *size;
     uint32_t* flags;   // per frame: 1 = an L value left int16 (unsupported)
 };
 
 bool sgbm_supported(const SgbmK& k);
 size_t sgbm_volume_bytes(const SgbmK& k);   // one volume, one frame
-// StereoSGBM.compute of every frame into s.d16 (frames x H x W int16, x16).
+// StereoSGBM.compute of every frame into s.d16 (frames x H x W int16, x16):
+// computeDisparitySGBM into s.raw, then medianBlur 3 into s.d16.
 hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_t* right, int frames,
                                const SgbmScratch& s, hipStream_t st);
 // filterSpeckles of s.d16 (frames x H x W) + TOZERO + scaling into out.

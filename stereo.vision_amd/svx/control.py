@@ -1,10 +1,10 @@
 """Host control plane for one-process-per-GPU runs, without PyTorch.
 
-The ranks of one node (torchrun's RANK / WORLD_SIZE / LOCAL_RANK, or the
-processes svx/launch.py starts) meet over plain TCP in a star: rank 0 listens
+The ranks of one node (torchrun's RANK / WORLD_SIZE / LOCAL_RANK, or processes
+a caller starts with those variables set) meet over plain TCP in a star: rank 0 listens
 on an ephemeral port of MASTER_ADDR (default 127.0.0.1) and publishes
 "host port" in a rendezvous file, the other ranks read it and connect. The
-file is SVX_CTRL_FILE when set (svx/launch.py sets it), else
+file is SVX_CTRL_FILE when set (a launcher of its own, e.g. the CPU tests, sets it), else
 /tmp/svx_ctrl_<MASTER_PORT>_<parent pid>: every rank of one torchrun has the
 same parent (the launcher agent), so concurrent jobs never share a file.
 Single node only (the contract's --nnodes=1).

@@ -10,7 +10,7 @@ it (sv_comm_broadcast_plane_dev + sv_batch_pipeline_dev): no host copy on the
 receivers, no host sync per step.
 
 Two ways to run N GPUs:
-  * one process per GPU (``torchrun --nproc-per-node N``, or svx.launch):
+  * one process per GPU (``torchrun --nproc-per-node N``):
     RANK / WORLD_SIZE / LOCAL_RANK from the environment, host control over
     svx.control.TcpControl (no PyTorch), RcclComm per rank;
   * one process driving all N: MultiComm (ncclCommInitAll), one

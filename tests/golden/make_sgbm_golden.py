@@ -20,13 +20,15 @@ calls:
   numpy: (d / 16.).astype(uint8), the crop [0:390, 135:W] and
   (x * (256. / max_disparity)).astype(uint8). Stored: digests of its output
   for every int16 value (a 256 x 256 image of -32768..32767) and for the
-  oracle's filtered SGBM of synthetic pairs 0 and 1, crop off/on,
+  oracle's filtered SGBM (compute = computeDisparitySGBM + medianBlur 3,
+  then filterSpeckles) of synthetic pairs 0 and 1, crop off/on,
   max_disparity 128 (the reference's) and 64.
 StereoSGBM itself and filterSpeckles cannot run here: PARITY UNPINNED
 (oracle/sgbm_oracle.c restates OpenCV's published algorithm).
 """
 import json
 import os
+import re
 import sys
 import types
 
@@ -74,8 +76,11 @@ def main():
                 rec[f"md{md}_crop{int(crop)}"] = {"digest": digest(r), "shape": list(r.shape)}
         scaled[name] = rec
     out["scaled"] = scaled
+    text = json.dumps(out, indent=1, separators=(",", ": "))
+    # integer lists (the gamma tables) on one line each
+    text = re.sub(r"\[\s*(-?\d+(?:,\s*-?\d+)*)\s*\]", lambda m: "[" + re.sub(r"\s+", "", m.group(1)) + "]", text)
     with open(os.path.join(HERE, "sgbm.json"), "w") as fh:
-        json.dump(out, fh, indent=1, separators=(",", ": "))
+        fh.write(text)
     print("wrote sgbm.json")
 
 

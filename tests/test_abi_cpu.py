@@ -46,6 +46,20 @@ def test_library_is_gfx950():
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
 
 
+def test_release_library_reads_no_knobs():
+    """The release libsvx.so carries no SVX_* knob (A/B selectors, placement probes,
+    ablations that make results invalid): they are compiled only into the diagnostic
+    libsvx_diag.so (-DSVX_DIAG, tools/prof.py). getenv itself may be linked (the HIP
+    runtime's own), but no SVX_ name is in the binary for it to read."""
+    from svx import _abi
+    blob = open(_abi.LIB_PATH, "rb").read()
+    assert b"SVX_" not in blob
+    diag = os.path.join(os.path.dirname(_abi.LIB_PATH), "libsvx_diag.so")
+    if os.path.exists(diag):
+        dblob = open(diag, "rb").read()
+        assert b"SVX_ABLATE" in dblob and b"SVX_RANSAC_ABLATE" in dblob
+
+
 def test_no_device_errors_are_raised_not_faked():
     """Without a GPU every compute entry point must fail loudly (no CPU fallback)."""
     import svx

@@ -52,7 +52,7 @@ def test_grey_equalize_matches_oracle(sv):
 
 
 SMALL = [(96, 320, "pair"), (3, 139, "rand"), (5, 256, "rand"), (21, 200, "rand"), (64, 512, "pair"),
-         (33, 300, "rand")]
+         (33, 300, "rand"), (1, 200, "rand"), (2, 160, "rand")]
 
 
 def _pair(H, W, kind, seed):

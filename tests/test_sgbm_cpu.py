@@ -142,4 +142,29 @@ def test_oracle_loop_matches_numpy_paths(kw, H, W):
     L, R = osg.synth_pair(7, H, W)
     L = L.copy()
     L[H // 4:H // 2, W // 2:W // 2 + 60] = 90
-    assert np.array_equal(osg.sgbm(L, R, **kw), sgbm_numpy.sgbm(L, R, **kw))
+    raw = sgbm_numpy.sgbm(L, R, **kw)
+    assert np.array_equal(osg.sgbm_raw(L, R, **kw), raw)
+    assert np.array_equal(osg.sgbm(L, R, **kw), median3_numpy(raw))
+
+
+def median3_numpy(a):
+    """cv2.medianBlur(a, 3) for a 2-D int16 image: the 5th of the 9 replicated-border
+    neighbours (OpenCV's 1-D median of 3 for a single row or column is the same thing)."""
+    H, W = a.shape
+    p = np.pad(a, 1, mode="edge")
+    return np.sort(np.stack([p[i:i + H, j:j + W] for i in range(3) for j in range(3)]), axis=0)[4]
+
+
+def test_median3_matches_numpy():
+    """compute()'s medianBlur(disp, disp, 3) (OpenCV StereoSGBMImpl::compute): the C
+    oracle against a numpy restatement, degenerate shapes included."""
+    rng = np.random.default_rng(11)
+    for H, W in [(1, 1), (1, 9), (9, 1), (2, 2), (3, 5), (40, 57), (544, 1024)]:
+        a = rng.integers(-16, 2048, (H, W)).astype(np.int16)
+        a[rng.random((H, W)) < 0.3] = -16
+        assert np.array_equal(osg.median3(a), median3_numpy(a)), (H, W)
+    L, R = osg.synth_pair(0)
+    raw = osg.sgbm_raw(L, R)
+    out = osg.sgbm(L, R)
+    assert np.array_equal(out, median3_numpy(raw))
+    assert (out != raw).mean() > 0.05   # the median changes a large share of a real frame

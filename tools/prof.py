@@ -38,6 +38,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "stereo.vision_amd")
 sys.path[:0] = [REPO, PKG]
 WHAT_TIMING = {"k1": "project", "pipe": "pipeline", "planes": "pipeline", "sgbm": "sgbm"}
+# The SVX_* knobs (A/B selectors, placement probes, ablations) exist only in the diagnostic build
+# (`make -C stereo.vision_amd/csrc diag`); this tool loads it unless SVX_LIB names another build.
+os.environ.setdefault("SVX_LIB", os.path.join(PKG, "svx", "_lib", "libsvx_diag.so"))
 
 
 def _batch(frames, what, mode="auto"):
