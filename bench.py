@@ -28,7 +28,7 @@ Also reported (same JSON line):
   latency_1frame_us  configs[1]: one frame, step 1, K1 kernel time.
   extras        SURVEY §8f components (N = 1): road raster + walk, pre-pass,
                 RANSAC (drop-in and batched), the per-frame-plane pipeline,
-                the drop-in chain, the SGBM disparity stage on 64 resident
+                the drop-in chain, the SGBM disparity stage on 128 resident
                 stereo pairs and the whole device frame loop from the pairs.
   cpu_baseline  configs[0]: the nested-loop CPU port (oracle/cpu_loop.py, the
                 numpy-scalar semantics of functions.py:178-323) on one pinned
@@ -56,6 +56,8 @@ PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 H, W = 544, 1024
 K1_BYTES_PER_POINT = 13        # 1 B disparity read + 12 B fp32 XYZ written
 GOLDEN_DIGESTS = os.path.join(REPO, "tests", "golden", "frame_digests.npz")
+GOLDEN_PLANES = os.path.join(REPO, "tests", "golden", "plane_digests.npz")
+DIGEST_FIELDS = ("n_valid", "n_kept", "n_kept2", "disp_hash", "hist_hash", "pts_hash")
 CARMASK = os.path.join(REPO, "tests", "golden", "carmask.npz")
 
 
@@ -77,19 +79,27 @@ def parse(argv=None):
     ap.add_argument("--no-extras", action="store_true", help="skip the SURVEY §8f component timings")
     ap.add_argument("--no-parity", action="store_true", help="skip the per-frame digest check")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--driver", choices=("auto", "single", "multi"), default="auto",
+                    help="auto: torchrun ranks when WORLD_SIZE is set, else one process (multi for N > 1); "
+                         "multi: force the one-process RCCL driver (ncclCommInitAll) even at N = 1 (tests)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--traffic-pipeline", default=os.path.join(REPO, "profiles", "traffic_pipeline.json"))
     ap.add_argument("--traffic-planes", default=os.path.join(REPO, "profiles", "traffic_planes.json"))
     return ap.parse_args(argv)
 
 
-def plan(gpus, environ):
+def plan(gpus, environ, driver="auto"):
     """How this process takes part in an N-GPU run:
     mode "ranks" (torchrun: one process per GPU), "multi" (one process, N GPUs)
     or "single". Returns dict(mode, n_gpus, rank, world, devices, shard_base):
-    this process drives `devices`, which hold global shards shard_base.. of n_gpus."""
+    this process drives `devices`, which hold global shards shard_base.. of n_gpus.
+    driver="multi" takes the one-process RCCL path at any N (N = 1 included)."""
     if gpus < 1:
         raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    if driver == "multi":
+        if "WORLD_SIZE" in environ:
+            raise SystemExit("bench.py: --driver multi is one process driving every GPU; do not launch it per rank")
+        return dict(mode="multi", n_gpus=gpus, rank=0, world=1, devices=list(range(gpus)), shard_base=0)
     if "WORLD_SIZE" in environ:
         world = int(environ["WORLD_SIZE"])
         if world != gpus:
@@ -98,7 +108,9 @@ def plan(gpus, environ):
                              f"`python bench.py --gpus {gpus}` without a launcher (one process, {gpus} GPUs)")
         rank, local = int(environ.get("RANK", 0)), int(environ.get("LOCAL_RANK", 0))
         return dict(mode="ranks", n_gpus=world, rank=rank, world=world, devices=[local], shard_base=rank)
-    if gpus == 1:
+    if gpus == 1 or driver == "single":
+        if gpus != 1:
+            raise SystemExit("bench.py: --driver single drives one GPU (--gpus 1)")
         return dict(mode="single", n_gpus=1, rank=0, world=1, devices=[0], shard_base=0)
     return dict(mode="multi", n_gpus=gpus, rank=0, world=1, devices=list(range(gpus)), shard_base=0)
 
@@ -264,7 +276,24 @@ def dropin_chain(fmod, disp, bgr, reps=5):
             "stages": "stereovision.py:84-113 via installed drop-ins, step 2, RANSAC 600"}
 
 
-def extras(b, args, with_cpu):
+def check_plane_parity(b, first):
+    """The per-frame-plane loop's device digests vs tests/golden/plane_digests.npz (the oracle's pre-pass ->
+    maskpoints -> RANSAC(random.seed(F)) -> pipeline chain, make_plane_digests.py); (frames checked, mismatching)."""
+    if b.step != 1 or not os.path.exists(GOLDEN_PLANES):
+        return 0, 0
+    gold = np.load(GOLDEN_PLANES)["planes"]
+    n = min(b.frames, len(gold) - first)
+    if first != 0 or n <= 0:
+        return 0, 0
+    got = b.digest("pipeline")[:n]
+    want = gold[first:first + n]
+    ok = got[:, 6] == 0
+    for k, name in enumerate(DIGEST_FIELDS):
+        ok &= got[:, k] == want[name].astype(np.uint64)
+    return n, int((~ok).sum())
+
+
+def extras(b, args, with_cpu, first=0):
     """SURVEY §8f components on the same resident batch (after the headline runs):
     road raster + non-zero walk of the pipeline's points, the disparity pre-pass
     (fillDisparity recurrence + carmask) over the batch, the RANSAC drop-in
@@ -291,6 +320,11 @@ def extras(b, args, with_cpu):
     ms = _timed(b, lambda: b.prepass("previous", sync=False), 3)
     ex["prepass_fill_previous_masked"] = {"ms_per_batch": round(ms, 3), "GBps": round(3 * px / ms / 1e6, 1),
                                           "bytes_per_pixel": 3, "kernel": "fill_prev_kernel"}
+    # the per-frame-plane workload below is pinned end to end (tests/golden/plane_digests.npz): fresh frames,
+    # ONE pre-pass over the batch in frame order (the timing above cleaned them four times), RANSAC with
+    # random.seed(F), the pipeline with each frame's plane
+    b.synth(first)
+    b.prepass("previous", sync=True)
     disp, _ = oracle.synth_frame(0)
     pts = list(oracle.project(oracle.mask_disparity(disp, mask), None, 2)[0])
     st = random.getstate()
@@ -314,7 +348,7 @@ def extras(b, args, with_cpu):
     # pipeline driven by each frame's own plane: stereovision.py:84-113 for the whole batch
     ms = _timed(b, lambda: b.ransac(seed_base=0, trials=600, sync=False), 2)
     rb = {"frames": b.frames, "trials": 600, "ms_per_batch": round(ms, 2),
-          "us_per_frame": round(ms / b.frames * 1e3, 2), "kernels": "maskpoints_kernel + ransac_batch_kernel",
+          "us_per_frame": round(ms / b.frames * 1e3, 2), "kernels": "maskpoints_kernel + ransac_draw_kernel + ransac_eval_kernel",
           "rng": "random.seed(frame) per frame"}
     if "cpu_restatement_ms_per_call" in r:
         rb["cpu_restatement_ms_per_frame"] = r["cpu_restatement_ms_per_call"]
@@ -335,6 +369,9 @@ def extras(b, args, with_cpu):
                                    "traffic": pipeline_traffic(args.traffic_planes, b.frames, args.step),
                                    "kernels": "frame_planes_kernel + resident_fused_kernel (each frame's plane)"
                                    if b.frames >= 512 else "frame_planes_kernel + tiled kernels"}
+    if not args.no_parity:
+        pc, pm = check_plane_parity(b, first)
+        ex["_planes_parity"] = [pc, pm]
 
     fmod = types.SimpleNamespace(camera_focal_length_px=399.9745178222656, stereo_camera_baseline_m=0.2090607502,
                                  image_centre_w=474.5, image_centre_h=262.0, carmask=mask)
@@ -412,7 +449,7 @@ def sgbm_extra(sb, device, with_cpu, frames=128, chunk=128):
         r = {"frames": frames, "chunk": chunk, "ms_per_batch": round(ms, 2),
              "us_per_frame": round(k_ms / max(k_n, 1) / frames * 1e3, 1),
              "frame0_matches_oracle": bool(np.array_equal(b.read_disp(0), ref)),
-             "kernels": "sgbm_hsum + sgbm_vertical + sgbm_diag + sgbm_row + cc_rows/union/count + out",
+             "kernels": "sgbm_hsum + sgbm_vertical + sgbm_diag + sgbm_row + sgbm_median3 + cc_rows/union/count + out",
              "parity": "unpinned vs OpenCV (absent); bit-exact vs oracle/sgbm_oracle.c"}
         if with_cpu:
             r["cpu_restatement_ms_per_frame"] = round(cpu_ms, 1)
@@ -434,7 +471,8 @@ def sgbm_extra(sb, device, with_cpu, frames=128, chunk=128):
             "ms_per_batch": round(ms, 2), "frames": frames, "frames_per_s": round(frames / ms * 1e3, 1),
             "stages": "BGR pairs: gamma 1.4 + grey/equalizeHist -> SGBM disparity -> prepass(previous+mask) -> "
                       "maskpoints+RANSAC(600) -> pipeline(per-frame planes, the corrected left image's colours) -> "
-                      "road raster -> non-zero walk (stereovision.py:40-136 minus cv2 drawing)"}
+                      "road raster -> non-zero walk (stereovision.py:40-136 minus the cv2 drawing and minus "
+                      "sanitiseRoadImage's morphology, functions.py:350-358: the walk is of the raw raster)"}
     return out
 
 
@@ -478,7 +516,7 @@ def check_parity(batches, shards, what, step):
 
 def main(argv=None):
     args = parse(argv)
-    pl = plan(args.gpus, os.environ)
+    pl = plan(args.gpus, os.environ, args.driver)
     from svx import batch as sb
     from svx import dist
 
@@ -629,20 +667,25 @@ def main(argv=None):
             c, m = check_parity(batches, shards, "pipeline", args.step)
             parity["pipeline"] = [c, m]
 
+    single = pl["n_gpus"] == 1
+    if want_pipe and not args.no_extras and single:   # §8f component timings: the N=1 run only
+        out["extras"] = extras(batches[0], args, not args.no_cpu, shards[0][1])
+        pp = out["extras"].pop("_planes_parity", None)
+        if pp is not None:
+            parity["pipeline_frame_planes"] = pp
+        out["extras"].update(sgbm_extra(sb, shards[0][0], not args.no_cpu))
+
     if parity:
         tot = ctrl.sum(np.array([v for pair in parity.values() for v in pair], np.float64))
         keys = list(parity)
         out["parity"] = {k: {"frames_checked": int(tot[2 * i]), "mismatched_frames": int(tot[2 * i + 1])}
                          for i, k in enumerate(keys)}
         out["parity"]["vs"] = "device per-frame digests vs tests/golden/frame_digests.npz (pinned C oracle, " \
-                              "global frame ids), every frame of every GPU"
+                              "global frame ids), every frame of every GPU; pipeline_frame_planes vs " \
+                              "tests/golden/plane_digests.npz (oracle pre-pass -> maskpoints -> RANSAC with " \
+                              "random.seed(F) -> pipeline, every frame)"
         out["parity"]["pass"] = all(v["mismatched_frames"] == 0 and v["frames_checked"] > 0
                                     for k, v in out["parity"].items() if isinstance(v, dict))
-
-    single = pl["n_gpus"] == 1
-    if want_pipe and not args.no_extras and single:   # §8f component timings: the N=1 run only
-        out["extras"] = extras(batches[0], args, not args.no_cpu)
-        out["extras"].update(sgbm_extra(sb, shards[0][0], not args.no_cpu))
 
     if pl["rank"] == 0 and single and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

@@ -257,11 +257,21 @@ int sv_batch_read_disp(sv_batch* b, int frame, uint8_t* disp, uint8_t* masked);
  * frame), their raster-order non-zero walks, and read-back (img and/or the
  * walk; n receives the walk's length). sv_batch_road_raster writes the images
  * and their walks in one pass (the walks are then already current and
- * sv_batch_nonzero only orders/syncs); with SVX_ROAD_FUSED=0 it writes the
- * images only and sv_batch_nonzero walks them. */
+ * sv_batch_nonzero only orders/syncs); with SVX_ROAD_FUSED=0 (diagnostic
+ * build only) it writes the images only and sv_batch_nonzero walks them. */
 int sv_batch_road_raster(sv_batch* b, int sync);
 int sv_batch_nonzero(sv_batch* b, int sync);
 int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int64_t cap, int64_t* n);
+/* stereovision.py:131-133 imageRoadMap: with enable != 0, later
+ * sv_batch_road_raster calls also write, in the same pass, a copy of each
+ * frame's BGR (the corrected imgL the pipeline read its colours from) with
+ * [0, 255, 0] at every [x, y] of its int32 planePoints (numpy's negative
+ * indices wrap as in the road image). Needs a with_bgr batch. For a batch of
+ * crop_disparity=True frames the map covers the batch's H x W (the top-left of
+ * the 544 x 1024 imgL; the rest of imgL is unpainted, as the pipeline's points
+ * never leave the disparity's own grid). Read-back: H x W x 3 u8. */
+int sv_batch_road_map(sv_batch* b, int enable);
+int sv_batch_read_road_map(sv_batch* b, int frame, uint8_t* out);
 
 /* Batched RANSAC (stereovision.py:84-94 for every frame):
  * maskpoints = the fp64 step-2 projection of the batch's disparity under the

@@ -301,13 +301,14 @@ int svo_pipeline_frame(const uint8_t* disp, const uint8_t* bgr, int H, int W, in
  * --------------------------------------------------------------------- */
 uint64_t svo_digest_mix(uint64_t z) { return svo_mix64(z); }
 
-int svo_frame_digest(int64_t frame_id, int H, int W, int step, const svo_camera* cam, const double* abc,
-                     double point_thr, int hist_thr, int64_t* counts, uint64_t* hashes) {
+/* The same digest of a given frame (disparity H x W, BGR H x W x 3): frames
+ * that are not the generator's, e.g. the pre-pass-cleaned ones of the
+ * per-frame-plane loop (tests/golden/make_plane_digests.py). */
+int svo_digest_frame(const uint8_t* disp, const uint8_t* bgr, int H, int W, int step, const svo_camera* cam,
+                     const double* abc, double point_thr, int hist_thr, int64_t* counts, uint64_t* hashes) {
     const int Hg = (H - 1 + step - 1) / step, Wg = (W - 1 + step - 1) / step;
     const size_t cap = (size_t)(Hg > 0 && Wg > 0 ? Hg * Wg : 1);
     const size_t px = (size_t)H * W;
-    uint8_t* disp = malloc(px);
-    uint8_t* bgr = malloc(px * 3);
     int32_t* pts = malloc(cap * 2 * sizeof(int32_t));
     int32_t* src2 = malloc(cap * 2 * sizeof(int32_t));
     double* s_xyz = malloc(cap * 3 * sizeof(double));
@@ -317,10 +318,8 @@ int svo_frame_digest(int64_t frame_id, int H, int W, int step, const svo_camera*
     int16_t* s_bin = malloc(cap * sizeof(int16_t));
     uint32_t hist[1024];
     int rc = -1;
-    if (!disp || !bgr || !pts || !src2 || !s_xyz || !s_rgb || !s_src || !s_keep || !s_bin || (px % 4) ||
-        W > 4096 || H > 4096)
+    if (!pts || !src2 || !s_xyz || !s_rgb || !s_src || !s_keep || !s_bin || (px % 4) || W > 4096 || H > 4096)
         goto out;
-    svo_synth_frame(frame_id, H, W, disp, bgr);
     svo_pipeline_frame(disp, bgr, H, W, step, cam, abc, point_thr, hist_thr, counts, hist, NULL, pts, src2,
                        s_xyz, s_rgb, s_src, s_keep, s_bin);
     uint64_t hd = 0, hh = 0, hp = 0;
@@ -342,7 +341,22 @@ int svo_frame_digest(int64_t frame_id, int H, int W, int step, const svo_camera*
     hashes[2] = hp;
     rc = 0;
 out:
-    free(disp); free(bgr); free(pts); free(src2);
+    free(pts); free(src2);
     free(s_xyz); free(s_rgb); free(s_src); free(s_keep); free(s_bin);
+    return rc;
+}
+
+int svo_frame_digest(int64_t frame_id, int H, int W, int step, const svo_camera* cam, const double* abc,
+                     double point_thr, int hist_thr, int64_t* counts, uint64_t* hashes) {
+    const size_t px = (size_t)H * W;
+    uint8_t* disp = malloc(px ? px : 1);
+    uint8_t* bgr = malloc(px ? px * 3 : 1);
+    int rc = -1;
+    if (disp && bgr) {
+        svo_synth_frame(frame_id, H, W, disp, bgr);
+        rc = svo_digest_frame(disp, bgr, H, W, step, cam, abc, point_thr, hist_thr, counts, hashes);
+    }
+    free(disp);
+    free(bgr);
     return rc;
 }

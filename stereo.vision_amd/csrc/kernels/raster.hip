@@ -142,11 +142,18 @@ struct RoadShared {
     uint32_t stage[256 * 16];             // a walk chunk's pixel indices, in output order
 };
 
+// With paint != nullptr the same pass also writes stereovision.py:131-133's
+// imageRoadMap: a copy of the frame's BGR (the gamma-corrected imgL, frames x H
+// x W x 3 at a row stride of 3 W) with [0, 255, 0] wherever the band's image is
+// marked — generatePointsAsImage and the paint index the same [y][x] with the
+// same wrap, so the band in LDS is exactly the paint mask (3 B read + 3 B
+// written per pixel, 8 bytes a lane).
 __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ px, const int32_t* __restrict__ py,
                                                    const int64_t* __restrict__ counts, int64_t cap,
                                                    uint8_t* __restrict__ img, int H, int W, int Wu, int R,
                                                    uint64_t W_m40, int32_t* __restrict__ nzout,
-                                                   int64_t* __restrict__ nzcount) {
+                                                   int64_t* __restrict__ nzcount, const uint8_t* __restrict__ bgr,
+                                                   uint8_t* __restrict__ paint) {
     __shared__ RoadShared sh;
     extern __shared__ uint4 road_band[];   // the band: R rows of W bytes (dynamic LDS)
     uint8_t* const band = reinterpret_cast<uint8_t*>(road_band);
@@ -221,6 +228,27 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
                 __builtin_nontemporal_store(*reinterpret_cast<const v2u*>(band + o),
                                             reinterpret_cast<v2u*>(fimg + (int64_t)r0 * W + o));
         }
+        if (paint) {   // uniform: imageRoadMap rows r0..r1 (byte j of the band's rows is pixel j / 3, channel j % 3)
+            const int64_t fo3 = ((int64_t)frame * H + r0) * W * 3;
+            const uint2* src = reinterpret_cast<const uint2*>(bgr + fo3);
+            v2u* dst = reinterpret_cast<v2u*>(paint + fo3);
+            const int nb8 = bpx * 3 / 8;   // W % 8 == 0: whole 8-byte units
+            for (int u = tid; u < nb8; u += 256) {
+                const uint2 q = src[u];
+                uint32_t w[2] = {q.x, q.y};
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t j = (uint32_t)(8 * u + k);
+                    const uint32_t pix = (j * 43691u) >> 17;   // j / 3 for j < 98304 (R W <= 16384)
+                    const uint32_t ch = j - 3 * pix;
+                    if (band[pix]) {
+                        const uint32_t sh8 = 8 * (k & 3);
+                        w[k >> 2] = (w[k >> 2] & ~(0xFFu << sh8)) | ((ch == 1 ? 0xFFu : 0u) << sh8);
+                    }
+                }
+                __builtin_nontemporal_store((v2u){w[0], w[1]}, dst + u);
+            }
+        }
         // the band's non-zero pixels in raster order (nonzero_kernel's chunk logic, from LDS)
         const uint32_t* bw = reinterpret_cast<const uint32_t*>(band);
         const int vecs = bz / 16;
@@ -268,7 +296,8 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
 }
 
 hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* counts, int64_t cap, uint8_t* img,
-                       int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, hipStream_t s) {
+                       int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr,
+                       uint8_t* paint, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
     if (W <= 0 || W > 4096 || W % 8 || H <= 0 || Wu <= 0 || Wu > W || (int64_t)H * W >= (1ll << 28))
         return hipErrorInvalidValue;
@@ -276,10 +305,10 @@ hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* coun
     if (const char* e = svx_knob("SVX_ROAD_BAND")) bytes = std::max(4096, std::min(65536, std::atoi(e)));
     const int R = std::max(1, bytes / W);   // rows per band
     const size_t dyn = ((size_t)R * W + 15) / 16 * 16;
-    if (dyn > 65536) return hipErrorInvalidValue;
+    if (dyn > 65536 || (paint && (!bgr || (size_t)R * W * 3 >= 98304))) return hipErrorInvalidValue;
     const uint64_t m40 = (((uint64_t)1 << 40) + (uint64_t)W - 1) / (uint64_t)W;
     hipLaunchKernelGGL(road_kernel, dim3(frames), dim3(256), dyn, s, px, py, counts, cap, img, H, W, Wu, R, m40, nzout,
-                       nzcount);
+                       nzcount, bgr, paint);
     return hipGetLastError();
 }
 

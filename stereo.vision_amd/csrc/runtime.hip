@@ -259,6 +259,8 @@ struct sv_batch {
     DevBuf mdisp, carmask;      // pre-pass: masked disparity (frames x H x W), 0x00/0xFF mask (H x W)
     DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
     bool nz_fresh = false;      // nz holds the walk of the current road images (road_kernel wrote both)
+    DevBuf rmap;                // imageRoadMap (stereovision.py:131-133): frames x H x W x 3, on request
+    bool want_rmap = false, rmap_fresh = false;
     DevBuf mpts, rres;          // maskpoints (frames x mcap x 3 fp64) + counts; batched RANSAC results
     DevBuf mpk;                 // maskpoints packed (frames x mcap words x | y << 12 | d << 24): RANSAC's fp32 screen
     DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
@@ -518,7 +520,7 @@ int sv_batch_destroy(sv_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppx, &b->ppy, &b->ctrl, &b->masks,
-                      &b->mdisp, &b->carmask, &b->road, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
+                      &b->mdisp, &b->carmask, &b->road, &b->rmap, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
                       &b->glut, &b->ghist, &b->sgflags})
         if (x->p) (void)hipFree(x->p);
@@ -1253,10 +1255,17 @@ int sv_batch_road_raster(sv_batch* b, int sync) {
     // the images and their non-zero walks in one pass (road_kernel); SVX_ROAD_FUSED=0: raster, then the walk
     const char* v = svx_knob("SVX_ROAD_FUSED");
     b->nz_fresh = !(v && v[0] == '0');
+    b->rmap_fresh = false;
     if (b->nz_fresh) {
+        uint8_t* paint = nullptr;
+        if (b->want_rmap) {   // imageRoadMap in the same pass (stereovision.py:131-133)
+            HIP_TRY(b->rmap.ensure(px * 3 * b->frames));
+            paint = b->rmap.as<uint8_t>();
+        }
         HIP_TRY(launch_road(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), b->counts, (int64_t)b->cap,
                             b->road.as<uint8_t>(), b->frames, b->H, b->W, b->Wu, b->nz.as<int32_t>(),
-                            b->nzcount.as<int64_t>(), b->stream));
+                            b->nzcount.as<int64_t>(), b->bgr.as<uint8_t>(), paint, b->stream));
+        b->rmap_fresh = paint != nullptr;
     } else {
         HIP_TRY(launch_raster(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), 1, b->counts, 4, 2, (int64_t)b->cap,
                               b->road.as<uint8_t>(), b->frames, b->H, b->W, b->Wu, b->stream));
@@ -1278,6 +1287,24 @@ int sv_batch_nonzero(sv_batch* b, int sync) {
     HIP_TRY(launch_nonzero(b->road.as<uint8_t>(), b->frames, (int64_t)b->H * b->W, b->W, b->nz.as<int32_t>(),
                            (int64_t)b->cap, b->nzcount.as<int64_t>(), b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_road_map(sv_batch* b, int enable) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    if (enable && !b->with_bgr) return fail(SV_E_STATE, "imageRoadMap needs the batch's BGR (with_bgr)");
+    b->want_rmap = enable != 0;
+    return SV_OK;
+}
+
+int sv_batch_read_road_map(sv_batch* b, int frame, uint8_t* out) {
+    if (!b || !out || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "bad args");
+    if (!b->rmap_fresh) return fail(SV_E_STATE, "no imageRoadMap (sv_batch_road_map(b, 1), then sv_batch_road_raster)");
+    HIP_TRY(hipSetDevice(b->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    const size_t px3 = (size_t)b->H * b->W * 3;
+    HIP_TRY(hipMemcpy2D(out, (size_t)b->Wu * 3, b->rmap.as<uint8_t>() + px3 * frame, (size_t)b->W * 3,
+                        (size_t)b->Wu * 3, b->H, hipMemcpyDeviceToHost));
     return SV_OK;
 }
 

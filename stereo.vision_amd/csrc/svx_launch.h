@@ -91,9 +91,11 @@ hipError_t launch_raster(const int32_t* px, const int32_t* py, int ps, const int
                          int64_t cap, uint8_t* img, int frames, int H, int W, int Wu, hipStream_t s);
 // The batch's road images and walks in one pass (road_kernel): the pipeline's points (two planes, frame f's
 // counts[4f + 2] points at f * cap, in the pipeline's raster order) -> img (frames x H x W, W % 8 == 0) and the
-// raster-order [j, i] of every non-zero pixel (frames x cap pairs) + nzcount[frame].
+// raster-order [j, i] of every non-zero pixel (frames x cap pairs) + nzcount[frame]; with paint != nullptr also
+// imageRoadMap (stereovision.py:131-133): bgr (frames x H x W x 3) with [0, 255, 0] at the marked pixels -> paint.
 hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* counts, int64_t cap, uint8_t* img,
-                       int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, hipStream_t s);
+                       int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr,
+                       uint8_t* paint, hipStream_t s);
 // img frames x px (px % 4 == 0, rows of W <= 4096 pixels)
 hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
                           hipStream_t s);

@@ -204,6 +204,16 @@ class Batch:
         """Raster-order non-zero walk of every road image (device)."""
         _abi.call("sv_batch_nonzero", self._h, int(sync))
 
+    def road_map(self, enable=True):
+        """Also write stereovision.py:131-133's imageRoadMap (the frame's BGR with [0, 255, 0] at its
+        planePoints) in every later road_raster() pass."""
+        _abi.call("sv_batch_road_map", self._h, int(bool(enable)))
+
+    def read_road_map(self, frame):
+        out = np.empty((self.H, self.W, 3), np.uint8)
+        _abi.call("sv_batch_read_road_map", self._h, frame, _abi.ptr(out))
+        return out
+
     def read_road(self, frame, walk=False):
         img = np.empty((self.H, self.W), np.uint8)
         if not walk:

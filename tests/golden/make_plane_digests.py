@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/plane_digests.npz: the per-frame-plane loop of
+stereovision.py:53-113 for frames 0..4095 of the synthetic batch, end to end
+through the ORACLE (the checker; never the product):
+
+  for frame F in order (stereovision.py:56-60, loop.py:57,78):
+    cleaned_F  = fillDisparity(disp_F, cleaned_{F-1})       functions.py:141-148 (frame 0: unchanged)
+    masked_F   = maskDisparity(cleaned_F)   (carmask)        functions.py:169-172
+    maskpoints = projectDisparityTo3d(masked_F, 128)         functions.py:178-198, step 2
+    random.seed(F); abc = RANSAC(maskpoints, 600)            functions.py:278-298 (oracle/ransac.py, CPython's
+                                                             random and the reference's numpy calls:
+                                                             abc = np.dot(np.linalg.inv(P), np.ones([3,1])), :267)
+    digest of the step-1 pipeline of (cleaned_F, bgr_F) with that abc, thresholds 0.05 / 10
+                                                             functions.py:178-323, stereovision.py:84-113
+
+i.e. what the device computes with sv_batch_prepass(previous, carmask) ->
+sv_batch_ransac(seed_base=0, trials=600) -> sv_batch_pipeline_planes (bench.py's
+pipeline_frame_planes workload). Every stage is the pinned oracle: the pre-pass
+by tests/golden/prepass.json, RANSAC by tests/golden/ransac.json, the pipeline
+by tests/golden/sparse.npz / digests.json.
+
+Per frame it stores the plane's float64 bits, the winning trial, the error of
+the winner and of the runner-up (to see near ties), the maskpoint count and
+the six digest columns of oracle.DIGEST_FIELDS.
+
+usage: python tests/golden/make_plane_digests.py [--frames 4096]   (a few minutes on 8 cores)
+"""
+import argparse
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+import oracle  # noqa: E402
+from oracle import ransac as oransac  # noqa: E402
+
+BLOCK = 32
+TRIALS = 600
+
+
+def carmask():
+    z = np.load(os.path.join(HERE, "carmask.npz"))
+    shape = tuple(int(v) for v in z["shape"])
+    return np.unpackbits(z["bits"])[: shape[0] * shape[1]].reshape(shape).astype(np.uint8) * 255
+
+
+def winning_trial(recs):
+    """the trial whose plane RANSAC returns: the first strict minimum of the errors
+    (functions.py:289-292, `if error < bestError`; a NaN error never wins)"""
+    win, best = -1, float("inf")
+    for i, r in enumerate(recs):
+        e = r.get("err")
+        if e is not None and e < best:
+            win, best = i, e
+    return win
+
+
+def _block(args):
+    first, count, prev, seed_base = args
+    mask = carmask()
+    rows = []
+    for f in range(first, first + count):
+        disp, bgr = oracle.synth_frame(f)
+        cleaned = disp.copy() if prev is None else oracle.fill_previous(disp, prev)
+        prev = cleaned
+        mpts = oracle.project(oracle.mask_disparity(cleaned, mask), None, 2)[0]
+        rng = random.Random(seed_base + f)
+        abc, recs = oransac.ransac(mpts, TRIALS, rng=rng)
+        if abc is None:
+            rows.append((f, len(mpts), -1, np.nan, np.nan, np.full(3, np.nan)) + (0,) * 6)
+            continue
+        win = winning_trial(recs)
+        e = np.sort(np.asarray([r["err"] for r in recs if r.get("err") is not None]))
+        d = oracle.digest_frame(cleaned, bgr, 1, abc=abc)
+        rows.append((f, len(mpts), win, float(e[0]), float(e[1]) if len(e) > 1 else np.inf,
+                     np.asarray(abc, np.float64).reshape(3)) + d)
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=4096)
+    ap.add_argument("--seed-base", type=int, default=0)
+    ap.add_argument("--procs", type=int, default=min(8, os.cpu_count() or 1))
+    a = ap.parse_args()
+    t0 = time.time()
+    # the fill recurrence is sequential: the cleaned frame before each block, computed here
+    jobs, prev = [], None
+    for f0 in range(0, a.frames, BLOCK):
+        n = min(BLOCK, a.frames - f0)
+        jobs.append((f0, n, prev, a.seed_base))
+        for f in range(f0, f0 + n):
+            d, _ = oracle.synth_frame(f)
+            prev = d.copy() if prev is None else oracle.fill_previous(d, prev)
+    print(f"fill chain: {time.time() - t0:.1f} s", flush=True)
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(a.procs) as pool:
+        rows = [r for part in pool.map(_block, jobs, chunksize=1) for r in part]
+    print(f"{len(rows)} frames: {time.time() - t0:.1f} s", flush=True)
+    dt = np.dtype([("frame", np.int64), ("n_maskpoints", np.int64), ("trial", np.int64), ("err", np.float64),
+                   ("err2", np.float64), ("abc", np.float64, (3,))]
+                  + [(n, np.int64) for n in oracle.DIGEST_FIELDS[:3]]
+                  + [(n, np.uint64) for n in oracle.DIGEST_FIELDS[3:]])
+    arr = np.array(rows, dtype=dt)
+    np.savez_compressed(os.path.join(HERE, "plane_digests.npz"), planes=arr,
+                        seed_base=np.int64(a.seed_base), trials=np.int64(TRIALS))
+    rel = (arr["err2"] - arr["err"]) / arr["err"]
+    print("closest runner-up (relative):", float(np.min(rel)), "frames within 1e-9:", int((rel < 1e-9).sum()))
+
+
+if __name__ == "__main__":
+    main()

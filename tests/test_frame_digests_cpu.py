@@ -44,3 +44,27 @@ def test_every_frame_is_non_trivial(fd):
         a = fd[key]
         assert (a["n_kept2"] > 0).all() and (a["n_kept2"] <= a["n_kept"]).all() and (a["n_kept"] <= a["n_valid"]).all()
         assert len(np.unique(a["disp_hash"])) == len(a)      # every frame distinct
+
+
+def test_plane_digests_rows_recompute():
+    """tests/golden/plane_digests.npz (the per-frame-plane loop through the oracle:
+    fill pre-pass chain + carmask -> maskpoints -> RANSAC(600), random.seed(F) ->
+    the step-1 pipeline with that plane) recomputed for frames 0..2 and for a
+    block starting at frame 640 from its predecessor's cleaned frame."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_plane_digests as mpd
+    z = np.load(os.path.join(GOLDEN, "plane_digests.npz"))
+    gold = z["planes"]
+    assert gold.shape == (4096,) and int(z["trials"]) == 600 and int(z["seed_base"]) == 0
+    assert (gold["trial"] >= 0).all() and (gold["n_kept2"] > 0).all()
+    prev = None
+    for f in range(640):
+        d, _ = oracle.synth_frame(f)
+        prev = d.copy() if prev is None else oracle.fill_previous(d, prev)
+    rows = mpd._block((0, 3, None, 0)) + mpd._block((640, 1, prev, 0))
+    for r in rows:
+        g = gold[r[0]]
+        assert r[1] == g["n_maskpoints"] and r[2] == g["trial"], r[0]
+        assert np.array_equal(np.asarray(r[5]).view(np.uint64), g["abc"].view(np.uint64)), r[0]
+        assert tuple(r[6:]) == tuple(int(g[n]) for n in oracle.DIGEST_FIELDS), r[0]

@@ -10,7 +10,11 @@ tests/golden/frame_digests.npz, written by the pinned C oracle
   * configs[2]: K1 dense projection of 4096 frames (counts, disparity, tolerance)
   * configs[3]: the pipeline over 4096 frames, resident and tiled kernels, steps 1 and 2
   * configs[4]: all 32,768 frames, generated and processed shard by shard as
-    the 8 ranks would (4096 frames each, global frame ids), on one GPU."""
+    the 8 ranks would (4096 frames each, global frame ids), on one GPU.
+  * the per-frame-plane loop (stereovision.py:53-113 for every frame of the
+    batch: fill pre-pass + carmask -> maskpoints -> RANSAC(600) with
+    random.seed(F) -> the pipeline with that frame's plane) against
+    tests/golden/plane_digests.npz, the oracle's chain (make_plane_digests.py)."""
 import os
 import types
 
@@ -80,3 +84,39 @@ def test_config5_every_shard(env):
             b.pipeline()
             got = b.digest("pipeline")
             assert _mismatches(got, want_all[first:first + count], FIELDS) == [], f"shard {rank}"
+
+
+def test_frame_planes_every_frame(env):
+    """bench.py's pipeline_frame_planes workload, all 4096 frames end to end: every
+    frame's RANSAC picks the oracle's winning trial, its plane is within 1e-12
+    relative of the oracle's np.dot(np.linalg.inv(P), ones) (functions.py:267; the
+    device solves the 3 x 3 system in fp64 by the adjugate, LAPACK's LU differs in
+    the last bits), and every frame's pipeline digest — counts, histogram, the
+    surviving points and their int32 back-projection — equals the oracle chain's."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from test_prepass_cpu import carmask
+    z = np.load(os.path.join(GOLDEN, "plane_digests.npz"))
+    want = z["planes"]
+    frames = len(want)
+    with env.batch.Batch(frames, step=1, with_bgr=True, with_points=True) as b:
+        b.synth(0)
+        b.set_mask(carmask())
+        b.prepass("previous")
+        b.ransac(seed_base=int(z["seed_base"]), trials=int(z["trials"]))
+        b.pipeline_planes()
+        got = b.digest("pipeline")
+        bad_planes, bad_trials, max_rel = [], [], 0.0
+        for f in range(frames):
+            r = b.read_ransac(f)
+            if r["trial"] != int(want["trial"][f]):
+                bad_trials.append(f)
+            ref = want["abc"][f]
+            if not np.array_equal(r["abc"], ref):
+                bad_planes.append(f)
+                max_rel = max(max_rel, float(np.max(np.abs(r["abc"] - ref) / np.abs(ref))))
+    assert bad_trials == [], bad_trials[:10]
+    mism = _mismatches(got, want, FIELDS)
+    assert mism == [], (mism, len(bad_planes), max_rel)
+    assert max_rel <= 1e-12, (len(bad_planes), max_rel)
+    print(f"planes: {frames - len(bad_planes)} / {frames} bit-identical to numpy's, max rel diff {max_rel:.3g}")

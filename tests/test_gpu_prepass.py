@@ -154,6 +154,7 @@ def test_batch_road_edge_frames(svx_mod, step):
         for f, d in enumerate(frames):
             b.upload(f, d, bgr)
         b.pipeline(**kw)
+        b.road_map(True)
         b.road_raster()
         b.nonzero()
         for f, d in enumerate(frames):
@@ -162,3 +163,49 @@ def test_batch_road_edge_frames(svx_mod, step):
             img, walk = b.read_road(f, walk=True)
             assert np.array_equal(img, rimg), f
             assert np.array_equal(walk, oracle.nonzero_points(rimg)), f
+            assert np.array_equal(b.read_road_map(f), oracle.road_map(bgr, ref["pts"])), f
+
+
+def test_batch_road_map_reference_fixture(svx_mod, golden):
+    """stereovision.py:131-133 (imageRoadMap) from the batch's road pass against the
+    reference's own statements run on the same planePoints (tests/golden/roadmap.json),
+    for the golden step-2 chains (each with its plane) and frame 0 at step 1; then a
+    crop-width batch (390 x 889 frames at a row stride of 896)."""
+    meta = json.load(open(os.path.join(GOLDEN, "roadmap.json")))["cases"]
+    for fid, m in golden.meta["full_frames_step2"].items():
+        disp, bgr = oracle.synth_frame(0 if fid == "0r" else int(fid))
+        with svx_mod.batch.Batch(1, step=2, with_bgr=True, with_points=True) as b:
+            b.upload(0, disp, bgr)
+            b.pipeline(plane=tuple(m["abc"]))
+            b.road_map(True)
+            b.road_raster()
+            out = b.read_road_map(0)
+            assert oracle.digest(out) == meta[f"step2_{fid}"]["image"], fid
+    with svx_mod.batch.Batch(3, step=1, with_bgr=True, with_points=True) as b:
+        b.synth(0)
+        b.pipeline()
+        with pytest.raises(svx_mod.svx.SvxError):
+            b.read_road_map(0)                   # not requested yet
+        b.road_map(True)
+        b.road_raster(sync=False)
+        b.nonzero()
+        assert oracle.digest(b.read_road_map(0)) == meta["step1_0"]["image"]
+        for f in (1, 2):
+            disp, bgr = oracle.synth_frame(f)
+            assert np.array_equal(b.read_road_map(f), oracle.road_map(bgr, oracle.pipeline_frame(disp, bgr, 1)["pts"]))
+    with svx_mod.batch.Batch(2, 390, 889, step=1, with_bgr=True, with_points=True) as b:
+        frames = []
+        for f in range(2):
+            d, bgr = oracle.synth_frame(60 + f)
+            d, bgr = np.ascontiguousarray(d[:390, :889]), np.ascontiguousarray(bgr[:390, :889])
+            frames.append((d, bgr))
+            b.upload(f, d, bgr)
+        b.pipeline()
+        b.road_map(True)
+        b.road_raster()
+        for f, (d, bgr) in enumerate(frames):
+            ref = oracle.pipeline_frame(d, bgr, 1)
+            assert np.array_equal(b.read_road_map(f), oracle.road_map(bgr, ref["pts"])), f
+    with svx_mod.batch.Batch(1, step=1, with_bgr=False) as b:
+        with pytest.raises(svx_mod.svx.SvxError):
+            b.road_map(True)                     # needs the batch's BGR

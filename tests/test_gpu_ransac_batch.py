@@ -184,9 +184,12 @@ def test_batch_degenerate_frame_gives_up(svb):
 def test_pipeline_with_frame_planes(svb, mode, step):
     """stereovision.py:84-113 per frame on the device: RANSAC's plane of each
     frame drives that frame's threshold / histogram / compaction. Each frame's
-    output equals the oracle chain run with that frame's plane; a frame with
-    no plane keeps nothing (the reference's plane step raises). Both kernel
-    families (the frame-resident one reads each frame's plane from memory)."""
+    output equals the oracle chain run with the ORACLE's plane for that frame
+    (oracle/ransac.py on the oracle's maskpoints with random.Random(seed_base +
+    F): the reference's np.dot(np.linalg.inv(P), ones) of the same draws); a
+    frame with no plane keeps nothing (the reference's plane step raises). Both
+    kernel families (the frame-resident one reads each frame's plane from
+    memory). tests/test_gpu_digests.py checks the same at 4096 frames."""
     m = carmask()
     frames = 4
     sparse = _sparse_frame(300, 9)   # 300 points: fewer than 600 -> no plane
@@ -210,7 +213,13 @@ def test_pipeline_with_frame_planes(svb, mode, step):
             a, bb, c = res["abc"]
             assert np.array_equal(fp[:3], res["abc"])
             assert fp[3] == np.sqrt(a * a + bb * bb + c * c)       # device sqrt == the reference's math.sqrt
-            ref = oracle.pipeline_frame(disp, bgr, step, abc=res["abc"])
+            mpts = oracle.project(oracle.mask_disparity(disp, m), None, 2)[0]
+            abc_ref, recs = oransac.ransac(mpts, 60, rng=random.Random(5 + f))
+            win = next(i for i, r in enumerate(recs) if r.get("err") is not None and r["err"] == min(
+                x["err"] for x in recs if x.get("err") is not None and not np.isnan(x["err"])))
+            assert res["trial"] == win, f
+            np.testing.assert_allclose(res["abc"], abc_ref.reshape(3), rtol=1e-12, atol=0)
+            ref = oracle.pipeline_frame(disp, bgr, step, abc=abc_ref.reshape(3))
             xyz, pts = b.read_points(f)
             assert tuple(int(v) for v in counts[f][:3]) == ref["counts"], f
             assert np.array_equal(b.read_hist(f)[:1000], ref["hist"][:1000]), f

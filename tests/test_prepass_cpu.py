@@ -11,6 +11,7 @@ from conftest import GOLDEN
 import sys
 sys.path.insert(0, GOLDEN)
 import prepass_inputs  # noqa: E402
+import roadmap_inputs  # noqa: E402
 
 META = json.load(open(os.path.join(GOLDEN, "prepass.json")))
 
@@ -44,6 +45,24 @@ def test_road_raster_matches_reference(golden):
         nzp = oracle.nonzero_points(img)
         assert len(nzp) == ref["nonzero"]
         assert (np.diff(nzp[:, 1] * 1024 + nzp[:, 0]) > 0).all()   # raster order
+
+
+def test_road_map_matches_reference():
+    """stereovision.py:131-133 (imageRoadMap) restated by oracle.road_map, against the
+    reference's own statements run on the same planePoints (tests/golden/roadmap.json)."""
+    meta = json.load(open(os.path.join(GOLDEN, "roadmap.json")))
+    seen = set()
+    for name, bgr, pp in roadmap_inputs.cases(oracle.digest):
+        ref = meta["cases"][name]
+        assert oracle.digest(pp) == ref["points_digest"]
+        img = oracle.road_map(bgr, pp)
+        green = int(((img[..., 0] == 0) & (img[..., 1] == 255) & (img[..., 2] == 0)).sum())
+        assert oracle.digest(img) == ref["image"] and green == ref["green"], name
+        seen.add(name)
+    assert seen == set(meta["cases"])
+    import pytest
+    with pytest.raises(IndexError):
+        oracle.road_map(bgr, np.array([[[1024, 0]]], np.int32))
 
 
 def test_fill_previous_semantics():
