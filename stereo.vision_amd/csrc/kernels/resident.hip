@@ -442,7 +442,9 @@ __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP, LC>& r, int c, u
                                          uint32_t keep) {
     const int lane = lane_id();
     nvalid += r_nvalid<STEP, QP, LC>(r.dw, r.g, p);
-    if constexpr (STEP == 1) fkb[c * 256 + threadIdx.x] = (uint16_t)keep;   // for pass 2 (read back by this lane)
+    // for pass 2 (read back by this lane); a chunk the plane rules out is skipped there, except the last
+    if constexpr (STEP == 1)
+        if (any || c + 1 == p.nchunks) fkb[c * 256 + threadIdx.x] = (uint16_t)keep;
     if (!any) {   // uniform: the plane rules out every grid point of the chunk: nothing to bin
         if (lane == 0) crange[4 * c + (threadIdx.x >> 6)] = 0u;
         return;
@@ -607,9 +609,12 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
                           : (uint32_t)((tot >> 0) & 0xFFFF) + (uint32_t)((tot >> 16) & 0xFFFF) +
                                 (uint32_t)((tot >> 32) & 0xFFFF) + (uint32_t)((tot >> 48) & 0xFFFF);
     if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (stage_of<QP>() - 1)] = sh.red[tid];   // the tail
-    if (T > (uint32_t)stage_of<QP>() - (running - flushed)) {
+    if (T > (uint32_t)stage_of<QP>() - (running - flushed)) {   // uniform
         p2_write<STEP, QP, LC>(sh.stage, flushed, running, oX, oY, oZ, oPx, oPy, p);
         flushed = running;
+        // the scatter below wraps onto the slots just written out: every wave must have read them first
+        // (without this barrier the other waves' scatter raced wave 0's read of the tail)
+        __syncthreads();
     }
     // descriptors (rdesc) with the back-projection delta bits of each point,
     // branch-free: a slot that is not kept writes to this lane's dump word
