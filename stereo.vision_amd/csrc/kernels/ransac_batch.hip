@@ -41,29 +41,72 @@ __device__ __forceinline__ uint32_t rb_pack(int x, int y, uint32_t d) {
     return (uint32_t)x | ((uint32_t)y << 12) | (d << 24);
 }
 
+// A packed maskpoint's fp64 X, Y, Z with the reference's arithmetic
+// (functions.py:191-193): Z = fB / d, X = ((x - cw) * Z) / f, Y = ((y - ch) *
+// Z) / f. On the step-2 grid X depends on (x / 2, d) only and Y on (y / 2, d),
+// so the three are gathered from tables the batch builds once per call
+// (ransac_tables_kernel, the same fp64 operations, -ffp-contract=off): a point
+// costs three independent gathers (L2-resident: (W/2 + H/2 + 1) x 256 doubles)
+// and no division on the RANSAC kernels' chains. Bit-identical to the
+// reference's values (tests/test_gpu_ransac_batch.py reads them back).
+struct RbTables {
+    const double* X;   // [(W/2) x 256]: X of column x = 2 i at disparity d
+    const double* Y;   // [(H/2) x 256]
+    const double* Z;   // [256]
+};
+
+__device__ __forceinline__ void rb_point(uint32_t pk, const RbTables& t, double& X, double& Y, double& Z) {
+    const uint32_t x2 = (pk & 0xFFF) >> 1, y2 = ((pk >> 12) & 0xFFF) >> 1, d = pk >> 24;
+    X = t.X[x2 * 256 + d];
+    Y = t.Y[y2 * 256 + d];
+    Z = t.Z[d];
+}
+
+// the tables for a frame of H x W (step 2): X rows 0..W/2-1, then Y rows 0..H/2-1, then Z
+__global__ void ransac_tables_kernel(int H, int W, KParams p, double* __restrict__ tab) {
+    const int nx = (W + 1) / 2, ny = (H + 1) / 2;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (nx + ny + 1) * 256; i += gridDim.x * blockDim.x) {
+        const int row = i >> 8, d = i & 255;
+        const double Z = d ? p.fB / (double)d : 0.0;   // functions.py:191
+        double v;
+        if (row < nx) v = (((double)(2 * row) - p.cw) * Z) / p.f;             // :192
+        else if (row < nx + ny) v = (((double)(2 * (row - nx)) - p.ch) * Z) / p.f;   // :193
+        else v = Z;
+        tab[i] = v;
+    }
+}
+
+size_t ransac_tables_bytes(int H, int W) { return sizeof(double) * 256 * (size_t)((W + 1) / 2 + (H + 1) / 2 + 1); }
+
+static RbTables rb_tables(const double* tab, int H, int W) {
+    const int nx = (W + 1) / 2, ny = (H + 1) / 2;
+    return RbTables{tab, tab + 256 * (size_t)nx, tab + 256 * (size_t)(nx + ny)};
+}
+
 // ---------------------------------------------------------------------------
-// maskpoints: step-2 grid of the (optionally masked) disparity -> fp64 XYZ
+// maskpoints: step-2 grid of the (optionally masked) disparity -> packed points
+// (the fp64 X, Y, Z of a point are a function of its packed word: rb_point)
 // ---------------------------------------------------------------------------
 // One lane = one quad (4 consecutive grid points of a row): an 8-byte load of
 // the row's pixels 8q..8q+7 holds the quad's 4 step-2 disparities (and one of
-// the mask). The chunk's fp64 X, Y, Z go to LDS in output order, then out as
-// contiguous doubles (coalesced).
+// the mask). The chunk's packed points go to LDS in output order, then out as
+// contiguous words (coalesced). (Until round 3 the fp64 X, Y, Z were written
+// too: 24 B per point, 2.6 GB per 4096 carmask frames, read back only by a few
+// gathers; they are now computed where used, rb_point.)
 struct MaskpointsShared {
     uint32_t wtot[4];
-    double stage[3 * 1024];
     uint32_t pk[1024];
 };
 
 __global__ __launch_bounds__(256) void maskpoints_kernel(const uint8_t* __restrict__ disp,
                                                          const uint8_t* __restrict__ mask_ff, int64_t frame_px,
-                                                         int H, int W, KParams p, double* __restrict__ out,
+                                                         int H, int W, KParams p,
                                                          uint32_t* __restrict__ packed, int64_t cap,
                                                          int64_t* __restrict__ counts) {
     __shared__ MaskpointsShared sh;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.x;
     const uint8_t* fd = disp + (int64_t)frame * frame_px;
-    double* fo = out + (int64_t)frame * cap * 3;
     uint32_t* fpk = packed + (int64_t)frame * cap;
     const int Hg = p.Hg, Wg = p.Wg;   // range(0, H-1, 2) x range(0, Wu-1, 2); W is the row stride
     const int Wq = (Wg + 3) / 4;
@@ -117,19 +160,9 @@ __global__ __launch_bounds__(256) void maskpoints_kernel(const uint8_t* __restri
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!(m & (1u << k))) continue;
-            const int y = 2 * gy, x = 2 * (gx0 + k);
-            const double Z = p.fB / (double)dv[k];           // functions.py:191
-            const double X = (((double)x - p.cw) * Z) / p.f;  // :192
-            const double Y = (((double)y - p.ch) * Z) / p.f;  // :193
-            sh.stage[3 * o + 0] = X;
-            sh.stage[3 * o + 1] = Y;
-            sh.stage[3 * o + 2] = Z;
-            sh.pk[o] = rb_pack(x, y, dv[k]);
-            ++o;
+            sh.pk[o++] = rb_pack(2 * (gx0 + k), 2 * gy, dv[k]);   // functions.py:191-193: rb_point
         }
-        __syncthreads();   // sh.stage complete; sh.wtot free
-        double* dst = fo + 3 * (int64_t)running;
-        for (uint32_t j = tid; j < 3 * tot; j += 256) __builtin_nontemporal_store(sh.stage[j], dst + j);
+        __syncthreads();   // sh.pk complete; sh.wtot free
         for (uint32_t j = tid; j < tot; j += 256) fpk[running + j] = sh.pk[j];
         running += tot;
     }
@@ -137,11 +170,37 @@ __global__ __launch_bounds__(256) void maskpoints_kernel(const uint8_t* __restri
 }
 
 hipError_t launch_maskpoints(const uint8_t* disp, const uint8_t* mask_ff, int frames, int H, int W, const KParams& p,
-                             double* out, uint32_t* packed, int64_t cap, int64_t* counts, hipStream_t s) {
+                             uint32_t* packed, int64_t cap, int64_t* counts, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
     if (H > 4096 || W > 4096) return hipErrorInvalidValue;   // rb_pack's 12-bit coordinates
-    hipLaunchKernelGGL(maskpoints_kernel, dim3(frames), dim3(256), 0, s, disp, mask_ff, (int64_t)H * W, H, W, p, out,
+    hipLaunchKernelGGL(maskpoints_kernel, dim3(frames), dim3(256), 0, s, disp, mask_ff, (int64_t)H * W, H, W, p,
                        packed, cap, counts);
+    return hipGetLastError();
+}
+
+// n packed points -> n x 3 fp64 (rb_point): the read-back of one frame's maskpoints
+__global__ void maskpoints_xyz_kernel(const uint32_t* __restrict__ packed, int64_t n, RbTables t,
+                                      double* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double X, Y, Z;
+        rb_point(packed[i], t, X, Y, Z);
+        out[3 * i] = X;
+        out[3 * i + 1] = Y;
+        out[3 * i + 2] = Z;
+    }
+}
+
+hipError_t launch_ransac_tables(int H, int W, const KParams& p, double* tab, hipStream_t s) {
+    const int n = 256 * ((W + 1) / 2 + (H + 1) / 2 + 1);
+    hipLaunchKernelGGL(ransac_tables_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, H, W, p, tab);
+    return hipGetLastError();
+}
+
+hipError_t launch_maskpoints_xyz(const uint32_t* packed, int64_t n, const double* tab, int H, int W, double* out,
+                                 hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(maskpoints_xyz_kernel, dim3(g), dim3(256), 0, s, packed, n, rb_tables(tab, H, W), out);
     return hipGetLastError();
 }
 
@@ -172,6 +231,7 @@ struct RansacShared {
     int32_t* pool;                            // pool branch: the shrinking list (same words)
     int k;
     uint32_t* dummy;                          // claims of rejected draws (one word a lane)
+    int ablate;                               // DIAGNOSTIC (SVX_RANSAC_ABLATE, diag build): 64 no sample stores
 };
 
 // CPython's init_genrand + init_by_array (Modules/_randommodule.c) for a
@@ -210,10 +270,17 @@ __device__ void rb_seed(uint32_t* mt, uint64_t seed) {
 // between lanes goes through this point (a compiler memory barrier + LDS wait).
 __device__ __forceinline__ void rb_wave_lds_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// MT19937 tempering; each masked step is a shift and one 3-input v_bitop3
+// ((a & b) ^ c: truth table 0x6a)
 __device__ __forceinline__ uint32_t rb_temper(uint32_t y) {
     y ^= (y >> 11);
+#ifndef SVX_RB_NO_BITOP3
+    y = __builtin_amdgcn_bitop3_b32(y << 7, 0x9d2c5680u, y, 0x6a);
+    y = __builtin_amdgcn_bitop3_b32(y << 15, 0xefc60000u, y, 0x6a);
+#else
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
+#endif
     y ^= (y >> 18);
     return y;
 }
@@ -321,7 +388,12 @@ __device__ void rb_draw_below(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
 // and its lowest lane (earliest draw) wins, otherwise every lane drawing it is
 // rejected. The k-th selection in stream order ends the sample; bits claimed
 // past it are released and the stream resumes right after it.
-constexpr int kRBWin = 3;   // 192 draws a round (the state holds 624 positions: a round must fit, RbStream)
+// 192 draws a round; a round must fit the state's 624 positions (RbStream): span <= 397, i.e. up to 6 windows
+#ifndef SVX_RB_WIN
+#define SVX_RB_WIN 3
+#endif
+constexpr int kRBWin = SVX_RB_WIN;
+static_assert(kRBWin >= 1 && 64 * kRBWin <= 397, "a round's draws must fit the MT state (RbStream)");
 
 template <class IdxT>
 __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, int kb, int k, IdxT* idx,
@@ -369,7 +441,7 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
             const int q = q0 + (int)__builtin_popcountll(sm & ((1ull << lane) - 1));
             if (sel) {
                 if (q < k) {
-                    idx[q] = (IdxT)r[w];
+                    if (!(sh.ablate & 64)) idx[q] = (IdxT)r[w];
                     if (tr) tr[q] = (int32_t)r[w];
                 }
                 else atomicAnd(&sh.bitmap[r[w] >> 5], ~bit);
@@ -410,17 +482,42 @@ __device__ void rb_sample_pool(RansacShared<IdxT>& sh, RbStream& st, uint32_t n,
 constexpr int kRBGather = 10;     // screen gathers a lane keeps in flight
 constexpr int kRBEvalThreads = 1024;   // eval: 16 waves screen 16 trials at a time
 
-// One trial's record written by the draw kernel: a, b, c, |abc|, flag
+// One trial's record: the draw kernel writes the triple's three indices into
+// its first words, the eval kernel replaces them by a, b, c, |abc|, flag
 // (0 ok, 1 singular: numpy's LinAlgError, skipped; 2 ill-conditioned).
 constexpr int kRBTri = 5;
 
+// The trial's plane and its record (one lane): inv([P1;P2;P3]) 1 = (r2 x r3 +
+// r3 x r1 + r1 x r2) / det (functions.py:267), |abc| (:272), and the flag: 1
+// singular (numpy raises LinAlgError, the trial is skipped), 2 ill-conditioned.
+__device__ __forceinline__ void rb_solve_record(const double* r1, const double* r2, const double* r3, double* o) {
+    const double c23[3] = {r2[1] * r3[2] - r2[2] * r3[1], r2[2] * r3[0] - r2[0] * r3[2], r2[0] * r3[1] - r2[1] * r3[0]};
+    const double c31[3] = {r3[1] * r1[2] - r3[2] * r1[1], r3[2] * r1[0] - r3[0] * r1[2], r3[0] * r1[1] - r3[1] * r1[0]};
+    const double c12[3] = {r1[1] * r2[2] - r1[2] * r2[1], r1[2] * r2[0] - r1[0] * r2[2], r1[0] * r2[1] - r1[1] * r2[0]};
+    const double det = r1[0] * c23[0] + r1[1] * c23[1] + r1[2] * c23[2];
+    const double a = (c23[0] + c31[0] + c12[0]) / det;
+    const double b = (c23[1] + c31[1] + c12[1]) / det;
+    const double c = (c23[2] + c31[2] + c12[2]) / det;
+    const double n1 = sqrt(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
+    const double n2 = sqrt(r2[0] * r2[0] + r2[1] * r2[1] + r2[2] * r2[2]);
+    const double n3 = sqrt(r3[0] * r3[0] + r3[1] * r3[1] + r3[2] * r3[2]);
+    double fl = 0.0;
+    if (det == 0.0) fl = 1.0;                                 // numpy: LinAlgError, trial skipped
+    else if (!(fabs(det) >= 1e-6 * n1 * n2 * n3)) fl = 2.0;   // ill-conditioned
+    o[0] = a;
+    o[1] = b;
+    o[2] = c;
+    o[3] = sqrt(a * a + b * b + c * c);
+    o[4] = fl;
+}
+
 template <class IdxT>
-__global__ __launch_bounds__(64) void ransac_draw_kernel(const double* __restrict__ pts, int64_t cap,
+__global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restrict__ packed, RbTables tb, int64_t cap,
                                                          const int64_t* __restrict__ counts, uint64_t seed_base,
                                                          int64_t first_frame, int trials, int k,
                                                          IdxT* __restrict__ sidx, double* __restrict__ tri,
                                                          int32_t* __restrict__ fstat, int32_t* __restrict__ trace,
-                                                         int trace_trials, int bitmap_words) {
+                                                         int trace_trials, int bitmap_words, int ablate) {
     __shared__ uint32_t mt[624];
     __shared__ uint32_t dummy[64];
     extern __shared__ uint32_t rb_dyn[];   // [bitmap_words] bitmap / pool list
@@ -430,10 +527,11 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const double* __restric
     sh.pool = reinterpret_cast<int32_t*>(rb_dyn);
     sh.k = k;
     sh.dummy = dummy;
+    sh.ablate = ablate;
     const int lane = lane_id();
     const int frame = blockIdx.x;
     const int64_t n64 = counts[frame];
-    const double* fp = pts + (int64_t)frame * cap * 3;
+    const uint32_t* fpk = packed + (int64_t)frame * cap;
     if (n64 < k || trials <= 0) {   // every trial's random.sample raises: (None, None)
         if (lane == 0) {
             fstat[2 * frame] = 0;
@@ -452,10 +550,14 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const double* __restric
     for (; s < trials; ++s) {
         IdxT* idx = sidx + ((int64_t)frame * trials + s) * k;
         int32_t* tr = s < trace_trials ? trace + ((int64_t)frame * trace_trials + s) * (k + 3) : nullptr;
-        if (pool) rb_sample_pool(sh, st, n, k, idx, tr);
-        else rb_sample_set(sh, st, n, kb, k, idx, tr);
+        if (ablate & 16) {   // DIAGNOSTIC: no sample
+        } else if (pool) {
+            rb_sample_pool(sh, st, n, k, idx, tr);
+        } else {
+            rb_sample_set(sh, st, n, kb, k, idx, tr);
+        }
         uint32_t t3[3] = {0, 0, 0};
-        const double *p1 = fp, *p2 = fp, *p3 = fp;
+        double p1[3], p2[3], p3[3];   // the triple's fp64 points (rb_point: the reference's X, Y, Z)
         int attempts = 0;
         bool degenerate = false;
         do {   // randomNonCollinearPoints
@@ -464,10 +566,10 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const double* __restric
                 break;
             }
             rb_draw_below(sh, st, n, kb, 3, t3);
-            p1 = fp + 3 * (int64_t)t3[0];
-            p2 = fp + 3 * (int64_t)t3[1];
-            p3 = fp + 3 * (int64_t)t3[2];
-        } while (st.pos < kRBMaxDraws && rb_collinear(p1, p2, p3));
+            rb_point(fpk[t3[0]], tb, p1[0], p1[1], p1[2]);
+            rb_point(fpk[t3[1]], tb, p2[0], p2[1], p2[2]);
+            rb_point(fpk[t3[2]], tb, p3[0], p3[1], p3[2]);
+        } while (st.pos < kRBMaxDraws && !(ablate & 8) && rb_collinear(p1, p2, p3));
         if (st.pos >= kRBMaxDraws) {
             status = 2;
             break;
@@ -477,33 +579,9 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const double* __restric
             break;
         }
         if (tr && lane < 3) tr[k + lane] = (int32_t)(lane == 0 ? t3[0] : lane == 1 ? t3[1] : t3[2]);
-        if (lane == 0) {
-            // inv([P1;P2;P3]) 1 = (r2 x r3 + r3 x r1 + r1 x r2) / det
-            const double* r1 = p1;
-            const double* r2 = p2;
-            const double* r3 = p3;
-            const double c23[3] = {r2[1] * r3[2] - r2[2] * r3[1], r2[2] * r3[0] - r2[0] * r3[2],
-                                   r2[0] * r3[1] - r2[1] * r3[0]};
-            const double c31[3] = {r3[1] * r1[2] - r3[2] * r1[1], r3[2] * r1[0] - r3[0] * r1[2],
-                                   r3[0] * r1[1] - r3[1] * r1[0]};
-            const double c12[3] = {r1[1] * r2[2] - r1[2] * r2[1], r1[2] * r2[0] - r1[0] * r2[2],
-                                   r1[0] * r2[1] - r1[1] * r2[0]};
-            const double det = r1[0] * c23[0] + r1[1] * c23[1] + r1[2] * c23[2];
-            const double a = (c23[0] + c31[0] + c12[0]) / det;
-            const double b = (c23[1] + c31[1] + c12[1]) / det;
-            const double c = (c23[2] + c31[2] + c12[2]) / det;
-            const double n1 = sqrt(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
-            const double n2 = sqrt(r2[0] * r2[0] + r2[1] * r2[1] + r2[2] * r2[2]);
-            const double n3 = sqrt(r3[0] * r3[0] + r3[1] * r3[1] + r3[2] * r3[2]);
-            double fl = 0.0;
-            if (det == 0.0) fl = 1.0;                                 // numpy: LinAlgError, trial skipped
-            else if (!(fabs(det) >= 1e-6 * n1 * n2 * n3)) fl = 2.0;   // ill-conditioned
-            double* o = tri + ((int64_t)frame * trials + s) * kRBTri;
-            o[0] = a;
-            o[1] = b;
-            o[2] = c;
-            o[3] = sqrt(a * a + b * b + c * c);
-            o[4] = fl;
+        if (lane < 3) {   // the triple (the eval kernel solves its plane, off this chain)
+            uint32_t* trip = reinterpret_cast<uint32_t*>(tri + ((int64_t)frame * trials + s) * kRBTri);
+            trip[lane] = lane == 0 ? t3[0] : lane == 1 ? t3[1] : t3[2];
         }
     }
     if (lane == 0) {
@@ -516,9 +594,9 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const double* __restric
 // per trial the screened mean and its bound (2 doubles).
 template <class IdxT, bool LDS_PTS>
 __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
-    const double* __restrict__ pts, const uint32_t* __restrict__ packed, int64_t cap, KParams cp,
+    const uint32_t* __restrict__ packed, RbTables tb, int64_t cap, KParams cp,
     const int64_t* __restrict__ counts, int trials, int k, const IdxT* __restrict__ sidx,
-    const double* __restrict__ tri, const int32_t* __restrict__ fstat, double* __restrict__ out_abc,
+    double* __restrict__ tri, const int32_t* __restrict__ fstat, double* __restrict__ out_abc,
     double* __restrict__ out_err, int32_t* __restrict__ out_trial, uint32_t* __restrict__ out_flags, int ablate,
     int lds_pts_words) {
     extern __shared__ uint32_t ev_dyn[];
@@ -535,7 +613,6 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
         return;
     }
     const int status = fstat[2 * frame], T = fstat[2 * frame + 1];
-    const double* fp = pts + (int64_t)frame * cap * 3;
     const uint32_t* fpk = packed + (int64_t)frame * cap;
     const uint32_t* P = fpk;
     if constexpr (LDS_PTS) {
@@ -543,9 +620,25 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
         P = ev_dyn;
     }
     double* scr = reinterpret_cast<double*>(ev_dyn + (LDS_PTS ? lds_pts_words : 0));   // [T][2]
-    const double* ftri = tri + (int64_t)frame * trials * kRBTri;
+    double* ftri = tri + (int64_t)frame * trials * kRBTri;
     const IdxT* fidx = sidx + (int64_t)frame * trials * k;
     __syncthreads();
+    // every trial's plane from its triple (the draw kernel wrote the three indices
+    // into the record's first words), one lane a trial: the record in place
+    if (!(ablate & 1)) {
+        const uint32_t nm1 = (uint32_t)n64 - 1;
+        for (int t = tid; t < T; t += kRBEvalThreads) {
+            double* rec = ftri + (int64_t)t * kRBTri;
+            const uint32_t* trip = reinterpret_cast<const uint32_t*>(rec);
+            const uint32_t i1 = min(trip[0], nm1), i2 = min(trip[1], nm1), i3 = min(trip[2], nm1);
+            double r1[3], r2[3], r3[3];
+            rb_point(P[i1], tb, r1[0], r1[1], r1[2]);
+            rb_point(P[i2], tb, r2[0], r2[1], r2[2]);
+            rb_point(P[i3], tb, r3[0], r3[1], r3[2]);
+            rb_solve_record(r1, r2, r3, rec);
+        }
+        __syncthreads();   // the records are read by other waves below (same workgroup: same L1)
+    }
     // screen every trial in fp32 (one wave a trial): the mean distance from the
     // packed points and, per point, the bound (|Xa| + |Yb| + |Zc| + 1) 2^-18 / |abc|
     // on its difference to the fp64 distance (fp32 X, Y, Z within 2^-21 relative,
@@ -676,18 +769,19 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
         const IdxT* idx = fidx + (int64_t)t * k;
         double sum = 0.0;
         for (int j0 = lane; j0 < k; j0 += 4 * kWave) {   // every gather in flight before the arithmetic
-            double qx[4], qy[4], qz[4];
+            uint32_t u[4];
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
                 const int j = j0 + kWave * v;
-                const double* q = fp + 3 * (int64_t)(j < k ? (uint32_t)idx[j] : 0u);
-                qx[v] = q[0];
-                qy[v] = q[1];
-                qz[v] = q[2];
+                u[v] = P[j < k ? (uint32_t)idx[j] : 0u];   // the packed point (LDS, or memory when it did not fit)
             }
 #pragma unroll
-            for (int v = 0; v < 4; ++v)
-                if (j0 + kWave * v < k) sum += fabs((qx[v] * a + qy[v] * b + qz[v] * c - 1.0) / d);
+            for (int v = 0; v < 4; ++v) {
+                if (j0 + kWave * v >= k) continue;
+                double qx, qy, qz;
+                rb_point(u[v], tb, qx, qy, qz);
+                sum += fabs((qx * a + qy * b + qz * c - 1.0) / d);
+            }
         }
 #pragma unroll
         for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
@@ -732,17 +826,18 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
 }
 
 template <class IdxT>
-static hipError_t launch_ransac_typed(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
+static hipError_t launch_ransac_typed(const uint32_t* packed, const RbTables& tb, int64_t cap, const KParams& cp,
                                       const int64_t* counts, int64_t max_n, int64_t words, uint64_t seed_base,
                                       int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs,
                                       double* abc, double* err, int32_t* trial, uint32_t* flags, int32_t* trace,
                                       int trace_trials, int ablate, hipStream_t s) {
     IdxT* sidx = reinterpret_cast<IdxT*>(rs.sidx);
-    hipLaunchKernelGGL(ransac_draw_kernel<IdxT>, dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words, s, pts, cap,
-                       counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace,
-                       trace ? trace_trials : 0, (int)words);
+    hipLaunchKernelGGL(ransac_draw_kernel<IdxT>, dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words, s,
+                       packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace,
+                       trace ? trace_trials : 0, (int)words, ablate);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (ablate & (8 | 16)) ablate |= 1;   // DIAGNOSTIC: no samples / planes drawn -> no evaluation of them
     // eval LDS: the points when they fit beside the screen results (160 KiB per workgroup)
     // per trial: screened mean + bound (2 doubles), candidate index and its fp64 error
     const size_t scr = sizeof(double) * 2 * (size_t)trials + sizeof(int32_t) * ((size_t)trials + 1) +
@@ -756,12 +851,12 @@ static hipError_t launch_ransac_typed(const double* pts, const uint32_t* packed,
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ransac_eval_kernel<IdxT, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((ransac_eval_kernel<IdxT, true>), dim3(frames), dim3(kRBEvalThreads), dyn, s, pts, packed,
-                           cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags, ablate,
+        hipLaunchKernelGGL((ransac_eval_kernel<IdxT, true>), dim3(frames), dim3(kRBEvalThreads), dyn, s, packed,
+                           tb, cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags, ablate,
                            (int)pts_words);
     } else {
-        hipLaunchKernelGGL((ransac_eval_kernel<IdxT, false>), dim3(frames), dim3(kRBEvalThreads), dyn, s, pts, packed,
-                           cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags, ablate, 0);
+        hipLaunchKernelGGL((ransac_eval_kernel<IdxT, false>), dim3(frames), dim3(kRBEvalThreads), dyn, s, packed,
+                           tb, cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags, ablate, 0);
     }
     return hipGetLastError();
 }
@@ -770,7 +865,7 @@ size_t ransac_sidx_bytes(int64_t max_n, int frames, int trials, int k) {
     return (max_n <= 65535 ? 2 : 4) * (size_t)frames * (size_t)trials * (size_t)k;
 }
 
-hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
+hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H, int W, int64_t cap, const KParams& cp,
                                const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
                                int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs, double* abc,
                                double* err, int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials,
@@ -784,10 +879,12 @@ hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_
     if (words < 1) words = 1;
     // the samples as u16 indices when every frame has < 65536 points
     if (max_n <= 65535)
-        return launch_ransac_typed<uint16_t>(pts, packed, cap, cp, counts, max_n, words, seed_base, first_frame,
+        return launch_ransac_typed<uint16_t>(packed, rb_tables(tab, H, W), cap, cp, counts, max_n, words, seed_base,
+                                             first_frame,
                                              frames, trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate,
                                              s);
-    return launch_ransac_typed<int32_t>(pts, packed, cap, cp, counts, max_n, words, seed_base, first_frame, frames,
+    return launch_ransac_typed<int32_t>(packed, rb_tables(tab, H, W), cap, cp, counts, max_n, words, seed_base,
+                                        first_frame, frames,
                                         trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate, s);
 }
 

@@ -80,6 +80,17 @@ __device__ __forceinline__ void path_step(int c0, int c1, PathState& s, int P1, 
     s.pmin = (int)(int16_t)wm;
 }
 
+// A path's L minus the cost it adds, as OpenCV computes it, is min(...) - delta
+// in [-P2, 0] (the min includes delta = pmin + P2 and no term is below pmin), so
+// for P2 <= 15 (the reference's default P2 is 5) the directions the row walk only
+// sums — (-1,-1), (0,-1), (+1,-1) — are stored as q = C - L in a nibble, both of
+// a lane's disparities in one byte (64 B per cell instead of 256): the row walk
+// adds 3 C - (q1 + q2 + q3). Exact whenever no L leaves int16 (the frame's range
+// flag is raised otherwise, and the call fails).
+__device__ __forceinline__ uint8_t q_byte(int c0, int c1, int L0, int L1) {
+    return (uint8_t)((c0 - L0) | ((c1 - L1) << 4));
+}
+
 // ---------------------------------------------------------------------------
 // Row features: for each image and channel (0: clipped x-derivative, 1: raw
 // intensity) value | half-neighbour min << 8 | max << 16 (calcPixelCostBT).
@@ -332,10 +343,11 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
 // The operands of a path step never depend on the recurrence, so every walk
 // below keeps the next U steps' loads in flight (registers, clamped addresses:
 // the loads past a path's end are redundant) while it runs the current U steps.
-template <int U>
+template <int U, bool DQ>
 __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint32_t* __restrict__ hvol,
                                                               uint32_t* __restrict__ cvol, uint32_t* __restrict__ l2vol,
-                                                              uint32_t* __restrict__ flags, int frames) {
+                                                              uint8_t* __restrict__ q2vol, uint32_t* __restrict__ flags,
+                                                              int frames) {
     const int wpb = blockDim.x >> 6;
     const int cols_blocks = (k.width1 + wpb - 1) / wpb;
     const int f = blockIdx.x / cols_blocks;
@@ -379,7 +391,10 @@ __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint3
             cvol[base + (size_t)y * rs] = pack16(cw0, cw1);
             int L0, L1;
             path_step(cw0, cw1, st, k.P1, k.P2, L0, L1, ovf);
-            l2vol[base + (size_t)y * rs] = pack16(L0, L1);
+            if constexpr (DQ)
+                q2vol[base + (size_t)y * rs] = q_byte(cw0, cw1, L0, L1);
+            else
+                l2vol[base + (size_t)y * rs] = pack16(L0, L1);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -394,10 +409,11 @@ __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint3
 // read once: the row a step drops (max(y - SH2 - 1, 0)) is the row added RS = 2 SH2 + 1 steps before it, or
 // one of rows 0 .. SH2 read for the first window, so the walk keeps the next RS drops in registers (a ring
 // indexed by the unrolled step) and loads only the added rows, the next block's in flight.
-template <int SH2C>
+template <int SH2C, bool DQ>
 __global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const uint32_t* __restrict__ hvol,
                                                                    uint32_t* __restrict__ cvol,
                                                                    uint32_t* __restrict__ l2vol,
+                                                                   uint8_t* __restrict__ q2vol,
                                                                    uint32_t* __restrict__ flags, int frames) {
     constexpr int RS = 2 * SH2C + 1;
     const int wpb = blockDim.x >> 6;
@@ -448,7 +464,10 @@ __global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const 
             cvol[base + (size_t)y * rs] = pack16(cw0, cw1);
             int L0, L1;
             path_step(cw0, cw1, st, k.P1, k.P2, L0, L1, ovf);
-            l2vol[base + (size_t)y * rs] = pack16(L0, L1);
+            if constexpr (DQ)
+                q2vol[base + (size_t)y * rs] = q_byte(cw0, cw1, L0, L1);
+            else
+                l2vol[base + (size_t)y * rs] = pack16(L0, L1);
         }
 #pragma unroll
         for (int u = 0; u < RS; ++u) add[u] = nadd[u];
@@ -459,9 +478,10 @@ __global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const 
 // ---------------------------------------------------------------------------
 // Diagonal paths: dir 1 from (x-1, y-1), dir 3 from (x+1, y-1).
 // ---------------------------------------------------------------------------
-template <int U>
+template <int U, bool DQ>
 __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t* __restrict__ cvol,
                                                           uint32_t* __restrict__ l1vol, uint32_t* __restrict__ l3vol,
+                                                          uint8_t* __restrict__ q1vol, uint8_t* __restrict__ q3vol,
                                                           uint32_t* __restrict__ flags, int frames) {
     const int wpb = blockDim.x >> 6;
     const int npaths = k.width1 + k.H - 1;   // per direction
@@ -487,6 +507,7 @@ __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t*
     const size_t a0 = (size_t)f * k.H * rs + (size_t)y * rs + (size_t)xi * 64 + lane;
     const size_t step = dir ? rs - 64 : rs + 64;
     uint32_t* out = dir ? l3vol : l1vol;
+    uint8_t* qout = dir ? q3vol : q1vol;
     PathState st;
     bool ovf = false;
     uint32_t cc[U];
@@ -502,7 +523,10 @@ __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t*
             if (t >= len) break;
             int L0, L1;
             path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1, ovf);
-            out[a0 + (size_t)t * step] = pack16(L0, L1);
+            if constexpr (DQ)
+                qout[a0 + (size_t)t * step] = q_byte(lo16(cc[u]), hi16(cc[u]), L0, L1);
+            else
+                out[a0 + (size_t)t * step] = pack16(L0, L1);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) cc[u] = nc[u];
@@ -516,10 +540,13 @@ __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t*
 template <typename T>
 __device__ __forceinline__ T ld_nt(const T* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
 
-template <int U, bool NT>
+template <int U, bool NT, bool DQ>
 __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* __restrict__ cvol,
                                                          uint32_t* __restrict__ l1p, const uint32_t* __restrict__ l2vol,
-                                                         const uint32_t* __restrict__ l3vol, int16_t* __restrict__ d16,
+                                                         const uint32_t* __restrict__ l3vol,
+                                                         uint8_t* __restrict__ q0vol, const uint8_t* __restrict__ q1vol,
+                                                         const uint8_t* __restrict__ q2vol,
+                                                         const uint8_t* __restrict__ q3vol, int16_t* __restrict__ d16,
                                                          uint32_t* __restrict__ flags, int frames) {
     extern __shared__ int16_t rsm[];
     const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
@@ -541,16 +568,20 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
     const size_t rb = ((size_t)f * k.H + y) * rs + lane;
     bool ovf = false;
     const int n = k.width1;
-    // pass A: x ascending, direction (-1, 0); P = sat16(L0 + L1 + L2 + L3) replaces L1
+    // pass A: x ascending, direction (-1, 0); P = sat16(L0 + L1 + L2 + L3) replaces L1.
+    // DQ: pass A stores only its own q (q0 = C - L0) and pass B forms P = sat16(4 C - (q0 + q1 + q2 + q3))
+    // from the four q bytes: C is read twice, the other directions once, as 64 B a cell.
     {
         PathState st;
         uint32_t cc[U], ca[U], cb[U], ce[U];
         const auto load = [&](int xi, uint32_t& c, uint32_t& a, uint32_t& b, uint32_t& e) {
             const size_t o = rb + (size_t)min(xi, n - 1) * 64;
             c = cvol[o];
-            a = ld_nt(l1p + o, NT);
-            b = ld_nt(l2vol + o, NT);
-            e = ld_nt(l3vol + o, NT);
+            if constexpr (!DQ) {
+                a = ld_nt(l1p + o, NT);
+                b = ld_nt(l2vol + o, NT);
+                e = ld_nt(l3vol + o, NT);
+            }
         };
 #pragma unroll
         for (int u = 0; u < U; ++u) load(u, cc[u], ca[u], cb[u], ce[u]);
@@ -564,12 +595,16 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
                 if (xi >= n) break;
                 int L0, L1;
                 path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1, ovf);
-                const uint32_t pv = pack16(sat16(L0 + lo16(ca[u]) + lo16(cb[u]) + lo16(ce[u])),
-                                           sat16(L1 + hi16(ca[u]) + hi16(cb[u]) + hi16(ce[u])));
-                if (NT)
-                    __builtin_nontemporal_store(pv, l1p + rb + (size_t)xi * 64);
-                else
-                    l1p[rb + (size_t)xi * 64] = pv;
+                if constexpr (DQ) {
+                    q0vol[rb + (size_t)xi * 64] = q_byte(lo16(cc[u]), hi16(cc[u]), L0, L1);
+                } else {
+                    const uint32_t pv = pack16(sat16(L0 + lo16(ca[u]) + lo16(cb[u]) + lo16(ce[u])),
+                                               sat16(L1 + hi16(ca[u]) + hi16(cb[u]) + hi16(ce[u])));
+                    if (NT)
+                        __builtin_nontemporal_store(pv, l1p + rb + (size_t)xi * 64);
+                    else
+                        l1p[rb + (size_t)xi * 64] = pv;
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -585,11 +620,16 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
         PathState st;
         const int d0 = 2 * lane;
         uint32_t cc[U], cp[U];
-        // step j visits xi = n - 1 - j (pass A's P of every cell is stored before these loads)
+        // step j visits xi = n - 1 - j (pass A's P of every cell is stored before these loads;
+        // DQ: pp = the four q bytes, q0 | q1 << 8 | q2 << 16 | q3 << 24)
         const auto load = [&](int j, uint32_t& c, uint32_t& pp) {
             const size_t o = rb + (size_t)max(n - 1 - j, 0) * 64;
             c = ld_nt(cvol + o, NT);
-            pp = ld_nt(l1p + o, NT);
+            if constexpr (DQ)
+                pp = (uint32_t)ld_nt(q0vol + o, NT) | (uint32_t)ld_nt(q1vol + o, NT) << 8 |
+                     (uint32_t)ld_nt(q2vol + o, NT) << 16 | (uint32_t)ld_nt(q3vol + o, NT) << 24;
+            else
+                pp = ld_nt(l1p + o, NT);
         };
 #pragma unroll
         for (int u = 0; u < U; ++u) load(u, cc[u], cp[u]);
@@ -603,7 +643,15 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
                 if (xi < 0) break;
                 int L0, L1;
                 path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1, ovf);
-                const int S0 = sat16(lo16(cp[u]) + L0), S1 = sat16(hi16(cp[u]) + L1);
+                int P0, P1;
+                if constexpr (DQ) {   // the byte sums of the low and the high nibbles (v_sad_u8 against 0)
+                    P0 = sat16(4 * lo16(cc[u]) - (int)__builtin_amdgcn_sad_u8(cp[u] & 0x0F0F0F0Fu, 0u, 0u));
+                    P1 = sat16(4 * hi16(cc[u]) - (int)__builtin_amdgcn_sad_u8((cp[u] >> 4) & 0x0F0F0F0Fu, 0u, 0u));
+                } else {
+                    P0 = lo16(cp[u]);
+                    P1 = hi16(cp[u]);
+                }
+                const int S0 = sat16(P0 + L0), S1 = sat16(P1 + L1);
                 const int key = min(((S0 + 32768) << 7) | d0, ((S1 + 32768) << 7) | (d0 + 1));
                 const int kmin = wave_min_i32(key);
                 const int minS = (kmin >> 7) - 32768, best = kmin & 127;
@@ -1026,27 +1074,38 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
     // 64 frames, faster in 4 of 5 alternations (SVX_SGBM_NT=0: plain accesses; A/B)
     const char* ntv = svx_knob("SVX_SGBM_NT");
     const bool nt = !(ntv && ntv[0] == '0');
-#define SVX_SGBM_WALKS(U)                                                                                         \
+    // the q-byte volumes of the four directions the row walk sums (P2 <= 15; SVX_SGBM_DQ=0: int16 L volumes and
+    // P, A/B): four volumes of 64 B a cell in the space of the fourth int16 volume
+    const char* dqv = svx_knob("SVX_SGBM_DQ");
+    const bool dq = k.P2 <= 15 && !(dqv && dqv[0] == '0');
+    const size_t qb = (size_t)frames * H * k.width1 * 64;
+    uint8_t* q0 = reinterpret_cast<uint8_t*>(s.l3);
+    uint8_t* q1 = q0 + qb;
+    uint8_t* q2 = q1 + qb;
+    uint8_t* q3 = q2 + qb;
+#define SVX_SGBM_WALKS(U, DQ)                                                                                     \
     if (vring)                                                                                                    \
-        hipLaunchKernelGGL(sgbm_vertical_ring_kernel<10>, dim3(frames * cb), dim3(256), 0, st, k, s.hl1, s.c,     \
-                           s.l2, s.flags, frames);                                                                \
+        hipLaunchKernelGGL((sgbm_vertical_ring_kernel<10, DQ>), dim3(frames * cb), dim3(256), 0, st, k, s.hl1,   \
+                           s.c, s.l2, q2, s.flags, frames);                                                       \
     else                                                                                                          \
-        hipLaunchKernelGGL(sgbm_vertical_kernel<U>, dim3(frames * cb), dim3(256), 0, st, k, s.hl1, s.c, s.l2,     \
-                           s.flags, frames);                                                                      \
-    hipLaunchKernelGGL(sgbm_diag_kernel<U>, dim3((paths + 3) / 4), dim3(256), 0, st, k, s.c, s.hl1, s.l3, s.flags, \
-                       frames);                                                                                    \
+        hipLaunchKernelGGL((sgbm_vertical_kernel<U, DQ>), dim3(frames * cb), dim3(256), 0, st, k, s.hl1, s.c,    \
+                           s.l2, q2, s.flags, frames);                                                            \
+    hipLaunchKernelGGL((sgbm_diag_kernel<U, DQ>), dim3((paths + 3) / 4), dim3(256), 0, st, k, s.c, s.hl1, s.l3,  \
+                       q1, q3, s.flags, frames);                                                                  \
     if (nt)                                                                                                       \
-        hipLaunchKernelGGL((sgbm_row_kernel<U, true>), dim3((frames * H + 3) / 4), dim3(256), lds4, st, k, s.c,   \
-                           s.hl1, s.l2, s.l3, s.raw, s.flags, frames);                                            \
+        hipLaunchKernelGGL((sgbm_row_kernel<U, true, DQ>), dim3((frames * H + 3) / 4), dim3(256), lds4, st, k,   \
+                           s.c, s.hl1, s.l2, s.l3, q0, q1, q2, q3, s.raw, s.flags, frames);                           \
     else                                                                                                          \
-        hipLaunchKernelGGL((sgbm_row_kernel<U, false>), dim3((frames * H + 3) / 4), dim3(256), lds4, st, k, s.c,  \
-                           s.hl1, s.l2, s.l3, s.raw, s.flags, frames)
-    if (pf == 1) {
-        SVX_SGBM_WALKS(1);
+        hipLaunchKernelGGL((sgbm_row_kernel<U, false, DQ>), dim3((frames * H + 3) / 4), dim3(256), lds4, st, k,  \
+                           s.c, s.hl1, s.l2, s.l3, q0, q1, q2, q3, s.raw, s.flags, frames)
+    if (dq) {
+        SVX_SGBM_WALKS(8, true);
+    } else if (pf == 1) {
+        SVX_SGBM_WALKS(1, false);
     } else if (pf == 4) {
-        SVX_SGBM_WALKS(4);
+        SVX_SGBM_WALKS(4, false);
     } else {
-        SVX_SGBM_WALKS(8);
+        SVX_SGBM_WALKS(8, false);
     }
 #undef SVX_SGBM_WALKS
     // StereoSGBM::compute's medianBlur(disp, disp, 3): raw -> d16

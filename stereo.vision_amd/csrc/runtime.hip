@@ -261,7 +261,8 @@ struct sv_batch {
     bool nz_fresh = false;      // nz holds the walk of the current road images (road_kernel wrote both)
     DevBuf rmap;                // imageRoadMap (stereovision.py:131-133): frames x H x W x 3, on request
     bool want_rmap = false, rmap_fresh = false;
-    DevBuf mpts, rres;          // maskpoints (frames x mcap x 3 fp64) + counts; batched RANSAC results
+    DevBuf mpts, rres;          // one frame's maskpoints as fp64 (read-back scratch); counts + batched RANSAC results
+    DevBuf rtab;                // fp64 X / Y / Z tables of the step-2 grid (the last sv_batch_ransac's camera)
     DevBuf mpk;                 // maskpoints packed (frames x mcap words x | y << 12 | d << 24): RANSAC's fp32 screen
     DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
     DevBuf rsidx, rtri;         // batched RANSAC scratch: every trial's sample; trial records + frame status
@@ -520,7 +521,7 @@ int sv_batch_destroy(sv_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppx, &b->ppy, &b->ctrl, &b->masks,
-                      &b->mdisp, &b->carmask, &b->road, &b->rmap, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
+                      &b->mdisp, &b->carmask, &b->road, &b->rmap, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtab, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
                       &b->glut, &b->ghist, &b->sgflags})
         if (x->p) (void)hipFree(x->p);
@@ -1334,9 +1335,10 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 // batched RANSAC (stereovision.py:85-94 per frame, seeded per frame)
 // ---------------------------------------------------------------------------
 
-// DIAGNOSTIC ONLY (env SVX_RANSAC_ABLATE, documented in DESIGN.md): 1 skips the trial evaluation,
-// 2 draws only the first two trials (results invalid); 4 evaluates every trial in fp64 (no fp32
-// screen; results valid, for A/B).
+// DIAGNOSTIC ONLY (env SVX_RANSAC_ABLATE, diagnostic build, documented in DESIGN.md): 1 skips the trial
+// evaluation, 2 draws only the first two trials (results invalid); 4 evaluates every trial in fp64 (no fp32
+// screen; results valid, for A/B); draw kernel (results invalid): 8 no triple loads / collinearity test /
+// plane solve, 16 no random.sample, 64 no sample stores.
 static int ransac_ablate() {
     const char* e = svx_knob("SVX_RANSAC_ABLATE");
     return e ? std::atoi(e) : 0;
@@ -1354,15 +1356,18 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
     HIP_TRY(hipSetDevice(b->device));
     const size_t F = (size_t)b->frames;
     if (b->H > 4096 || b->W > 4096) return fail(SV_E_ARG, "sv_batch_ransac: frames up to 4096 x 4096");
-    HIP_TRY(b->mpts.ensure(sizeof(double) * 3 * (size_t)(mcap > 0 ? mcap : 1) * F));
     HIP_TRY(b->mpk.ensure(sizeof(uint32_t) * (size_t)(mcap > 0 ? mcap : 1) * F));
     HIP_TRY(b->rres.ensure(F * (sizeof(double) * 4 + sizeof(int64_t) + sizeof(int32_t) + sizeof(uint32_t))));
     b->mcap = mcap;
     const RansacRes r = ransac_res(b);
     const KParams p = make_params(b->H, b->W, 2, *cam, b->Wu);
+    // the fp64 X / Y / Z tables of the step-2 grid for this camera (the RANSAC kernels and the read-back gather
+    // them instead of dividing)
+    HIP_TRY(b->rtab.ensure(ransac_tables_bytes(b->H, b->W)));
+    HIP_TRY(launch_ransac_tables(b->H, b->W, p, b->rtab.as<double>(), b->stream));
     const uint8_t* mff = b->have_mask ? b->carmask.as<uint8_t>() : nullptr;
-    HIP_TRY(launch_maskpoints(b->disp.as<uint8_t>(), mff, b->frames, b->H, b->W, p, b->mpts.as<double>(),
-                              b->mpk.as<uint32_t>(), mcap, r.mcount, b->stream));
+    HIP_TRY(launch_maskpoints(b->disp.as<uint8_t>(), mff, b->frames, b->H, b->W, p, b->mpk.as<uint32_t>(), mcap,
+                              r.mcount, b->stream));
     int32_t* trace = nullptr;
     if (b->trace_trials > 0) {
         HIP_TRY(b->rtrace.ensure(sizeof(int32_t) * F * b->trace_trials * (size_t)(k + 3)));
@@ -1386,7 +1391,8 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
     HIP_TRY(b->rtri.ensure(sizeof(double) * 5 * F * (size_t)std::max(trials, 1) + sizeof(int32_t) * 2 * F));
     const RansacScratch rs{b->rsidx.p, b->rtri.as<double>(),
                            reinterpret_cast<int32_t*>(b->rtri.as<double>() + 5 * F * (size_t)std::max(trials, 1))};
-    HIP_TRY(launch_ransac_batch(b->mpts.as<double>(), b->mpk.as<uint32_t>(), mcap, p, r.mcount, max_n, max_pool_n,
+    HIP_TRY(launch_ransac_batch(b->mpk.as<uint32_t>(), b->rtab.as<double>(), b->H, b->W, mcap, p, r.mcount, max_n,
+                                max_pool_n,
                                 seed_base, first_frame, b->frames, trials, k, rs, r.abc, r.err, r.trial, r.flags, trace,
                                 b->trace_trials, ransac_ablate(), b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
@@ -1436,9 +1442,13 @@ int sv_batch_read_maskpoints(sv_batch* b, int frame, double* xyz, int64_t cap, i
     HIP_TRY(hipMemcpy(&k, r.mcount + frame, sizeof k, hipMemcpyDeviceToHost));
     *n = k;
     if (k > cap) return fail(SV_E_CAP, "capacity %lld < %lld", (long long)cap, (long long)k);
-    if (k && xyz)
-        HIP_TRY(hipMemcpy(xyz, b->mpts.as<double>() + 3 * (size_t)b->mcap * frame, sizeof(double) * 3 * k,
-                          hipMemcpyDeviceToHost));
+    if (k && xyz) {   // the frame's fp64 X, Y, Z from its packed points (the reference's arithmetic)
+        HIP_TRY(b->mpts.ensure(sizeof(double) * 3 * (size_t)k));
+        HIP_TRY(launch_maskpoints_xyz(b->mpk.as<uint32_t>() + (size_t)b->mcap * frame, k, b->rtab.as<double>(), b->H,
+                                      b->W, b->mpts.as<double>(), b->stream));
+        HIP_TRY(hipMemcpyAsync(xyz, b->mpts.p, sizeof(double) * 3 * k, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
+    }
     return SV_OK;
 }
 

@@ -111,11 +111,19 @@ hipError_t launch_ransac_eval(const double* pts, int64_t ld, const int32_t* sidx
                               int k, double* abc, double* err, uint8_t* flag, hipStream_t s);
 
 // kernels/ransac_batch.hip -------------------------------------------------
-// maskpoints of every frame: fp64 XYZ of the d > 0 points of (disp & mask_ff)
-// on the step-2 grid, raster order; out frames x cap x 3, counts[frame].
-// packed (optional use by RANSAC): frames x cap words x | y << 12 | d << 24 (H, W <= 4096).
+// maskpoints of every frame: the d > 0 points of (disp & mask_ff) on the step-2
+// grid, raster order, as packed words x | y << 12 | d << 24 (frames x cap,
+// H, W <= 4096), counts[frame]; their fp64 X, Y, Z are computed where used
+// (launch_maskpoints_xyz, and inside the RANSAC kernels).
 hipError_t launch_maskpoints(const uint8_t* disp, const uint8_t* mask_ff, int frames, int H, int W, const KParams& p,
-                             double* out, uint32_t* packed, int64_t cap, int64_t* counts, hipStream_t s);
+                             uint32_t* packed, int64_t cap, int64_t* counts, hipStream_t s);
+// fp64 X (per x / 2, d), Y (per y / 2, d) and Z (per d) of the step-2 grid of an H x W frame, the reference's
+// arithmetic (functions.py:191-193): ransac_tables_bytes(H, W) bytes
+size_t ransac_tables_bytes(int H, int W);
+hipError_t launch_ransac_tables(int H, int W, const KParams& p, double* tab, hipStream_t s);
+// n packed maskpoints -> n x 3 fp64 X, Y, Z (from the tables)
+hipError_t launch_maskpoints_xyz(const uint32_t* packed, int64_t n, const double* tab, int H, int W, double* out,
+                                 hipStream_t s);
 // RANSAC of every frame with random.seed(seed_base + first_frame + frame):
 // abc (frames x 3), err, winning trial (-1: none ran), flags (1 a singular
 // trial, 2 ill-conditioned winner, 4 near-tie). cap <= 163,840, k <= 1024.
@@ -144,7 +152,7 @@ struct RansacScratch {
 size_t ransac_sidx_bytes(int64_t max_n, int frames, int trials, int k);
 // max_n: the largest frame's point count; max_pool_n: the largest count that takes random.sample's pool
 // branch (n <= setsize(k)), 0 if none (both size the draw kernel's LDS). trials <= 4096.
-hipError_t launch_ransac_batch(const double* pts, const uint32_t* packed, int64_t cap, const KParams& cp,
+hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H, int W, int64_t cap, const KParams& cp,
                                const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
                                int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs, double* abc,
                                double* err, int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials,

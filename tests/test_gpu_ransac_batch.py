@@ -161,6 +161,49 @@ def test_batch_sample_branches(svb, ns, k, seed_base):
             _check(b.read_ransac(f), *ref, what=f"n={n} k={k}")
 
 
+def _lines_frame(rows, n_per_row, n_rest, seed):
+    """n_rest random step-2 points plus n_per_row points on each given grid row at one disparity (50): every
+    triple drawn from one row is collinear (same Y and Z)."""
+    rng = np.random.default_rng(seed)
+    d = _sparse_frame(n_rest, seed + 1)
+    for r in rows:
+        d[r, :] = 0
+        d[r, 2 * rng.choice(W // 2, n_per_row, replace=False)] = 50
+    return d
+
+
+def test_batch_collinear_redraws(svb):
+    """Frames whose points lie largely on a few lines: many triples are collinear, so
+    randomNonCollinearPoints redraws often (set branch with nine full rows, pool branch with one and two
+    rows). The draw kernel checks each triple on a second wave while the next sample is drawn and rewinds
+    the stream when it was collinear; every trial's sample and triple, the winner and the plane must still
+    be CPython's and the reference's."""
+    trials = 300
+    frames = [_lines_frame(range(100, 118, 2), 512, 400, 70), _lines_frame([100], 500, 500, 71),
+              _lines_frame([100, 300], 300, 150, 72)]
+    with svb.Batch(len(frames), H=H, W=W, step=2, with_bgr=False) as b:
+        for f, d in enumerate(frames):
+            b.upload(f, d)
+        b.set_mask(None)
+        b.ransac_trace(trials)
+        b.ransac(seed_base=33, trials=trials)
+        redraws = 0
+        for f in range(len(frames)):
+            pts = b.read_maskpoints(f)
+            _check_draws(b, f, pts, 33 + f, trials)
+            _check(b.read_ransac(f), *_oracle_frame(pts, trials, 33 + f), what=f"frame {f}")
+            r = random.Random(33 + f)
+            P = np.asarray(pts)
+            for _ in range(trials):   # how many redraws the frame exercised
+                r.sample(range(len(P)), 600)
+                while True:
+                    i1, i2, i3 = (r.sample(range(len(P)), 1)[0] for _ in range(3))
+                    if np.cross(P[i1] - P[i2], P[i2] - P[i3]).any():
+                        break
+                    redraws += 1
+        assert redraws >= 20, redraws
+
+
 def test_batch_degenerate_frame_gives_up(svb):
     """All maskpoints on one line: the reference loops for ever in
     randomNonCollinearPoints; the kernel stops, flags the frame (8) and the

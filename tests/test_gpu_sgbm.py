@@ -68,8 +68,12 @@ def test_sgbm_compute_small(sv, H, W, kind):
     assert np.array_equal(sv.disp.sgbm_compute(L, R), osg.sgbm(L, R))
 
 
+# P2 <= 15 runs the q-nibble walks (C - L stored in 4 bits, kernels/sgbm.hip q_byte), larger P2 the int16
+# L volumes: P2 = 15 is the largest nibble, 16 the first int16 case
 @pytest.mark.parametrize("kw", [dict(block=5), dict(block=9, P1=8, P2=32), dict(uniqueness=10),
-                                dict(disp12_max_diff=3, prefilter_cap=31), dict(block=1), dict(block=35)])
+                                dict(disp12_max_diff=3, prefilter_cap=31), dict(block=1), dict(block=35),
+                                dict(P1=2, P2=15), dict(P1=1, P2=15, uniqueness=0), dict(P1=8, P2=16),
+                                dict(block=7, P1=14, P2=15)])
 def test_sgbm_parameters(sv, kw):
     L, R = osg.synth_pair(7, 80, 400)
     L = L.copy()

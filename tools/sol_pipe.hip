@@ -19,6 +19,10 @@
 //   mode 10 read-then-write, each frame's output region taken from a global counter (atomicAdd) after its reads
 //   mode 11 five planes, frame stride cap, every frame writing all cap outputs (no gaps; more bytes)
 //   mode 12 mode 1 (chunk-interleaved reads and writes) into a region taken from the counter after the first chunk's reads
+//   mode 13..17  the resident pipeline's shape: all of the frame read (pass 1), then pass 2 re-reading the
+//           disparity and writing, in groups of K = 1, 2, 4, 8, 64 chunks (K chunks' disparity reads, then
+//           their K chunks' writes), into a region taken from the counter after pass 1
+//   mode 18..22  the same with the frame-strided planes (no counter)
 // argv: frames (4096), outputs per frame (277200), 1 = output planes physically contiguous (0)
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/_sol_pipe tools/sol_pipe.hip
 #include <hip/hip_runtime.h>
@@ -50,6 +54,7 @@ struct Args {
     int nplanes;         // planes written
     int64_t nper;        // floats per plane per frame
     unsigned long long* counter;
+    int kgroup;          // modes 13..22: chunks per read/write group
 };
 
 __device__ __forceinline__ uint32_t read_range(const Args& a, int f, int64_t w0, int64_t w1) {
@@ -101,7 +106,28 @@ __global__ __launch_bounds__(256) void sol_kernel(Args a) {
     const int f = blockIdx.x;
     uint32_t acc = 0;
     const float v = (float)f;
-    if (a.mode == 12) {
+    if (a.mode >= 13) {
+        const int K = a.kgroup, n = 64;
+        acc ^= read_range(a, f, 0, a.px16);   // pass 1
+        __shared__ int64_t base13;
+        if (threadIdx.x == 0) base13 = a.mode <= 17 ? (int64_t)atomicAdd(a.counter, (unsigned long long)a.kept)
+                                                    : (int64_t)f * a.cap;
+        __syncthreads();
+        const uint4* d = a.disp + f * a.px16;
+        for (int c0 = 0; c0 < n; c0 += K) {
+            for (int c = c0; c < c0 + K; ++c)
+                for (int64_t w = a.px16 * c / n + threadIdx.x; w < a.px16 * (c + 1) / n; w += 256) {
+                    const uint4 x = *(d + w);
+                    acc ^= x.x ^ x.w;
+                }
+            const int64_t g0 = (a.kept / 4 * c0 / n) * 4, g1 = (a.kept / 4 * (c0 + K) / n) * 4;
+            for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
+                const v4f q = {v, v, v, v};
+#pragma unroll
+                for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + base13 + g));
+            }
+        }
+    } else if (a.mode == 12) {
         const int n = 64;   // chunks
         __shared__ int64_t base12;
         for (int c = 0; c < n; ++c) {
@@ -182,11 +208,19 @@ int main(int argc, char** argv) {
     const char* names[] = {"read-then-write", "interleaved", "read only", "write only", "read, re-read disp, write",
                            "write: dense frames", "write: one AoS plane", "write: stride cap+64", "write: dense sweep",
                            "write: 32 B per lane", "read-then-write, atomic regions", "write: full frames, stride cap",
-                           "interleaved, atomic regions"};
+                           "interleaved, atomic regions", "pass1 + K-grouped pass2, atomic regions",
+                           "pass1 + K-grouped pass2, atomic regions", "pass1 + K-grouped pass2, atomic regions",
+                           "pass1 + K-grouped pass2, atomic regions", "pass1 + K-grouped pass2, atomic regions",
+                           "pass1 + K-grouped pass2, strided", "pass1 + K-grouped pass2, strided",
+                           "pass1 + K-grouped pass2, strided", "pass1 + K-grouped pass2, strided",
+                           "pass1 + K-grouped pass2, strided"};
+    const int kgroups[5] = {1, 2, 4, 8, 64};
     const int64_t cap0 = cap - 64;
     for (int round = 0; round < 2; ++round)
-        for (int mode = 0; mode < 13; ++mode) {
+        for (int mode = 0; mode < 23; ++mode) {
+            if (round == 0 && mode < 13) continue;   // (the earlier modes: profiles/r02/sol_pipe_session8.txt)
             a.mode = mode;
+            a.kgroup = mode >= 13 ? kgroups[(mode - 13) % 5] : 1;
             a.nplanes = 5;
             a.nper = kept;
             a.stride = cap0;
@@ -217,11 +251,12 @@ int main(int argc, char** argv) {
                 best = ms < best ? ms : best;
                 tot += ms;
             }
-            const double rd = ((mode == 3 || mode >= 5) && mode != 10 && mode != 12 ? 0. : 4. * px * frames) + (mode == 4 ? 1. * px * frames : 0.);
+            const double rd = ((mode == 3 || mode >= 5) && mode != 10 && mode < 12 ? 0. : 4. * px * frames) +
+                              (mode == 4 || mode >= 13 ? 1. * px * frames : 0.);
             const double wr = mode == 2 ? 0. : 20. * (mode == 11 ? cap0 : kept) * frames;
-            std::printf("{\"round\": %d, \"mode\": %d, \"what\": \"%s\", \"GB\": %.2f, \"best_ms\": %.3f, \"mean_ms\": %.3f, "
-                        "\"TBps_best\": %.2f}\n",
-                        round, mode, names[mode], (rd + wr) / 1e9, best, tot / reps, (rd + wr) / best / 1e9);
+            std::printf("{\"round\": %d, \"mode\": %d, \"what\": \"%s\", \"K\": %d, \"GB\": %.2f, \"best_ms\": %.3f, "
+                        "\"mean_ms\": %.3f, \"TBps_best\": %.2f}\n",
+                        round, mode, names[mode], a.kgroup, (rd + wr) / 1e9, best, tot / reps, (rd + wr) / best / 1e9);
             std::fflush(stdout);
         }
     return 0;
