@@ -231,7 +231,7 @@ struct RansacShared {
     int32_t* pool;                            // pool branch: the shrinking list (same words)
     int k;
     uint32_t* dummy;                          // claims of rejected draws (one word a lane)
-    int ablate;                               // DIAGNOSTIC (SVX_RANSAC_ABLATE, diag build): 64 no sample stores
+    int ablate;                               // DIAGNOSTIC (SVX_RANSAC_ABLATE, diag build)
 };
 
 // CPython's init_genrand + init_by_array (Modules/_randommodule.c) for a
@@ -269,6 +269,14 @@ __device__ void rb_seed(uint32_t* mt, uint64_t seed) {
 // load of mt[j - 35]) and may move loads above earlier stores: every hand-off
 // between lanes goes through this point (a compiler memory barrier + LDS wait).
 __device__ __forceinline__ void rb_wave_lds_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ double rb_readlane_f64(double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+// the wave's lane mask of a condition, straight from the compare (no 0/1 register in between)
+__device__ __forceinline__ uint64_t rb_ballot(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 
 // MT19937 tempering; each masked step is a shift and one 3-input v_bitop3
 // ((a & b) ^ c: truth table 0x6a)
@@ -285,33 +293,37 @@ __device__ __forceinline__ uint32_t rb_temper(uint32_t y) {
     return y;
 }
 
-// One MT19937 twist of mt (in place, one wave) and its tempered outputs into
-// out. The sequential in-place recurrence new[kk] = f(old[kk], old[kk+1],
-// src) reads src = old[kk+397] for kk < 227 and new[kk-227] above, so it has
-// three dependency levels: [0, 227) from old words only, [227, 454) from level
-// 1, [454, 624) from level 2 (word 623 also reads new[0]). Within a level every
-// lane reads all its inputs (up to 4 words a lane) before any lane writes, so
-// no read sees a word of its own level already replaced.
-__device__ __forceinline__ void rb_twist_level(uint32_t* mt, int lo, int hi) {
+// One dependency level of an MT19937 twist of mt (in place, one wave). The
+// sequential in-place recurrence new[kk] = f(old[kk], old[kk+1], src) reads src
+// = old[kk+397] for kk < 227 and new[kk-227] above, so it has three levels: [0,
+// 227) from old words only, [227, 454) from level 1, [454, 624) from level 2
+// (word 623 also reads new[0]). Within a level every lane reads all its inputs
+// (up to 4 words a lane) before any lane writes, so no read sees a word of its
+// own level already replaced. Branch-free: a lane's slot past the level's end
+// computes from a clamped word and writes its lane's dummy word instead.
+template <int LEV>
+__device__ __forceinline__ void rb_twist_level(uint32_t* mt, uint32_t* dummy) {
     constexpr uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, A = 0x9908b0dfu;
+    constexpr int lo = LEV == 0 ? 0 : LEV == 1 ? 227 : 454;
+    constexpr int hi = LEV == 0 ? 227 : LEV == 1 ? 454 : 624;
+    constexpr int NJ = (hi - lo + 63) / 64;
     const int lane = lane_id();
-    uint32_t nv[4];
+    uint32_t nv[NJ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int kk = lo + lane + 64 * j;
-        nv[j] = 0;
-        if (kk < hi) {
-            const uint32_t nxt = mt[kk == 623 ? 0 : kk + 1];
-            const uint32_t y = (mt[kk] & UPPER) | (nxt & LOWER);
-            const uint32_t src = kk < 227 ? mt[kk + 397] : mt[kk - 227];
-            nv[j] = src ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
-        }
+    for (int j = 0; j < NJ; ++j) {
+        int kk = lo + lane + 64 * j;
+        if (lo + 64 * j + 63 >= hi) kk = min(kk, hi - 1);   // (compile-time: the level's last, partial slot)
+        const uint32_t nxt = mt[LEV == 2 && kk == 623 ? 0 : kk + 1];
+        const uint32_t y = (mt[kk] & UPPER) | (nxt & LOWER);
+        const uint32_t src = LEV == 0 ? mt[kk + 397] : mt[kk - 227];
+        nv[j] = src ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
     }
     rb_wave_lds_sync();   // every read of this level before any write of it
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
         const int kk = lo + lane + 64 * j;
-        if (kk < hi) mt[kk] = nv[j];
+        uint32_t* dst = (lo + 64 * j + 63 < hi || kk < hi) ? &mt[kk] : &dummy[lane];
+        *dst = nv[j];
     }
     rb_wave_lds_sync();   // the next level reads this one's words
 }
@@ -335,9 +347,9 @@ struct RbStream {   // wave 0's view of the frame's output stream (uniform)
 template <class IdxT>
 __device__ __forceinline__ void rb_advance(RansacShared<IdxT>& sh, RbStream& st, uint32_t span) {
     while (st.pos + span > st.G()) {
-        const int lo = st.lev == 0 ? 0 : st.lev == 1 ? 227 : 454;
-        const int hi = st.lev == 0 ? 227 : st.lev == 1 ? 454 : 624;
-        rb_twist_level(sh.mt, lo, hi);
+        if (st.lev == 0) rb_twist_level<0>(sh.mt, sh.dummy);
+        else if (st.lev == 1) rb_twist_level<1>(sh.mt, sh.dummy);
+        else rb_twist_level<2>(sh.mt, sh.dummy);
         if (++st.lev == 3) {
             st.lev = 0;
             ++st.T;
@@ -366,7 +378,7 @@ __device__ void rb_draw_below(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
     while (got < m && st.pos < kRBMaxDraws) {
         rb_advance(sh, st, 64u);
         const uint32_t r = rb_word(sh, st.pos + lane) >> (32 - kb);
-        uint64_t acc = __ballot(r < n);
+        uint64_t acc = rb_ballot(r < n);
         int last = 63;
         while (acc && got < m) {
             const int l = __builtin_ctzll(acc);
@@ -395,7 +407,7 @@ __device__ void rb_draw_below(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
 constexpr int kRBWin = SVX_RB_WIN;
 static_assert(kRBWin >= 1 && 64 * kRBWin <= 397, "a round's draws must fit the MT state (RbStream)");
 
-template <class IdxT>
+template <class IdxT, bool TR>
 __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, int kb, int k, IdxT* idx,
                               int32_t* tr) {
     const int lane = lane_id();
@@ -426,27 +438,27 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
         for (int w = 0; w < kRBWin; ++w) {
             const bool acc = r[w] < n;
             const uint32_t bit = 1u << (r[w] & 31);
-            uint64_t hm = __ballot(acc && (old[w] & bit));
+            uint64_t hm = rb_ballot(acc && (old[w] & bit));
             uint64_t rej = hm;
             while (hm) {   // rare
                 const int l = __builtin_ctzll(hm);
                 const uint32_t v = __builtin_amdgcn_readlane(r[w], l);   // uniform lane: no LDS round trip
-                const uint64_t eq = __ballot(acc && r[w] == v);
-                const uint64_t fresh = __ballot(acc && r[w] == v && !(old[w] & bit));
+                const uint64_t eq = rb_ballot(acc && r[w] == v);
+                const uint64_t fresh = rb_ballot(acc && r[w] == v && !(old[w] & bit));
                 hm &= ~eq;
                 rej = fresh ? ((rej & ~eq) | (eq & (eq - 1))) : (rej | eq);
             }
             const bool sel = acc && !((rej >> lane) & 1ull);
-            const uint64_t sm = __ballot(sel);
+            const uint64_t sm = rb_ballot(sel);
             const int q = q0 + (int)__builtin_popcountll(sm & ((1ull << lane) - 1));
             if (sel) {
                 if (q < k) {
-                    if (!(sh.ablate & 64)) idx[q] = (IdxT)r[w];
-                    if (tr) tr[q] = (int32_t)r[w];
+                    idx[q] = (IdxT)r[w];
+                    if (TR && tr) tr[q] = (int32_t)r[w];
                 }
                 else atomicAnd(&sh.bitmap[r[w] >> 5], ~bit);
             }
-                const uint64_t lastm = __ballot(sel && q == k - 1);
+                const uint64_t lastm = rb_ballot(sel && q == k - 1);
             if (lastm) consumed = 64u * w + (uint32_t)__builtin_ctzll(lastm) + 1u;
             q0 += (int)__builtin_popcountll(sm);
         }
@@ -454,13 +466,14 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
         st.pos += consumed;
         rb_wave_lds_sync();   // the next round reads bits set/cleared by other lanes
     }
-    // clear the sample's bits (the whole bitmap: a few words a lane)
-    for (uint32_t q = lane; q < (n + 31) / 32; q += kWave) sh.bitmap[q] = 0;
+    // clear the sample's bits (the whole bitmap, 16 bytes a store: the launch rounds it to 4 words)
+    uint4* b4 = reinterpret_cast<uint4*>(sh.bitmap);
+    for (uint32_t q = lane; q < (n + 127) / 128; q += kWave) b4[q] = make_uint4(0u, 0u, 0u, 0u);
     rb_wave_lds_sync();
 }
 
 // wave 0, lane 0 drives: random.sample(range(n), k), pool branch (n <= setsize)
-template <class IdxT>
+template <class IdxT, bool TR>
 __device__ void rb_sample_pool(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, int k, IdxT* idx, int32_t* tr) {
     const int lane = lane_id();
     for (uint32_t q = lane; q < n; q += kWave) sh.pool[q] = (int32_t)q;
@@ -472,7 +485,7 @@ __device__ void rb_sample_pool(RansacShared<IdxT>& sh, RbStream& st, uint32_t n,
         rb_draw_below(sh, st, bound, kb, 1, &j);
         if (lane == 0) {
             idx[i] = (IdxT)sh.pool[j];
-            if (tr) tr[i] = sh.pool[j];
+            if (TR && tr) tr[i] = sh.pool[j];
             sh.pool[j] = sh.pool[n - i - 1];
         }
     }
@@ -511,7 +524,7 @@ __device__ __forceinline__ void rb_solve_record(const double* r1, const double* 
     o[4] = fl;
 }
 
-template <class IdxT>
+template <class IdxT, bool TR>
 __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restrict__ packed, RbTables tb, int64_t cap,
                                                          const int64_t* __restrict__ counts, uint64_t seed_base,
                                                          int64_t first_frame, int trials, int k,
@@ -520,7 +533,8 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
                                                          int trace_trials, int bitmap_words, int ablate) {
     __shared__ uint32_t mt[624];
     __shared__ uint32_t dummy[64];
-    extern __shared__ uint32_t rb_dyn[];   // [bitmap_words] bitmap / pool list
+    extern __shared__ uint4 rb_dyn4[];   // [bitmap_words] bitmap / pool list (16-byte aligned, 4-word multiple)
+    uint32_t* rb_dyn = reinterpret_cast<uint32_t*>(rb_dyn4);
     RansacShared<IdxT> sh;
     sh.mt = mt;
     sh.bitmap = rb_dyn;
@@ -546,15 +560,16 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
     if (lane == 0) rb_seed(sh.mt, seed_base + (uint64_t)(first_frame + frame));
     __syncthreads();   // one wave: orders lane 0's seeding before every lane's reads
     RbStream st{0, 0, 0};
+    const int g_pt = lane % 3, g_co = min(lane / 3, 2);   // the triple gather: point, coordinate (rb_point's tables)
     int status = 0, s = 0;
     for (; s < trials; ++s) {
         IdxT* idx = sidx + ((int64_t)frame * trials + s) * k;
-        int32_t* tr = s < trace_trials ? trace + ((int64_t)frame * trace_trials + s) * (k + 3) : nullptr;
+        int32_t* tr = TR && s < trace_trials ? trace + ((int64_t)frame * trace_trials + s) * (k + 3) : nullptr;
         if (ablate & 16) {   // DIAGNOSTIC: no sample
         } else if (pool) {
-            rb_sample_pool(sh, st, n, k, idx, tr);
+            rb_sample_pool<IdxT, TR>(sh, st, n, k, idx, tr);
         } else {
-            rb_sample_set(sh, st, n, kb, k, idx, tr);
+            rb_sample_set<IdxT, TR>(sh, st, n, kb, k, idx, tr);
         }
         uint32_t t3[3] = {0, 0, 0};
         double p1[3], p2[3], p3[3];   // the triple's fp64 points (rb_point: the reference's X, Y, Z)
@@ -566,9 +581,17 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
                 break;
             }
             rb_draw_below(sh, st, n, kb, 3, t3);
-            rb_point(fpk[t3[0]], tb, p1[0], p1[1], p1[2]);
-            rb_point(fpk[t3[1]], tb, p2[0], p2[1], p2[2]);
-            rb_point(fpk[t3[2]], tb, p3[0], p3[1], p3[2]);
+            // lane 3 c + i (< 9) gathers coordinate c of point i: one load of the packed words, one of the
+            // tables (two memory round trips); every lane then takes the nine values from lanes 0..8
+            const uint32_t pk = fpk[g_pt == 0 ? t3[0] : g_pt == 1 ? t3[1] : t3[2]];
+            const uint32_t x2 = (pk & 0xFFF) >> 1, y2 = ((pk >> 12) & 0xFFF) >> 1, dd = pk >> 24;
+            const double v = g_co == 0 ? tb.X[x2 * 256 + dd] : g_co == 1 ? tb.Y[y2 * 256 + dd] : tb.Z[dd];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                p1[c] = rb_readlane_f64(v, 3 * c + 0);
+                p2[c] = rb_readlane_f64(v, 3 * c + 1);
+                p3[c] = rb_readlane_f64(v, 3 * c + 2);
+            }
         } while (st.pos < kRBMaxDraws && !(ablate & 8) && rb_collinear(p1, p2, p3));
         if (st.pos >= kRBMaxDraws) {
             status = 2;
@@ -578,7 +601,7 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
             status = 1;
             break;
         }
-        if (tr && lane < 3) tr[k + lane] = (int32_t)(lane == 0 ? t3[0] : lane == 1 ? t3[1] : t3[2]);
+        if (TR && tr && lane < 3) tr[k + lane] = (int32_t)(lane == 0 ? t3[0] : lane == 1 ? t3[1] : t3[2]);
         if (lane < 3) {   // the triple (the eval kernel solves its plane, off this chain)
             uint32_t* trip = reinterpret_cast<uint32_t*>(tri + ((int64_t)frame * trials + s) * kRBTri);
             trip[lane] = lane == 0 ? t3[0] : lane == 1 ? t3[1] : t3[2];
@@ -641,65 +664,34 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
     }
     // screen every trial in fp32 (one wave a trial): the mean distance from the
     // packed points and, per point, the bound (|Xa| + |Yb| + |Zc| + 1) 2^-18 / |abc|
-    // on its difference to the fp64 distance (fp32 X, Y, Z within 2^-21 relative,
-    // fp32 a, b, c and two fmas); sums in fp64
+    // on its difference to the fp64 distance. A term's error: fp32 X, Y, Z within
+    // 2^-21 relative, a, b, c rounded to fp32, a product and two fmas, the -1:
+    // <= (T + 1) 2^-20.33 (T = |Xa| + |Yb| + |Zc|); a lane's fp32 sum of <= 10
+    // terms adds <= 9 x 2^-24 of them, <= (T + 1) 2^-20.83 each: together
+    // <= (T + 1) 2^-19.55, under the bound's 2^-18 (computed in fp32 as well: it
+    // is low by at most ~2^-19.3 relative) with a margin of ~2.9x. The lanes'
+    // sums are added in fp64.
     if (!(ablate & 1)) {
         // software-pipelined over the wave's trials: the next trial's indices and
         // record are loaded (global, just written by the draw kernel) while this
         // trial's points are gathered from LDS
         constexpr int NW = kRBEvalThreads / 64;
-        auto load = [&](int t, uint32_t (&ix)[kRBGather], double (&rec)[kRBTri]) {
-            const IdxT* idx = fidx + (int64_t)t * k;
-#pragma unroll
-            for (int v = 0; v < kRBGather; ++v) {
-                const int j = lane + kWave * v;
-                ix[v] = j < k ? (uint32_t)idx[j] : 0u;
-            }
-#pragma unroll
-            for (int q = 0; q < kRBTri; ++q) rec[q] = ftri[(int64_t)t * kRBTri + q];
+        // one point's fp32 distance term and bound term, summed per lane in fp32 (at most 10 terms a lane per
+        // batch; the batches and the lanes in fp64): the sum's rounding, <= 9 x 2^-24 of the summed terms, stays
+        // inside the bound's margin (see the note at the eval kernel)
+        const auto point = [&](uint32_t u, float a, float b, float c, float fa, float fb, float fc, float& sum,
+                               float& bnd) {
+            const int x = (int)(u & 0xFFF), y = (int)((u >> 12) & 0xFFF);
+            const float rr = __builtin_amdgcn_rcpf((float)(u >> 24));
+            const float K = cp.B32 * rr;
+            const float X = centred(x, cp.cw_hi, cp.cw_lo) * K;
+            const float Y = centred(y, cp.ch_hi, cp.ch_lo) * K;
+            const float Z = cp.fB32 * rr;
+            const float dot = __builtin_fmaf(Z, c, __builtin_fmaf(X, a, Y * b));
+            sum += __builtin_fabsf(dot - 1.0f);
+            bnd += __builtin_fmaf(fa, __builtin_fabsf(X), __builtin_fmaf(fb, __builtin_fabsf(Y), fc * Z)) + 1.0f;
         };
-        uint32_t nix[kRBGather];
-        double nrec[kRBTri];
-        if (wave < T) load(wave, nix, nrec);
-        for (int t = wave; t < T; t += NW) {
-            uint32_t ix[kRBGather];
-            double rec[kRBTri];
-#pragma unroll
-            for (int v = 0; v < kRBGather; ++v) ix[v] = nix[v];
-#pragma unroll
-            for (int q = 0; q < kRBTri; ++q) rec[q] = nrec[q];
-            if (t + NW < T) load(t + NW, nix, nrec);
-            double sum = 0.0, bnd = 0.0;
-            if (rec[4] != 1.0) {
-                const float a = (float)rec[0], b = (float)rec[1], c = (float)rec[2];
-                const float fa = __builtin_fabsf(a), fb = __builtin_fabsf(b), fc = __builtin_fabsf(c);
-                for (int j0 = lane, g = 0; j0 < k; j0 += kRBGather * kWave, ++g) {
-                    uint32_t u[kRBGather];
-                    if (g > 0) {   // k > 640: the rest of the sample (same order as the first batch)
-#pragma unroll
-                        for (int v = 0; v < kRBGather; ++v) {
-                            const int j = j0 + kWave * v;
-                            ix[v] = j < k ? (uint32_t)fidx[(int64_t)t * k + j] : 0u;
-                        }
-                    }
-#pragma unroll
-                    for (int v = 0; v < kRBGather; ++v) u[v] = P[ix[v]];
-#pragma unroll
-                    for (int v = 0; v < kRBGather; ++v) {
-                        if (j0 + kWave * v >= k) continue;
-                        const int x = (int)(u[v] & 0xFFF), y = (int)((u[v] >> 12) & 0xFFF);
-                        const float rr = __builtin_amdgcn_rcpf((float)(u[v] >> 24));
-                        const float K = cp.B32 * rr;
-                        const float X = centred(x, cp.cw_hi, cp.cw_lo) * K;
-                        const float Y = centred(y, cp.ch_hi, cp.ch_lo) * K;
-                        const float Z = cp.fB32 * rr;
-                        const float dot = __builtin_fmaf(Z, c, __builtin_fmaf(X, a, Y * b));
-                        sum += (double)__builtin_fabsf(dot - 1.0f);
-                        bnd += (double)(__builtin_fmaf(fa, __builtin_fabsf(X),
-                                                       __builtin_fmaf(fb, __builtin_fabsf(Y), fc * Z)) + 1.0f);
-                    }
-                }
-            }
+        const auto finish = [&](int t, const double (&rec)[kRBTri], double sum, double bnd) {
 #pragma unroll
             for (int o = kWave / 2; o > 0; o >>= 1) {
                 sum += __shfl_xor(sum, o, kWave);
@@ -709,6 +701,56 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
                 const double d = rec[3];
                 scr[2 * t] = sum / (d * k);
                 scr[2 * t + 1] = rec[4] == 1.0 ? -1.0 : bnd * 0x1p-18 / (d * k);
+            }
+        };
+        {
+            auto load = [&](int t, uint32_t (&ix)[kRBGather], double (&rec)[kRBTri]) {
+                const IdxT* idx = fidx + (int64_t)t * k;
+#pragma unroll
+                for (int v = 0; v < kRBGather; ++v) {
+                    const int j = lane + kWave * v;
+                    ix[v] = j < k ? (uint32_t)idx[j] : 0u;
+                }
+#pragma unroll
+                for (int q = 0; q < kRBTri; ++q) rec[q] = ftri[(int64_t)t * kRBTri + q];
+            };
+            uint32_t nix[kRBGather];
+            double nrec[kRBTri];
+            if (wave < T) load(wave, nix, nrec);
+            for (int t = wave; t < T; t += NW) {
+                uint32_t ix[kRBGather];
+                double rec[kRBTri];
+#pragma unroll
+                for (int v = 0; v < kRBGather; ++v) ix[v] = nix[v];
+#pragma unroll
+                for (int q = 0; q < kRBTri; ++q) rec[q] = nrec[q];
+                if (t + NW < T) load(t + NW, nix, nrec);
+                double sum = 0.0, bnd = 0.0;
+                if (rec[4] != 1.0) {
+                    const float a = (float)rec[0], b = (float)rec[1], c = (float)rec[2];
+                    const float fa = __builtin_fabsf(a), fb = __builtin_fabsf(b), fc = __builtin_fabsf(c);
+                    for (int j0 = lane, g = 0; j0 < k; j0 += kRBGather * kWave, ++g) {
+                        uint32_t u[kRBGather];
+                        float s32 = 0.0f, b32 = 0.0f;
+                        if (g > 0) {   // k > 640: the rest of the sample (same order as the first batch)
+#pragma unroll
+                            for (int v = 0; v < kRBGather; ++v) {
+                                const int j = j0 + kWave * v;
+                                ix[v] = j < k ? (uint32_t)fidx[(int64_t)t * k + j] : 0u;
+                            }
+                        }
+#pragma unroll
+                        for (int v = 0; v < kRBGather; ++v) u[v] = P[ix[v]];
+#pragma unroll
+                        for (int v = 0; v < kRBGather; ++v) {
+                            if (j0 + kWave * v >= k) continue;
+                            point(u[v], a, b, c, fa, fb, fc, s32, b32);
+                        }
+                        sum += (double)s32;
+                        bnd += (double)b32;
+                    }
+                }
+                finish(t, rec, sum, bnd);
             }
         }
     } else {
@@ -749,10 +791,10 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
             bool c = in && !singular && !(e32 - eb > ex * (1.0 + 2e-9));   // NaN / inf: a candidate
             if (ablate & 4) c = in && !singular;
             if (ablate & 1) c = false;                                     // DIAGNOSTIC 1: no evaluation
-            const uint64_t m = __ballot(c);
+            const uint64_t m = rb_ballot(c);
             if (c) cand[nc + __builtin_popcountll(m & ((1ull << lane) - 1))] = t;
             nc += (uint32_t)__builtin_popcountll(m);
-            sing |= __ballot(singular) != 0 ? 1u : 0u;
+            sing |= rb_ballot(singular) != 0 ? 1u : 0u;
             carry = fmin(carry, __shfl(inc, kWave - 1, kWave));
         }
         if (lane == 0) {
@@ -832,9 +874,14 @@ static hipError_t launch_ransac_typed(const uint32_t* packed, const RbTables& tb
                                       double* abc, double* err, int32_t* trial, uint32_t* flags, int32_t* trace,
                                       int trace_trials, int ablate, hipStream_t s) {
     IdxT* sidx = reinterpret_cast<IdxT*>(rs.sidx);
-    hipLaunchKernelGGL(ransac_draw_kernel<IdxT>, dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words, s,
-                       packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace,
-                       trace ? trace_trials : 0, (int)words, ablate);
+    if (trace)
+        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, true>), dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words,
+                           s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace,
+                           trace_trials, (int)words, ablate);
+    else
+        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, false>), dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words,
+                           s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat,
+                           nullptr, 0, (int)words, ablate);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ablate & (8 | 16)) ablate |= 1;   // DIAGNOSTIC: no samples / planes drawn -> no evaluation of them
@@ -877,6 +924,7 @@ hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H,
     int64_t words = (max_n + 31) / 32;
     if (max_pool_n > words) words = max_pool_n;
     if (words < 1) words = 1;
+    words = (words + 3) & ~3ll;   // the bitmap is cleared 4 words a store
     // the samples as u16 indices when every frame has < 65536 points
     if (max_n <= 65535)
         return launch_ransac_typed<uint16_t>(packed, rb_tables(tab, H, W), cap, cp, counts, max_n, words, seed_base,
