@@ -9,3 +9,6 @@ python3 tools/prof.py pmc --groups "FETCH_SIZE;WRITE_SIZE" --out "$OUT/pmc_k1" -
 python3 tools/prof.py pmc --groups "FETCH_SIZE;WRITE_SIZE" --out "$OUT/pmc_pipe" --traffic 4096 -- --what pipe --frames 4096 --reps 1 || exit $?
 python3 tools/prof.py pmc --groups "FETCH_SIZE;WRITE_SIZE" --out "$OUT/pmc_planes" --traffic 4096 -- --what planes --frames 4096 --reps 1 || exit $?
 cat "$OUT/pmc_k1/traffic.json" "$OUT/pmc_pipe/traffic.json" "$OUT/pmc_planes/traffic.json"
+# HBM bytes per kernel of the SGBM stage (128 frames, one chunk) and of the batched RANSAC (4096 frames)
+python3 tools/prof.py pmc --groups "FETCH_SIZE;WRITE_SIZE" --out "$OUT/pmc_sgbm" -- --what sgbm --frames 128 --reps 1 > "$OUT/pmc_sgbm.txt" || exit $?
+python3 tools/prof.py pmc --groups "FETCH_SIZE;WRITE_SIZE" --out "$OUT/pmc_ransac" -- --what ransac --frames 4096 --reps 1 > "$OUT/pmc_ransac.txt" || exit $?

@@ -212,7 +212,7 @@ def _load_pmc(root):
     files = set(glob.glob(f"{root}/**/run_counter_collection.csv", recursive=True))
     for f in sorted(files):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)", "anon").split("(")[0].replace("void ", "")
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return acc
 
