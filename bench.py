@@ -318,8 +318,11 @@ def extras(b, args, with_cpu, first=0):
     mask = carmask()
     b.set_mask(mask)
     ms = _timed(b, lambda: b.prepass("previous", sync=False), 3)
-    ex["prepass_fill_previous_masked"] = {"ms_per_batch": round(ms, 3), "GBps": round(3 * px / ms / 1e6, 1),
-                                          "bytes_per_pixel": 3, "kernel": "fill_prev_kernel"}
+    # fillDisparity's recurrence: the disparity read, the cleaned frame written in place (maskDisparity is applied
+    # by maskpoints as it reads the cleaned frame, not materialised)
+    ex["prepass_fill_previous"] = {"ms_per_batch": round(ms, 3), "GBps": round(2 * px / ms / 1e6, 1),
+                                   "bytes_per_pixel": 2, "kernel": "fill_prev_kernel",
+                                   "mask": "carmask applied inside maskpoints_kernel"}
     # the per-frame-plane workload below is pinned end to end (tests/golden/plane_digests.npz): fresh frames,
     # ONE pre-pass over the batch in frame order (the timing above cleaned them four times), RANSAC with
     # random.seed(F), the pipeline with each frame's plane

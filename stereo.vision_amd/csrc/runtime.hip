@@ -256,7 +256,7 @@ struct sv_batch {
     DevBuf oxb, oyb, ozb;       // pipeline X, Y, Z: three planes of frames x cap (default; SoA in xyz: A/B)
     bool out_planes = false;
     bool pipe_placed = false;   // the resident pipeline's outputs were placed (pipe_place)
-    DevBuf mdisp, carmask;      // pre-pass: masked disparity (frames x H x W), 0x00/0xFF mask (H x W)
+    DevBuf carmask;             // maskDisparity's 0x00/0xFF mask (H x W)
     DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
     bool nz_fresh = false;      // nz holds the walk of the current road images (road_kernel wrote both)
     DevBuf rmap;                // imageRoadMap (stereovision.py:131-133): frames x H x W x 3, on request
@@ -521,7 +521,7 @@ int sv_batch_destroy(sv_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppx, &b->ppy, &b->ctrl, &b->masks,
-                      &b->mdisp, &b->carmask, &b->road, &b->rmap, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtab, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
+                      &b->carmask, &b->road, &b->rmap, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtab, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
                       &b->glut, &b->ghist, &b->sgflags})
         if (x->p) (void)hipFree(x->p);
@@ -1146,12 +1146,11 @@ int sv_batch_prepass(sv_batch* b, int option, const uint8_t* prev0, int sync) {
     if (option < 0 || option > 2) return fail(SV_E_ARG, "prepass option must be 0 (none), 1 (previous) or 2 (mean)");
     HIP_TRY(hipSetDevice(b->device));
     const int64_t px = (int64_t)b->H * b->W;
+    // maskDisparity (functions.py:169-172) is not materialised: its only consumer on the device, maskpoints, applies
+    // the mask as it reads the cleaned disparity (the fill pass moves 2 B a pixel, not 3); sv_batch_read_disp
+    // applies it to the frame it reads back
     uint8_t* masked = nullptr;
-    const uint8_t* mff = b->have_mask ? b->carmask.as<uint8_t>() : nullptr;
-    if (b->have_mask) {
-        HIP_TRY(b->mdisp.ensure((size_t)px * b->frames));
-        masked = b->mdisp.as<uint8_t>();
-    }
+    const uint8_t* mff = nullptr;
     uint8_t* disp = b->disp.as<uint8_t>();
     if (option == 1) {
         const uint8_t* p0 = nullptr;
@@ -1166,8 +1165,6 @@ int sv_batch_prepass(sv_batch* b, int option, const uint8_t* prev0, int sync) {
         HIP_TRY(launch_fill_prev(disp, disp, masked, mff, p0, b->frames, px, b->stream));
     } else if (option == 2) {
         HIP_TRY(launch_fill_mean(disp, masked, mff, b->frames, b->H, b->W, b->Wu, b->stream));
-    } else if (masked) {
-        HIP_TRY(launch_mask(disp, masked, mff, b->frames, px, b->stream));
     }
     if (sync || prev0) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
@@ -1175,14 +1172,23 @@ int sv_batch_prepass(sv_batch* b, int option, const uint8_t* prev0, int sync) {
 
 int sv_batch_read_disp(sv_batch* b, int frame, uint8_t* disp, uint8_t* masked) {
     if (!b || frame < 0 || frame >= b->frames) return fail(SV_E_ARG, "bad args");
-    if (masked && !b->mdisp.p) return fail(SV_E_STATE, "no masked disparity (set a mask and run the pre-pass)");
+    if (masked && !b->have_mask) return fail(SV_E_STATE, "no masked disparity (set a mask first)");
     HIP_TRY(hipSetDevice(b->device));
-    HIP_TRY(hipStreamSynchronize(b->stream));
     const size_t px = (size_t)b->H * b->W;
+    uint8_t* mframe = nullptr;
+    if (masked) {   // maskDisparity of this frame (the batch does not hold masked copies)
+        Device* d;
+        if (int rc = dev_get(b->device, &d)) return rc;
+        HIP_TRY(d->aux.ensure(px));
+        mframe = d->aux.as<uint8_t>();
+        HIP_TRY(launch_mask(b->disp.as<uint8_t>() + px * frame, mframe, b->carmask.as<uint8_t>(), 1, (int64_t)px,
+                            b->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(b->stream));
     if (disp)
         HIP_TRY(hipMemcpy2D(disp, b->Wu, b->disp.as<uint8_t>() + px * frame, b->W, b->Wu, b->H, hipMemcpyDeviceToHost));
     if (masked)
-        HIP_TRY(hipMemcpy2D(masked, b->Wu, b->mdisp.as<uint8_t>() + px * frame, b->W, b->Wu, b->H,
+        HIP_TRY(hipMemcpy2D(masked, b->Wu, mframe, b->W, b->Wu, b->H,
                             hipMemcpyDeviceToHost));
     return SV_OK;
 }
