@@ -398,8 +398,8 @@ __device__ void rb_draw_below(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
 // an index selected earlier (rejected) or a value drawn twice in the same
 // window, resolved by ballots: if some lane saw the bit clear, the value is new
 // and its lowest lane (earliest draw) wins, otherwise every lane drawing it is
-// rejected. The k-th selection in stream order ends the sample; bits claimed
-// past it are released and the stream resumes right after it.
+// rejected. The k-th selection in stream order ends the sample and the stream
+// resumes right after it (bits claimed past it stay: the bitmap is cleared).
 // 192 draws a round; a round must fit the state's 624 positions (RbStream): span <= 397, i.e. up to 6 windows
 #ifndef SVX_RB_WIN
 #define SVX_RB_WIN 3
@@ -430,8 +430,8 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
             old[w] = atomicOr(a, acc ? 1u << (r[w] & 31) : 0u);
         }
         // Selections are numbered in stream order from `have`; number q < k is the
-        // sample's q-th pick, q >= k was drawn past the sample's end (its claim is
-        // released). The pick numbered k - 1 fixes where the stream resumes.
+        // sample's q-th pick, q >= k was drawn past the sample's end. The pick
+        // numbered k - 1 fixes where the stream resumes.
         uint32_t consumed = 64u * kRBWin;
         int q0 = have;
 #pragma unroll
@@ -451,16 +451,18 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
             const bool sel = acc && !((rej >> lane) & 1ull);
             const uint64_t sm = rb_ballot(sel);
             const int q = q0 + (int)__builtin_popcountll(sm & ((1ull << lane) - 1));
-            if (sel) {
-                if (q < k) {
-                    idx[q] = (IdxT)r[w];
-                    if (TR && tr) tr[q] = (int32_t)r[w];
-                }
-                else atomicAnd(&sh.bitmap[r[w] >> 5], ~bit);
+            // picks numbered >= k keep their claims: no later draw of this sample can see them (they are
+            // past its end in stream order) and the whole bitmap is cleared after the sample
+            if (sel && q < k) {
+                idx[q] = (IdxT)r[w];
+                if (TR && tr) tr[q] = (int32_t)r[w];
             }
+            const int nsel = (int)__builtin_popcountll(sm);
+            if (q0 < k && q0 + nsel >= k) {   // (uniform) the sample's last pick is in this window
                 const uint64_t lastm = rb_ballot(sel && q == k - 1);
-            if (lastm) consumed = 64u * w + (uint32_t)__builtin_ctzll(lastm) + 1u;
-            q0 += (int)__builtin_popcountll(sm);
+                consumed = 64u * w + (uint32_t)__builtin_ctzll(lastm) + 1u;
+            }
+            q0 += nsel;
         }
         have = q0 < k ? q0 : k;
         st.pos += consumed;
