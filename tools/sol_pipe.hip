@@ -107,19 +107,27 @@ __global__ __launch_bounds__(256) void sol_kernel(Args a) {
     uint32_t acc = 0;
     const float v = (float)f;
     if (a.mode >= 13) {
+        // 23 / 24: as 13 / 18 (K = 1) with pass 2 walking the chunks last to first (what pass 1 read last is
+        // re-read first, while it may still be cached); 25 / 26: pass 1 + the re-read only (no writes),
+        // first to last / last to first
         const int K = a.kgroup, n = 64;
+        const bool rev = a.mode == 23 || a.mode == 24 || a.mode == 26;
+        const bool nowr = a.mode >= 25;
         acc ^= read_range(a, f, 0, a.px16);   // pass 1
         __shared__ int64_t base13;
-        if (threadIdx.x == 0) base13 = a.mode <= 17 ? (int64_t)atomicAdd(a.counter, (unsigned long long)a.kept)
+        if (threadIdx.x == 0)
+            base13 = (a.mode <= 17 || a.mode == 23) ? (int64_t)atomicAdd(a.counter, (unsigned long long)a.kept)
                                                     : (int64_t)f * a.cap;
         __syncthreads();
         const uint4* d = a.disp + f * a.px16;
-        for (int c0 = 0; c0 < n; c0 += K) {
+        for (int cc = 0; cc < n; cc += K) {
+            const int c0 = rev ? n - K - cc : cc;
             for (int c = c0; c < c0 + K; ++c)
                 for (int64_t w = a.px16 * c / n + threadIdx.x; w < a.px16 * (c + 1) / n; w += 256) {
                     const uint4 x = *(d + w);
                     acc ^= x.x ^ x.w;
                 }
+            if (nowr) continue;
             const int64_t g0 = (a.kept / 4 * c0 / n) * 4, g1 = (a.kept / 4 * (c0 + K) / n) * 4;
             for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
                 const v4f q = {v, v, v, v};
@@ -213,14 +221,17 @@ int main(int argc, char** argv) {
                            "pass1 + K-grouped pass2, atomic regions", "pass1 + K-grouped pass2, atomic regions",
                            "pass1 + K-grouped pass2, strided", "pass1 + K-grouped pass2, strided",
                            "pass1 + K-grouped pass2, strided", "pass1 + K-grouped pass2, strided",
-                           "pass1 + K-grouped pass2, strided"};
+                           "pass1 + K-grouped pass2, strided", "pass1 + pass2 last chunk first, atomic regions",
+                           "pass1 + pass2 last chunk first, strided", "pass1 + re-read only, first chunk first",
+                           "pass1 + re-read only, last chunk first"};
     const int kgroups[5] = {1, 2, 4, 8, 64};
     const int64_t cap0 = cap - 64;
     for (int round = 0; round < 2; ++round)
-        for (int mode = 0; mode < 23; ++mode) {
-            if (round == 0 && mode < 13) continue;   // (the earlier modes: profiles/r02/sol_pipe_session8.txt)
+        for (int mode = 0; mode < 27; ++mode) {
+            if (mode < 13 || (mode > 13 && mode < 18) || (mode > 18 && mode < 23)) continue;   // (earlier results:
+                                                       // profiles/r02/sol_pipe_session8.txt, r03/sol_pipe_kgroup.txt)
             a.mode = mode;
-            a.kgroup = mode >= 13 ? kgroups[(mode - 13) % 5] : 1;
+            a.kgroup = mode >= 13 && mode <= 22 ? kgroups[(mode - 13) % 5] : 1;
             a.nplanes = 5;
             a.nper = kept;
             a.stride = cap0;
@@ -253,7 +264,7 @@ int main(int argc, char** argv) {
             }
             const double rd = ((mode == 3 || mode >= 5) && mode != 10 && mode < 12 ? 0. : 4. * px * frames) +
                               (mode == 4 || mode >= 13 ? 1. * px * frames : 0.);
-            const double wr = mode == 2 ? 0. : 20. * (mode == 11 ? cap0 : kept) * frames;
+            const double wr = (mode == 2 || mode >= 25) ? 0. : 20. * (mode == 11 ? cap0 : kept) * frames;
             std::printf("{\"round\": %d, \"mode\": %d, \"what\": \"%s\", \"K\": %d, \"GB\": %.2f, \"best_ms\": %.3f, "
                         "\"mean_ms\": %.3f, \"TBps_best\": %.2f}\n",
                         round, mode, names[mode], a.kgroup, (rd + wr) / 1e9, best, tot / reps, (rd + wr) / best / 1e9);
