@@ -168,3 +168,45 @@ def test_median3_matches_numpy():
     out = osg.sgbm(L, R)
     assert np.array_equal(out, median3_numpy(raw))
     assert (out != raw).mean() > 0.05   # the median changes a large share of a real frame
+
+
+@pytest.mark.parametrize("P1,P2,block", [(2, 5, 21), (8, 15, 9), (1, 15, 3), (4, 32, 5)])
+def test_path_minus_cost_in_p2_band(P1, P2, block):
+    """The identity behind the GPU's 4-bit direction volumes (kernels/sgbm.hip q_byte): every
+    path value OpenCV's recurrence produces is L = C + min(Lp(d), Lp(d +- 1) + P1, min Lp + P2) - (min Lp + P2),
+    so q = C - L is in [0, P2] in every direction, on random and textureless pairs alike, and the row walk's
+    P = sat16(L0 + L1 + L2 + L3) is sat16(4 C - (q0 + q1 + q2 + q3)) from 4-bit q's whenever P2 <= 15."""
+    import sgbm_numpy as sn
+    rng = np.random.default_rng(P2 * 100 + block)
+    H, W = 24, 200
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = np.roll(L, 7, axis=1) if P2 != 15 else rng.integers(0, 256, (H, W), dtype=np.uint8)
+    L[5:12, 40:90] = 77   # a textureless patch: flat path costs
+    C = sn.cost_volume(L, R, 128, 15, block // 2, block // 2)
+    w1 = W - 128
+    qs = []
+    for sh in (1, 0, -1):   # the three row-to-row directions
+        prev = np.zeros((w1, 128), np.int64)
+        pmin = np.zeros(w1, np.int64)
+        q = np.zeros((H, w1, 128), np.int64)
+        for y in range(H):
+            if y == 0:
+                p, pm = np.zeros_like(prev), np.zeros_like(pmin)
+            elif sh == 1:
+                p, pm = np.vstack([np.zeros((1, 128), np.int64), prev[:-1]]), np.concatenate([[0], pmin[:-1]])
+            elif sh == -1:
+                p, pm = np.vstack([prev[1:], np.zeros((1, 128), np.int64)]), np.concatenate([pmin[1:], [0]])
+            else:
+                p, pm = prev, pmin
+            Lv, prev, pmin = sn._step(C[y], p, pm, P1, P2)
+            q[y] = C[y] - Lv
+        qs.append(q)
+    prev = np.zeros((H, 128), np.int64)   # the row walk's own forward direction
+    pmin = np.zeros(H, np.int64)
+    q0 = np.zeros((H, w1, 128), np.int64)
+    for x in range(w1):
+        Lv, prev, pmin = sn._step(C[:, x], prev, pmin, P1, P2)
+        q0[:, x] = C[:, x] - Lv
+    qs.append(q0)
+    for q in qs:
+        assert q.min() >= 0 and q.max() <= P2, (q.min(), q.max())
