@@ -23,6 +23,9 @@
 //           disparity and writing, in groups of K = 1, 2, 4, 8, 64 chunks (K chunks' disparity reads, then
 //           their K chunks' writes), into a region taken from the counter after pass 1
 //   mode 18..22  the same with the frame-strided planes (no counter)
+//   mode 27..29  mode 18's shape (K = 1) with frame-interleaved tiles: output o of frame f at
+//           ((o / B) * frames + f) * B + o % B, B = 256, 1024, 4096 outputs (round 3, session 3)
+//   mode 30..32  writes only, the same three tiled layouts
 // argv: frames (4096), outputs per frame (277200), 1 = output planes physically contiguous (0)
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/_sol_pipe tools/sol_pipe.hip
 #include <hip/hip_runtime.h>
@@ -55,6 +58,8 @@ struct Args {
     int64_t nper;        // floats per plane per frame
     unsigned long long* counter;
     int kgroup;          // modes 13..22: chunks per read/write group
+    int lb;              // modes 27..32: log2 of the tile (outputs)
+    int frames;
 };
 
 __device__ __forceinline__ uint32_t read_range(const Args& a, int f, int64_t w0, int64_t w1) {
@@ -102,11 +107,37 @@ __global__ __launch_bounds__(256) void sweep_kernel(Args a, int64_t total) {   /
     }
 }
 
+__device__ __forceinline__ int64_t tiled(const Args& a, int f, int64_t g) {
+    return ((((g >> a.lb) * a.frames) + f) << a.lb) + (g & ((1 << a.lb) - 1));
+}
+
 __global__ __launch_bounds__(256) void sol_kernel(Args a) {
     const int f = blockIdx.x;
     uint32_t acc = 0;
     const float v = (float)f;
-    if (a.mode >= 13) {
+    if (a.mode >= 30) {
+        for (int64_t g = 4 * threadIdx.x; g < a.kept; g += 1024) {
+            const v4f q = {v, v, v, v};
+#pragma unroll
+            for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + tiled(a, f, g)));
+        }
+    } else if (a.mode >= 27) {
+        const int n = 64;
+        acc ^= read_range(a, f, 0, a.px16);   // pass 1
+        const uint4* d = a.disp + f * a.px16;
+        for (int c = 0; c < n; ++c) {
+            for (int64_t w = a.px16 * c / n + threadIdx.x; w < a.px16 * (c + 1) / n; w += 256) {
+                const uint4 x = *(d + w);
+                acc ^= x.x ^ x.w;
+            }
+            const int64_t g0 = (a.kept / 4 * c / n) * 4, g1 = (a.kept / 4 * (c + 1) / n) * 4;
+            for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
+                const v4f q = {v, v, v, v};
+#pragma unroll
+                for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + tiled(a, f, g)));
+            }
+        }
+    } else if (a.mode >= 13) {
         // 23 / 24: as 13 / 18 (K = 1) with pass 2 walking the chunks last to first (what pass 1 read last is
         // re-read first, while it may still be cached); 25 / 26: pass 1 + the re-read only (no writes),
         // first to last / last to first
@@ -223,16 +254,20 @@ int main(int argc, char** argv) {
                            "pass1 + K-grouped pass2, strided", "pass1 + K-grouped pass2, strided",
                            "pass1 + K-grouped pass2, strided", "pass1 + pass2 last chunk first, atomic regions",
                            "pass1 + pass2 last chunk first, strided", "pass1 + re-read only, first chunk first",
-                           "pass1 + re-read only, last chunk first"};
+                           "pass1 + re-read only, last chunk first", "pass1 + pass2, tiles of 256",
+                           "pass1 + pass2, tiles of 1024", "pass1 + pass2, tiles of 4096", "write: tiles of 256",
+                           "write: tiles of 1024", "write: tiles of 4096"};
     const int kgroups[5] = {1, 2, 4, 8, 64};
     const int64_t cap0 = cap - 64;
     for (int round = 0; round < 2; ++round)
-        for (int mode = 0; mode < 27; ++mode) {
-            if (mode < 13 || (mode > 13 && mode < 18) || (mode > 18 && mode < 23)) continue;   // (earlier results:
-                                                       // profiles/r02/sol_pipe_session8.txt, r03/sol_pipe_kgroup.txt)
+        for (int mode = 0; mode < 33; ++mode) {
+            // earlier results: profiles/r02/sol_pipe_session8.txt, r03/sol_pipe_kgroup.txt, r03/sol_pipe_reverse.txt
+            if (!(mode == 3 || mode == 5 || mode == 13 || mode == 18 || mode >= 27)) continue;
             a.mode = mode;
             a.kgroup = mode >= 13 && mode <= 22 ? kgroups[(mode - 13) % 5] : 1;
             a.nplanes = 5;
+            a.frames = frames;
+            a.lb = mode >= 27 ? (const int[]){8, 10, 12}[(mode - 27) % 3] : 0;
             a.nper = kept;
             a.stride = cap0;
             if (mode == 5) a.stride = kept;
@@ -262,9 +297,9 @@ int main(int argc, char** argv) {
                 best = ms < best ? ms : best;
                 tot += ms;
             }
-            const double rd = ((mode == 3 || mode >= 5) && mode != 10 && mode < 12 ? 0. : 4. * px * frames) +
-                              (mode == 4 || mode >= 13 ? 1. * px * frames : 0.);
-            const double wr = (mode == 2 || mode >= 25) ? 0. : 20. * (mode == 11 ? cap0 : kept) * frames;
+            const double rd = ((mode == 3 || mode >= 5) && mode != 10 && (mode < 12 || mode >= 30) ? 0. : 4. * px * frames) +
+                              ((mode == 4 || mode >= 13) && mode < 30 ? 1. * px * frames : 0.);
+            const double wr = (mode == 2 || (mode >= 25 && mode < 27)) ? 0. : 20. * (mode == 11 ? cap0 : kept) * frames;
             std::printf("{\"round\": %d, \"mode\": %d, \"what\": \"%s\", \"K\": %d, \"GB\": %.2f, \"best_ms\": %.3f, "
                         "\"mean_ms\": %.3f, \"TBps_best\": %.2f}\n",
                         round, mode, names[mode], a.kgroup, (rd + wr) / 1e9, best, tot / reps, (rd + wr) / best / 1e9);
