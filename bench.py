@@ -277,8 +277,10 @@ def dropin_chain(fmod, disp, bgr, reps=5):
 
 
 def check_plane_parity(b, first):
-    """The per-frame-plane loop's device digests vs tests/golden/plane_digests.npz (the oracle's pre-pass ->
-    maskpoints -> RANSAC(random.seed(F)) -> pipeline chain, make_plane_digests.py); (frames checked, mismatching)."""
+    """The per-frame-plane loop vs tests/golden/plane_digests.npz (the oracle's pre-pass -> maskpoints ->
+    RANSAC(random.seed(F)) -> pipeline chain, make_plane_digests.py): each frame's winning trial, its error and
+    plane bit for bit (numpy's rounding, functions.py:267-289) and its pipeline digests; (frames checked,
+    mismatching)."""
     if b.step != 1 or not os.path.exists(GOLDEN_PLANES):
         return 0, 0
     gold = np.load(GOLDEN_PLANES)["planes"]
@@ -290,6 +292,10 @@ def check_plane_parity(b, first):
     ok = got[:, 6] == 0
     for k, name in enumerate(DIGEST_FIELDS):
         ok &= got[:, k] == want[name].astype(np.uint64)
+    for f in range(n):
+        r = b.read_ransac(f)
+        ok[f] &= bool(r["trial"] == want["trial"][f] and r["err"] == want["err"][f] and
+                      np.array_equal(r["abc"].view(np.uint64), want["abc"][f].view(np.uint64)))
     return n, int((~ok).sum())
 
 

@@ -281,9 +281,10 @@ int sv_batch_read_road_map(sv_batch* b, int frame, uint8_t* out);
  * device, one workgroup per frame. Per frame: abc (the plane), err (its mean
  * distance), trial (the winning trial, -1 when fewer than k points: the
  * reference returns (None, None)), flags (1: a trial was singular and
- * skipped; 2: the winner's 3x3 system is ill-conditioned; 4: the runner-up's
- * error is within 1e-9 relative — only these frames can differ from numpy's
- * LAPACK-based choice; 8: every triple drawn in 65,536 attempts was collinear
+ * skipped; 2: unused since round 3; 4: the runner-up's error is within 1e-9
+ * relative, information only: planes, errors and the choice are computed with
+ * numpy's rounding — LAPACK dgesv + dot, gemv, pairwise mean — so abc, err and
+ * trial equal the reference's bit for bit; 8: every triple drawn in 65,536 attempts was collinear
  * — the reference never returns there — trial = -1; 16: more than 2^28
  * draws in one frame, trial = -1). Step-2 grids of
  * <= 163,840 points, frames up to 4096 x 4096; 1 <= k <= 1024. The call

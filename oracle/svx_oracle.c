@@ -166,6 +166,103 @@ void svo_point_errors(const double* xyz, int64_t n, int64_t ld, const double* ab
 }
 
 /* ------------------------------------------------------------------------
+ * RANSAC's plane and error with numpy's rounding — functions.py:267-275, :289.
+ *   abc = np.dot(np.linalg.inv([P1; P2; P3]), np.ones([3, 1]))
+ * numpy's inv is LAPACK dgesv(A, I) of its bundled OpenBLAS (0.3.29 here):
+ * dgetf2 (left-looking LU: pivot = the first largest |a|, the column below the
+ * pivot scaled by the pivot's reciprocal, update products rounded before they
+ * are subtracted, column 2's two-term update as one fma chain), then dgetrs
+ * (the permuted identity through trsm: unit-lower forward with fused
+ * multiply-subtracts; upper backward with the diagonal applied as a multiply by
+ * its reciprocal, row 2's update of rows 0 and 1 a rounded product); the dot
+ * with ones adds each row left to right. Returns 1 when a pivot is exactly 0
+ * (dgesv info > 0: numpy raises LinAlgError). The device's rb_solve_record is
+ * the same sequence. Pinned to numpy by tests/test_ransac_cpu.py.
+ * --------------------------------------------------------------------- */
+int svo_plane_lapack(const double* P1, const double* P2, const double* P3, double* abc) {
+    double m[3][3] = {{P1[0], P1[1], P1[2]}, {P2[0], P2[1], P2[2]}, {P3[0], P3[1], P3[2]}};
+    int perm[3] = {0, 1, 2};
+    int piv = 0;
+    for (int i = 1; i < 3; ++i)
+        if (fabs(m[i][0]) > fabs(m[piv][0])) piv = i;
+    if (piv) {
+        for (int c = 0; c < 3; ++c) { double t = m[0][c]; m[0][c] = m[piv][c]; m[piv][c] = t; }
+        int t = perm[0]; perm[0] = perm[piv]; perm[piv] = t;
+    }
+    const double u00 = m[0][0];
+    double l10 = m[1][0], l20 = m[2][0];
+    if (u00 != 0.0) { const double r = 1.0 / u00; l10 *= r; l20 *= r; }
+    double b1 = m[1][1] - l10 * m[0][1], b2 = m[2][1] - l20 * m[0][1];
+    double c1 = m[1][2], c2 = m[2][2];
+    if (fabs(b2) > fabs(b1)) {
+        double t = b1; b1 = b2; b2 = t;
+        t = l10; l10 = l20; l20 = t;
+        t = c1; c1 = c2; c2 = t;
+        int q = perm[1]; perm[1] = perm[2]; perm[2] = q;
+    }
+    const double u11 = b1;
+    double l21 = b2;
+    if (u11 != 0.0) l21 *= 1.0 / u11;
+    const double u01 = m[0][1], u02 = m[0][2];
+    const double u12 = c1 - l10 * u02;
+    const double u22 = c2 - fma(l21, u12, l20 * u02);
+    const double i00 = 1.0 / u00, i11 = 1.0 / u11, i22 = 1.0 / u22;
+    for (int c = 0; c < 3; ++c) {
+        double x0 = perm[0] == c, x1 = perm[1] == c, x2 = perm[2] == c;
+        x1 = fma(-x0, l10, x1);
+        x2 = fma(-x0, l20, x2);
+        x2 = fma(-x1, l21, x2);
+        x2 = x2 * i22;
+        x0 = x0 - u02 * x2;
+        x1 = x1 - u12 * x2;
+        x1 = x1 * i11;
+        x0 = fma(-x1, u01, x0);
+        x0 = x0 * i00;
+        if (c == 0) { abc[0] = x0; abc[1] = x1; abc[2] = x2; }
+        else { abc[0] += x0; abc[1] += x1; abc[2] += x2; }
+    }
+    return u00 == 0.0 || u11 == 0.0 || u22 == 0.0;
+}
+
+/* numpy's pairwise summation (numpy/_core/src/umath/loops_utils.h.src), as
+ * add.reduce runs it from the initial 0.0. */
+static double np_pairwise(const double* a, int64_t n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int64_t i = 0; i < n; ++i) r += a[i];
+        return r;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int64_t i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return np_pairwise(a, n2) + np_pairwise(a + n2, n - n2);
+}
+
+/* error = np.mean(abs((np.dot(T, abc) - 1) / d)), d = math.sqrt(a a + b b + c c)
+ * (functions.py:269-275, :289) over the n rows of T (stride ld): the gemv's dot as
+ * plane_dist's fma chain (one row is a (1, 3) x (3, 1) product, which numpy sends
+ * to ddot instead: x a first, then y b and z c fused in order), then numpy's
+ * pairwise sum / n. */
+double svo_ransac_err(const double* T, int64_t n, int64_t ld, const double* abc) {
+    const double nrm = plane_norm(abc);
+    double* t = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    for (int64_t i = 0; i < n; ++i) t[i] = plane_dist(T[i * ld], T[i * ld + 1], T[i * ld + 2], abc, nrm);
+    if (n == 1) t[0] = fabs((fma(T[2], abc[2], fma(T[1], abc[1], T[0] * abc[0])) - 1.0) / nrm);
+    const double s = np_pairwise(t, n);
+    free(t);
+    return s / (double)n;
+}
+
+/* ------------------------------------------------------------------------
  * a4: BGRtoHSVHue + colorsys.rgb_to_hsv — functions.py:73-78 (inputs are
  * numpy uint8 scalars). Key str(round(h,3)) <-> integer bin rint(h*1000):
  *   rc,gc,bc = (mx-c)/(mx-mn)   (fp64 true division of exact integers)

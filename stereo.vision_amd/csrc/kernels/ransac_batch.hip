@@ -16,18 +16,16 @@
 //      accepted draws, an LDS bitmap the already-selected indices, draws
 //      repeated inside one round resolved in lane = stream order), then the
 //      three sample(points, 1) draws and numpy's cross-product test
-//      (functions.py:240-260), redrawn while collinear, and abc from the
-//      adjugate in fp64. Writes every trial's sample and plane to memory.
+//      (functions.py:240-260), redrawn while collinear. Writes every trial's
+//      sample and triple to memory.
 //  * ransac_eval_kernel — one workgroup per frame: the frame's packed points
-//      staged in LDS; every trial screened in fp32 from LDS (one wave per
-//      trial, a rigorous bound to the fp64 mean), then the trials in order:
-//      those the screen cannot rule out evaluated in fp64 exactly (mean
-//      |P.abc - 1| / |abc| over the sample) and the first strict minimum
-//      kept (functions.py:289-293).
-//      The plane is the GPU's fp64 solve of the winning 3x3 system (within
-//      ~1e-15 relative of numpy's LAPACK solve, not bit-identical); frames
-//      whose decision could hinge on that (a singular system, an
-//      ill-conditioned winner, a near-tie) are flagged.
+//      staged in LDS; every trial's plane solved from its triple with numpy's
+//      rounding (the LAPACK dgesv + dot of functions.py:267 restated, round 3),
+//      every trial screened in fp32 from LDS (one wave per trial, a rigorous
+//      bound to the fp64 mean), then the trials the screen cannot rule out
+//      evaluated in fp64 exactly as numpy does (the gemv's fmas, the pairwise
+//      sum of np.mean) and the first strict minimum kept (functions.py:289-293):
+//      the plane, its error and the winning trial are numpy's, bit for bit.
 //   (One kernel doing both, wave 0 drawing beside wave 1 evaluating, was
 //   bound by the screen's random 4-byte gathers: ~94 GB of sector traffic per
 //   4096 frames, the points of the ~4096 frames in flight not fitting L2.)
@@ -499,31 +497,109 @@ constexpr int kRBEvalThreads = 1024;   // eval: 16 waves screen 16 trials at a t
 
 // One trial's record: the draw kernel writes the triple's three indices into
 // its first words, the eval kernel replaces them by a, b, c, |abc|, flag
-// (0 ok, 1 singular: numpy's LinAlgError, skipped; 2 ill-conditioned).
+// (0 ok, 1 singular: numpy's LinAlgError, skipped).
 constexpr int kRBTri = 5;
 
-// The trial's plane and its record (one lane): inv([P1;P2;P3]) 1 = (r2 x r3 +
-// r3 x r1 + r1 x r2) / det (functions.py:267), |abc| (:272), and the flag: 1
-// singular (numpy raises LinAlgError, the trial is skipped), 2 ill-conditioned.
+// The trial's plane and its record (one lane): abc = np.dot(np.linalg.inv([P1;P2;P3]),
+// np.ones([3, 1])) (functions.py:267) rounded exactly as numpy computes it, |abc| as
+// math.sqrt does (:269), and the flag (1: singular, numpy raises LinAlgError and the
+// trial is skipped). numpy's inv is LAPACK dgesv(A, I) from its bundled OpenBLAS
+// 0.3.29: dgetf2's left-looking LU (partial pivoting on the first largest |a|, the
+// column below a pivot scaled by its reciprocal, the update products rounded before
+// they are subtracted, column 2's two-term update as fma(l21, u12, l20 u02)), then
+// dgetrs's two triangular solves of the permuted identity (trsm: the diagonal
+// applied as a multiply by its reciprocal, fused multiply-subtracts, except the
+// backward solve's row-2 update of rows 0 and 1, a rounded product subtracted); then
+// the dot with ones adds each row's three entries left to right. The restatement
+// is oracle/svx_oracle.c svo_plane_lapack, which tests/test_ransac_cpu.py pins to
+// numpy bit for bit on random and near-collinear systems.
 __device__ __forceinline__ void rb_solve_record(const double* r1, const double* r2, const double* r3, double* o) {
-    const double c23[3] = {r2[1] * r3[2] - r2[2] * r3[1], r2[2] * r3[0] - r2[0] * r3[2], r2[0] * r3[1] - r2[1] * r3[0]};
-    const double c31[3] = {r3[1] * r1[2] - r3[2] * r1[1], r3[2] * r1[0] - r3[0] * r1[2], r3[0] * r1[1] - r3[1] * r1[0]};
-    const double c12[3] = {r1[1] * r2[2] - r1[2] * r2[1], r1[2] * r2[0] - r1[0] * r2[2], r1[0] * r2[1] - r1[1] * r2[0]};
-    const double det = r1[0] * c23[0] + r1[1] * c23[1] + r1[2] * c23[2];
-    const double a = (c23[0] + c31[0] + c12[0]) / det;
-    const double b = (c23[1] + c31[1] + c12[1]) / det;
-    const double c = (c23[2] + c31[2] + c12[2]) / det;
-    const double n1 = sqrt(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
-    const double n2 = sqrt(r2[0] * r2[0] + r2[1] * r2[1] + r2[2] * r2[2]);
-    const double n3 = sqrt(r3[0] * r3[0] + r3[1] * r3[1] + r3[2] * r3[2]);
-    double fl = 0.0;
-    if (det == 0.0) fl = 1.0;                                 // numpy: LinAlgError, trial skipped
-    else if (!(fabs(det) >= 1e-6 * n1 * n2 * n3)) fl = 2.0;   // ill-conditioned
-    o[0] = a;
-    o[1] = b;
-    o[2] = c;
-    o[3] = sqrt(a * a + b * b + c * c);
-    o[4] = fl;
+    // the rows, pivoted in place (a row swap at step j equals dgetf2's swap of the
+    // columns <= j plus its later re-application to the columns > j)
+    double m0[3] = {r1[0], r1[1], r1[2]}, m1[3] = {r2[0], r2[1], r2[2]}, m2[3] = {r3[0], r3[1], r3[2]};
+    int p0 = 0, p1 = 1, p2 = 2;   // original row of each position (the permutation dgetrs applies to I)
+    const auto swap_rows = [](double (&x)[3], double (&y)[3], int& px, int& py) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double t = x[c];
+            x[c] = y[c];
+            y[c] = t;
+        }
+        const int t = px;
+        px = py;
+        py = t;
+    };
+    // column 0: pivot = the first largest |a| (idamax)
+    int piv = 0;
+    double amax = fabs(m0[0]);
+    if (fabs(m1[0]) > amax) {
+        piv = 1;
+        amax = fabs(m1[0]);
+    }
+    if (fabs(m2[0]) > amax) piv = 2;
+    if (piv == 1) swap_rows(m0, m1, p0, p1);
+    else if (piv == 2) swap_rows(m0, m2, p0, p2);
+    const double u00 = m0[0];
+    double l10 = m1[0], l20 = m2[0];
+    if (u00 != 0.0) {
+        const double r = 1.0 / u00;
+        l10 *= r;
+        l20 *= r;
+    }
+    // column 1: the gemv update (rounded product, then subtracted), pivot among rows 1, 2
+    double b1 = m1[1] - l10 * m0[1], b2 = m2[1] - l20 * m0[1];
+    double c1 = m1[2], c2 = m2[2];
+    if (fabs(b2) > fabs(b1)) {
+        double t = b1;
+        b1 = b2;
+        b2 = t;
+        t = l10;
+        l10 = l20;
+        l20 = t;
+        t = c1;
+        c1 = c2;
+        c2 = t;
+        const int q = p1;
+        p1 = p2;
+        p2 = q;
+    }
+    const double u11 = b1;
+    double l21 = b2;
+    if (u11 != 0.0) l21 *= 1.0 / u11;
+    // column 2: u12 by the dot (rounded product), u22 by the two-term gemv
+    const double u01 = m0[1], u02 = m0[2];
+    const double u12 = c1 - l10 * u02;
+    const double u22 = c2 - fma(l21, u12, l20 * u02);
+    const bool singular = u00 == 0.0 || u11 == 0.0 || u22 == 0.0;   // dgesv info > 0
+    const double i00 = 1.0 / u00, i11 = 1.0 / u11, i22 = 1.0 / u22;
+    double abc[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {   // column c of the inverse: L U x = P e_c
+        double x0 = p0 == c ? 1.0 : 0.0, x1 = p1 == c ? 1.0 : 0.0, x2 = p2 == c ? 1.0 : 0.0;
+        x1 = fma(-x0, l10, x1);   // forward, unit lower
+        x2 = fma(-x0, l20, x2);
+        x2 = fma(-x1, l21, x2);
+        x2 = x2 * i22;            // backward, upper
+        x0 = x0 - u02 * x2;
+        x1 = x1 - u12 * x2;
+        x1 = x1 * i11;
+        x0 = fma(-x1, u01, x0);
+        x0 = x0 * i00;
+        if (c == 0) {   // np.dot(inv, ones): ((inv[r][0] + inv[r][1]) + inv[r][2])
+            abc[0] = x0;
+            abc[1] = x1;
+            abc[2] = x2;
+        } else {
+            abc[0] += x0;
+            abc[1] += x1;
+            abc[2] += x2;
+        }
+    }
+    o[0] = abc[0];
+    o[1] = abc[1];
+    o[2] = abc[2];
+    o[3] = sqrt(abc[0] * abc[0] + abc[1] * abc[1] + abc[2] * abc[2]);   // ((a a + b b) + c c), no fma
+    o[4] = singular ? 1.0 : 0.0;
 }
 
 template <class IdxT, bool TR>
@@ -613,6 +689,122 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
         fstat[2 * frame] = status;   // 1: the reference would never return; 2: draw budget
         fstat[2 * frame + 1] = s;    // trials drawn (the failing one excluded)
     }
+}
+
+// A lane's value read by every lane (src uniform across the wave).
+__device__ __forceinline__ int rb_readlane(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+__device__ __forceinline__ double rb_readlane(double v, int src) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+
+// np.mean's sum of a trial's k distance terms (functions.py:289), by one wave, in
+// numpy's pairwise order (numpy/_core/src/umath/loops_utils.h.src pairwise_sum,
+// reached from add.reduce with the initial 0.0): n < 8 terms summed in order from
+// 0.0; n <= 128 in eight accumulators r[j] (terms j, j + 8, ... below n - n % 8,
+// in order), combined ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the
+// last n % 8 added in order; n > 128 split at n2 = n/2 - (n/2) % 8 and the halves'
+// sums added. So every leaf starts at a multiple of 8, and k <= 1024 has at most
+// 16 leaves. The leaves are listed by a uniform walk of the split tree (a task
+// stack held one entry a lane), their sums computed eight leaves at a time (lane
+// 8g + j runs accumulator j of leaf g), and the tree walked again to add them.
+// load(i) -> the packed point of sample entry i, term(u) -> its distance term.
+template <class LoadF, class TermF>
+__device__ double rb_np_pairwise(int k, LoadF load, TermF term) {
+    const int lane = lane_id();
+    int st_lo = 0, st_n = k;   // task stack, slot s in lane s; st_n < 0 marks an addition
+    int sp = 1;
+    int leaf_lo = 0, leaf_n = 0, nleaf = 0;   // leaf l in lane l
+    while (sp > 0) {
+        const int lo = rb_readlane(st_lo, sp - 1), n = rb_readlane(st_n, sp - 1);
+        --sp;
+        if (n <= 128) {
+            if (lane == nleaf) {
+                leaf_lo = lo;
+                leaf_n = n;
+            }
+            ++nleaf;
+        } else {
+            const int n2 = n / 2 - (n / 2) % 8;
+            if (lane == sp) {   // the right half, summed after the left
+                st_lo = lo + n2;
+                st_n = n - n2;
+            }
+            if (lane == sp + 1) {
+                st_lo = lo;
+                st_n = n2;
+            }
+            sp += 2;
+        }
+    }
+    double leafsum = 0.0;   // leaf l's sum in lane l
+    const int g = lane >> 3, j = lane & 7;
+    for (int q = 0; q < nleaf; q += 8) {
+        const int l = q + g;
+        const bool live = l < nleaf;
+        const int lo = __shfl(leaf_lo, live ? l : 0, kWave), n = live ? __shfl(leaf_n, l, kWave) : 0;
+        const int mm = n >= 8 ? n - (n & 7) : 0;
+        double r = 0.0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {   // accumulator j: terms j, j + 8, ... < mm (at most 16), eight loads in flight
+            uint32_t u[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                const int i = j + 8 * (8 * h + v);
+                u[v] = i < mm ? load(lo + i) : 0u;
+            }
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                const int i = j + 8 * (8 * h + v);
+                if (i < mm) {
+                    const double t = term(u[v]);
+                    r = (h == 0 && v == 0) ? t : r + t;
+                }
+            }
+        }
+        double s = r + __shfl_xor(r, 1, kWave);
+        s = s + __shfl_xor(s, 2, kWave);
+        s = s + __shfl_xor(s, 4, kWave);
+        if (live && j == 0)
+            for (int i = mm; i < n; ++i) s += term(load(lo + i));   // n < 8: s = 0.0 + the n terms in order
+        const double v = __shfl(s, ((lane - q) & 7) << 3, kWave);
+        if (lane >= q && lane < q + 8) leafsum = v;
+    }
+    double vst = 0.0;   // value stack, slot s in lane s
+    int vsp = 0, li = 0;
+    st_lo = 0;
+    st_n = k;
+    sp = 1;
+    while (sp > 0) {
+        const int lo = rb_readlane(st_lo, sp - 1), n = rb_readlane(st_n, sp - 1);
+        --sp;
+        double push;
+        if (n < 0) {   // both halves done: left + right
+            const double b = rb_readlane(vst, vsp - 1), a = rb_readlane(vst, vsp - 2);
+            vsp -= 2;
+            push = a + b;
+        } else if (n <= 128) {
+            push = rb_readlane(leafsum, li++);
+        } else {
+            const int n2 = n / 2 - (n / 2) % 8;
+            if (lane == sp) st_n = -1;
+            if (lane == sp + 1) {
+                st_lo = lo + n2;
+                st_n = n - n2;
+            }
+            if (lane == sp + 2) {
+                st_lo = lo;
+                st_n = n2;
+            }
+            sp += 3;
+            continue;
+        }
+        if (lane == vsp) vst = push;
+        ++vsp;
+    }
+    return rb_readlane(vst, 0);
 }
 
 // Screen + decision. LDS: the frame's packed points (LDS_PTS) or none, then
@@ -811,24 +1003,18 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
         const double* tr = ftri + (int64_t)t * kRBTri;
         const double a = tr[0], b = tr[1], c = tr[2], d = tr[3];
         const IdxT* idx = fidx + (int64_t)t * k;
-        double sum = 0.0;
-        for (int j0 = lane; j0 < k; j0 += 4 * kWave) {   // every gather in flight before the arithmetic
-            uint32_t u[4];
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int j = j0 + kWave * v;
-                u[v] = P[j < k ? (uint32_t)idx[j] : 0u];   // the packed point (LDS, or memory when it did not fit)
-            }
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                if (j0 + kWave * v >= k) continue;
+        // abs((np.dot(T, abc) - 1) / d) per sample point (functions.py:275): numpy's
+        // gemv rounds each row's dot as fma(z, c, fma(x, a, y b)) (k = 1 is a (1, 3) x
+        // (3, 1) product, numpy's ddot: fma(z, c, fma(y, b, x a))); np.mean (:289) =
+        // the pairwise sum / k. Bit-identical to numpy (tests/test_ransac_cpu.py).
+        const double sum = rb_np_pairwise(
+            k, [&](int i) { return P[(uint32_t)idx[i]]; },   // the packed point (LDS, or memory when it did not fit)
+            [&](uint32_t u) {
                 double qx, qy, qz;
-                rb_point(u[v], tb, qx, qy, qz);
-                sum += fabs((qx * a + qy * b + qz * c - 1.0) / d);
-            }
-        }
-#pragma unroll
-        for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
+                rb_point(u, tb, qx, qy, qz);
+                const double dot = k == 1 ? fma(qz, c, fma(qy, b, qx * a)) : fma(qz, c, fma(qx, a, qy * b));
+                return fabs((dot - 1.0) / d);
+            });
         if (lane == 0) ce[ci] = sum / k;
     }
     __syncthreads();
@@ -848,7 +1034,6 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
                 babc[0] = tr[0];
                 babc[1] = tr[1];
                 babc[2] = tr[2];
-                flags = (flags & ~2u) | (tr[4] == 2.0 ? 2u : 0u);
             } else if (e < second) {
                 second = e;
             }

@@ -88,3 +88,67 @@ def test_host_draw_rejects_bad_state():
     st[624] = 700
     with pytest.raises(_abi.SvxError):
         _draw((3, tuple(st), None), np.zeros((10, 3)), 1, 1)
+
+
+def _systems(rng, n):
+    """3 x 3 systems as RANSAC meets them: maskpoint-like triples, scaled normals, near-collinear triples."""
+    out = []
+    for kind in range(3):
+        P = np.empty((n, 3, 3))
+        if kind == 0:
+            P[:, :, 0] = rng.uniform(-20, 20, (n, 3))
+            P[:, :, 1] = rng.uniform(-3, 3, (n, 3))
+            P[:, :, 2] = rng.uniform(2, 80, (n, 3))
+        elif kind == 1:
+            P = rng.standard_normal((n, 3, 3)) * 10 ** rng.uniform(-3, 3, (n, 1, 1))
+        else:
+            a, b = rng.uniform(-10, 10, (n, 3)), rng.uniform(-10, 10, (n, 3))
+            t = rng.uniform(0, 1, (n, 1))
+            P[:, 0], P[:, 1] = a, b
+            P[:, 2] = a + t * (b - a) + rng.standard_normal((n, 3)) * 1e-4
+        out.append(P)
+    return np.concatenate(out)
+
+
+def test_plane_lapack_matches_numpy():
+    """functions.py:267, abc = np.dot(np.linalg.inv(P), np.ones([3, 1])): the restated
+    dgesv + dot (oracle svo_plane_lapack, the sequence the device's rb_solve_record
+    runs) equals numpy's bits on every system, maskpoint triples included, and is
+    singular exactly where numpy raises LinAlgError."""
+    rng = np.random.default_rng(2024)
+    P = _systems(rng, 4000)
+    m = carmask()
+    pts = ransac_inputs.case_points(next(iter(ransac_inputs.CASES)), oracle, m)
+    tri = pts[rng.integers(0, len(pts), (4000, 3))][:, :, :3]
+    P = np.concatenate([P, tri, np.round(P[:200]), P[:50, [0, 0, 1]]])   # integer and repeated-row systems
+    bad = []
+    for i, p in enumerate(P):
+        got, sing = oracle.plane_lapack(*p)
+        try:
+            want = np.dot(np.linalg.inv(p), np.ones([3, 1]))[:, 0]
+        except np.linalg.LinAlgError:
+            if not sing:
+                bad.append((i, "numpy singular"))
+            continue
+        if sing or not np.array_equal(got.view(np.uint64), want.view(np.uint64)):
+            bad.append((i, got, want))
+    assert bad == [], (len(bad), bad[:3])
+
+
+@pytest.mark.parametrize("k", [1, 5, 7, 8, 9, 100, 128, 129, 600, 1000, 1023, 1024])
+def test_ransac_err_matches_numpy(k):
+    """functions.py:269-275, :289 — error = np.mean(abs((np.dot(T, abc) - 1) / d)):
+    the restated gemv fmas and numpy's pairwise sum (oracle svo_ransac_err, the
+    order the device's rb_np_pairwise uses) equal numpy's bits, for every sample
+    size the batch accepts up to 1024."""
+    import math
+    rng = np.random.default_rng(k)
+    m = carmask()
+    pts = ransac_inputs.case_points(next(iter(ransac_inputs.CASES)), oracle, m)
+    for _ in range(20):
+        T = pts[rng.choice(len(pts), k, replace=False)]
+        abc = np.dot(np.linalg.inv(pts[rng.integers(0, len(pts), 3)][:, :3]), np.ones([3, 1]))
+        d = math.sqrt(abc[0, 0] * abc[0, 0] + abc[1, 0] * abc[1, 0] + abc[2, 0] * abc[2, 0])
+        rp = [[x[0], x[1], x[2]] for x in T]
+        want = np.mean(abs((np.dot(rp, abc) - 1) / d))
+        assert oracle.ransac_err(T, abc) == float(want)
