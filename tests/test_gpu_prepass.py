@@ -98,6 +98,38 @@ def test_batch_prepass(svx_mod, option):
             assert np.array_equal(b.read_disp(f), ref[f])
 
 
+@pytest.mark.parametrize("frames", [130, 300, 520])
+@pytest.mark.parametrize("with_prev0", [False, True])
+def test_batch_fill_previous_long(svx_mod, frames, with_prev0):
+    """fillDisparity's frame recurrence (functions.py:141-148, stereovision.py:56-60) over hundreds of frames:
+    columns that stay 0 throughout (each frame takes prev0 or 0), columns of 1s and 2s whose sums saturate at
+    255, columns mostly <= 2, columns that switch from 0 to 7 mid-batch, and synthetic frames, against the
+    oracle chain, twice on one batch."""
+    H, W = 32, 256
+    rng = np.random.default_rng(frames + with_prev0)
+    raw = rng.integers(3, 256, (frames, H, W)).astype(np.uint8)
+    raw[:, :, :16] = 0                                                    # open in every group
+    raw[:, :, 16:32] = rng.integers(1, 3, (frames, H, 16))                # accumulate and saturate
+    low = rng.random((frames, H, 64)) < 0.97
+    raw[:, :, 32:96] = np.where(low, rng.integers(0, 3, (frames, H, 64)), raw[:, :, 32:96])
+    raw[:, :, 96:100] = 0
+    raw[frames // 2:, :, 96:100] = 7                                      # opens, then closes mid-batch
+    for f in range(frames):
+        raw[f, :, 128:] = oracle.synth_frame(f, H=H, W=W)[0][:, 128:]
+    prev0 = rng.integers(0, 256, (H, W)).astype(np.uint8) if with_prev0 else None
+    with svx_mod.batch.Batch(frames, H=H, W=W, with_bgr=False) as b:
+        for f in range(frames):
+            b.upload(f, raw[f])
+        for rep in range(2):   # the second run re-uses the batch's scratch (flags reset per launch)
+            if rep:
+                for f in range(frames):
+                    b.upload(f, raw[f])
+            b.prepass("previous", prev0=prev0)
+            ref = oracle.fill_previous_chain(list(raw), prev0)
+            for f in range(frames):
+                assert np.array_equal(b.read_disp(f), ref[f]), (rep, f)
+
+
 def test_road_raster_reference_fixture(svx_mod, golden):
     for fid, ref in META["road_raster_step2"].items():
         m = golden.meta["full_frames_step2"][fid]
