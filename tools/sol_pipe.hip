@@ -26,6 +26,11 @@
 //   mode 27..29  mode 18's shape (K = 1) with frame-interleaved tiles: output o of frame f at
 //           ((o / B) * frames + f) * B + o % B, B = 256, 1024, 4096 outputs (round 3, session 3)
 //   mode 30..32  writes only, the same three tiled layouts
+//   mode 33..36  persistent: 1280 workgroups (the resident kernel's 5 a CU), each taking frames
+//           blockIdx + r * 1280, launched cooperatively: 33 mode 18's shape (no barriers); 34 the same with a
+//           grid barrier after every round's pass 1 and after its pass 2 (so the whole chip reads, then writes);
+//           35 mode 34 with pass 2 as K = 64 (all re-reads, then all writes); 36 mode 34 with only the barrier
+//           after pass 1
 // argv: frames (4096), outputs per frame (277200), 1 = output planes physically contiguous (0)
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/_sol_pipe tools/sol_pipe.hip
 #include <hip/hip_runtime.h>
@@ -59,6 +64,7 @@ struct Args {
     unsigned long long* counter;
     int kgroup;          // modes 13..22: chunks per read/write group
     int lb;              // modes 27..32: log2 of the tile (outputs)
+    unsigned* bar;       // modes 33..36: grid barrier counter
     int frames;
 };
 
@@ -109,6 +115,51 @@ __global__ __launch_bounds__(256) void sweep_kernel(Args a, int64_t total) {   /
 
 __device__ __forceinline__ int64_t tiled(const Args& a, int f, int64_t g) {
     return ((((g >> a.lb) * a.frames) + f) << a.lb) + (g & ((1 << a.lb) - 1));
+}
+
+__device__ void grid_barrier(unsigned* ctr, unsigned target) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // relaxed: the phases order no data here (an agent-scope release / acquire per arrival and poll is an L2
+        // write-back / invalidate on gfx950: 14-16 ms instead of 6 with them, profiles/r03/sol_pipe_persist.txt)
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(8);
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void persist_kernel(Args a) {   // modes 33..36
+    const int G = gridDim.x;
+    uint32_t acc = 0;
+    unsigned nb = 0;
+    const int rounds = (a.frames + G - 1) / G;
+    for (int r = 0; r < rounds; ++r) {
+        const int f = blockIdx.x + r * G;
+        const bool live = f < a.frames;
+        if (live) acc ^= read_range(a, f, 0, a.px16);   // pass 1
+        if (a.mode >= 34) grid_barrier(a.bar, ++nb * G);
+        if (live) {
+            const float v = (float)f;
+            const uint4* d = a.disp + f * a.px16;
+            const int n = 64, K = a.mode == 35 ? 64 : 1;
+            for (int c0 = 0; c0 < n; c0 += K) {
+                for (int c = c0; c < c0 + K; ++c)
+                    for (int64_t w = a.px16 * c / n + threadIdx.x; w < a.px16 * (c + 1) / n; w += 256) {
+                        const uint4 x = *(d + w);
+                        acc ^= x.x ^ x.w;
+                    }
+                const int64_t g0 = (a.kept / 4 * c0 / n) * 4, g1 = (a.kept / 4 * (c0 + K) / n) * 4;
+                for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
+                    const v4f q = {v, v, v, v};
+#pragma unroll
+                    for (int k = 0; k < 5; ++k)
+                        __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + (int64_t)f * a.cap + g));
+                }
+            }
+        }
+        if (a.mode == 34 || a.mode == 35) grid_barrier(a.bar, ++nb * G);
+    }
+    if (acc == 0x12345678u) a.sink[blockIdx.x] = acc;
 }
 
 __global__ __launch_bounds__(256) void sol_kernel(Args a) {
@@ -238,6 +289,8 @@ int main(int argc, char** argv) {
     a.sink = (uint32_t*)p;
     CK(hipMalloc(&p, 8));
     a.counter = (unsigned long long*)p;
+    CK(hipMalloc(&p, 8));
+    a.bar = (unsigned*)p;
     a.px16 = px / 16;
     a.cap = cap;
     a.kept = kept;
@@ -256,13 +309,16 @@ int main(int argc, char** argv) {
                            "pass1 + pass2 last chunk first, strided", "pass1 + re-read only, first chunk first",
                            "pass1 + re-read only, last chunk first", "pass1 + pass2, tiles of 256",
                            "pass1 + pass2, tiles of 1024", "pass1 + pass2, tiles of 4096", "write: tiles of 256",
-                           "write: tiles of 1024", "write: tiles of 4096"};
+                           "write: tiles of 1024", "write: tiles of 4096", "persistent, no barriers",
+                           "persistent, barrier after pass 1 and pass 2", "persistent, barriers, pass 2 K = 64",
+                           "persistent, barrier after pass 1"};
     const int kgroups[5] = {1, 2, 4, 8, 64};
     const int64_t cap0 = cap - 64;
     for (int round = 0; round < 2; ++round)
-        for (int mode = 0; mode < 33; ++mode) {
-            // earlier results: profiles/r02/sol_pipe_session8.txt, r03/sol_pipe_kgroup.txt, r03/sol_pipe_reverse.txt
-            if (!(mode == 3 || mode == 5 || mode == 13 || mode == 18 || mode >= 27)) continue;
+        for (int mode = 0; mode < 37; ++mode) {
+            // earlier results: profiles/r02/sol_pipe_session8.txt, r03/sol_pipe_kgroup.txt, r03/sol_pipe_reverse.txt,
+            // r03/sol_pipe_tiles.txt
+            if (!(mode == 18 || mode >= 33)) continue;
             a.mode = mode;
             a.kgroup = mode >= 13 && mode <= 22 ? kgroups[(mode - 13) % 5] : 1;
             a.nplanes = 5;
@@ -279,7 +335,11 @@ int main(int argc, char** argv) {
             if (mode == 7) a.stride = cap;
             if (mode == 11) a.nper = cap0;
             auto launch = [&]() {
-                if (mode == 8) hipLaunchKernelGGL(sweep_kernel, dim3(4096), dim3(256), 0, 0, a, kept * frames);
+                if (mode >= 33) {
+                    CK(hipMemsetAsync(a.bar, 0, 4, 0));
+                    void* kargs[] = {&a};
+                    CK(hipLaunchCooperativeKernel((const void*)persist_kernel, dim3(1280), dim3(256), kargs, 0, 0));
+                } else if (mode == 8) hipLaunchKernelGGL(sweep_kernel, dim3(4096), dim3(256), 0, 0, a, kept * frames);
                 else hipLaunchKernelGGL(sol_kernel, dim3(frames), dim3(256), 0, 0, a);
             };
             float best = 1e30f, tot = 0.f;
@@ -297,8 +357,8 @@ int main(int argc, char** argv) {
                 best = ms < best ? ms : best;
                 tot += ms;
             }
-            const double rd = ((mode == 3 || mode >= 5) && mode != 10 && (mode < 12 || mode >= 30) ? 0. : 4. * px * frames) +
-                              ((mode == 4 || mode >= 13) && mode < 30 ? 1. * px * frames : 0.);
+            const double rd = ((mode == 3 || mode >= 5) && mode != 10 && (mode < 12 || (mode >= 30 && mode < 33)) ? 0. : 4. * px * frames) +
+                              ((mode == 4 || mode >= 13) && (mode < 30 || mode >= 33) ? 1. * px * frames : 0.);
             const double wr = (mode == 2 || (mode >= 25 && mode < 27)) ? 0. : 20. * (mode == 11 ? cap0 : kept) * frames;
             std::printf("{\"round\": %d, \"mode\": %d, \"what\": \"%s\", \"K\": %d, \"GB\": %.2f, \"best_ms\": %.3f, "
                         "\"mean_ms\": %.3f, \"TBps_best\": %.2f}\n",
