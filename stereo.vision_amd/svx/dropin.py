@@ -13,8 +13,9 @@ reference:
 
 * ``projectDisparityTo3d(disparity, max_disparity, rgb=[])`` (functions.py:178-198):
   ``max_disparity`` is accepted and ignored (as in the reference); ``rgb`` is
-  used iff ``len(rgb) > 0``. Returns a ``list`` (a Sequence: ``random.sample``
-  in RANSAC needs one, functions.py:252,286) of rows supporting ``row[0..5]``
+  used iff ``len(rgb) > 0``. Returns a Sequence (``random.sample`` in RANSAC
+  needs one, functions.py:252,286; svx/points.py: rows made when first read, a
+  plain list after a mutation) of rows supporting ``row[0..5]``
   and ``row[:3]``; XYZ are ``np.float64`` bit-identical to the reference and
   R,G,B are numpy scalars (np.float64), which keeps ``BGRtoHSVHue`` keys
   identical (Python ints would not: SURVEY §0 trap 3).
@@ -102,7 +103,7 @@ from .points import PointList, as_points_array  # noqa: E402,F401  (re-exported)
 
 
 def projectDisparityTo3d(disparity, max_disparity, rgb=[]):  # noqa: N802,B006 (reference signature)
-    """functions.py:178-198 on the GPU. Returns a list of rows (see module doc)."""
+    """functions.py:178-198 on the GPU. Returns a Sequence of rows (see module doc)."""
     xyz, rgbs = project_frame(disparity, rgb)
     if rgbs is None:
         rows = xyz

@@ -1,6 +1,17 @@
-"""The point lists the drop-ins pass between stages (functions.py:178-323):
-a Python list of row views, as the reference's callers expect, that remembers
-the array behind it so the next GPU stage does not re-stack rows."""
+"""The point sequences the drop-ins pass between stages (functions.py:178-323).
+
+The reference's callers need a Sequence of rows (random.sample, functions.py:252,
+286; row[0..5] and row[:3], :205-207,218,252,272,304), not a list as such (SURVEY
+§8b). Building 74,200 row views per frame was most of the drop-in chain's host
+time (a1 alone 5-8 ms a call), so the sequence is lazy: it holds the (N, 3|6)
+float64 array behind it and makes a row view the first time that row is read,
+then keeps it, so the same row is the same object every time it is read, through
+the sequence and through every selection of it (the selecting stages return the
+caller's own row objects, as the reference's list comprehensions do). The GPU
+stages take the array itself and never create rows. A mutation turns the
+sequence into a plain list of its rows (created then) and it forgets the array.
+"""
+import collections.abc
 import operator
 
 import numpy as np
@@ -16,60 +27,110 @@ def select_rows(seq, idx):
     return list(operator.itemgetter(*idx)(seq))
 
 
-class PointList(list):
-    """The list of row views projectDisparityTo3d returns, remembering the (N, 3|6)
-    array behind it while the list is unmodified, so later GPU stages (RANSAC,
-    back-projection, the a2-a6 stage drop-ins) skip re-stacking N Python rows.
-    Any list mutation drops it; writes through a row view write the array
-    itself, so they stay consistent.
+class PointList(collections.abc.MutableSequence):
+    """A lazy sequence of the rows of an (N, c) array: projectDisparityTo3d's return
+    value and, through PointList.subset, the selections computePlanarThreshold and
+    filterPointsByHistogram return. Rows are views of the array (a write through a
+    row is a write to the array), made on first read and shared with every
+    selection. array() is the (n, c) C-contiguous float64 array of the current
+    rows (zero-copy for a whole array; a selection gathers it on every call, so
+    writes through rows are seen); None once the sequence was mutated."""
 
-    PointList.subset(parent, idx) is a selection of a PointList (the stages
-    that filter, functions.py:314-323, :228-230): its items are the parent's own
-    row objects, as the reference returns them, and its array is parent[idx],
-    gathered when asked for (so writes through the rows stay visible)."""
-
-    __slots__ = ("_array", "_idx")
+    __slots__ = ("_base", "_cache", "_idx", "_rows")
 
     def __init__(self, array):
-        super().__init__(array)
-        self._array = array
-        self._idx = None
+        self._base = array
+        self._cache = [None] * len(array)   # base row index -> its row view, once read
+        self._idx = None                    # base row indices of this selection (None: all rows)
+        self._rows = None                   # a plain list after a mutation
 
     @classmethod
     def subset(cls, parent, idx):
-        out = list.__new__(cls)
-        list.__init__(out, select_rows(parent, idx))
-        base = parent.array() if isinstance(parent, PointList) else None
-        out._array = base
-        out._idx = np.asarray(idx, np.int64) if base is not None else None
+        """parent's rows idx (a selection of a selection maps through to the base rows)."""
+        if not isinstance(parent, PointList) or parent._rows is not None:
+            return select_rows(parent, idx)
+        out = cls.__new__(cls)
+        out._base, out._cache, out._rows = parent._base, parent._cache, None
+        idx = np.asarray(idx, np.int64)
+        out._idx = idx if parent._idx is None else parent._idx[idx]
         return out
 
+    # --- Sequence ----------------------------------------------------------
+    def __len__(self):
+        if self._rows is not None:
+            return len(self._rows)
+        return len(self._base) if self._idx is None else len(self._idx)
+
+    def _row(self, b):
+        r = self._cache[b]
+        if r is None:
+            r = self._cache[b] = self._base[b]
+        return r
+
+    def __getitem__(self, i):
+        if self._rows is not None:
+            return self._rows[i]
+        if isinstance(i, slice):
+            sel = np.arange(len(self), dtype=np.int64)[i]
+            return PointList.subset(self, sel)
+        n = len(self)
+        i = operator.index(i)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError("list index out of range")
+        return self._row(i if self._idx is None else int(self._idx[i]))
+
+    def __iter__(self):
+        if self._rows is not None:
+            return iter(self._rows)
+        ids = range(len(self._base)) if self._idx is None else self._idx.tolist()
+        return map(self._row, ids)
+
+    # --- mutation: become a plain list --------------------------------------
+    def _materialise(self):
+        if self._rows is None:
+            self._rows = list(iter(self))
+            self._base = self._cache = self._idx = None
+        return self._rows
+
+    def __setitem__(self, i, v):
+        self._materialise()[i] = v
+
+    def __delitem__(self, i):
+        del self._materialise()[i]
+
+    def insert(self, i, v):
+        self._materialise().insert(i, v)
+
+    def sort(self, *a, **k):
+        self._materialise().sort(*a, **k)
+
+    def copy(self):
+        return list(iter(self))
+
+    def __repr__(self):
+        return repr(list(iter(self)))
+
+    def __eq__(self, other):   # as a list compares (rows by identity first, then ==)
+        if isinstance(other, (list, PointList)):
+            return list(iter(self)) == list(iter(other))
+        return NotImplemented
+
+    __hash__ = None
+
     def array(self):
-        a = self._array
-        if a is None:
+        if self._rows is not None:
             return None
-        if self._idx is not None:
-            return np.ascontiguousarray(a[self._idx]) if len(self._idx) == len(self) else None
-        return a if len(a) == len(self) else None
-
-    def _drop(name):  # noqa: N805
-        base = getattr(list, name)
-
-        def f(self, *a, **k):
-            self._array = None
-            return base(self, *a, **k)
-        f.__name__ = name
-        return f
-
-    for _n in ("append", "extend", "insert", "remove", "pop", "clear", "sort", "reverse", "__setitem__",
-               "__delitem__", "__iadd__", "__imul__"):
-        locals()[_n] = _drop(_n)
-    del _n, _drop
+        if self._idx is None:
+            return self._base
+        return np.ascontiguousarray(self._base[self._idx])
 
 
 def as_points_array(points):
-    """(N, >=3) float64 C-contiguous array of a point sequence (zero-copy for a PointList)."""
+    """(N, >=3) float64 C-contiguous array of a point sequence (zero-copy for a whole PointList)."""
     if isinstance(points, PointList) and points.array() is not None:
         return points.array()
-    arr = points if isinstance(points, np.ndarray) else np.asarray(points)
+    arr = points if isinstance(points, np.ndarray) else np.asarray(list(points) if isinstance(points, PointList)
+                                                                   else points)
     return np.ascontiguousarray(arr, dtype=np.float64)

@@ -112,19 +112,39 @@ def test_header_cites_reference():
 
 
 def test_point_list_tracks_its_array():
+    """The lazy row sequence projectDisparityTo3d returns (svx/points.py): a Sequence random.sample takes
+    (functions.py:252,286), rows made on first read and the same objects afterwards (also through selections,
+    as the reference's list comprehensions share rows), writes through rows reach the array, and a mutation
+    turns it into a plain list that forgot the array."""
+    import collections.abc
+    import random
     from svx.dropin import PointList, as_points_array
     a = np.arange(12, dtype=np.float64).reshape(4, 3)
     pl = PointList(a)
-    assert isinstance(pl, list) and len(pl) == 4 and as_points_array(pl) is a
+    assert isinstance(pl, collections.abc.Sequence) and len(pl) == 4 and as_points_array(pl) is a
+    assert pl[1] is pl[1] and pl[-1] is pl[3] and type(pl[0][0]) is np.float64
+    with pytest.raises(IndexError):
+        pl[4]
     pl[1][0] = 99.0                       # a write through a row view is a write to the array
     assert a[1, 0] == 99.0 and as_points_array(pl) is a
+    rows = list(pl)
+    assert len(rows) == 4 and all(r is pl[i] for i, r in enumerate(rows))
+    sub = PointList.subset(pl, [3, 1])
+    assert len(sub) == 2 and sub[0] is pl[3] and sub[1] is pl[1] and np.array_equal(sub.array(), a[[3, 1]])
+    sub2 = PointList.subset(sub, [1])
+    assert sub2[0] is pl[1] and np.array_equal(sub2.array(), a[[1]])
+    sl = pl[1:3]
+    assert len(sl) == 2 and sl[0] is pl[1] and np.array_equal(as_points_array(sl), a[1:3])
     pl.append(np.zeros(3))
-    assert pl.array() is None and as_points_array(pl).shape == (5, 3)
+    assert pl.array() is None and as_points_array(pl).shape == (5, 3) and pl[1] is rows[1]
     pl2 = PointList(a)
     del pl2[0]
     assert pl2.array() is None and np.array_equal(as_points_array(pl2), a[1:])
-    import random
     assert len(random.Random(0).sample(PointList(a), 2)) == 2
+    pl3 = PointList(a)
+    assert PointList(np.zeros((0, 3))) == [] and not PointList(np.zeros((0, 3))) and pl3 == list(pl3)
+    big = PointList(np.zeros((74200, 6)))
+    assert len(random.Random(1).sample(big, 600)) == 600 and sum(r is not None for r in big._cache) == 600
 
 
 def test_hue_keys_match_reference_strings():

@@ -1,6 +1,7 @@
 """GPU parity: the HIP path (through the C ABI) against the oracle and the golden
 fixtures. Bit-exact for integer/index/byte outputs and for the fp64 drop-in;
 fp32 XYZ within 1e-5 relative (BASELINE.json north_star tolerance)."""
+import collections.abc
 import random
 import types
 
@@ -125,7 +126,7 @@ def test_dropin_sequence_protocol(svx_mod):
     """What the unchanged downstream reference functions need."""
     disp, bgr = oracle.synth_frame(0)
     pts = svx_mod.dropin.projectDisparityTo3d(disp, 128, bgr)
-    assert isinstance(pts, list)
+    assert isinstance(pts, collections.abc.Sequence)                 # SURVEY §8b: a Sequence of rows
     assert len(random.sample(pts, 600)) == 600                     # functions.py:286
     p = pts[0]
     assert len(p[:3]) == 3 and type(p[0]) is np.float64 and isinstance(p[3], np.generic)
