@@ -66,7 +66,10 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=4096, help="frames per GPU")
+    ap.add_argument("--frames", type=int, default=4096, help="frames per GPU (weak scaling)")
+    ap.add_argument("--global-frames", type=int, default=0,
+                    help="strong scaling (SURVEY §8d config 5): this many frames in all, split over the GPUs "
+                         "(overrides --frames; 0 = weak scaling, --frames per GPU)")
     ap.add_argument("--step", type=int, default=1, help="grid step (reference hard-codes 2)")
     ap.add_argument("--chunk", type=int, default=0, help="pipeline frames per wave (0 = default)")
     ap.add_argument("--qpl", type=int, default=1, help="K1 quads (4 points) per lane: 1, 2, 4")
@@ -115,10 +118,13 @@ def plan(gpus, environ, driver="auto"):
     return dict(mode="multi", n_gpus=gpus, rank=0, world=1, devices=list(range(gpus)), shard_base=0)
 
 
-def shards_of(pl, frames_per_gpu):
-    """(device, first global frame id, frames) of each GPU this process drives."""
+def shards_of(pl, frames_per_gpu, global_frames=0):
+    """(device, first global frame id, frames) of each GPU this process drives: frames_per_gpu each (weak
+    scaling), or global_frames > 0 in all, split in contiguous ranges (strong scaling)."""
     from svx.dist import shard
-    total = frames_per_gpu * pl["n_gpus"]
+    total = global_frames if global_frames > 0 else frames_per_gpu * pl["n_gpus"]
+    if total < pl["n_gpus"]:
+        raise SystemExit(f"bench.py: {total} frames over {pl['n_gpus']} GPUs")
     return [(dev, *shard(total, pl["n_gpus"], pl["shard_base"] + j)) for j, dev in enumerate(pl["devices"])]
 
 
@@ -534,7 +540,8 @@ def main(argv=None):
     if pl["mode"] == "multi" and svx.device_count() < args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but {svx.device_count()} GPU(s) visible")
     want_pipe = not args.no_pipeline
-    shards = shards_of(pl, args.frames)
+    shards = shards_of(pl, args.frames, args.global_frames)
+    strong = args.global_frames > 0
     comm = mcomm = None
     if pl["mode"] == "ranks":   # RCCL over every rank (also at world size 1: the collective path runs)
         comm = dist.RcclComm(ctrl, pl["devices"][0])
@@ -594,19 +601,20 @@ def main(argv=None):
             traffic = None
 
     frames_gpu = batches[0].frames
+    global_frames = int(ctrl.sum([sum(b.frames for b in batches)])[0])
     par = {"ranks": f"one process per GPU (torchrun), RCCL communicator per rank",
            "multi": f"one process, {pl['n_gpus']} GPUs (ncclCommInitAll)",
            "single": "one process, one GPU"}[pl["mode"]]
     out = {
         "metric": METRIC, "value": round(agg["value"], 1), "unit": "Mpoints/s", "n_gpus": pl["n_gpus"],
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(agg["ms_per_step"], 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8->f32",
+        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8->f32",
         "data": "synthetic (counter-based generator of SURVEY §8d, generated on device)",
         "config": {"workload": f"configs[2]: batch={frames_gpu}/GPU synthetic {W}x{H} disparity maps, "
                                f"step {args.step}, dense fp32 XYZ planes (K1)"
-                               + (f"; configs[4]: {frames_gpu * pl['n_gpus']} frames over {pl['n_gpus']} GPUs"
-                                  if pl["n_gpus"] > 1 else ""),
-                   "frames_per_gpu": frames_gpu, "global_frames": frames_gpu * pl["n_gpus"], "H": H, "W": W,
+                               + (f"; configs[4]: {global_frames} frames over {pl['n_gpus']} GPUs"
+                                  + (" (strong scaling)" if strong else "") if pl["n_gpus"] > 1 or strong else ""),
+                   "frames_per_gpu": frames_gpu, "global_frames": global_frames, "H": H, "W": W,
                    "step": args.step, "grid_points_per_frame": ng,
                    "parallelism": f"frame-sharded x{pl['n_gpus']} (no data-path collective); {par}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",

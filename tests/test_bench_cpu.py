@@ -92,3 +92,20 @@ def test_tcp_control_three_ranks(tmp_path):
         assert got == bytes([7] * 128)
         assert mx == [2.0, 0.0, 0.5] and sm == [3.0, 3.0]
     assert not os.path.exists(path)   # rank 0 removes the rendezvous file once everyone is in
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_strong_scaling_shards(n):
+    """--global-frames 32768 (SURVEY §8d config 5, strong scaling): the same 32768 global frame ids split over
+    n GPUs in contiguous ranges, by the one-process driver and by n ranks alike."""
+    total = 32768
+    multi = bench.shards_of(bench.plan(n, {}), 4096, total)
+    ranks = [s for r in range(n)
+             for s in bench.shards_of(bench.plan(n, {"WORLD_SIZE": str(n), "RANK": str(r), "LOCAL_RANK": str(r)}),
+                                      4096, total)]
+    assert multi == ranks
+    ids = np.concatenate([np.arange(f, f + c) for _, f, c in multi])
+    assert np.array_equal(ids, np.arange(total)) and all(c == total // n for _, _, c in multi)
+    assert bench.parse(["--global-frames", str(total)]).global_frames == total
+    with pytest.raises(SystemExit):
+        bench.shards_of(bench.plan(8, {}), 4096, 4)

@@ -63,3 +63,14 @@ def test_bench_ranks_driver(monkeypatch):
     assert "torchrun" in out["config"]["parallelism"]
     assert out["pipeline"]["plane_broadcast"].startswith("RCCL ncclBroadcast")
     assert len(calls) >= 3
+
+
+def test_bench_strong_scaling_flag(monkeypatch):
+    """--global-frames (SURVEY §8d config 5's strong scaling): the given frames in all, split over the GPUs;
+    at one GPU the whole batch, reported as strong scaling, with every frame's digests checked."""
+    import bench
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(v, raising=False)
+    out = bench.main([a for a in ARGS if a not in ("--frames", "512")] + ["--global-frames", "512"])
+    _check(out)
+    assert out["scaling"] == "strong" and out["config"]["global_frames"] == 512
