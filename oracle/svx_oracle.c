@@ -129,6 +129,52 @@ void svo_project_dense(const uint8_t* disp, int H, int W, int step, const svo_ca
     }
 }
 
+/* Checker of one frame of the device's dense fp32 planes (Hg rows at a stride of pitch)
+ * against the fp64 values of svo_project_dense on the synthetic frame
+ * `frame_id` (generated here): returns the number of grid points whose zero
+ * pattern differs or whose relative error exceeds rtol, and the worst
+ * relative error in *max_rel. Used by the GPU tests for EVERY frame of the
+ * headline batch (the device's own digest kernel is not the checker there). */
+int64_t svo_check_dense_f32(int64_t frame_id, int H, int W, int step, const svo_camera* cam, int pitch,
+                            const float* X, const float* Y, const float* Z, double rtol, double* max_rel) {
+    uint8_t* disp = (uint8_t*)malloc((size_t)H * W);
+    if (!disp) return -1;
+    svo_synth_frame(frame_id, H, W, disp, NULL);
+    const double f = cam->f, fB = cam->f * cam->B;
+    const int Hg = (H - 1 + step - 1) / step, Wg = (W - 1 + step - 1) / step;
+    int64_t bad = 0;
+    double worst = 0.0;
+    for (int gy = 0; gy < Hg; ++gy) {
+        for (int gx = 0; gx < Wg; ++gx) {   /* the reference's grid; pad columns up to pitch are not points */
+            double v[3] = {0, 0, 0};
+            {
+                const int y = gy * step, x = gx * step;
+                const uint8_t d = disp[(int64_t)y * W + x];
+                if (d) {
+                    v[2] = fB / (double)d;
+                    v[0] = (((double)x - cam->cw) * v[2]) / f;
+                    v[1] = (((double)y - cam->ch) * v[2]) / f;
+                }
+            }
+            const int64_t o = (int64_t)gy * pitch + gx;
+            const float g[3] = {X[o], Y[o], Z[o]};
+            for (int k = 0; k < 3; ++k) {
+                if ((v[k] == 0.0) != (g[k] == 0.0f)) {
+                    ++bad;
+                    continue;
+                }
+                if (v[k] == 0.0) continue;
+                const double rel = fabs((double)g[k] - v[k]) / fabs(v[k]);
+                if (rel > worst) worst = rel;
+                if (!(rel <= rtol)) ++bad;
+            }
+        }
+    }
+    free(disp);
+    *max_rel = worst;
+    return bad;
+}
+
 /* ------------------------------------------------------------------------
  * a7: project3DPointsTo2DImagePoints — functions.py:201-209 (fp64):
  *   x = ((X*f)/Z) + cw ; y = ((Y*f)/Z) + ch
