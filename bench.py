@@ -75,7 +75,8 @@ def parse(argv=None):
     ap.add_argument("--qpl", type=int, default=1, help="K1 quads (4 points) per lane: 1, 2, 4")
     ap.add_argument("--nt", type=int, default=1, help="non-temporal K1 stores (1 = measured faster)")
     ap.add_argument("--ramp-ms", type=float, default=300.0,
-                    help="untimed K1 launches before the warmup steps, to let clocks settle")
+                    help="untimed launches before the warmup steps of K1 and of the pipeline (a third of it before the "
+                         "§8f stage timings), to let clocks settle")
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the 1-frame latency probe")
     ap.add_argument("--no-cpu", action="store_true")
@@ -223,11 +224,24 @@ def pipeline_traffic(path, frames, step):
     return tj.get("pipeline_hbm_bytes_per_call")
 
 
-def _timed(b, fn, reps, reset=False):
+def ramp(fn, syncs, ms):
+    """untimed calls of fn for `ms` of wall time, then a sync: the GPU's clocks settle before a timed region.
+    A kernel run cold after host-side work (parity checks, the CPU legs) starts slow and speeds up over its first
+    ~8 calls (the resident pipeline 6.8-7.0 ms -> 5.7-5.8 ms, profiles/r03/resident_dispatches_s*.json), as K1 did
+    before --ramp-ms."""
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        fn()
+        for s in syncs:
+            s()
+
+
+def _timed(b, fn, reps, reset=False, ramp_ms=0.0):
     """mean ms of fn() over reps, HIP-synchronised around the loop (device work on the batch stream);
-    reset: the batch's kernel timing starts after the warm-up call too."""
+    reset: the batch's kernel timing starts after the warm-up call too; ramp_ms: untimed calls first (ramp)."""
     fn()
     b.sync()
+    ramp(fn, (b.sync,), ramp_ms)
     if reset:
         b.reset_timing()
     t0 = time.perf_counter()
@@ -321,7 +335,7 @@ def extras(b, args, with_cpu, first=0):
     ex = {}
     px = b.frames * H * W
     n2 = int(b.read_counts()[:, 2].sum())
-    ms = _timed(b, lambda: (b.road_raster(sync=False), b.nonzero(sync=False)), 3)
+    ms = _timed(b, lambda: (b.road_raster(sync=False), b.nonzero(sync=False)), 3, ramp_ms=args.ramp_ms / 3)
     # one pass (road_kernel): the points in (8 B each), the images out once, 8 B per non-zero pixel out (at most
     # one per point: counted as one per point, so approx_GBps is an upper bound)
     byts = 8 * n2 + px + 8 * n2
@@ -329,7 +343,7 @@ def extras(b, args, with_cpu, first=0):
                                  "points": n2, "kernels": "road_kernel (raster + non-zero walk in one pass)"}
     mask = carmask()
     b.set_mask(mask)
-    ms = _timed(b, lambda: b.prepass("previous", sync=False), 3)
+    ms = _timed(b, lambda: b.prepass("previous", sync=False), 3, ramp_ms=args.ramp_ms / 3)
     # fillDisparity's recurrence: the disparity read, the cleaned frame written in place (maskDisparity is applied
     # by maskpoints as it reads the cleaned frame, not materialised)
     ex["prepass_fill_previous"] = {"ms_per_batch": round(ms, 3), "GBps": round(2 * px / ms / 1e6, 1),
@@ -361,7 +375,7 @@ def extras(b, args, with_cpu, first=0):
     ex["ransac_dropin"] = r
     # batched RANSAC of every frame (maskpoints + seeded CPython-random replay on the device), then the
     # pipeline driven by each frame's own plane: stereovision.py:84-113 for the whole batch
-    ms = _timed(b, lambda: b.ransac(seed_base=0, trials=600, sync=False), 2)
+    ms = _timed(b, lambda: b.ransac(seed_base=0, trials=600, sync=False), 2, ramp_ms=args.ramp_ms / 3)
     rb = {"frames": b.frames, "trials": 600, "ms_per_batch": round(ms, 2),
           "us_per_frame": round(ms / b.frames * 1e3, 2), "kernels": "maskpoints_kernel + ransac_draw_kernel + ransac_eval_kernel",
           "rng": "random.seed(frame) per frame"}
@@ -370,7 +384,7 @@ def extras(b, args, with_cpu, first=0):
     ex["ransac_batch"] = rb
     # the first call after the RANSAC batch is a warm-up (6.9-7.0 ms against 6.5-6.7 for the calls after it,
     # profiles/r02/bench_session8_resident_dispatches.json), excluded from both clocks like the headline's
-    ms = _timed(b, lambda: b.pipeline_planes(sync=False), 5, reset=True)
+    ms = _timed(b, lambda: b.pipeline_planes(sync=False), 5, reset=True, ramp_ms=args.ramp_ms)
     k_ms, k_n = b.timing("pipeline")
     kept = int(b.read_counts()[:, 2].sum())
     fp_bytes = 4 * b.Ng * b.frames + 20 * kept + 4096 * b.frames   # the config-4 accounting, this call's points
@@ -645,6 +659,9 @@ def main(argv=None):
         else:
             def pipe_step():
                 batches[0].pipeline(plane=plane, chunk=args.chunk, sync=False)
+        pipe_step()   # the first call places the output planes (pipe_place)
+        sync_all()
+        ramp(pipe_step, (sync_all,), args.ramp_ms)
         for _ in range(max(1, args.warmup)):
             pipe_step()
         for b in batches:

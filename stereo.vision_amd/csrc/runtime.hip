@@ -714,39 +714,49 @@ static hipError_t pipe_place(sv_batch* b, const KParams& p, PipeBuffers bf, hipS
     if (tries <= 1) return hipSuccess;
     std::vector<std::array<DevBuf, 5>> sets((size_t)tries);
     sets[0] = {b->oxb, b->oyb, b->ozb, b->ppx, b->ppy};
-    int best = -1;
-    float best_ms = 0.f;
+    std::vector<float> set_ms((size_t)tries, 0.f);
+    int placed = tries;   // sets allocated
     hipError_t e = hipSuccess;
-    for (int t = 0; t < tries && e == hipSuccess; ++t) {
-        auto& c = sets[(size_t)t];
-        for (int k = 0; k < 5 && e == hipSuccess && t > 0; ++k) e = c[k].ensure(plane, false, 4);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            e = hipSuccess;
-            break;
-        }
-        bf.ox = c[0].as<float>();
-        bf.oy = c[1].as<float>();
-        bf.oz = c[2].as<float>();
-        bf.ofs = (int64_t)b->cap;
-        bf.px = c[3].as<int32_t>();
-        bf.py = c[4].as<int32_t>();
-        float ms = 0.f;
-        for (int rep = 0; rep < 2 && e == hipSuccess; ++rep) {   // the second call is timed
-            e = hipEventRecord(b->ev[0], s);
-            if (e == hipSuccess) e = launch_pipeline_resident(p, bf, b->frames, true, s, true);
-            if (e == hipSuccess) e = hipEventRecord(b->ev[1], s);
-            if (e == hipSuccess) e = hipEventSynchronize(b->ev[1]);
-            if (e == hipSuccess) e = hipEventElapsedTime(&ms, b->ev[0], b->ev[1]);
-        }
-        if (e != hipSuccess) break;
-        if (svx_knob("SVX_CONTIG_LOG")) std::fprintf(stderr, "svx: pipeline placement %d: %.3f ms\n", t, ms);
-        if (best < 0 || ms < best_ms) {
-            best = t;
-            best_ms = ms;
+    // Two passes over the sets, each set's time the faster of its two timed calls: the kernel speeds up over
+    // its first calls on a cold GPU (clocks; 6.8-7.0 -> 5.8 ms), which a single pass in set order would charge
+    // to the first sets.
+    for (int pass = 0; pass < 2 && e == hipSuccess; ++pass) {
+        for (int t = 0; t < placed && e == hipSuccess; ++t) {
+            auto& c = sets[(size_t)t];
+            for (int k = 0; k < 5 && e == hipSuccess && t > 0 && pass == 0; ++k) e = c[k].ensure(plane, false, 4);
+            if (e != hipSuccess) {   // out of memory: place among the sets held so far
+                (void)hipGetLastError();
+                for (int k = 0; k < 5; ++k)
+                    if (c[k].p) {
+                        (void)hipFree(c[k].p);
+                        c[k] = DevBuf();
+                    }
+                e = hipSuccess;
+                placed = t;
+                break;
+            }
+            bf.ox = c[0].as<float>();
+            bf.oy = c[1].as<float>();
+            bf.oz = c[2].as<float>();
+            bf.ofs = (int64_t)b->cap;
+            bf.px = c[3].as<int32_t>();
+            bf.py = c[4].as<int32_t>();
+            float ms = 0.f;
+            for (int rep = pass == 0 ? 0 : 1; rep < 2 && e == hipSuccess; ++rep) {   // the last call is timed
+                e = hipEventRecord(b->ev[0], s);
+                if (e == hipSuccess) e = launch_pipeline_resident(p, bf, b->frames, true, s, true);
+                if (e == hipSuccess) e = hipEventRecord(b->ev[1], s);
+                if (e == hipSuccess) e = hipEventSynchronize(b->ev[1]);
+                if (e == hipSuccess) e = hipEventElapsedTime(&ms, b->ev[0], b->ev[1]);
+            }
+            if (e != hipSuccess) break;
+            if (svx_knob("SVX_CONTIG_LOG")) std::fprintf(stderr, "svx: pipeline placement %d: %.3f ms\n", t, ms);
+            set_ms[(size_t)t] = pass == 0 ? ms : std::min(set_ms[(size_t)t], ms);
         }
     }
-    if (best < 0) best = 0;
+    int best = 0;
+    for (int t = 1; t < placed; ++t)
+        if (set_ms[(size_t)t] < set_ms[(size_t)best]) best = t;
     for (int t = 0; t < (int)sets.size(); ++t)
         for (int k = 0; k < 5; ++k) {
             DevBuf& x = sets[(size_t)t][k];
