@@ -359,6 +359,7 @@ struct P2Regs {
     uint32_t fx[kRDN / 8], fy;   // the chunk's staged delta words (this lane's share)
     int dlo, ywb;                // first staged disparity; the chunk's 32-row word
     bool narrow;                 // the chunk's keep1 range and rows fit the stage
+    bool staged, reuse;          // a window is staged in LDS; this chunk reuses it (no loads, no stage writes)
 };
 
 template <int STEP, int QP, bool LC>
@@ -389,6 +390,15 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP, LC>& r, int c, int tid,
     constexpr int per = RCfg<STEP, QP, LC>::QPL * 256;   // quads per chunk
     const int ywb = (fastdiv40(c * per, p.Q_m40) * STEP) >> 5;
     const int ywl = (fastdiv40(min((c + 1) * per, p.frame_quads) - 1, p.Q_m40) * STEP) >> 5;
+    // the window staged for the last chunk pass 2 ran still covers this one (same row word, keep1 range inside):
+    // no delta loads and no stage writes (8192: DIAGNOSTIC A/B, always reload)
+    r.reuse = !(p.ablate & 8192) && r.staged && !(p.ablate & 1024) && p.dx_words <= 32 && ywl == ywb &&
+              ywb == r.ywb && dmn >= r.dlo && dmx < r.dlo + kRDN;
+    if (r.reuse) {
+        r.narrow = true;
+        return;
+    }
+    r.staged = true;
     r.dlo = dlo;
     r.ywb = ywb;
     r.narrow = !(p.ablate & 1024) && p.dx_words <= 32 && dmx - dlo < kRDN && ywl == ywb;   // 1024: DIAGNOSTIC A/B
@@ -557,7 +567,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
     // this chunk's delta words into LDS, read by its scatter after the next
     // barrier (every wave has finished chunk c - 1's scatter)
     uint32_t* dl = sh.dlt;
-    p2_stage_deltas<STEP, QP, LC>(r, dl);
+    if (!r.reuse) p2_stage_deltas<STEP, QP, LC>(r, dl);
     const int dlo = r.dlo;
     const bool narrow = r.narrow;
     if ((dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: candidate chunk (rare)
@@ -787,6 +797,7 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     };
     const uint16_t* fkb = bf.kbits + (int64_t)frame * p.nchunks * 256;
     P2Regs<STEP, QP, LC> r2;
+    r2.staged = false;
     if (PF && n2 > 0) p2_load<STEP, QP, LC>(r2, 0, tid, fdisp, sh.crange, bf, p, false, run(0), fkb);
     for (int c = 0; c < n2; ++c) {
         if (!PF) p2_load<STEP, QP, LC>(r2, c, tid, fdisp, sh.crange, bf, p, c > 0, run(c), fkb);
