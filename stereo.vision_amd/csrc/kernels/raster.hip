@@ -18,6 +18,7 @@
 namespace svx {
 
 typedef int v2i __attribute__((ext_vector_type(2)));
+typedef int v4i __attribute__((ext_vector_type(4)));
 
 // point i of frame f: x = px[(f cap + i) * ps], y = py[(f cap + i) * ps] (ps = 1: the pipeline's two planes;
 // ps = 2: interleaved (x, y) pairs); counts[frame * cstride + cidx] = points of the frame
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
                                                    uint8_t* __restrict__ img, int H, int W, int Wu, int R,
                                                    uint64_t W_m40, int32_t* __restrict__ nzout,
                                                    int64_t* __restrict__ nzcount, const uint8_t* __restrict__ bgr,
-                                                   uint8_t* __restrict__ paint) {
+                                                   uint8_t* __restrict__ paint, bool vec) {
     __shared__ RoadShared sh;
     extern __shared__ uint4 road_band[];   // the band: R rows of W bytes (dynamic LDS)
     uint8_t* const band = reinterpret_cast<uint8_t*>(road_band);
@@ -166,14 +167,23 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
     uint8_t* fimg = img + (int64_t)frame * H * W;
     int2* fo = reinterpret_cast<int2*>(nzout) + (int64_t)frame * cap;
     if (tid < 128) sh.wrap[tid] = 0;
-    // this lane's kRoadPts points of the 256 * kRoadPts-point chunk at i0 (qy = -2: past the list)
+    // this lane's kRoadPts consecutive points of the 256 * kRoadPts-point chunk at i0 (qy = -2: past the
+    // list): one 16-byte load per plane when the planes are 16-byte aligned (vec), 4-byte loads at the list's end
+    static_assert(kRoadPts == 4, "one int4 of x and one of y per lane");
     const auto load = [&](int64_t i0, int (&qx)[kRoadPts], int (&qy)[kRoadPts]) {
+        const int64_t i = i0 + kRoadPts * tid;
+        if (vec && i + kRoadPts <= n) {
+            const int4 vx = *reinterpret_cast<const int4*>(fx + i);
+            const int4 vy = *reinterpret_cast<const int4*>(fy + i);
+            qx[0] = vx.x, qx[1] = vx.y, qx[2] = vx.z, qx[3] = vx.w;
+            qy[0] = vy.x, qy[1] = vy.y, qy[2] = vy.z, qy[3] = vy.w;
+        } else {
 #pragma unroll
-        for (int t = 0; t < kRoadPts; ++t) {
-            const int64_t i = i0 + t * 256 + tid;
-            const bool ok = i < n;
-            qx[t] = ok ? fx[i] : 0;
-            qy[t] = ok ? fy[i] : -2;
+            for (int t = 0; t < kRoadPts; ++t) {
+                const bool ok = i + t < n;
+                qx[t] = ok ? fx[i + t] : 0;
+                qy[t] = ok ? fy[i + t] : -2;
+            }
         }
     };
     int64_t cur = 0;
@@ -284,10 +294,22 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
             }
             __syncthreads();   // sh.wtot is rewritten next chunk; sh.stage is complete
             v2i* dst = reinterpret_cast<v2i*>(fo + running);
-            for (uint32_t j = tid; j < tot; j += 256) {
-                const uint32_t p = sh.stage[j];
+            const auto xy = [&](uint32_t p) {
                 const int y = fastdiv40((int)p, W_m40);
-                __builtin_nontemporal_store((v2i){(int)(p - (uint32_t)y * (uint32_t)W), y}, dst + j);
+                return (v2i){(int)(p - (uint32_t)y * (uint32_t)W), y};
+            };
+            if (vec) {   // two outputs a lane, 16-byte stores: output `running` alone when it is odd, the last alone when left over
+                const uint32_t lead = (running & 1u) && tot > 0 ? 1u : 0u;
+                const uint32_t pairs = (tot - lead) / 2;
+                if (lead && tid == 0) __builtin_nontemporal_store(xy(sh.stage[0]), dst);
+                for (uint32_t m = tid; m < pairs; m += 256) {
+                    const uint32_t j = lead + 2 * m;
+                    const v2i a = xy(sh.stage[j]), b2 = xy(sh.stage[j + 1]);
+                    __builtin_nontemporal_store((v4i){a.x, a.y, b2.x, b2.y}, reinterpret_cast<v4i*>(dst + j));
+                }
+                if (((tot - lead) & 1u) && tid == 0) __builtin_nontemporal_store(xy(sh.stage[tot - 1]), dst + tot - 1);
+            } else {
+                for (uint32_t j = tid; j < tot; j += 256) __builtin_nontemporal_store(xy(sh.stage[j]), dst + j);
             }
             running += tot;
         }
@@ -307,8 +329,12 @@ hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* coun
     const size_t dyn = ((size_t)R * W + 15) / 16 * 16;
     if (dyn > 65536 || (paint && (!bgr || (size_t)R * W * 3 >= 98304))) return hipErrorInvalidValue;
     const uint64_t m40 = (((uint64_t)1 << 40) + (uint64_t)W - 1) / (uint64_t)W;
+    // vec: the point planes and the walk's output 16-byte aligned at every frame (cap % 4 == 0), so a lane takes
+    // its 4 points with one load per plane and writes two walk outputs with one store
+    const bool vec = cap % 4 == 0 && ((reinterpret_cast<uintptr_t>(px) | reinterpret_cast<uintptr_t>(py) |
+                                       reinterpret_cast<uintptr_t>(nzout)) & 15u) == 0;
     hipLaunchKernelGGL(road_kernel, dim3(frames), dim3(256), dyn, s, px, py, counts, cap, img, H, W, Wu, R, m40, nzout,
-                       nzcount, bgr, paint);
+                       nzcount, bgr, paint, vec);
     return hipGetLastError();
 }
 
