@@ -557,8 +557,16 @@ def main(argv=None):
     shards = shards_of(pl, args.frames, args.global_frames)
     strong = args.global_frames > 0
     comm = mcomm = None
+    comm_note = None
     if pl["mode"] == "ranks":   # RCCL over every rank (also at world size 1: the collective path runs)
-        comm = dist.RcclComm(ctrl, pl["devices"][0])
+        try:
+            comm = dist.RcclComm(ctrl, pl["devices"][0])
+        except svx.SvxError as e:   # every rank fails alike (a collective init): fall back, say so in the line
+            comm_note = f"RCCL communicator unavailable ({e}); rank 0's plane sent over the host control plane"
+        if ctrl.sum([0.0 if comm else 1.0])[0] > 0 and comm:
+            comm.close()
+            comm = None
+            comm_note = comm_note or "RCCL communicator failed on another rank; plane over the host control plane"
     elif pl["mode"] == "multi":
         mcomm = dist.MultiComm(pl["devices"])
 
@@ -656,7 +664,10 @@ def main(argv=None):
         elif mcomm:
             def pipe_step():
                 mcomm.pipeline(batches, plane, root=0)
-        else:
+        else:   # one GPU, or ranks without RCCL: rank 0's plane (the same synthetic plane) over the control plane
+            if pl["mode"] == "ranks":
+                plane = tuple(float(v) for v in ctrl.sum(np.asarray(plane, np.float64) * (pl["rank"] == 0)))
+
             def pipe_step():
                 batches[0].pipeline(plane=plane, chunk=args.chunk, sync=False)
         pipe_step()   # the first call places the output planes (pipe_place)
@@ -687,9 +698,10 @@ def main(argv=None):
                           "in pass 2, the disparity) of chunks the plane rules out, so it moves fewer bytes "
                           "(traffic = PMC bytes per call, frac_of_traffic = traffic / time / peak)",
             "counts_total": {"valid": int(counts[0]), "kept": int(counts[1]), "kept2": int(counts[2])},
-            "plane_broadcast": {"ranks": "RCCL ncclBroadcast into device memory every step (sv_comm_broadcast_plane_dev)",
-                                "multi": "RCCL grouped ncclBroadcast to every device every step (sv_multi_pipeline)",
-                                "single": "host plane (single GPU)"}[pl["mode"]],
+            "plane_broadcast": comm_note or {
+                "ranks": "RCCL ncclBroadcast into device memory every step (sv_comm_broadcast_plane_dev)",
+                "multi": "RCCL grouped ncclBroadcast to every device every step (sv_multi_pipeline)",
+                "single": "host plane (single GPU)"}[pl["mode"]],
             "kernels": "resident_fused_kernel (one workgroup per frame, keep1 from the plane in device memory)"
                        if frames_gpu >= 512 else "tiled: stage_kernel + offsets_kernel",
         }

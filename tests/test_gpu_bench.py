@@ -74,3 +74,23 @@ def test_bench_strong_scaling_flag(monkeypatch):
     out = bench.main([a for a in ARGS if a not in ("--frames", "512")] + ["--global-frames", "512"])
     _check(out)
     assert out["scaling"] == "strong" and out["config"]["global_frames"] == 512
+
+
+def test_bench_ranks_without_rccl(monkeypatch):
+    """"ranks" mode when the RCCL communicator cannot be made (every rank fails alike, a collective init): the
+    bench still measures, with rank 0's plane over the host control plane, and says so in its line."""
+    import bench
+    from svx import SvxError, dist
+
+    def fail(self, *a, **k):
+        raise SvxError("simulated ncclCommInitRank failure")
+
+    monkeypatch.setattr(dist.RcclComm, "__init__", fail)
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "29532")
+    out = bench.main(ARGS)
+    _check(out)
+    assert out["pipeline"]["plane_broadcast"].startswith("RCCL communicator unavailable")
