@@ -46,7 +46,14 @@ constexpr int kRBins = 1000;    // bins 0..999: t < 1000 - 1000/(6*255) so rint(
 constexpr int kRDN = 32;
 constexpr int kRDxStride = 33;
 constexpr int kRDyOff = kRDN * kRDxStride;
-constexpr int kRDeltaWords = kRDyOff + kRDN;
+// Lane-contiguous quads (LC) stage the same window transposed, from dxT / dyT (tables.hip): one word per
+// x whose bit dd is the delta bit of d = dlo + dd, in groups of 16 x at a stride of 20 words (16-byte aligned,
+// so a lane's 16 consecutive x are four ds_read_b128 without bank conflicts between its 8-lane groups), then
+// one word per row of the chunk's 32-row word. A lane's 16 points then cost four LDS reads for dx and one
+// for dy instead of 16 + 16.
+constexpr int kRTxGroup = 20;
+constexpr int kRTyOff = 64 * kRTxGroup;   // x < 1024 (dx_words <= 32)
+constexpr int kRDeltaWords = kRTyOff + 32 > kRDyOff + kRDN ? kRTyOff + 32 : kRDyOff + kRDN;
 
 // both 16-bit halves: max (v_pk_max_u16)
 __device__ __forceinline__ uint32_t pk_max16(uint32_t a, uint32_t b) {
@@ -357,6 +364,7 @@ struct P2Regs {
     uint32_t dw[RCfg<STEP, QP, LC>::QPL][STEP];
     uint32_t kb;                 // step 1: the keep1 bits of pass 1 (step 2 evaluates keep1 again)
     uint32_t fx[kRDN / 8], fy;   // the chunk's staged delta words (this lane's share)
+    uint32_t fx2[4], fy2;        // LC: the transposed window's next words (funnel-shifted with fx, fy)
     int dlo, ywb;                // first staged disparity; the chunk's 32-row word
     bool narrow;                 // the chunk's keep1 range and rows fit the stage
     bool staged, reuse;          // a window is staged in LDS; this chunk reuses it (no loads, no stage writes)
@@ -402,10 +410,23 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP, LC>& r, int c, int tid,
     r.dlo = dlo;
     r.ywb = ywb;
     r.narrow = !(p.ablate & 1024) && p.dx_words <= 32 && dmx - dlo < kRDN && ywl == ywb;   // 1024: DIAGNOSTIC A/B
-    const int xw = min(tid & 31, p.dx_words - 1);
+    if constexpr (LC) {   // transposed: words dlo >> 5 and the next of x = 4 tid .. 4 tid + 3 and of row 32 ywb + tid
+        const int j0 = dlo >> 5, j1 = min(j0 + 1, 7);
+        const int nx = 32 * p.dx_words, ny = 32 * p.dy_words;
+        const int x4 = min(4 * tid, nx - 4);   // nx is a multiple of 32
+        const uint4 a = *reinterpret_cast<const uint4*>(bf.dxT + j0 * nx + x4);
+        const uint4 b = *reinterpret_cast<const uint4*>(bf.dxT + j1 * nx + x4);
+        r.fx[0] = a.x, r.fx[1] = a.y, r.fx[2] = a.z, r.fx[3] = a.w;
+        r.fx2[0] = b.x, r.fx2[1] = b.y, r.fx2[2] = b.z, r.fx2[3] = b.w;
+        const int yr = min(32 * ywb + (tid & 31), ny - 1);
+        r.fy = bf.dyT[j0 * ny + yr];
+        r.fy2 = bf.dyT[j1 * ny + yr];
+    } else {
+        const int xw = min(tid & 31, p.dx_words - 1);
 #pragma unroll
-    for (int j = 0; j < kRDN / 8; ++j) r.fx[j] = bf.dxbits[(dlo + 8 * j + (tid >> 5)) * p.dx_words + xw];
-    r.fy = bf.dybits[(dlo + (tid & (kRDN - 1))) * p.dy_words + min(ywb, p.dy_words - 1)];
+        for (int j = 0; j < kRDN / 8; ++j) r.fx[j] = bf.dxbits[(dlo + 8 * j + (tid >> 5)) * p.dx_words + xw];
+        r.fy = bf.dybits[(dlo + (tid & (kRDN - 1))) * p.dy_words + min(ywb, p.dy_words - 1)];
+    }
 }
 
 // stage the chunk's delta words (loaded by p2_load) into dl: dx word (d, xw) at
@@ -413,9 +434,20 @@ __device__ __forceinline__ void p2_load(P2Regs<STEP, QP, LC>& r, int c, int tid,
 template <int STEP, int QP, bool LC>
 __device__ __forceinline__ void p2_stage_deltas(const P2Regs<STEP, QP, LC>& r, uint32_t* dl) {
     const int tid = threadIdx.x;
+    if constexpr (LC) {   // x = 4 tid .. 4 tid + 3: bits dlo .. dlo + 31 of each x's 256-bit row
+        const uint32_t sh = (uint32_t)(r.dlo & 31);
+        uint4 w;
+        w.x = __builtin_amdgcn_alignbit(r.fx2[0], r.fx[0], sh);
+        w.y = __builtin_amdgcn_alignbit(r.fx2[1], r.fx[1], sh);
+        w.z = __builtin_amdgcn_alignbit(r.fx2[2], r.fx[2], sh);
+        w.w = __builtin_amdgcn_alignbit(r.fx2[3], r.fx[3], sh);
+        *reinterpret_cast<uint4*>(dl + (tid >> 2) * kRTxGroup + 4 * (tid & 3)) = w;
+        if (tid < 32) dl[kRTyOff + tid] = __builtin_amdgcn_alignbit(r.fy2, r.fy, sh);
+    } else {
 #pragma unroll
-    for (int j = 0; j < kRDN / 8; ++j) dl[(8 * j + (tid >> 5)) * kRDxStride + (tid & 31)] = r.fx[j];
-    if (tid < kRDN) dl[kRDyOff + tid] = r.fy;
+        for (int j = 0; j < kRDN / 8; ++j) dl[(8 * j + (tid >> 5)) * kRDxStride + (tid & 31)] = r.fx[j];
+        if (tid < kRDN) dl[kRDyOff + tid] = r.fy;
+    }
 }
 
 // this wave's keep1 disparity range of the chunk as (255 - dmin) << 16 | dmax
@@ -630,6 +662,8 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
     // branch-free: a slot that is not kept writes to this lane's dump word
     uint32_t rowbase = running;
     uint32_t olc = running + (uint32_t)excl;   // LC: the lane's outputs are one run
+    // LC, narrow: the lane's one row's transposed dy word (bit dd = the dy bit of d = dlo + dd)
+    const uint32_t tyl = (LC && narrow) ? dl[kRTyOff + (((uint32_t)max(r.g.gy[0], 0) * STEP) & 31u)] : 0u;
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
         uint32_t o = LC ? olc : rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
@@ -638,7 +672,17 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
         uint32_t dv[4], bx[4], by[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) dv[k] = r_d<STEP, QP, LC>(r.dw[i], k);
-        if (narrow) {   // uniform: every kept d in [dlo, dlo + kRDN), the chunk's rows in word ywb
+        if (narrow && LC) {   // uniform; transposed stage: the lane's 16 x are 4 quads of one row (x0 % 16 == 0)
+            const uint32_t x0 = 4u * (uint32_t)r.g.q[0];
+            const uint4 tw = *reinterpret_cast<const uint4*>(dl + (x0 >> 4) * kRTxGroup + 4 * i);
+            const uint32_t t4[4] = {tw.x, tw.y, tw.z, tw.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t dd = min(dv[k] - (uint32_t)dlo, (uint32_t)kRDN - 1);   // clamp: slots not kept
+                bx[k] = (t4[k] >> dd) & 1u;
+                by[k] = (tyl >> dd) & 1u;
+            }
+        } else if (narrow) {   // uniform: every kept d in [dlo, dlo + kRDN), the chunk's rows in word ywb
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t dd = min(dv[k] - (uint32_t)dlo, (uint32_t)kRDN - 1);   // clamp: slots not kept

@@ -64,4 +64,31 @@ hipError_t launch_delta_tables(const KParams& p, uint32_t* dxbits, uint32_t* dyb
     return hipGetLastError();
 }
 
+// One lane per (j, coordinate) of either transposed table: bit b of the word = the delta bit of d = 32 j + b.
+__global__ __launch_bounds__(256) void delta_transpose_kernel(const uint32_t* __restrict__ dxbits,
+                                                              const uint32_t* __restrict__ dybits,
+                                                              uint32_t* __restrict__ dxT, uint32_t* __restrict__ dyT,
+                                                              int dx_words, int dy_words) {
+    const int nx = 8 * 32 * dx_words, ny = 8 * 32 * dy_words;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nx + ny) return;
+    const bool is_x = i < nx;
+    const int j0 = is_x ? i : i - nx;
+    const int words = is_x ? dx_words : dy_words;
+    const int n = 32 * words;
+    const int j = j0 / n, c = j0 - j * n;
+    const uint32_t* src = is_x ? dxbits : dybits;
+    uint32_t bits = 0;
+    for (int b = 0; b < 32; ++b) bits |= ((src[(32 * j + b) * words + (c >> 5)] >> (c & 31)) & 1u) << b;
+    (is_x ? dxT : dyT)[j0] = bits;
+}
+
+hipError_t launch_delta_transpose(const KParams& p, const uint32_t* dxbits, const uint32_t* dybits, uint32_t* dxT,
+                                  uint32_t* dyT, hipStream_t s) {
+    const int n = 8 * 32 * (p.dx_words + p.dy_words);
+    hipLaunchKernelGGL(delta_transpose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dxbits, dybits, dxT, dyT,
+                       p.dx_words, p.dy_words);
+    return hipGetLastError();
+}
+
 }  // namespace svx

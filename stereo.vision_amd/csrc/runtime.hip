@@ -125,6 +125,7 @@ struct Tables {
     int H = 0, W = 0;
     sv_camera cam{};
     DevBuf dx, dy;
+    DevBuf dxT, dyT;   // transposed (launch_delta_transpose): the resident pipeline's lane-contiguous delta stage
 };
 
 struct Device {
@@ -226,6 +227,10 @@ int ensure_tables(Device& d, int H, int W, const sv_camera& cam, hipStream_t s) 
     HIP_TRY(t.dx.ensure(sizeof(uint32_t) * 256 * p.dx_words));
     HIP_TRY(t.dy.ensure(sizeof(uint32_t) * 256 * p.dy_words));
     HIP_TRY(launch_delta_tables(p, t.dx.as<uint32_t>(), t.dy.as<uint32_t>(), nullptr, nullptr, s));
+    HIP_TRY(t.dxT.ensure(sizeof(uint32_t) * 8 * 32 * p.dx_words));
+    HIP_TRY(t.dyT.ensure(sizeof(uint32_t) * 8 * 32 * p.dy_words));
+    HIP_TRY(launch_delta_transpose(p, t.dx.as<uint32_t>(), t.dy.as<uint32_t>(), t.dxT.as<uint32_t>(),
+                                   t.dyT.as<uint32_t>(), s));
     HIP_TRY(hipStreamSynchronize(s));
     t.valid = true;
     t.H = H;
@@ -798,6 +803,8 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     point_planes(b, bf);
     bf.dxbits = d->tables.dx.as<uint32_t>();
     bf.dybits = d->tables.dy.as<uint32_t>();
+    bf.dxT = d->tables.dxT.as<uint32_t>();
+    bf.dyT = d->tables.dyT.as<uint32_t>();
     bf.planes = planes;
     bf.plane_stride = plane_stride;
     int mode = b->pipe_mode;

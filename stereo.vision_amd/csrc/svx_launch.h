@@ -25,6 +25,9 @@ int project_compact_tiles(const KParams& p);
 // kernels/tables.hip --------------------------------------------------------
 hipError_t launch_hue_lut(int16_t* lut, hipStream_t s);
 // dx bits [256][dx_words], dy bits [256][dy_words]; optional int8 tables.
+// dxT / dyT (PipeBuffers) from dxbits / dybits: 8 x 32 dx_words + 8 x 32 dy_words words
+hipError_t launch_delta_transpose(const KParams& p, const uint32_t* dxbits, const uint32_t* dybits, uint32_t* dxT,
+                                  uint32_t* dyT, hipStream_t s);
 hipError_t launch_delta_tables(const KParams& p, uint32_t* dxbits, uint32_t* dybits, int8_t* dx8,
                                int8_t* dy8, hipStream_t s);
 
@@ -46,6 +49,10 @@ struct PipeBuffers {
     int32_t* py;         //   (frame f's at f * cap)
     const uint32_t* dxbits;
     const uint32_t* dybits;
+    // the same bits transposed: word j of coordinate c holds d = 32 j .. 32 j + 31 (bit d mod 32), as
+    // dxT[j * 32 dx_words + x] and dyT[j * 32 dy_words + y] (launch_delta_transpose)
+    const uint32_t* dxT = nullptr;
+    const uint32_t* dyT = nullptr;
     int64_t cap;         // points per frame (Ng)
     const FramePlane* planes = nullptr;   // device planes: frame f uses planes[f * plane_stride] (else the KParams plane)
     int plane_stride = 1;                 // 0: one device plane for every frame (a broadcast plane)
