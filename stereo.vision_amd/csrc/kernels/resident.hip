@@ -498,10 +498,22 @@ __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP, LC>& r, int c, u
     }
     uint32_t pos0;
     bool cand = false;
-    {
+    // a point is a candidate while its bin holds fewer than hist_thr points (never for hist_thr < 0)
+    const uint32_t lim = p.hist_thr < 0 ? 0u : (uint32_t)p.hist_thr;
+    constexpr int NPL = 4 * RCfg<STEP, QP, LC>::QPL;   // grid points a lane holds
+    if (!(p.ablate & 16384) && wave_sum((uint32_t)__builtin_popcount(keep)) * 4u >= 3u * 64u * NPL) {
+        // uniform: a dense wave (>= 3/4 of its points kept, the road) bins its colours from registers, each lane
+        // its own kept points in turn: at most 1/4 of the lanes idle, and no LDS staging writes and reads
+        // (16384: DIAGNOSTIC A/B, always stage)
+#pragma unroll
+        for (int b = 0; b < NPL; ++b) {
+            if ((keep >> b) & 1u) {
+                const uint32_t o = atomicAdd(&hist[r_bin_sel(r_col<STEP, QP, LC>(r.cw[b >> 2], b & 3))], 1u);
+                cand |= o < lim;
+            }
+        }
+    } else {
         const uint32_t wtotal = r_stage_colours_sel<STEP, QP, LC>(keep, r.cw, wstage, dump, pos0);
-        // a point is a candidate while its bin holds fewer than hist_thr points (never for hist_thr < 0)
-        const uint32_t lim = p.hist_thr < 0 ? 0u : (uint32_t)p.hist_thr;
         for (uint32_t j = lane; j < ((p.ablate & 512) ? 0u : wtotal); j += 2 * kWave) {   // two colours in flight
             const bool v1 = j + kWave < wtotal;
             const uint32_t c0 = wstage[j];
