@@ -501,7 +501,9 @@ __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP, LC>& r, int c, u
     // a point is a candidate while its bin holds fewer than hist_thr points (never for hist_thr < 0)
     const uint32_t lim = p.hist_thr < 0 ? 0u : (uint32_t)p.hist_thr;
     constexpr int NPL = 4 * RCfg<STEP, QP, LC>::QPL;   // grid points a lane holds
-    if (!(p.ablate & 16384) && wave_sum((uint32_t)__builtin_popcount(keep)) * 4u >= 3u * 64u * NPL) {
+    // density threshold in eighths (DIAGNOSTIC A/B: ablate bits 15-16 pick 6, 4, 5 or 7; release: 6)
+    const uint32_t dense8 = (0x7546u >> (4 * ((p.ablate >> 15) & 3))) & 0xFu;
+    if (!(p.ablate & 16384) && wave_sum((uint32_t)__builtin_popcount(keep)) * 8u >= dense8 * 64u * NPL) {
         // uniform: a dense wave (>= 3/4 of its points kept, the road) bins its colours from registers, each lane
         // its own kept points in turn: at most 1/4 of the lanes idle, and no LDS staging writes and reads
         // (16384: DIAGNOSTIC A/B, always stage)
