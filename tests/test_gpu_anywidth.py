@@ -142,3 +142,26 @@ def test_synth_and_sgbm_batch_need_aligned_width(sv):
             b.synth(0)
         with pytest.raises(sv.svx.SvxError):
             b.synth_pair(0)
+
+
+@pytest.mark.parametrize("shape", [(300, 512), (300, 784), (291, 1024), (270, 16), (280, 1280)])
+def test_resident_lane_contiguous_widths(sv, shape):
+    """Widths that take the resident kernel's lane-contiguous layout (W % 16 == 0) and its transposed delta
+    stage (dx_words <= 32; 1280 columns read the tables in memory): synthetic frames of that size, whose road
+    rows keep chunks of a narrow disparity range under the synthetic plane, against the oracle point for point
+    (functions.py:178-230, :201-209)."""
+    H, W = shape
+    frames = 3
+    data = [oracle.synth_frame(40 + f, H, W) for f in range(frames)]
+    plane = (0.0, 2.8699791779470996, 0.444875113548583)
+    with sv.batch.Batch(frames, H, W, step=1, with_bgr=True, with_points=True) as b:
+        b.pipeline_mode("resident")
+        for f, (d, c) in enumerate(data):
+            b.upload(f, d, c)
+        b.pipeline(plane=plane, point_thr=0.05, hist_thr=10)
+        counts = b.read_counts()
+        for f, (d, c) in enumerate(data):
+            ref = oracle.pipeline_frame(d, c, 1, abc=np.array(plane), point_thr=0.05, hist_thr=10)
+            assert ref["counts"][1] > 0   # keep1 points (at 16 columns the histogram may drop them all)
+            xyz, pts = b.read_points(f)
+            check(dict(counts=tuple(int(v) for v in counts[f]), hist=b.read_hist(f), pts=pts, xyz2=xyz), ref)
