@@ -106,16 +106,43 @@ class RcclComm:
     """RCCL communicator of one rank (sv_comm_* in libsvx), one process per GPU."""
 
     def __init__(self, ctrl, device):
+        """Every rank agrees on the outcome of each setup step (ctrl.sum of a failure flag) before the next
+        collective one, so a failure on some ranks raises SvxError on all of them instead of leaving the others
+        waiting in a broadcast or in the collective init. (A rank that fails INSIDE ncclCommInitRank while the
+        others wait in it cannot be caught from here; the device check before it makes that unlikely.)"""
+        self._h = None
+        self.rank = ctrl.rank
         uid = (ctypes.c_uint8 * _abi.SV_UNIQUE_ID_BYTES)()
-        if ctrl.rank == 0:
-            _abi.call("sv_comm_unique_id", ctypes.cast(uid, ctypes.c_void_p))
+        err = None
+        try:
+            _abi.call("sv_init", device)   # the device is there and selectable, before any collective step
+            if ctrl.rank == 0:
+                _abi.call("sv_comm_unique_id", ctypes.cast(uid, ctypes.c_void_p))
+        except _abi.SvxError as e:
+            err = e
+        self._agree(ctrl, err, "device check / ncclGetUniqueId")
         data = ctrl.broadcast_bytes(bytes(uid), src=0)
         uid = (ctypes.c_uint8 * _abi.SV_UNIQUE_ID_BYTES).from_buffer_copy(data)
         h = ctypes.c_void_p()
-        _abi.call("sv_comm_init", ctrl.world, ctrl.rank, ctypes.cast(uid, ctypes.c_void_p), device,
-                  ctypes.byref(h))
-        self._h = h
-        self.rank = ctrl.rank
+        try:
+            _abi.call("sv_comm_init", ctrl.world, ctrl.rank, ctypes.cast(uid, ctypes.c_void_p), device,
+                      ctypes.byref(h))
+        except _abi.SvxError as e:
+            err = e
+        if err is None:
+            self._h = h
+        try:
+            self._agree(ctrl, err, "ncclCommInitRank")
+        except _abi.SvxError:
+            self.close()
+            raise
+
+    @staticmethod
+    def _agree(ctrl, err, step):
+        failed = int(ctrl.sum([0.0 if err is None else 1.0])[0])
+        if failed:
+            raise _abi.SvxError(f"RCCL {step} failed on {failed} of {ctrl.world} rank(s)"
+                                + (f"; this rank: {err}" if err is not None else ""))
 
     def broadcast_plane(self, plane, root=0):
         """Host round trip (reporting/tests)."""

@@ -230,23 +230,35 @@ from .stages import (calculateColourHistogram, calculatePointErrors, computePlan
                      filterPointsByHistogram)
 from .disparity import disparity, gammaChange, greyscale, preProcessImages  # noqa: E402,F401 (functions.py:61-128)
 
-PATCHED = ("projectDisparityTo3d", "project3DPointsTo2DImagePoints", "fillDisparity", "fillAltDisparity",
-           "maskDisparity", "capDisparity", "generatePointsAsImage", "RANSAC", "calculatePointErrors",
-           "computePlanarThreshold", "calculateColourHistogram", "filterPointsByHistogram", "gammaChange",
-           "preProcessImages", "greyscale", "disparity")
+# Functions whose GPU results are pinned against the reference itself (fixtures made by running the reference's
+# own code, tests/golden/): installed by default.
+PINNED = ("projectDisparityTo3d", "project3DPointsTo2DImagePoints", "fillAltDisparity", "capDisparity",
+          "generatePointsAsImage", "RANSAC", "calculatePointErrors", "computePlanarThreshold",
+          "calculateColourHistogram", "filterPointsByHistogram", "gammaChange", "preProcessImages")
+# Functions that restate OpenCV calls (cv2 is absent here, so nothing pins them to the reference's OpenCV 3.x):
+# StereoSGBM + filterSpeckles (functions.py:104-128), cvtColor + equalizeHist (:88-96), cv2.threshold / bitwise /
+# add (:140-147) and bitwise_and with the carmask (:169-171). Installed only on request (install(.., unpinned=True)).
+UNPINNED = ("disparity", "greyscale", "fillDisparity", "maskDisparity")
+PATCHED = PINNED + UNPINNED
 ALIASES = {"project_disparity_to_3d": "projectDisparityTo3d",
            "project_3D_points_to_2D": "project3DPointsTo2DImagePoints"}
 _saved = {}
 _ABSENT = object()
 
 
-def install(functions_module):
+def install(functions_module, unpinned=False):
     """Patch the reference's `functions` module in place (stereovision.py resolves
-    f.<name> at call time, so performStereoVision picks the GPU path up)."""
+    f.<name> at call time, so performStereoVision picks the GPU path up).
+
+    By default only the PINNED functions are replaced: the ones whose outputs equal the
+    reference's own on its fixtures. unpinned=True also replaces the UNPINNED ones, the
+    restatements of OpenCV (SGBM, grey + equalizeHist, fillDisparity, maskDisparity) whose
+    equality with the reference's cv2 cannot be checked here."""
     global _module
     _abi.lib()  # fail loudly now if libsvx is missing
     _module = functions_module
-    for name in PATCHED + tuple(ALIASES):
+    names = PINNED + (UNPINNED if unpinned else ()) + tuple(ALIASES)
+    for name in names:
         if name not in _saved:
             _saved[name] = getattr(functions_module, name, _ABSENT)
         setattr(functions_module, name, globals()[ALIASES.get(name, name)])

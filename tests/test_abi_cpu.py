@@ -105,6 +105,36 @@ def test_install_patches_module_attributes():
     assert (cam.f, cam.B, cam.cw, cam.ch) == dropin.DEFAULT_CAMERA
 
 
+def test_install_default_is_the_pinned_set():
+    """install(functions) replaces only the functions pinned against the reference's own outputs; the four
+    restatements of OpenCV (disparity, greyscale, fillDisparity, maskDisparity: functions.py:88-96,104-128,
+    140-147,169-171) stay the module's originals unless install(.., unpinned=True)."""
+    import types
+
+    from svx import dropin
+    orig = {name: (lambda *a, _n=name: _n) for name in dropin.PATCHED}
+    m = types.SimpleNamespace(camera_focal_length_px=1.0, stereo_camera_baseline_m=2.0,
+                              image_centre_w=3.0, image_centre_h=4.0, **orig)
+    assert set(dropin.UNPINNED) == {"disparity", "greyscale", "fillDisparity", "maskDisparity"}
+    dropin.install(m)
+    try:
+        for name in dropin.UNPINNED:
+            assert getattr(m, name) is orig[name], name
+        for name in dropin.PINNED:
+            assert getattr(m, name) is not orig[name], name
+    finally:
+        dropin.uninstall()
+    assert all(getattr(m, n) is orig[n] for n in dropin.PATCHED)
+    dropin.install(m, unpinned=True)
+    try:
+        for name in dropin.PATCHED:
+            assert getattr(m, name) is not orig[name], name
+        assert m.maskDisparity is dropin.maskDisparity and m.disparity is dropin.disparity
+    finally:
+        dropin.uninstall()
+    assert all(getattr(m, n) is orig[n] for n in dropin.PATCHED)
+
+
 def test_header_cites_reference():
     src = open(HEADER).read()
     for cite in ("functions.py:178-198", "functions.py:201-209", "stereovision.py:84"):

@@ -51,7 +51,7 @@ def test_mask_and_cap(svx_mod):
     m = carmask()
     d, _ = oracle.synth_frame(9)
     f = types.SimpleNamespace(carmask=m)
-    svx_mod.dropin.install(f)
+    svx_mod.dropin.install(f, unpinned=True)   # maskDisparity restates cv2 (not in the default set)
     try:
         assert np.array_equal(f.maskDisparity(d), oracle.mask_disparity(d, m))
         assert f.capDisparity(d) is d

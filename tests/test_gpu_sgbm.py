@@ -232,7 +232,7 @@ def test_dropin_installed_module(sv):
     object; a stereoProcessor with OpenCV's getters is honoured."""
     mod = types.SimpleNamespace(camera_focal_length_px=399.9745178222656, stereo_camera_baseline_m=0.2090607502,
                                 image_centre_w=474.5, image_centre_h=262.0)
-    sv.dropin.install(mod)
+    sv.dropin.install(mod, unpinned=True)   # disparity / greyscale restate cv2 (opt-in)
     try:
         L, R = osg.synth_pair(2, 128, 384)
         assert np.array_equal(mod.disparity(L, R, 128, False), osg.disparity(L, R))

@@ -326,7 +326,7 @@ def cmd_dropin(a):
     from test_prepass_cpu import carmask
     f = types.SimpleNamespace(camera_focal_length_px=399.9745178222656, stereo_camera_baseline_m=0.2090607502,
                               image_centre_w=474.5, image_centre_h=262.0, carmask=carmask())
-    dropin.install(f)
+    dropin.install(f, unpinned=True)
     disp, bgr = oracle.synth_frame(0)
     T = defaultdict(float)
 
