@@ -467,51 +467,71 @@ def extras(b, args, with_cpu, first=0):
     finally:
         dropin.uninstall()
 
-    # the whole per-frame loop of stereovision.py:53-136 that is not cv2, back to back on the resident batch:
-    # fill + mask pre-pass, maskpoints + RANSAC, the pipeline with each frame's plane, road raster + walk
-    def frame_loop():
-        b.prepass("previous", sync=False)
-        b.ransac(seed_base=0, trials=600, sync=False)
-        b.pipeline_planes(sync=False)
-        b.road_raster(sync=False)
-        b.nonzero(sync=False)
-    ms = _timed(b, frame_loop, 2)
-    ex["device_frame_loop"] = {"ms_per_batch": round(ms, 2), "frames": b.frames,
-                               "frames_per_s": round(b.frames / ms * 1e3, 1),
-                               "stages": "prepass(previous+mask) -> maskpoints+RANSAC(600) -> pipeline(per-frame "
-                                         "planes) -> road raster -> non-zero walk"}
-    # the same loop with two batches in flight, each on its own stream: the RANSAC draws (one wave's dependent
-    # chain per frame) leave the HBM idle, and the other batch's pre-pass, pipeline and road pass fill it
-    from svx import batch as sbm
-    with sbm.Batch(b.frames, H, W, args.step, with_bgr=True, with_points=True, device=b.device) as b2:
-        b2.synth(b.frames)
-        b2.set_mask(mask)
-        pair = (b, b2)
-
-        def two_loops():
-            for x in pair:
-                x.prepass("previous", sync=False)
-                x.ransac(seed_base=0, trials=600, sync=False)
-            for x in pair:
-                x.pipeline_planes(sync=False)
-                x.road_raster(sync=False)
-                x.nonzero(sync=False)
-        two_loops()
-        for x in pair:
-            x.sync()
-        reps = 3
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            two_loops()
-        for x in pair:
-            x.sync()
-        ms2 = (time.perf_counter() - t0) / reps / 2 * 1e3
-    ex["device_frame_loop_two_batches"] = {"ms_per_batch": round(ms2, 2), "frames": b.frames,
-                                           "frames_per_s": round(b.frames / ms2 * 1e3, 1),
-                                           "stages": "as device_frame_loop, two batches of frames in flight on two "
-                                                     "streams (each batch's pre-pass + RANSAC, then each batch's "
-                                                     "pipeline + road)"}
     return ex
+
+
+def loop_extra(args, device, first, mask):
+    """stereovision.py:53-136 minus the cv2 drawing over a SEQUENCE of 4096-frame batches (svx.loop.FrameLoop):
+    input (synthetic frames of the batch's global ids) -> pre-pass -> maskpoints -> RANSAC(600) -> pipeline with
+    each frame's plane -> road raster + walk, two batches in flight on two streams (batch k + 1's RANSAC beside
+    batch k's pipeline and road), against the same loop with one batch at a time. Steady state: `warm` batches
+    first (buffers, tables, clocks), then `reps` batches timed host-side from the end of the last warm-up batch
+    to the end of the last one. Then the parity leg: frames 0..4095 as two 2048-frame batches in flight, every
+    frame against tests/golden/plane_digests.npz. Run after the headline batch is freed (two slots hold
+    ~200 GB)."""
+    from svx.loop import STAGES, FrameLoop
+    out = {}
+    frames, warm, reps = args.frames, 2, 4
+    for slots in (2, 1):
+        with FrameLoop(frames, slots=slots, carmask=mask, device=device) as loop:
+            seq = None
+            for i in range(warm):
+                seq = loop.submit(first + i * frames)
+            loop.wait(seq)
+            t0 = time.perf_counter()
+            seqs = [loop.submit(first + (warm + i) * frames) for i in range(reps)]
+            loop.wait(seqs[-1])
+            ms = (time.perf_counter() - t0) / reps * 1e3
+            held = seqs[-slots:]
+            tls = [loop.timeline(q) for q in held]
+        stage_ms = {name: round(float(np.mean([tl[name][1] - tl[name][0] for tl in tls])), 3) for name in STAGES}
+        r = {"ms_per_batch": round(ms, 2), "frames": frames, "frames_per_s": round(frames / ms * 1e3, 1),
+             "slots": slots, "batches_timed": reps,
+             "stage_ms": stage_ms,
+             "stages": "synthetic input (global ids) -> prepass(previous+carmask) -> maskpoints -> RANSAC(600, "
+                       "random.seed(g)) -> pipeline(per-frame planes) -> road raster + walk"}
+        if slots == 2:
+            a, b = tls[0], tls[1]   # batch k and k + 1: how much of k + 1's RANSAC ran beside k's pipeline + road
+            lo, hi = max(b["ransac"][0], a["pipeline"][0]), min(b["ransac"][1], a["road"][1])
+            r["ransac_overlap_ms"] = round(max(0.0, hi - lo), 3)
+            r["api"] = "svx.loop.FrameLoop / sv_loop_create + sv_loop_submit (two slots, one stream each)"
+            out["device_frame_loop"] = r
+        else:
+            r["api"] = "the same loop with slots=1 (one batch at a time)"
+            out["device_frame_loop_serial"] = r
+    par = None
+    if not args.no_parity and os.path.exists(GOLDEN_PLANES) and args.step == 1 and first == 0:
+        gold = np.load(GOLDEN_PLANES)["planes"]
+        half = 2048
+        if len(gold) >= 2 * half:
+            bad = 0
+            with FrameLoop(half, slots=2, carmask=mask, device=device) as loop:
+                seqs = [loop.submit(0), loop.submit(half)]
+                for q in seqs:
+                    loop.wait(q)
+                    b, f0 = loop.batch(q)
+                    got = b.digest("pipeline")
+                    want = gold[f0:f0 + half]
+                    ok = got[:, 6] == 0
+                    for k, name in enumerate(DIGEST_FIELDS):
+                        ok &= got[:, k] == want[name].astype(np.uint64)
+                    for f in range(half):
+                        rr = b.read_ransac(f)
+                        ok[f] &= bool(rr["trial"] == want["trial"][f] and rr["err"] == want["err"][f] and
+                                      np.array_equal(rr["abc"].view(np.uint64), want["abc"][f].view(np.uint64)))
+                    bad += int((~ok).sum())
+            par = [2 * half, bad]
+    return out, par
 
 
 def sgbm_extra(sb, device, with_cpu, frames=128, chunk=128):
@@ -699,7 +719,11 @@ def main(argv=None):
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                      "kernel": "project_dense_kernel", "kernel_ms": round(k_avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": bytes_launch,
-                     "bytes_per_point": K1_BYTES_PER_POINT},
+                     "bytes_per_point": K1_BYTES_PER_POINT,
+                     "placement": dict(batches[0].placement("project"),
+                                       note="k1_place: on the batch's first projection up to 3 contiguous sets of "
+                                            "X/Y/Z planes, one K1 launch timed on each, the fastest kept "
+                                            "(outside the timed region; DESIGN §4)")},
     }
     parity = {}
     if not args.no_parity:
@@ -760,6 +784,10 @@ def main(argv=None):
                 "single": "host plane (single GPU)"}[pl["mode"]],
             "kernels": "resident_fused_kernel (one workgroup per frame, keep1 from the plane in device memory)"
                        if frames_gpu >= 512 else "tiled: stage_kernel + offsets_kernel",
+            "placement": dict(batches[0].placement("pipeline"),
+                              note="pipe_place: on the first resident call the current set of the five output "
+                                   "planes and up to two more, each timed (the faster of two passes), the fastest "
+                                   "kept (outside the timed region; DESIGN §4.1)"),
         }
         ptraffic = pipeline_traffic(args.traffic_pipeline, frames_gpu, args.step)
         if ptraffic:
@@ -777,23 +805,27 @@ def main(argv=None):
             parity["pipeline_frame_planes"] = pp
         out["extras"].update(sgbm_extra(sb, shards[0][0], not args.no_cpu))
 
+    if pl["rank"] == 0 and single and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+
+    for b in batches:
+        b.close()
+    if want_pipe and not args.no_extras and single:   # the frame loop needs the headline batch's memory back
+        lx, lpar = loop_extra(args, shards[0][0], shards[0][1], carmask())
+        out["extras"].update(lx)
+        if lpar is not None:
+            parity["frame_loop"] = lpar
     if parity:
         tot = ctrl.sum(np.array([v for pair in parity.values() for v in pair], np.float64))
         keys = list(parity)
         out["parity"] = {k: {"frames_checked": int(tot[2 * i]), "mismatched_frames": int(tot[2 * i + 1])}
                          for i, k in enumerate(keys)}
         out["parity"]["vs"] = "device per-frame digests vs tests/golden/frame_digests.npz (pinned C oracle, " \
-                              "global frame ids), every frame of every GPU; pipeline_frame_planes vs " \
-                              "tests/golden/plane_digests.npz (oracle pre-pass -> maskpoints -> RANSAC with " \
-                              "random.seed(F) -> pipeline, every frame)"
+                              "global frame ids), every frame of every GPU; pipeline_frame_planes and frame_loop " \
+                              "(two 2048-frame batches in flight) vs tests/golden/plane_digests.npz (oracle " \
+                              "pre-pass -> maskpoints -> RANSAC with random.seed(F) -> pipeline, every frame)"
         out["parity"]["pass"] = all(v["mismatched_frames"] == 0 and v["frames_checked"] > 0
                                     for k, v in out["parity"].items() if isinstance(v, dict))
-
-    if pl["rank"] == 0 and single and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-
-    for b in batches:
-        b.close()
     if comm:
         comm.close()
     if mcomm:

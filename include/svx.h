@@ -342,12 +342,58 @@ int sv_batch_last_ms(sv_batch* b, int which, float* ms);
  * Synchronises the batch stream. */
 int sv_batch_timing(sv_batch* b, int which, double* total_ms, int64_t* count);
 int sv_batch_timing_reset(sv_batch* b);
+/* The output-plane placement probe of a large batch's first call (which: 0 = K1's X/Y/Z planes, k1_place;
+ * 1 = the resident pipeline's five output planes, pipe_place): up to 3 sets of planes are allocated and one call
+ * is timed on each (the pipeline: the faster of two passes); the fastest set is kept. ms[0..n-1] = each set's
+ * timed call, *kept = the kept set's index (-1 when no probe ran: small batch, too little free memory). */
+int sv_batch_placement(sv_batch* b, int which, float* ms, int cap, int* n, int* kept);
 
 /* Read back. */
 int sv_batch_read_dense(sv_batch* b, int frame, float* X, float* Y, float* Z);
 int sv_batch_read_counts(sv_batch* b, int64_t* counts /* frames x 3 */);
 int sv_batch_read_hist(sv_batch* b, int frame, uint32_t* hist /* 1024 */);
 int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64_t cap, int64_t* n);
+
+/* ---- software-pipelined frame loop (stereovision.py:53-136, minus the cv2 drawing) -------------- */
+/* The reference's per-frame loop (loop.py:59-78 -> performStereoVision) over a SEQUENCE of device batches:
+ * every batch goes through input -> pre-pass (functions.py:130-172) -> maskpoints (stereovision.py:74-85) ->
+ * RANSAC (functions.py:278-298, stereovision.py:94) -> the pipeline with each frame's own plane
+ * (stereovision.py:97-113) -> road raster + non-zero walk (+ imageRoadMap) (stereovision.py:131-156,
+ * functions.py:339-365), on its slot's stream. Each stage of batch k also waits for the same stage of batch
+ * k - 1, so with slots = 2 the RANSAC of batch k + 1 (a latency-bound draw chain per frame) runs beside the
+ * HBM-bound pipeline and road pass of batch k. fillDisparity's previous cleaned frame is carried from batch to
+ * batch, so the results equal one long batch's (frame g draws after random.seed(seed_base + g)). */
+typedef struct {
+    int frames;          /* frames per batch                                                          */
+    int H, W, step;      /* frame shape; pipeline grid step (1, or the reference's 2)                  */
+    int slots;           /* batches in flight (1..8; 2 = the software pipeline)                        */
+    int source;          /* 0: the caller fills each batch (sv_loop_acquire + sv_batch_upload / sv_batch_sgbm);
+                            1: synthetic frames of the batch's global ids, generated on the device      */
+    int prepass;         /* 0 none, 1 fillDisparity with the previous cleaned frame, 2 fillAltDisparity */
+    int trials, k;       /* RANSAC trials and sample size (600, 600)                                    */
+    uint64_t seed_base;  /* frame g draws what CPython draws after random.seed(seed_base + g)           */
+    double point_thr;    /* computePlanarThreshold threshold (0.05)                                    */
+    int hist_thr;        /* filterPointsByHistogram threshold (10)                                     */
+    int road;            /* 0 none, 1 road raster + walk, 2 + imageRoadMap                             */
+} sv_loop_params;
+typedef struct sv_loop sv_loop;
+/* carmask: the grey H x W mask of maskDisparity (functions.py:35, :169-172), NULL for none. */
+int sv_loop_create(int device, const sv_loop_params* prm, const sv_camera* cam, const uint8_t* carmask,
+                   sv_loop** out);
+int sv_loop_destroy(sv_loop* L);
+/* The batch the next sv_loop_submit runs (waits on the host until its slot's previous batch is done): with
+ * source 0 the caller uploads its frames (or runs sv_batch_sgbm on it) before submitting. */
+int sv_loop_acquire(sv_loop* L, sv_batch** out);
+/* Enqueue one batch (global frame ids first_frame_id..) through every stage; returns its sequence number. The
+ * host waits inside only for this batch's maskpoint counts (they size the RANSAC launch), never for a stage of
+ * the batch before. */
+int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq);
+/* Wait for batch seq's last stage. sv_loop_batch: the batch holding seq's results (sv_batch_read_* work on it)
+ * until batch seq + slots is acquired or submitted. sv_loop_timeline: the start and end of each of the six
+ * stages (input, pre-pass, maskpoints, RANSAC, pipeline, road) in ms since the loop's first submit, 12 doubles. */
+int sv_loop_wait(sv_loop* L, int64_t seq);
+int sv_loop_batch(sv_loop* L, int64_t seq, sv_batch** out, int64_t* first_frame_id);
+int sv_loop_timeline(sv_loop* L, int64_t seq, double* out);
 
 /* ---- verification helpers (device computes, host compares) -------------- */
 /* Per-frame verification digests of the batch's current outputs (test and

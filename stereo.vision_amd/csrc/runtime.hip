@@ -267,6 +267,10 @@ struct sv_batch {
     DevBuf rmap;                // imageRoadMap (stereovision.py:131-133): frames x H x W x 3, on request
     bool want_rmap = false, rmap_fresh = false;
     DevBuf mpts, rres;          // one frame's maskpoints as fp64 (read-back scratch); counts + batched RANSAC results
+    DevBuf prev0buf, rdbuf;     // the host prev0 of sv_batch_prepass; sv_batch_read_disp's masked frame (batch-owned:
+                                // the device-wide drop-in scratch is used on other streams)
+    int64_t* hcnt = nullptr;    // pinned host copy of the maskpoints counts (sized frames), read by the RANSAC launch
+    hipEvent_t cnt_ev = nullptr;   // the counts' copy has landed in hcnt
     DevBuf rtab;                // fp64 X / Y / Z tables of the step-2 grid (the last sv_batch_ransac's camera)
     DevBuf mpk;                 // maskpoints packed (frames x mcap words x | y << 12 | d << 24): RANSAC's fp32 screen
     DevBuf rtrace;              // optional: frames x trace_trials x (k + 3) drawn indices
@@ -298,7 +302,16 @@ struct sv_batch {
     std::vector<hipEvent_t> pool;
     std::vector<std::pair<int, int>> pending[3];  // (start idx, end idx) per op kind: project, pipeline, sgbm
     size_t pool_next = 0;
+    // the placement probes of the first K1 / resident pipeline call (k1_place / pipe_place): each set's timed
+    // call (ms), how many sets were tried and which one was kept (-1: no probe ran)
+    float place_ms[2][8] = {};
+    int place_n[2] = {0, 0}, place_kept[2] = {-1, -1};
+    bool timing = true;        // record per-launch timing events (off for a frame loop's slots: they run unbounded)
     hipError_t timed_event(int* idx) {
+        if (!timing) {
+            *idx = -1;
+            return hipSuccess;
+        }
         if (pool_next == pool.size()) {
             hipEvent_t e;
             hipError_t r = hipEventCreate(&e);
@@ -528,8 +541,10 @@ int sv_batch_destroy(sv_batch* b) {
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppx, &b->ppy, &b->ctrl, &b->masks,
                       &b->carmask, &b->road, &b->rmap, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtab, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
-                      &b->glut, &b->ghist, &b->sgflags})
+                      &b->glut, &b->ghist, &b->sgflags, &b->prev0buf, &b->rdbuf})
         if (x->p) (void)hipFree(x->p);
+    if (b->hcnt) (void)hipHostFree(b->hcnt);
+    if (b->cnt_ev) (void)hipEventDestroy(b->cnt_ev);
     b->sg.release();
     for (auto& ev : b->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -639,6 +654,10 @@ static int k1_place(sv_batch* b, const KParams& p, size_t plane) {
             }
             if (e != hipSuccess) break;
             if (svx_knob("SVX_CONTIG_LOG")) std::fprintf(stderr, "svx: K1 placement %d: %.3f ms\n", t, ms);
+            if (t < 8) {
+                b->place_ms[0][t] = ms;
+                b->place_n[0] = t + 1;
+            }
             if (best < 0 || ms < best_ms) {
                 best = t;
                 best_ms = ms;
@@ -649,6 +668,7 @@ static int k1_place(sv_batch* b, const KParams& p, size_t plane) {
     }
     int rc = SV_OK;
     if (best < 0) rc = fail(SV_E_HIP, "K1 planes: allocation failed (%zu bytes each)", plane);
+    b->place_kept[0] = tries > 1 ? best : -1;
     for (int t = 0; t < (int)sets.size(); ++t) {
         for (int k = 0; k < 3; ++k) {
             DevBuf& x = sets[(size_t)t][k];
@@ -677,7 +697,7 @@ int sv_batch_project(sv_batch* b, const sv_camera* cam, int sync) {
                                  b->frames, b->qpl, b->nontemporal, b->stream));
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[1], b->stream));
-    b->pending[0].push_back({t0, t1});
+    if (t0 >= 0) b->pending[0].push_back({t0, t1});
     b->have_ms[0] = true;
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
@@ -762,6 +782,9 @@ static hipError_t pipe_place(sv_batch* b, const KParams& p, PipeBuffers bf, hipS
     int best = 0;
     for (int t = 1; t < placed; ++t)
         if (set_ms[(size_t)t] < set_ms[(size_t)best]) best = t;
+    b->place_n[1] = std::min(placed, 8);
+    for (int t = 0; t < b->place_n[1]; ++t) b->place_ms[1][t] = set_ms[(size_t)t];
+    b->place_kept[1] = best;
     for (int t = 0; t < (int)sets.size(); ++t)
         for (int k = 0; k < 5; ++k) {
             DevBuf& x = sets[(size_t)t][k];
@@ -841,7 +864,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     }
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[3], b->stream));
-    b->pending[1].push_back({t0, t1});
+    if (t0 >= 0) b->pending[1].push_back({t0, t1});
     b->have_ms[1] = true;
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
@@ -892,6 +915,15 @@ int sv_batch_read_frame_plane(sv_batch* b, int frame, double* out4) {
     out4[1] = fp.b;
     out4[2] = fp.c;
     out4[3] = fp.valid ? fp.nrm : -1.0;
+    return SV_OK;
+}
+
+int sv_batch_placement(sv_batch* b, int which, float* ms, int cap, int* n, int* kept) {
+    if (!b || which < 0 || which > 1 || !n || !kept || cap < 0 || (cap > 0 && !ms))
+        return fail(SV_E_ARG, "sv_batch_placement: bad arguments");
+    *n = b->place_n[which];
+    *kept = b->place_kept[which];
+    for (int t = 0; t < std::min(cap, *n); ++t) ms[t] = b->place_ms[which][t];
     return SV_OK;
 }
 
@@ -1158,6 +1190,20 @@ int sv_batch_set_mask(sv_batch* b, const uint8_t* mask) {
     return SV_OK;
 }
 
+// The pre-pass over the batch's frames in order; dprev0: frame 0's previous cleaned frame in device memory (the
+// frame loop's carry from the batch before), or null.
+static int batch_prepass_impl(sv_batch* b, int option, const uint8_t* dprev0) {
+    uint8_t* masked = nullptr;
+    const uint8_t* mff = nullptr;
+    uint8_t* disp = b->disp.as<uint8_t>();
+    if (option == 1) {
+        HIP_TRY(launch_fill_prev(disp, disp, masked, mff, dprev0, b->frames, (int64_t)b->H * b->W, b->stream));
+    } else if (option == 2) {
+        HIP_TRY(launch_fill_mean(disp, masked, mff, b->frames, b->H, b->W, b->Wu, b->stream));
+    }
+    return SV_OK;
+}
+
 int sv_batch_prepass(sv_batch* b, int option, const uint8_t* prev0, int sync) {
     if (!b) return fail(SV_E_ARG, "null batch");
     if (option < 0 || option > 2) return fail(SV_E_ARG, "prepass option must be 0 (none), 1 (previous) or 2 (mean)");
@@ -1166,23 +1212,14 @@ int sv_batch_prepass(sv_batch* b, int option, const uint8_t* prev0, int sync) {
     // maskDisparity (functions.py:169-172) is not materialised: its only consumer on the device, maskpoints, applies
     // the mask as it reads the cleaned disparity (the fill pass moves 2 B a pixel, not 3); sv_batch_read_disp
     // applies it to the frame it reads back
-    uint8_t* masked = nullptr;
-    const uint8_t* mff = nullptr;
-    uint8_t* disp = b->disp.as<uint8_t>();
-    if (option == 1) {
-        const uint8_t* p0 = nullptr;
-        if (prev0) {
-            Device* d;
-            if (int rc = dev_get(b->device, &d)) return rc;
-            HIP_TRY(d->aux.ensure((size_t)px));
-            HIP_TRY(hipMemsetAsync(d->aux.p, 0, (size_t)px, b->stream));
-            HIP_TRY(hipMemcpy2DAsync(d->aux.p, b->W, prev0, b->Wu, b->Wu, b->H, hipMemcpyHostToDevice, b->stream));
-            p0 = d->aux.as<uint8_t>();
-        }
-        HIP_TRY(launch_fill_prev(disp, disp, masked, mff, p0, b->frames, px, b->stream));
-    } else if (option == 2) {
-        HIP_TRY(launch_fill_mean(disp, masked, mff, b->frames, b->H, b->W, b->Wu, b->stream));
+    const uint8_t* p0 = nullptr;
+    if (option == 1 && prev0) {
+        HIP_TRY(b->prev0buf.ensure((size_t)px));
+        HIP_TRY(hipMemsetAsync(b->prev0buf.p, 0, (size_t)px, b->stream));
+        HIP_TRY(hipMemcpy2DAsync(b->prev0buf.p, b->W, prev0, b->Wu, b->Wu, b->H, hipMemcpyHostToDevice, b->stream));
+        p0 = b->prev0buf.as<uint8_t>();
     }
+    if (int rc = batch_prepass_impl(b, option, p0)) return rc;
     if (sync || prev0) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }
@@ -1194,10 +1231,8 @@ int sv_batch_read_disp(sv_batch* b, int frame, uint8_t* disp, uint8_t* masked) {
     const size_t px = (size_t)b->H * b->W;
     uint8_t* mframe = nullptr;
     if (masked) {   // maskDisparity of this frame (the batch does not hold masked copies)
-        Device* d;
-        if (int rc = dev_get(b->device, &d)) return rc;
-        HIP_TRY(d->aux.ensure(px));
-        mframe = d->aux.as<uint8_t>();
+        HIP_TRY(b->rdbuf.ensure(px));
+        mframe = b->rdbuf.as<uint8_t>();
         HIP_TRY(launch_mask(b->disp.as<uint8_t>() + px * frame, mframe, b->carmask.as<uint8_t>(), 1, (int64_t)px,
                             b->stream));
     }
@@ -1367,20 +1402,26 @@ static int ransac_ablate() {
     return e ? std::atoi(e) : 0;
 }
 
-int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame, int trials, int k,
-                    int sync) {
-    if (!b || !cam || trials < 0 || k < 1 || k > 1024 || first_frame < 0)
+// Batched RANSAC in two phases, so that a caller with other streams to feed (the frame loop) is not held by the
+// one read-back: phase 1 enqueues the step-2 tables, maskpoints and the copy of the per-frame counts into pinned
+// host memory (+ an event); phase 2 waits for that event — the largest frame sizes the draw kernel's LDS (bitmap /
+// pool list) and the sample index width — and enqueues the draw and evaluation kernels.
+static int batch_ransac_prepare(sv_batch* b, const sv_camera* cam, int trials, int k) {
+    if (!b || !cam || trials < 0 || k < 1 || k > 1024)
         return fail(SV_E_ARG, "sv_batch_ransac: bad arguments (1 <= k <= 1024, trials >= 0)");
+    if (trials > 4096) return fail(SV_E_ARG, "sv_batch_ransac: trials <= 4096");
     const int Hg = grid_len(b->H, 2), Wg = grid_len(b->W, 2);
     const int64_t mcap = (int64_t)Hg * Wg;
     if (mcap > 163840)
         return fail(SV_E_ARG, "sv_batch_ransac: %lld step-2 grid points per frame > 163,840 (LDS sample bitmap)",
                     (long long)mcap);
+    if (b->H > 4096 || b->W > 4096) return fail(SV_E_ARG, "sv_batch_ransac: frames up to 4096 x 4096");
     HIP_TRY(hipSetDevice(b->device));
     const size_t F = (size_t)b->frames;
-    if (b->H > 4096 || b->W > 4096) return fail(SV_E_ARG, "sv_batch_ransac: frames up to 4096 x 4096");
     HIP_TRY(b->mpk.ensure(sizeof(uint32_t) * (size_t)(mcap > 0 ? mcap : 1) * F));
     HIP_TRY(b->rres.ensure(F * (sizeof(double) * 4 + sizeof(int64_t) + sizeof(int32_t) + sizeof(uint32_t))));
+    if (!b->hcnt) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&b->hcnt), sizeof(int64_t) * F));
+    if (!b->cnt_ev) HIP_TRY(hipEventCreateWithFlags(&b->cnt_ev, hipEventDisableTiming));
     b->mcap = mcap;
     const RansacRes r = ransac_res(b);
     const KParams p = make_params(b->H, b->W, 2, *cam, b->Wu);
@@ -1391,6 +1432,19 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
     const uint8_t* mff = b->have_mask ? b->carmask.as<uint8_t>() : nullptr;
     HIP_TRY(launch_maskpoints(b->disp.as<uint8_t>(), mff, b->frames, b->H, b->W, p, b->mpk.as<uint32_t>(), mcap,
                               r.mcount, b->stream));
+    HIP_TRY(hipMemcpyAsync(b->hcnt, r.mcount, sizeof(int64_t) * F, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipEventRecord(b->cnt_ev, b->stream));
+    return SV_OK;
+}
+
+static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame,
+                               int trials, int k) {
+    if (first_frame < 0) return fail(SV_E_ARG, "sv_batch_ransac: first_frame >= 0");
+    HIP_TRY(hipSetDevice(b->device));
+    const size_t F = (size_t)b->frames;
+    const int64_t mcap = b->mcap;
+    const RansacRes r = ransac_res(b);
+    const KParams p = make_params(b->H, b->W, 2, *cam, b->Wu);
     int32_t* trace = nullptr;
     if (b->trace_trials > 0) {
         HIP_TRY(b->rtrace.ensure(sizeof(int32_t) * F * b->trace_trials * (size_t)(k + 3)));
@@ -1399,17 +1453,15 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
     }
     b->trace_k = k;
     b->traced_trials = trace ? b->trace_trials : 0;   // what rtrace holds now (read back by sv_batch_read_ransac_trace)
-    // the largest frame sizes the kernel's LDS (bitmap / pool list): one small read-back
-    std::vector<int64_t> cnt(F);
-    HIP_TRY(hipMemcpyAsync(cnt.data(), r.mcount, sizeof(int64_t) * F, hipMemcpyDeviceToHost, b->stream));
-    HIP_TRY(hipStreamSynchronize(b->stream));
+    // the largest frame sizes the kernel's LDS (bitmap / pool list): the counts phase 1 copied back
+    HIP_TRY(hipEventSynchronize(b->cnt_ev));
     int64_t max_n = 0, max_pool_n = 0;
     const int64_t setsize = ransac_setsize(k);
-    for (int64_t c : cnt) {
+    for (size_t f = 0; f < F; ++f) {
+        const int64_t c = b->hcnt[f];
         max_n = std::max(max_n, c);
         if (c >= k && c <= setsize) max_pool_n = std::max(max_pool_n, c);
     }
-    if (trials > 4096) return fail(SV_E_ARG, "sv_batch_ransac: trials <= 4096");
     HIP_TRY(b->rsidx.ensure(std::max<size_t>(ransac_sidx_bytes(max_n, b->frames, trials, k), 4)));
     HIP_TRY(b->rtri.ensure(sizeof(double) * 5 * F * (size_t)std::max(trials, 1) + sizeof(int32_t) * 2 * F));
     const RansacScratch rs{b->rsidx.p, b->rtri.as<double>(),
@@ -1418,6 +1470,14 @@ int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64
                                 max_pool_n,
                                 seed_base, first_frame, b->frames, trials, k, rs, r.abc, r.err, r.trial, r.flags, trace,
                                 b->trace_trials, ransac_ablate(), b->stream));
+    return SV_OK;
+}
+
+int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame, int trials, int k,
+                    int sync) {
+    if (first_frame < 0) return fail(SV_E_ARG, "sv_batch_ransac: bad arguments (first_frame >= 0)");
+    if (int rc = batch_ransac_prepare(b, cam, trials, k)) return rc;
+    if (int rc = batch_ransac_launch(b, cam, seed_base, first_frame, trials, k)) return rc;
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }
@@ -2032,8 +2092,224 @@ int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[5], b->stream));
     if (int rc = sgbm_check_flags(b->sgflags.as<uint32_t>(), b->frames, b->stream)) return rc;
-    b->pending[2].push_back({t0, t1});
+    if (t0 >= 0) b->pending[2].push_back({t0, t1});
     b->have_ms[2] = true;
+    return SV_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// software-pipelined frame loop (stereovision.py:53-136 minus the cv2 drawing, over a sequence of batches)
+// ---------------------------------------------------------------------------
+// Every batch goes through the same stages on its slot's stream: input -> pre-pass -> maskpoints -> RANSAC ->
+// pipeline with the frames' own planes -> road raster + walk. A stage of batch k also waits for the same stage of
+// batch k - 1 (an event on the other slot's stream), so each stage handles one batch at a time and in order, and
+// with two slots batch k + 1's maskpoints and RANSAC (one wave's dependent draw chain per frame, HBM nearly idle)
+// run beside batch k's pipeline and road pass (HBM-bound). fillDisparity's previous cleaned frame is carried from
+// batch to batch in a loop-owned buffer, so a sequence of batches cleans exactly as one long batch would.
+namespace {
+enum LoopStage { kLsInput = 0, kLsPrepass, kLsMaskpoints, kLsRansac, kLsPipeline, kLsRoad, kLsCount };
+}
+
+struct sv_loop {
+    int device = 0;
+    sv_loop_params prm{};
+    sv_camera cam{};
+    std::vector<sv_batch*> slot;
+    std::vector<int64_t> slot_seq, slot_first;
+    std::vector<std::array<hipEvent_t, kLsCount>> t0, t1;   // per slot: start / end of each stage (its last batch)
+    hipEvent_t epoch = nullptr;
+    DevBuf carry;              // the previous batch's last cleaned frame (fillDisparity's previousDisparity)
+    bool carry_valid = false;
+    int64_t next = 0;          // sequence number of the next submitted batch
+};
+
+extern "C" {
+
+int sv_loop_destroy(sv_loop* L) {
+    if (!L) return SV_OK;
+    (void)hipSetDevice(L->device);
+    for (sv_batch* b : L->slot)
+        if (b && b->stream) (void)hipStreamSynchronize(b->stream);
+    for (auto& a : L->t0)
+        for (auto& e : a)
+            if (e) (void)hipEventDestroy(e);
+    for (auto& a : L->t1)
+        for (auto& e : a)
+            if (e) (void)hipEventDestroy(e);
+    if (L->epoch) (void)hipEventDestroy(L->epoch);
+    if (L->carry.p) (void)hipFree(L->carry.p);
+    for (sv_batch* b : L->slot) sv_batch_destroy(b);
+    delete L;
+    return SV_OK;
+}
+
+int sv_loop_create(int device, const sv_loop_params* prm, const sv_camera* cam, const uint8_t* carmask,
+                   sv_loop** out) {
+    if (!prm || !cam || !out) return fail(SV_E_ARG, "sv_loop_create: null argument");
+    *out = nullptr;
+    const sv_loop_params& q = *prm;
+    if (q.frames < 1 || q.slots < 1 || q.slots > 8 || (q.source != 0 && q.source != 1) || q.prepass < 0 ||
+        q.prepass > 2 || q.road < 0 || q.road > 2 || (q.step != 1 && q.step != 2) || q.trials < 0 || q.k < 1)
+        return fail(SV_E_ARG, "sv_loop_create: bad parameters (frames >= 1, 1 <= slots <= 8, source 0/1, prepass "
+                              "0..2, road 0..2, step 1/2, trials >= 0, k >= 1)");
+    sv_loop* L = new sv_loop;
+    L->device = device;
+    L->prm = q;
+    L->cam = *cam;
+    L->slot.assign((size_t)q.slots, nullptr);
+    L->slot_seq.assign((size_t)q.slots, -1);
+    L->slot_first.assign((size_t)q.slots, 0);
+    L->t0.resize((size_t)q.slots);
+    L->t1.resize((size_t)q.slots);
+    for (auto& a : L->t0) a.fill(nullptr);
+    for (auto& a : L->t1) a.fill(nullptr);
+    int rc = SV_OK;
+    for (int i = 0; i < q.slots && rc == SV_OK; ++i) {
+        rc = sv_batch_create(device, q.frames, q.H, q.W, q.step, 1, 1, &L->slot[(size_t)i]);
+        if (rc == SV_OK) L->slot[(size_t)i]->timing = false;
+        if (rc == SV_OK && carmask) rc = sv_batch_set_mask(L->slot[(size_t)i], carmask);
+        if (rc == SV_OK && q.road == 2) rc = sv_batch_road_map(L->slot[(size_t)i], 1);
+    }
+    hipError_t e = hipSuccess;
+    if (rc == SV_OK) {
+        e = hipSetDevice(device);
+        for (int i = 0; i < q.slots && e == hipSuccess; ++i)
+            for (int st = 0; st < kLsCount && e == hipSuccess; ++st) {
+                e = hipEventCreate(&L->t0[(size_t)i][st]);
+                if (e == hipSuccess) e = hipEventCreate(&L->t1[(size_t)i][st]);
+            }
+        if (e == hipSuccess) e = hipEventCreate(&L->epoch);
+        if (e == hipSuccess) e = L->carry.ensure((size_t)L->slot[0]->H * L->slot[0]->W);
+        if (e != hipSuccess) rc = fail(SV_E_HIP, "sv_loop_create: %s", hipGetErrorString(e));
+    }
+    if (rc != SV_OK) {
+        const std::string msg = g_err;
+        sv_loop_destroy(L);
+        g_err = msg;
+        return rc;
+    }
+    *out = L;
+    return SV_OK;
+}
+
+// The batch the next sv_loop_submit processes (source 0: the caller fills it first); waits on the host until
+// the batch that last used its slot has finished every stage.
+int sv_loop_acquire(sv_loop* L, sv_batch** out) {
+    if (!L || !out) return fail(SV_E_ARG, "sv_loop_acquire: null argument");
+    const size_t s = (size_t)(L->next % L->prm.slots);
+    HIP_TRY(hipSetDevice(L->device));
+    if (L->slot_seq[s] >= 0) HIP_TRY(hipEventSynchronize(L->t1[s][kLsRoad]));
+    *out = L->slot[s];
+    return SV_OK;
+}
+
+int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
+    if (!L) return fail(SV_E_ARG, "sv_loop_submit: null loop");
+    if (first_frame_id < 0) return fail(SV_E_ARG, "sv_loop_submit: first_frame_id >= 0");
+    const sv_loop_params& q = L->prm;
+    const int64_t seq = L->next;
+    const size_t s = (size_t)(seq % q.slots), ps = (size_t)((seq + q.slots - 1) % q.slots);
+    sv_batch* b = L->slot[s];
+    hipStream_t st = b->stream;
+    HIP_TRY(hipSetDevice(L->device));
+    if (seq == 0) HIP_TRY(hipEventRecord(L->epoch, st));
+    auto begin = [&](int stage) -> hipError_t {
+        if (seq > 0 && ps != s) {   // the same stage of the batch before, on the other slot's stream
+            hipError_t e = hipStreamWaitEvent(st, L->t1[ps][stage], 0);
+            if (e != hipSuccess) return e;
+        }
+        return hipEventRecord(L->t0[s][stage], st);
+    };
+    auto end = [&](int stage) { return hipEventRecord(L->t1[s][stage], st); };
+    // input: for synthetic frames, the batch's global frame ids generated on the device
+    HIP_TRY(begin(kLsInput));
+    if (q.source == 1) {
+        if (b->Wu != b->W) return fail(SV_E_ARG, "synthetic frames need W %% 8 == 0 (W=%d)", b->Wu);
+        HIP_TRY(launch_synth(b->kp, b->disp.as<uint8_t>(), b->bgr.as<uint8_t>(), b->frames, first_frame_id, st));
+    }
+    HIP_TRY(end(kLsInput));
+    // pre-pass (stereovision.py:53-76): frame 0 cleaned with the previous batch's last cleaned frame
+    HIP_TRY(begin(kLsPrepass));
+    if (q.prepass) {
+        if (int rc = batch_prepass_impl(b, q.prepass, q.prepass == 1 && L->carry_valid ? L->carry.as<uint8_t>()
+                                                                                       : nullptr))
+            return rc;
+        if (q.prepass == 1) {
+            const size_t px = (size_t)b->H * b->W;
+            HIP_TRY(hipMemcpyAsync(L->carry.p, b->disp.as<uint8_t>() + px * (b->frames - 1), px,
+                                   hipMemcpyDeviceToDevice, st));
+            L->carry_valid = true;
+        }
+    }
+    HIP_TRY(end(kLsPrepass));
+    // maskpoints (stereovision.py:74-85): the masked step-2 points of every frame, their counts to the host
+    HIP_TRY(begin(kLsMaskpoints));
+    if (int rc = batch_ransac_prepare(b, &L->cam, q.trials, q.k)) return rc;
+    HIP_TRY(end(kLsMaskpoints));
+    // RANSAC (stereovision.py:94): frame g draws after random.seed(seed_base + g). The host waits here for this
+    // batch's counts; the previous batch's stages are all enqueued already.
+    HIP_TRY(begin(kLsRansac));
+    if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k)) return rc;
+    HIP_TRY(end(kLsRansac));
+    // the pipeline with every frame's own plane (stereovision.py:97-113)
+    HIP_TRY(begin(kLsPipeline));
+    if (int rc = sv_batch_pipeline_planes(b, &L->cam, q.point_thr, q.hist_thr, 0, 0)) return rc;
+    HIP_TRY(end(kLsPipeline));
+    // road raster + non-zero walk (+ imageRoadMap) (stereovision.py:131-156)
+    HIP_TRY(begin(kLsRoad));
+    if (q.road) {
+        if (int rc = sv_batch_road_raster(b, 0)) return rc;
+    }
+    HIP_TRY(end(kLsRoad));
+    L->slot_seq[s] = seq;
+    L->slot_first[s] = first_frame_id;
+    L->next = seq + 1;
+    if (out_seq) *out_seq = seq;
+    return SV_OK;
+}
+
+static int loop_slot_of(sv_loop* L, int64_t seq, size_t* out) {
+    if (!L || seq < 0) return fail(SV_E_ARG, "sv_loop: bad arguments");
+    const size_t s = (size_t)(seq % L->prm.slots);
+    if (L->slot_seq[s] != seq)
+        return fail(SV_E_STATE, "sv_loop: batch %lld is not held (submitted: %lld, slots: %d)", (long long)seq,
+                    (long long)L->next, L->prm.slots);
+    *out = s;
+    return SV_OK;
+}
+
+int sv_loop_wait(sv_loop* L, int64_t seq) {
+    size_t s;
+    if (int rc = loop_slot_of(L, seq, &s)) return rc;
+    HIP_TRY(hipSetDevice(L->device));
+    HIP_TRY(hipEventSynchronize(L->t1[s][kLsRoad]));
+    return SV_OK;
+}
+
+int sv_loop_batch(sv_loop* L, int64_t seq, sv_batch** out, int64_t* first_frame_id) {
+    size_t s;
+    if (!out) return fail(SV_E_ARG, "sv_loop_batch: null out");
+    if (int rc = loop_slot_of(L, seq, &s)) return rc;
+    *out = L->slot[s];
+    if (first_frame_id) *first_frame_id = L->slot_first[s];
+    return SV_OK;
+}
+
+int sv_loop_timeline(sv_loop* L, int64_t seq, double* out) {
+    size_t s;
+    if (!out) return fail(SV_E_ARG, "sv_loop_timeline: null out");
+    if (int rc = loop_slot_of(L, seq, &s)) return rc;
+    HIP_TRY(hipSetDevice(L->device));
+    HIP_TRY(hipEventSynchronize(L->t1[s][kLsRoad]));
+    for (int st = 0; st < kLsCount; ++st) {
+        float a = 0.f, z = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, L->epoch, L->t0[s][st]));
+        HIP_TRY(hipEventElapsedTime(&z, L->epoch, L->t1[s][st]));
+        out[2 * st] = a;
+        out[2 * st + 1] = z;
+    }
     return SV_OK;
 }
 

@@ -26,6 +26,14 @@ class Plane(ctypes.Structure):
     _fields_ = [("a", ctypes.c_double), ("b", ctypes.c_double), ("c", ctypes.c_double)]
 
 
+class LoopParams(ctypes.Structure):
+    """sv_loop_params (include/svx.h)."""
+    _fields_ = [("frames", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int), ("step", ctypes.c_int),
+                ("slots", ctypes.c_int), ("source", ctypes.c_int), ("prepass", ctypes.c_int),
+                ("trials", ctypes.c_int), ("k", ctypes.c_int), ("seed_base", ctypes.c_uint64),
+                ("point_thr", ctypes.c_double), ("hist_thr", ctypes.c_int), ("road", ctypes.c_int)]
+
+
 P = ctypes.c_void_p
 I = ctypes.c_int
 I64 = ctypes.c_int64
@@ -95,6 +103,7 @@ SIGNATURES = {
     "sv_batch_last_ms": [P, I, PF],
     "sv_batch_timing": [P, I, ctypes.POINTER(D), PI64],
     "sv_batch_timing_reset": [P],
+    "sv_batch_placement": [P, I, PF, I, ctypes.POINTER(I), ctypes.POINTER(I)],
     "sv_batch_read_dense": [P, I, P, P, P],
     "sv_batch_read_counts": [P, P],
     "sv_batch_read_hist": [P, I, P],
@@ -103,6 +112,13 @@ SIGNATURES = {
     "sv_hue_lut": [I, P],
     "sv_delta_tables": [I, I, I, ctypes.POINTER(Camera), P, P],
     "sv_synth_frame": [I, I64, I, I, P, P],
+    "sv_loop_create": [I, ctypes.POINTER(LoopParams), ctypes.POINTER(Camera), P, ctypes.POINTER(P)],
+    "sv_loop_destroy": [P],
+    "sv_loop_acquire": [P, ctypes.POINTER(P)],
+    "sv_loop_submit": [P, I64, PI64],
+    "sv_loop_wait": [P, I64],
+    "sv_loop_batch": [P, I64, ctypes.POINTER(P), PI64],
+    "sv_loop_timeline": [P, I64, P],
     "sv_comm_unique_id": [P],
     "sv_comm_init": [I, I, P, I, ctypes.POINTER(P)],
     "sv_comm_destroy": [P],

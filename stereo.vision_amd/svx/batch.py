@@ -32,16 +32,29 @@ class Batch:
         _abi.call("sv_batch_create", device, frames, H, W, step, int(with_bgr), int(with_points),
                   ctypes.byref(h))
         self._h = h
+        self._owned = True
+        self._init_info(frames, H, W, step, device)
+
+    def _init_info(self, frames, H, W, step, device):
         self.frames, self.H, self.W, self.step, self.device = frames, H, W, step, device
         info = np.zeros(8, np.int64)
         _abi.call("sv_batch_info", self._h, _abi.ptr(info))
         self.Hg, self.Wg, self.pitch, self.Ng = (int(v) for v in info[:4])
 
+    @classmethod
+    def _view(cls, handle, frames, H, W, step, device):
+        """A Batch over a handle some other object owns (a FrameLoop slot): never destroyed by this object."""
+        b = cls.__new__(cls)
+        b._h = ctypes.c_void_p(handle)
+        b._owned = False
+        b._init_info(frames, H, W, step, device)
+        return b
+
     # -- lifetime ---------------------------------------------------------------
     def close(self):
-        if self._h:
+        if self._h and self._owned:
             _abi.call("sv_batch_destroy", self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -192,6 +205,16 @@ class Batch:
         cnt = ctypes.c_int64(0)
         _abi.call("sv_batch_timing", self._h, _WHICH[which], ctypes.byref(tot), ctypes.byref(cnt))
         return float(tot.value), int(cnt.value)
+
+    def placement(self, which="project"):
+        """The first large call's output-plane placement probe: {"tried_ms": [...], "kept": index or None}
+        (which = "project" for K1's planes, "pipeline" for the resident pipeline's; sv_batch_placement)."""
+        ms = (ctypes.c_float * 8)()
+        n, kept = ctypes.c_int(0), ctypes.c_int(-1)
+        _abi.call("sv_batch_placement", self._h, 0 if which == "project" else 1, ms, 8, ctypes.byref(n),
+                  ctypes.byref(kept))
+        return {"tried_ms": [round(float(ms[i]), 4) for i in range(n.value)],
+                "kept": kept.value if kept.value >= 0 else None}
 
     def reset_timing(self):
         _abi.call("sv_batch_timing_reset", self._h)

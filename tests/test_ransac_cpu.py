@@ -174,3 +174,16 @@ def test_ransac_err_matches_numpy(k):
         rp = [[x[0], x[1], x[2]] for x in T]
         want = np.mean(abs((np.dot(rp, abc) - 1) / d))
         assert oracle.ransac_err(T, abc) == float(want)
+
+
+def test_numpy_blas_build_is_the_goldens():
+    """The bit-exact plane / error restatement follows ONE numpy + OpenBLAS build; the golden
+    planes were made with the build recorded in tests/golden/blas_env.json. Another build may round the 3x3
+    solve or the gemv differently in the last bit: say so here, by name. (The OpenBLAS kernel architecture
+    picked at run time is recorded for information; the pins above are checked on every host they run on.)"""
+    sys.path.insert(0, GOLDEN)
+    import make_blas_env
+    want = json.load(open(os.path.join(GOLDEN, "blas_env.json")))
+    got = make_blas_env.env()
+    for key in ("numpy", "blas_name", "blas_version", "openblas_configuration"):
+        assert got[key] == want[key], f"{key}: running {got[key]!r}, goldens made with {want[key]!r}"
