@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Generate tests/golden/plane_digests.npz: the per-frame-plane loop of
-stereovision.py:53-113 for frames 0..4095 of the synthetic batch, end to end
+stereovision.py:53-113 for frames 0..8191 of the synthetic sequence, end to end
 through the ORACLE (the checker; never the product):
 
   for frame F in order (stereovision.py:56-60, loop.py:57,78):
@@ -23,7 +23,8 @@ Per frame it stores the plane's float64 bits, the winning trial, the error of
 the winner and of the runner-up (to see near ties), the maskpoint count and
 the six digest columns of oracle.DIGEST_FIELDS.
 
-usage: python tests/golden/make_plane_digests.py [--frames 4096]   (a few minutes on 8 cores)
+usage: python tests/golden/make_plane_digests.py [--frames 8192]   (about 13 minutes on 6 cores; the committed file
+       holds frames 0..8191: the frame-loop tests run sequences of batches across 4096)
 """
 import argparse
 import os
@@ -85,7 +86,7 @@ def _block(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=4096)
+    ap.add_argument("--frames", type=int, default=8192)
     ap.add_argument("--seed-base", type=int, default=0)
     ap.add_argument("--procs", type=int, default=min(8, os.cpu_count() or 1))
     a = ap.parse_args()
