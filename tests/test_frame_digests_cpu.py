@@ -56,7 +56,7 @@ def test_plane_digests_rows_recompute():
     import make_plane_digests as mpd
     z = np.load(os.path.join(GOLDEN, "plane_digests.npz"))
     gold = z["planes"]
-    assert gold.shape == (4096,) and int(z["trials"]) == 600 and int(z["seed_base"]) == 0
+    assert gold.shape == (8192,) and int(z["trials"]) == 600 and int(z["seed_base"]) == 0
     assert (gold["trial"] >= 0).all() and (gold["n_kept2"] > 0).all()
     prev = None
     for f in range(640):
