@@ -472,43 +472,48 @@ def extras(b, args, with_cpu, first=0):
 
 def loop_extra(args, device, first, mask):
     """stereovision.py:53-136 minus the cv2 drawing over a SEQUENCE of 4096-frame batches (svx.loop.FrameLoop):
-    input (synthetic frames of the batch's global ids) -> pre-pass -> maskpoints -> RANSAC(600) -> pipeline with
-    each frame's plane -> road raster + walk, two batches in flight on two streams (batch k + 1's RANSAC beside
-    batch k's pipeline and road), against the same loop with one batch at a time. Steady state: `warm` batches
-    first (buffers, tables, clocks), then `reps` batches timed host-side from the end of the last warm-up batch
-    to the end of the last one. Then the parity leg: frames 0..4095 as two 2048-frame batches in flight, every
-    frame against tests/golden/plane_digests.npz. Run after the headline batch is freed (two slots hold
-    ~200 GB)."""
+    pre-pass -> maskpoints -> RANSAC(600) -> pipeline with each frame's plane -> road raster + walk, two batches in
+    flight on two streams (batch k + 1's RANSAC beside batch k's pipeline and road), against the same loop with
+    one batch at a time. `device_frame_loop` / `_serial`: the frames stay resident in the slots (generated once,
+    as the round-3 device loop ran on a resident batch), so a batch's time is the stages' alone;
+    `device_frame_loop_with_input`: every batch first generates its synthetic frames on the device (global ids).
+    Steady state: `warm` batches first (buffers, tables, clocks), then `reps` batches timed host-side from the end
+    of the last warm-up batch to the end of the last one. Then the parity leg: frames 0..4095 as two 2048-frame
+    batches in flight, every frame against tests/golden/plane_digests.npz. Run after the headline batch is freed
+    (two slots hold ~200 GB)."""
     from svx.loop import STAGES, FrameLoop
     out = {}
     frames, warm, reps = args.frames, 2, 4
-    for slots in (2, 1):
-        with FrameLoop(frames, slots=slots, carmask=mask, device=device) as loop:
+    for key, slots, source in (("device_frame_loop", 2, "caller"), ("device_frame_loop_serial", 1, "caller"),
+                               ("device_frame_loop_with_input", 2, "synth")):
+        with FrameLoop(frames, slots=slots, source=source, carmask=mask, device=device) as loop:
             seq = None
-            for i in range(warm):
+            for i in range(warm + reps):
+                if i == warm:
+                    loop.wait(seq)
+                    t0 = time.perf_counter()
+                if source == "caller" and i < slots:   # the slot's frames, generated once and kept
+                    loop.acquire().synth(first + i * frames)
                 seq = loop.submit(first + i * frames)
             loop.wait(seq)
-            t0 = time.perf_counter()
-            seqs = [loop.submit(first + (warm + i) * frames) for i in range(reps)]
-            loop.wait(seqs[-1])
             ms = (time.perf_counter() - t0) / reps * 1e3
-            held = seqs[-slots:]
-            tls = [loop.timeline(q) for q in held]
+            tls = [loop.timeline(q) for q in range(seq - slots + 1, seq + 1)]
         stage_ms = {name: round(float(np.mean([tl[name][1] - tl[name][0] for tl in tls])), 3) for name in STAGES}
         r = {"ms_per_batch": round(ms, 2), "frames": frames, "frames_per_s": round(frames / ms * 1e3, 1),
-             "slots": slots, "batches_timed": reps,
+             "slots": slots, "batches_timed": reps, "input": "synthetic frames generated per batch on the device"
+             if source == "synth" else "resident frames (generated once per slot)",
              "stage_ms": stage_ms,
-             "stages": "synthetic input (global ids) -> prepass(previous+carmask) -> maskpoints -> RANSAC(600, "
-                       "random.seed(g)) -> pipeline(per-frame planes) -> road raster + walk"}
+             "stages": ("synthetic input (global ids) -> " if source == "synth" else "") +
+                       "prepass(previous+carmask) -> maskpoints -> RANSAC(600, random.seed(g)) -> pipeline(per-frame "
+                       "planes) -> road raster + walk",
+             "api": "svx.loop.FrameLoop / sv_loop_create + sv_loop_submit"
+                    + (" (two slots, one stream each; RANSAC on a high-priority stream)" if slots == 2 else
+                       " with slots=1 (one batch at a time)")}
         if slots == 2:
             a, b = tls[0], tls[1]   # batch k and k + 1: how much of k + 1's RANSAC ran beside k's pipeline + road
             lo, hi = max(b["ransac"][0], a["pipeline"][0]), min(b["ransac"][1], a["road"][1])
             r["ransac_overlap_ms"] = round(max(0.0, hi - lo), 3)
-            r["api"] = "svx.loop.FrameLoop / sv_loop_create + sv_loop_submit (two slots, one stream each)"
-            out["device_frame_loop"] = r
-        else:
-            r["api"] = "the same loop with slots=1 (one batch at a time)"
-            out["device_frame_loop_serial"] = r
+        out[key] = r
     par = None
     if not args.no_parity and os.path.exists(GOLDEN_PLANES) and args.step == 1 and first == 0:
         gold = np.load(GOLDEN_PLANES)["planes"]

@@ -602,27 +602,13 @@ __device__ __forceinline__ void rb_solve_record(const double* r1, const double* 
     o[4] = singular ? 1.0 : 0.0;
 }
 
-// SPEC: the speculative draw. The reference redraws a triple while it is collinear (functions.py:251-259),
-// which is the only way the point VALUES reach the stream's consumption; exact collinearity (numpy's cross
-// product all zero) needs three points with equal Y and Z, i.e. one row and one disparity, so it is rare. The
-// speculative kernel takes every first triple as accepted: no gather of the three points and no test in the
-// chain — no global load at all, so the chain never waits behind its own sample stores (vmcnt counts loads and
-// stores in issue order). The evaluation kernel tests every trial's triple while it solves the planes and
-// flags a frame that met a collinear one (`redo`); the exact kernel (only != nullptr) then draws the flagged
-// frames again from their seeds, and the evaluation runs for them again. Results are the exact kernel's.
-template <class IdxT, bool TR, bool SPEC>
+template <class IdxT, bool TR>
 __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restrict__ packed, RbTables tb, int64_t cap,
                                                          const int64_t* __restrict__ counts, uint64_t seed_base,
                                                          int64_t first_frame, int trials, int k,
                                                          IdxT* __restrict__ sidx, double* __restrict__ tri,
                                                          int32_t* __restrict__ fstat, int32_t* __restrict__ trace,
-                                                         int trace_trials, int bitmap_words, int ablate, int prio,
-                                                         const int32_t* __restrict__ only) {
-    if (only && !only[blockIdx.x]) return;   // the exact pass after a speculative one: flagged frames only
-    // Wave priority for issue arbitration: the draw is one wave's dependent instruction chain per frame; beside
-    // a throughput kernel of another stream (the frame loop runs the next batch's RANSAC beside this batch's
-    // pipeline), the oldest-first arbitration would hand the older co-resident waves every contended issue slot.
-    if (prio) __builtin_amdgcn_s_setprio(3);
+                                                         int trace_trials, int bitmap_words, int ablate) {
     __shared__ uint32_t mt[624];
     __shared__ uint32_t dummy[64];
     extern __shared__ uint4 rb_dyn4[];   // [bitmap_words] bitmap / pool list (16-byte aligned, 4-word multiple)
@@ -667,9 +653,7 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
         double p1[3], p2[3], p3[3];   // the triple's fp64 points (rb_point: the reference's X, Y, Z)
         int attempts = 0;
         bool degenerate = false;
-        if constexpr (SPEC) {
-            rb_draw_below(sh, st, n, kb, 3, t3);   // accepted as drawn: the evaluation checks it (see above)
-        } else do {   // randomNonCollinearPoints
+        do {   // randomNonCollinearPoints
             if (++attempts > kRBMaxAttempts) {
                 degenerate = true;
                 break;
@@ -831,19 +815,13 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
     const int64_t* __restrict__ counts, int trials, int k, const IdxT* __restrict__ sidx,
     double* __restrict__ tri, const int32_t* __restrict__ fstat, double* __restrict__ out_abc,
     double* __restrict__ out_err, int32_t* __restrict__ out_trial, uint32_t* __restrict__ out_flags, int ablate,
-    int lds_pts_words, int prio, int32_t* __restrict__ redo, const int32_t* __restrict__ only) {
-    // redo != nullptr: after the speculative draw — test every triple for collinearity, flag the frame and stop
-    // when one is (the exact draw and this kernel with only == redo then redo it); only: flagged frames only
-    if (only && !only[blockIdx.x]) return;
-    if (prio) __builtin_amdgcn_s_setprio(2);   // as the draw kernel's, one step lower
+    int lds_pts_words) {
     extern __shared__ uint32_t ev_dyn[];
-    __shared__ int s_collinear;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.x;
     const int64_t n64 = counts[frame];
     if (n64 < k || trials <= 0) {
         if (tid == 0) {
-            if (redo) redo[frame] = 0;
             out_trial[frame] = -1;
             out_flags[frame] = 0;
             out_err[frame] = 0.0;
@@ -861,7 +839,6 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
     double* scr = reinterpret_cast<double*>(ev_dyn + (LDS_PTS ? lds_pts_words : 0));   // [T][2]
     double* ftri = tri + (int64_t)frame * trials * kRBTri;
     const IdxT* fidx = sidx + (int64_t)frame * trials * k;
-    if (tid == 0) s_collinear = 0;
     __syncthreads();
     // every trial's plane from its triple (the draw kernel wrote the three indices
     // into the record's first words), one lane a trial: the record in place
@@ -875,14 +852,9 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
             rb_point(P[i1], tb, r1[0], r1[1], r1[2]);
             rb_point(P[i2], tb, r2[0], r2[1], r2[2]);
             rb_point(P[i3], tb, r3[0], r3[1], r3[2]);
-            if (redo && rb_collinear(r1, r2, r3)) s_collinear = 1;   // (a benign race: every writer writes 1)
             rb_solve_record(r1, r2, r3, rec);
         }
         __syncthreads();   // the records are read by other waves below (same workgroup: same L1)
-    }
-    if (redo) {   // (uniform) after the speculative draw
-        if (tid == 0) redo[frame] = s_collinear;
-        if (s_collinear) return;   // this frame is drawn and evaluated again, exactly
     }
     // screen every trial in fp32 (one wave a trial): the mean distance from the
     // packed points and, per point, the bound (|Xa| + |Yb| + |Zc| + 1) 2^-18 / |abc|
@@ -1087,9 +1059,19 @@ static hipError_t launch_ransac_typed(const uint32_t* packed, const RbTables& tb
                                       const int64_t* counts, int64_t max_n, int64_t words, uint64_t seed_base,
                                       int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs,
                                       double* abc, double* err, int32_t* trial, uint32_t* flags, int32_t* trace,
-                                      int trace_trials, int ablate, int prio, int spec, hipStream_t s) {
+                                      int trace_trials, int ablate, hipStream_t s) {
     IdxT* sidx = reinterpret_cast<IdxT*>(rs.sidx);
-    const size_t dlds = sizeof(uint32_t) * (size_t)words;
+    if (trace)
+        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, true>), dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words,
+                           s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace,
+                           trace_trials, (int)words, ablate);
+    else
+        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, false>), dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words,
+                           s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat,
+                           nullptr, 0, (int)words, ablate);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (ablate & (8 | 16)) ablate |= 1;   // DIAGNOSTIC: no samples / planes drawn -> no evaluation of them
     // eval LDS: the points when they fit beside the screen results (160 KiB per workgroup)
     // per trial: screened mean + bound (2 doubles), candidate index and its fp64 error
     const size_t scr = sizeof(double) * 2 * (size_t)trials + sizeof(int32_t) * ((size_t)trials + 1) +
@@ -1100,49 +1082,17 @@ static hipError_t launch_ransac_typed(const uint32_t* packed, const RbTables& tb
     const size_t dyn = (lds_pts ? pts_b : 0) + scr;
     if (lds_pts) {
         // dynamic LDS above 64 KiB needs the per-kernel opt-in (on the current device)
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ransac_eval_kernel<IdxT, true>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ransac_eval_kernel<IdxT, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
         if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((ransac_eval_kernel<IdxT, true>), dim3(frames), dim3(kRBEvalThreads), dyn, s, packed,
+                           tb, cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags, ablate,
+                           (int)pts_words);
+    } else {
+        hipLaunchKernelGGL((ransac_eval_kernel<IdxT, false>), dim3(frames), dim3(kRBEvalThreads), dyn, s, packed,
+                           tb, cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags, ablate, 0);
     }
-    const int eval_ablate = (ablate & (8 | 16)) ? (ablate | 1) : ablate;   // DIAGNOSTIC: nothing drawn -> no eval
-    const auto eval = [&](int32_t* redo, const int32_t* only) {
-        if (lds_pts)
-            hipLaunchKernelGGL((ransac_eval_kernel<IdxT, true>), dim3(frames), dim3(kRBEvalThreads), dyn, s, packed,
-                               tb, cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags,
-                               eval_ablate, (int)pts_words, prio, redo, only);
-        else
-            hipLaunchKernelGGL((ransac_eval_kernel<IdxT, false>), dim3(frames), dim3(kRBEvalThreads), dyn, s, packed,
-                               tb, cap, cp, counts, trials, k, sidx, rs.tri, rs.fstat, abc, err, trial, flags,
-                               eval_ablate, 0, prio, redo, only);
-        return hipGetLastError();
-    };
-    if (trace) {   // the trace records the exact draws
-        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, true, false>), dim3(frames), dim3(64), dlds, s, packed, tb, cap,
-                           counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace, trace_trials,
-                           (int)words, ablate, prio, nullptr);
-        hipError_t e = hipGetLastError();
-        return e != hipSuccess ? e : eval(nullptr, nullptr);
-    }
-    if (!spec || (ablate & (8 | 16))) {
-        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, false, false>), dim3(frames), dim3(64), dlds, s, packed, tb, cap,
-                           counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, nullptr, 0, (int)words,
-                           ablate, prio, nullptr);
-        hipError_t e = hipGetLastError();
-        return e != hipSuccess ? e : eval(nullptr, nullptr);
-    }
-    // speculative draw -> evaluation with the collinearity test -> exact draw and evaluation of the flagged
-    // frames (both launches cover the batch; unflagged frames return at once)
-    hipLaunchKernelGGL((ransac_draw_kernel<IdxT, false, true>), dim3(frames), dim3(64), dlds, s, packed, tb, cap,
-                       counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, nullptr, 0, (int)words,
-                       ablate, prio, nullptr);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = eval(rs.redo, nullptr);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((ransac_draw_kernel<IdxT, false, false>), dim3(frames), dim3(64), dlds, s, packed, tb, cap,
-                       counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, nullptr, 0, (int)words,
-                       ablate, prio, rs.redo);
-    e = hipGetLastError();
-    return e != hipSuccess ? e : eval(nullptr, rs.redo);
+    return hipGetLastError();
 }
 
 size_t ransac_sidx_bytes(int64_t max_n, int frames, int trials, int k) {
@@ -1153,7 +1103,7 @@ hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H,
                                const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
                                int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs, double* abc,
                                double* err, int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials,
-                               int ablate, int prio, int spec, hipStream_t s) {
+                               int ablate, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
     if (k < 1 || k > kRBMaxK || trials > kRBMaxTrials || cap > (int64_t)kRBBitmapWords * 32 || max_n > cap)
         return hipErrorInvalidValue;
@@ -1167,11 +1117,10 @@ hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H,
         return launch_ransac_typed<uint16_t>(packed, rb_tables(tab, H, W), cap, cp, counts, max_n, words, seed_base,
                                              first_frame,
                                              frames, trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate,
-                                             prio, spec, s);
+                                             s);
     return launch_ransac_typed<int32_t>(packed, rb_tables(tab, H, W), cap, cp, counts, max_n, words, seed_base,
                                         first_frame, frames,
-                                        trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate, prio, spec,
-                                        s);
+                                        trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate, s);
 }
 
 // keep1 plane fields of every frame (plane_fields, as the host's set_plane)

@@ -254,7 +254,9 @@ struct sv_batch {
     size_t cap = 0;            // per-frame point capacity of the pipeline outputs (Ng rounded up to 64)
     int64_t dense_per_frame = 0;
     hipStream_t stream = nullptr;    // K1, pass 1 (stream A)
-    hipStream_t stream2 = nullptr;   // pipeline offsets kernels (stream B), beside the stage launches
+    hipStream_t stream2 = nullptr;   // tiled pipeline's offsets kernels (stream B), beside the stage launches; made
+                                     // on the first tiled call: streams share the device's few hardware queues (4),
+                                     // and two streams on one queue run in order, so no stream is made unused
     std::vector<hipEvent_t> sync_ev; // pipeline hand-offs between A and B (timing disabled)
     DevBuf disp, bgr, X, Y, Z, xyz, ctrl, masks;
     DevBuf ppx, ppy;            // the pipeline's int32 (x, y): two planes of frames x cap
@@ -524,7 +526,6 @@ int sv_batch_create(int device, int frames, int H, int W, int step, int with_bgr
         }
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking);
     for (int i = 0; i < 6 && e == hipSuccess; ++i) e = hipEventCreate(&b->ev[i]);
     if (e != hipSuccess) {
         sv_batch_destroy(b);
@@ -859,6 +860,7 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
             HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             b->sync_ev.push_back(e);
         }
+        if (!b->stream2) HIP_TRY(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
         HIP_TRY(hipMemsetAsync(b->ctrl.p, 0, b->ctrl_bytes, b->stream));
         HIP_TRY(launch_pipeline(p, bf, b->frames, chunk, b->stream, b->stream2, b->sync_ev.data()));
     }
@@ -1437,20 +1439,6 @@ static int batch_ransac_prepare(sv_batch* b, const sv_camera* cam, int trials, i
     return SV_OK;
 }
 
-// Wave priority of the RANSAC kernels (s_setprio, kernels/ransac_batch.hip): on by default; the diagnostic
-// build's SVX_RANSAC_PRIO=0 turns it off (A/B).
-static int ransac_prio() {
-    const char* e = svx_knob("SVX_RANSAC_PRIO");
-    return e ? std::atoi(e) : 1;
-}
-
-// Speculative draws (kernels/ransac_batch.hip): on by default; the diagnostic build's SVX_RANSAC_SPEC=0 draws
-// every frame with the in-chain collinearity check (A/B).
-static int ransac_spec() {
-    const char* e = svx_knob("SVX_RANSAC_SPEC");
-    return e ? std::atoi(e) : 1;
-}
-
 // stream: where the draw and evaluation kernels go (the batch's own, or the frame loop's RANSAC stream, which
 // has waited for phase 1 there)
 static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame,
@@ -1479,13 +1467,13 @@ static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_
         if (c >= k && c <= setsize) max_pool_n = std::max(max_pool_n, c);
     }
     HIP_TRY(b->rsidx.ensure(std::max<size_t>(ransac_sidx_bytes(max_n, b->frames, trials, k), 4)));
-    HIP_TRY(b->rtri.ensure(sizeof(double) * 5 * F * (size_t)std::max(trials, 1) + sizeof(int32_t) * 3 * F));
-    int32_t* fstat = reinterpret_cast<int32_t*>(b->rtri.as<double>() + 5 * F * (size_t)std::max(trials, 1));
-    const RansacScratch rs{b->rsidx.p, b->rtri.as<double>(), fstat, fstat + 2 * F};
+    HIP_TRY(b->rtri.ensure(sizeof(double) * 5 * F * (size_t)std::max(trials, 1) + sizeof(int32_t) * 2 * F));
+    const RansacScratch rs{b->rsidx.p, b->rtri.as<double>(),
+                           reinterpret_cast<int32_t*>(b->rtri.as<double>() + 5 * F * (size_t)std::max(trials, 1))};
     HIP_TRY(launch_ransac_batch(b->mpk.as<uint32_t>(), b->rtab.as<double>(), b->H, b->W, mcap, p, r.mcount, max_n,
                                 max_pool_n,
                                 seed_base, first_frame, b->frames, trials, k, rs, r.abc, r.err, r.trial, r.flags, trace,
-                                b->trace_trials, ransac_ablate(), ransac_prio(), ransac_spec(), stream));
+                                b->trace_trials, ransac_ablate(), stream));
     return SV_OK;
 }
 
@@ -2135,7 +2123,6 @@ struct sv_loop {
     std::vector<sv_batch*> slot;
     std::vector<int64_t> slot_seq, slot_first;
     std::vector<std::array<hipEvent_t, kLsCount>> t0, t1;   // per slot: start / end of each stage (its last batch)
-    std::vector<hipStream_t> rstream;   // per slot: the RANSAC stage's stream, at the device's highest priority
     hipEvent_t epoch = nullptr;
     DevBuf carry;              // the previous batch's last cleaned frame (fillDisparity's previousDisparity)
     bool carry_valid = false;
@@ -2149,11 +2136,6 @@ int sv_loop_destroy(sv_loop* L) {
     (void)hipSetDevice(L->device);
     for (sv_batch* b : L->slot)
         if (b && b->stream) (void)hipStreamSynchronize(b->stream);
-    for (hipStream_t r : L->rstream)
-        if (r) {
-            (void)hipStreamSynchronize(r);
-            (void)hipStreamDestroy(r);
-        }
     for (auto& a : L->t0)
         for (auto& e : a)
             if (e) (void)hipEventDestroy(e);
@@ -2203,17 +2185,6 @@ int sv_loop_create(int device, const sv_loop_params* prm, const sv_camera* cam, 
                 if (e == hipSuccess) e = hipEventCreate(&L->t1[(size_t)i][st]);
             }
         if (e == hipSuccess) e = hipEventCreate(&L->epoch);
-        // The RANSAC stage runs on a stream of its own at the highest priority, so that when it and the other
-        // slot's pipeline are both waiting for compute units the dispatcher places the draw kernel's waves first
-        // (its frames are dependent chains that must all be resident to finish in one pass). The diagnostic
-        // build's SVX_LOOP_RSTREAM=0 keeps it on the slot's stream (A/B).
-        const char* rsv = svx_knob("SVX_LOOP_RSTREAM");
-        const bool own = !(rsv && rsv[0] == '0');
-        int least = 0, greatest = 0;
-        if (e == hipSuccess && own) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-        L->rstream.assign((size_t)q.slots, nullptr);
-        for (int i = 0; i < q.slots && e == hipSuccess && own; ++i)
-            e = hipStreamCreateWithPriority(&L->rstream[(size_t)i], hipStreamNonBlocking, greatest);
         if (e == hipSuccess) e = L->carry.ensure((size_t)L->slot[0]->H * L->slot[0]->W);
         if (e != hipSuccess) rc = fail(SV_E_HIP, "sv_loop_create: %s", hipGetErrorString(e));
     }
@@ -2283,13 +2254,9 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     HIP_TRY(end(kLsMaskpoints));
     // RANSAC (stereovision.py:94): frame g draws after random.seed(seed_base + g). The host waits here for this
     // batch's counts; the previous batch's stages are all enqueued already.
-    hipStream_t rs = L->rstream[s] ? L->rstream[s] : st;
-    if (rs != st) HIP_TRY(hipStreamWaitEvent(rs, L->t1[s][kLsMaskpoints], 0));
-    if (seq > 0 && ps != s) HIP_TRY(hipStreamWaitEvent(rs, L->t1[ps][kLsRansac], 0));
-    HIP_TRY(hipEventRecord(L->t0[s][kLsRansac], rs));
-    if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k, rs)) return rc;
-    HIP_TRY(hipEventRecord(L->t1[s][kLsRansac], rs));
-    if (rs != st) HIP_TRY(hipStreamWaitEvent(st, L->t1[s][kLsRansac], 0));
+    HIP_TRY(begin(kLsRansac));
+    if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k, st)) return rc;
+    HIP_TRY(end(kLsRansac));
     // the pipeline with every frame's own plane (stereovision.py:97-113)
     HIP_TRY(begin(kLsPipeline));
     if (int rc = sv_batch_pipeline_planes(b, &L->cam, q.point_thr, q.hist_thr, 0, 0)) return rc;

@@ -155,7 +155,6 @@ struct RansacScratch {
     void* sidx;
     double* tri;
     int32_t* fstat;
-    int32_t* redo;   // frames x 1: the speculative draw met a collinear triple, the frame is drawn again exactly
 };
 size_t ransac_sidx_bytes(int64_t max_n, int frames, int trials, int k);
 // max_n: the largest frame's point count; max_pool_n: the largest count that takes random.sample's pool
@@ -164,7 +163,7 @@ hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H,
                                const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
                                int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs, double* abc,
                                double* err, int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials,
-                               int ablate, int prio, int spec, hipStream_t s);
+                               int ablate, hipStream_t s);
 // out[i] = plane_fields of abc[3i..3i+2] (trial[i] < 0, or trial NULL and a NaN plane: valid = 0);
 // trial may be NULL (a device plane, e.g. the RCCL broadcast buffer).
 hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, const KParams& p, double thr,

@@ -203,30 +203,6 @@ def test_batch_collinear_redraws(svb):
         assert redraws >= 20, redraws
 
 
-def test_batch_collinear_speculative_redo(svb):
-    """Without the trace the batch draws speculatively: every first triple is taken and the evaluation tests
-    it; a frame that met a collinear triple is drawn again exactly. Frames with redraws (the line frames above)
-    sit between frames without any: every frame's winner, error and plane must still be the reference's, and
-    the same as the traced (exact) run's."""
-    trials = 300
-    frames = [_sparse_frame(5000, 11), _lines_frame(range(100, 118, 2), 512, 400, 70), _sparse_frame(3000, 12),
-              _lines_frame([100], 500, 500, 71), _lines_frame([100, 300], 300, 150, 72), _sparse_frame(20000, 13)]
-    with svb.Batch(len(frames), H=H, W=W, step=2, with_bgr=False) as b:
-        for f, d in enumerate(frames):
-            b.upload(f, d)
-        b.set_mask(None)
-        b.ransac(seed_base=33, trials=trials)
-        spec = [b.read_ransac(f) for f in range(len(frames))]
-        for f in range(len(frames)):
-            _check(spec[f], *_oracle_frame(b.read_maskpoints(f), trials, 33 + f), what=f"frame {f}")
-        b.ransac_trace(2)   # the traced run draws exactly, without speculation
-        b.ransac(seed_base=33, trials=trials)
-        for f in range(len(frames)):
-            r = b.read_ransac(f)
-            assert (r["trial"], r["err"], r["flags"]) == (spec[f]["trial"], spec[f]["err"], spec[f]["flags"]), f
-            assert np.array_equal(_bits(r["abc"]), _bits(spec[f]["abc"])), f
-
-
 def test_batch_degenerate_frame_gives_up(svb):
     """All maskpoints on one line: the reference loops for ever in
     randomNonCollinearPoints; the kernel stops, flags the frame (8) and the

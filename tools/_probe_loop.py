@@ -15,18 +15,29 @@ def show(loop, seqs):
         tl = loop.timeline(q)
         print(f"  batch {q}: " + "  ".join(f"{n[:4]} {tl[n][0]:8.2f}-{tl[n][1]:8.2f}" for n in STAGES), flush=True)
 
-for slots in (2, 1):
-    with FrameLoop(F, slots=slots, carmask=mask) as loop:
-        for i in range(2):
+for source, slots in (("caller", 2), ("caller", 1), ("synth", 2)):
+    with FrameLoop(F, slots=slots, source=source, carmask=mask) as loop:
+        for i in range(6):
+            if i == 2:
+                loop.wait(s)
+                t0 = time.perf_counter()
+            if source == "caller" and i < slots:
+                loop.acquire().synth(i * F)
             s = loop.submit(i * F)
         loop.wait(s)
-        t0 = time.perf_counter()
-        seqs = [loop.submit((2 + i) * F) for i in range(4)]
-        t_sub = [(time.perf_counter() - t0) * 1e3]
-        loop.wait(seqs[-1])
         dt = (time.perf_counter() - t0) / 4 * 1e3
-        print(f"slots={slots}: {dt:.2f} ms/batch (host submit of 4 took {t_sub[0]:.1f} ms)", flush=True)
-        show(loop, seqs[-slots:])
+        print(f"source={source} slots={slots}: {dt:.2f} ms/batch", flush=True)
+        show(loop, range(s - slots + 1, s + 1))
+
+# the batched RANSAC alone (maskpoints + draw + eval), 4096 carmask frames
+with sb.Batch(F, step=1, with_bgr=True, with_points=True) as rb:
+    rb.synth(0); rb.set_mask(mask); rb.prepass("previous")
+    rb.ransac(seed_base=0, trials=600)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        rb.ransac(seed_base=0, trials=600, sync=False)
+    rb.sync()
+    print(f"ransac alone: {(time.perf_counter() - t0) / 5 * 1e3:.3f} ms", flush=True)
 
 # two streams, K1 on each: concurrent?
 a = sb.Batch(2048, step=1, with_bgr=False); a.synth(0)
