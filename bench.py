@@ -504,15 +504,15 @@ def loop_extra(args, device, first, mask):
              if source == "synth" else "resident frames (generated once per slot)",
              "stage_ms": stage_ms,
              "stages": ("synthetic input (global ids) -> " if source == "synth" else "") +
-                       "prepass(previous+carmask) -> maskpoints -> RANSAC(600, random.seed(g)) -> pipeline(per-frame "
-                       "planes) -> road raster + walk",
+                       "prepass(previous+carmask) -> maskpoints -> RANSAC(600, random.seed(g)): draw, eval -> "
+                       "pipeline(per-frame planes) -> road raster + walk",
              "api": "svx.loop.FrameLoop / sv_loop_create + sv_loop_submit"
-                    + (" (two slots, one stream each; RANSAC on a high-priority stream)" if slots == 2 else
+                    + (" (two slots, one stream each)" if slots == 2 else
                        " with slots=1 (one batch at a time)")}
         if slots == 2:
-            a, b = tls[0], tls[1]   # batch k and k + 1: how much of k + 1's RANSAC ran beside k's pipeline + road
-            lo, hi = max(b["ransac"][0], a["pipeline"][0]), min(b["ransac"][1], a["road"][1])
-            r["ransac_overlap_ms"] = round(max(0.0, hi - lo), 3)
+            a, b = tls[0], tls[1]   # batch k and k + 1: how much of k + 1's draw ran beside k's pipeline + road
+            lo, hi = max(b["draw"][0], a["pipeline"][0]), min(b["draw"][1], a["road"][1])
+            r["draw_overlap_ms"] = round(max(0.0, hi - lo), 3)
         out[key] = r
     par = None
     if not args.no_parity and os.path.exists(GOLDEN_PLANES) and args.step == 1 and first == 0:

@@ -359,9 +359,11 @@ int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64
  * every batch goes through input -> pre-pass (functions.py:130-172) -> maskpoints (stereovision.py:74-85) ->
  * RANSAC (functions.py:278-298, stereovision.py:94) -> the pipeline with each frame's own plane
  * (stereovision.py:97-113) -> road raster + non-zero walk (+ imageRoadMap) (stereovision.py:131-156,
- * functions.py:339-365), on its slot's stream. Each stage of batch k also waits for the same stage of batch
- * k - 1, so with slots = 2 the RANSAC of batch k + 1 (a latency-bound draw chain per frame) runs beside the
- * HBM-bound pipeline and road pass of batch k. fillDisparity's previous cleaned frame is carried from batch to
+ * functions.py:339-365), on its slot's stream; RANSAC runs as two stages (the draw replay, the evaluation).
+ * Each stage of batch k also waits for the same stage of batch k - 1, and the evaluation for batch k - 1's
+ * road pass, so with slots = 2 the draw of batch k + 1 (one wave's dependent chain per frame) runs beside the
+ * HBM-bound pipeline and road pass of batch k, and the evaluation of batch k + 1 (a CU's LDS per frame)
+ * beside the pre-pass and maskpoints of batch k + 2. fillDisparity's previous cleaned frame is carried from batch to
  * batch, so the results equal one long batch's (frame g draws after random.seed(seed_base + g)). */
 typedef struct {
     int frames;          /* frames per batch                                                          */
@@ -389,8 +391,9 @@ int sv_loop_acquire(sv_loop* L, sv_batch** out);
  * the batch before. */
 int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq);
 /* Wait for batch seq's last stage. sv_loop_batch: the batch holding seq's results (sv_batch_read_* work on it)
- * until batch seq + slots is acquired or submitted. sv_loop_timeline: the start and end of each of the six
- * stages (input, pre-pass, maskpoints, RANSAC, pipeline, road) in ms since the loop's first submit, 12 doubles. */
+ * until batch seq + slots is acquired or submitted. sv_loop_timeline: the start and end of each of the seven
+ * stages (input, pre-pass, maskpoints, RANSAC draw, RANSAC evaluation, pipeline, road) in ms since the loop's
+ * first submit, 14 doubles. */
 int sv_loop_wait(sv_loop* L, int64_t seq);
 int sv_loop_batch(sv_loop* L, int64_t seq, sv_batch** out, int64_t* first_frame_id);
 int sv_loop_timeline(sv_loop* L, int64_t seq, double* out);

@@ -608,7 +608,12 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
                                                          int64_t first_frame, int trials, int k,
                                                          IdxT* __restrict__ sidx, double* __restrict__ tri,
                                                          int32_t* __restrict__ fstat, int32_t* __restrict__ trace,
-                                                         int trace_trials, int bitmap_words, int ablate) {
+                                                         int trace_trials, int bitmap_words, int ablate,
+                                                         uint64_t* __restrict__ started, uint64_t epoch) {
+    // the frame loop's dispatch signal: the last workgroup of the grid is placed after every other one, so once it
+    // runs, every frame's wave is resident and another stream's kernel may take the rest of the CUs (loop_gate)
+    if (started && blockIdx.x == gridDim.x - 1 && lane_id() == 0)
+        __hip_atomic_store(started, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ uint32_t mt[624];
     __shared__ uint32_t dummy[64];
     extern __shared__ uint4 rb_dyn4[];   // [bitmap_words] bitmap / pool list (16-byte aligned, 4-word multiple)
@@ -1059,18 +1064,20 @@ static hipError_t launch_ransac_typed(const uint32_t* packed, const RbTables& tb
                                       const int64_t* counts, int64_t max_n, int64_t words, uint64_t seed_base,
                                       int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs,
                                       double* abc, double* err, int32_t* trial, uint32_t* flags, int32_t* trace,
-                                      int trace_trials, int ablate, hipStream_t s) {
+                                      int trace_trials, int ablate, int phases, uint64_t* started, uint64_t epoch,
+                                      hipStream_t s) {
     IdxT* sidx = reinterpret_cast<IdxT*>(rs.sidx);
-    if (trace)
+    if (!(phases & 1)) {
+    } else if (trace)
         hipLaunchKernelGGL((ransac_draw_kernel<IdxT, true>), dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words,
                            s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace,
-                           trace_trials, (int)words, ablate);
+                           trace_trials, (int)words, ablate, started, epoch);
     else
         hipLaunchKernelGGL((ransac_draw_kernel<IdxT, false>), dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words,
                            s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat,
-                           nullptr, 0, (int)words, ablate);
+                           nullptr, 0, (int)words, ablate, started, epoch);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || !(phases & 2)) return e;
     if (ablate & (8 | 16)) ablate |= 1;   // DIAGNOSTIC: no samples / planes drawn -> no evaluation of them
     // eval LDS: the points when they fit beside the screen results (160 KiB per workgroup)
     // per trial: screened mean + bound (2 doubles), candidate index and its fp64 error
@@ -1103,7 +1110,7 @@ hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H,
                                const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
                                int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs, double* abc,
                                double* err, int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials,
-                               int ablate, hipStream_t s) {
+                               int ablate, int phases, uint64_t* started, uint64_t epoch, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
     if (k < 1 || k > kRBMaxK || trials > kRBMaxTrials || cap > (int64_t)kRBBitmapWords * 32 || max_n > cap)
         return hipErrorInvalidValue;
@@ -1117,10 +1124,30 @@ hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H,
         return launch_ransac_typed<uint16_t>(packed, rb_tables(tab, H, W), cap, cp, counts, max_n, words, seed_base,
                                              first_frame,
                                              frames, trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate,
-                                             s);
+                                             phases, started, epoch, s);
     return launch_ransac_typed<int32_t>(packed, rb_tables(tab, H, W), cap, cp, counts, max_n, words, seed_base,
                                         first_frame, frames,
-                                        trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate, s);
+                                        trials, k, rs, abc, err, trial, flags, trace, trace_trials, ablate, phases,
+                                        started, epoch, s);
+}
+
+// The frame loop's dispatch gate (one wave): returns once *flag >= epoch — the RANSAC draw kernel's last
+// workgroup has been placed, so all its waves are resident — or after max_ns of wall clock (ordering is a
+// performance heuristic only: nothing computed depends on it, so the gate never waits unboundedly). The kernel
+// enqueued after it on the same stream then takes the CU resources the draw left.
+__global__ __launch_bounds__(64) void loop_gate_kernel(const uint64_t* __restrict__ flag, uint64_t epoch,
+                                                       uint64_t max_ticks) {
+    if (lane_id() != 0) return;
+    const uint64_t t0 = wall_clock64();   // constant 100 MHz counter
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch &&
+           wall_clock64() - t0 < max_ticks)
+        __builtin_amdgcn_s_sleep(8);
+}
+
+hipError_t launch_loop_gate(const uint64_t* flag, uint64_t epoch, double max_ms, hipStream_t s) {
+    const uint64_t ticks = (uint64_t)(max_ms * 1e5);   // wall_clock64 ticks at 100 MHz
+    hipLaunchKernelGGL(loop_gate_kernel, dim3(1), dim3(64), 0, s, flag, epoch, ticks);
+    return hipGetLastError();
 }
 
 // keep1 plane fields of every frame (plane_fields, as the host's set_plane)

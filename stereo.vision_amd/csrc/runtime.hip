@@ -286,6 +286,7 @@ struct sv_batch {
     SgbmBufs sg;                // SGBM scratch for one chunk of frames
     DevBuf sgflags;             // SGBM range flags, one word per frame of the batch
     int64_t mcap = 0;
+    int64_t rmax_n = 0, rmax_pool_n = 0;   // the last RANSAC draw launch's largest frame (they size the eval too)
     int trace_trials = 0, trace_k = 0, traced_trials = 0;   // requested; k and trials of the recorded trace
     bool have_mask = false;
     // pipeline control block (one memset per call): hist | counts | err
@@ -1439,10 +1440,12 @@ static int batch_ransac_prepare(sv_batch* b, const sv_camera* cam, int trials, i
     return SV_OK;
 }
 
-// stream: where the draw and evaluation kernels go (the batch's own, or the frame loop's RANSAC stream, which
-// has waited for phase 1 there)
+// phases: 1 = the draw kernel (waits for phase 1's counts on the host), 2 = the evaluation kernel (after a phase-1
+// launch with the same arguments), 3 = both. The frame loop enqueues the two as separate stages.
+// started / epoch: the frame loop's dispatch signal (the draw kernel's last workgroup stores epoch there)
 static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame,
-                               int trials, int k, hipStream_t stream) {
+                               int trials, int k, hipStream_t stream, int phases = 3, uint64_t* started = nullptr,
+                               uint64_t epoch = 0) {
     if (first_frame < 0) return fail(SV_E_ARG, "sv_batch_ransac: first_frame >= 0");
     HIP_TRY(hipSetDevice(b->device));
     const size_t F = (size_t)b->frames;
@@ -1450,22 +1453,29 @@ static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_
     const RansacRes r = ransac_res(b);
     const KParams p = make_params(b->H, b->W, 2, *cam, b->Wu);
     int32_t* trace = nullptr;
-    if (b->trace_trials > 0) {
+    if (b->trace_trials > 0 && (phases & 1)) {
         HIP_TRY(b->rtrace.ensure(sizeof(int32_t) * F * b->trace_trials * (size_t)(k + 3)));
         HIP_TRY(hipMemsetAsync(b->rtrace.p, 0xff, sizeof(int32_t) * F * b->trace_trials * (size_t)(k + 3), stream));
         trace = b->rtrace.as<int32_t>();
     }
-    b->trace_k = k;
-    b->traced_trials = trace ? b->trace_trials : 0;   // what rtrace holds now (read back by sv_batch_read_ransac_trace)
-    // the largest frame sizes the kernel's LDS (bitmap / pool list): the counts phase 1 copied back
-    HIP_TRY(hipEventSynchronize(b->cnt_ev));
-    int64_t max_n = 0, max_pool_n = 0;
-    const int64_t setsize = ransac_setsize(k);
-    for (size_t f = 0; f < F; ++f) {
-        const int64_t c = b->hcnt[f];
-        max_n = std::max(max_n, c);
-        if (c >= k && c <= setsize) max_pool_n = std::max(max_pool_n, c);
+    if (phases & 1) {
+        b->trace_k = k;
+        b->traced_trials = trace ? b->trace_trials : 0;   // what rtrace holds now (sv_batch_read_ransac_trace)
     }
+    // the largest frame sizes the kernel's LDS (bitmap / pool list): the counts phase 1 copied back
+    if (phases & 1) {
+        HIP_TRY(hipEventSynchronize(b->cnt_ev));
+        int64_t max_n = 0, max_pool_n = 0;
+        const int64_t setsize = ransac_setsize(k);
+        for (size_t f = 0; f < F; ++f) {
+            const int64_t c = b->hcnt[f];
+            max_n = std::max(max_n, c);
+            if (c >= k && c <= setsize) max_pool_n = std::max(max_pool_n, c);
+        }
+        b->rmax_n = max_n;
+        b->rmax_pool_n = max_pool_n;
+    }
+    const int64_t max_n = b->rmax_n, max_pool_n = b->rmax_pool_n;
     HIP_TRY(b->rsidx.ensure(std::max<size_t>(ransac_sidx_bytes(max_n, b->frames, trials, k), 4)));
     HIP_TRY(b->rtri.ensure(sizeof(double) * 5 * F * (size_t)std::max(trials, 1) + sizeof(int32_t) * 2 * F));
     const RansacScratch rs{b->rsidx.p, b->rtri.as<double>(),
@@ -1473,7 +1483,7 @@ static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_
     HIP_TRY(launch_ransac_batch(b->mpk.as<uint32_t>(), b->rtab.as<double>(), b->H, b->W, mcap, p, r.mcount, max_n,
                                 max_pool_n,
                                 seed_base, first_frame, b->frames, trials, k, rs, r.abc, r.err, r.trial, r.flags, trace,
-                                b->trace_trials, ransac_ablate(), stream));
+                                b->trace_trials, ransac_ablate(), phases, started, epoch, stream));
     return SV_OK;
 }
 
@@ -2106,14 +2116,15 @@ int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int
 // ---------------------------------------------------------------------------
 // software-pipelined frame loop (stereovision.py:53-136 minus the cv2 drawing, over a sequence of batches)
 // ---------------------------------------------------------------------------
-// Every batch goes through the same stages on its slot's stream: input -> pre-pass -> maskpoints -> RANSAC ->
-// pipeline with the frames' own planes -> road raster + walk. A stage of batch k also waits for the same stage of
-// batch k - 1 (an event on the other slot's stream), so each stage handles one batch at a time and in order, and
-// with two slots batch k + 1's maskpoints and RANSAC (one wave's dependent draw chain per frame, HBM nearly idle)
-// run beside batch k's pipeline and road pass (HBM-bound). fillDisparity's previous cleaned frame is carried from
+// Every batch goes through the same stages on its slot's stream: input -> pre-pass -> maskpoints -> RANSAC draw ->
+// RANSAC evaluation -> pipeline with the frames' own planes -> road raster + walk. A stage of batch k also waits
+// for the same stage of batch k - 1 (an event on the other slot's stream), so each stage handles one batch at a
+// time and in order; the evaluation of batch k also waits for batch k - 1's road pass. With two slots the steady
+// state alternates two phases: batch k's evaluation beside batch k + 1's pre-pass and maskpoints, then batch k's
+// pipeline and road pass beside batch k + 1's draw (one wave's dependent chain per frame). fillDisparity's previous cleaned frame is carried from
 // batch to batch in a loop-owned buffer, so a sequence of batches cleans exactly as one long batch would.
 namespace {
-enum LoopStage { kLsInput = 0, kLsPrepass, kLsMaskpoints, kLsRansac, kLsPipeline, kLsRoad, kLsCount };
+enum LoopStage { kLsInput = 0, kLsPrepass, kLsMaskpoints, kLsDraw, kLsEval, kLsPipeline, kLsRoad, kLsCount };
 }
 
 struct sv_loop {
@@ -2126,7 +2137,9 @@ struct sv_loop {
     hipEvent_t epoch = nullptr;
     DevBuf carry;              // the previous batch's last cleaned frame (fillDisparity's previousDisparity)
     bool carry_valid = false;
+    DevBuf gate;               // uint64: the last draw kernel whose grid is resident (its epoch = seq + 1)
     int64_t next = 0;          // sequence number of the next submitted batch
+    int64_t pending = -1;      // the batch whose pipeline + road pass are not enqueued yet (see sv_loop_submit)
 };
 
 extern "C" {
@@ -2186,6 +2199,8 @@ int sv_loop_create(int device, const sv_loop_params* prm, const sv_camera* cam, 
             }
         if (e == hipSuccess) e = hipEventCreate(&L->epoch);
         if (e == hipSuccess) e = L->carry.ensure((size_t)L->slot[0]->H * L->slot[0]->W);
+        if (e == hipSuccess) e = L->gate.ensure(sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMemset(L->gate.p, 0, sizeof(uint64_t));
         if (e != hipSuccess) rc = fail(SV_E_HIP, "sv_loop_create: %s", hipGetErrorString(e));
     }
     if (rc != SV_OK) {
@@ -2198,17 +2213,65 @@ int sv_loop_create(int device, const sv_loop_params* prm, const sv_camera* cam, 
     return SV_OK;
 }
 
+static int loop_flush(sv_loop* L);
+
 // The batch the next sv_loop_submit processes (source 0: the caller fills it first); waits on the host until
 // the batch that last used its slot has finished every stage.
 int sv_loop_acquire(sv_loop* L, sv_batch** out) {
     if (!L || !out) return fail(SV_E_ARG, "sv_loop_acquire: null argument");
     const size_t s = (size_t)(L->next % L->prm.slots);
     HIP_TRY(hipSetDevice(L->device));
+    if (L->pending >= 0 && (size_t)(L->pending % L->prm.slots) == s)
+        if (int rc = loop_flush(L)) return rc;   // (one slot) the batch held there still has its tail to run
     if (L->slot_seq[s] >= 0) HIP_TRY(hipEventSynchronize(L->t1[s][kLsRoad]));
     *out = L->slot[s];
     return SV_OK;
 }
 
+// The pipeline and road pass of batch seq (slot s), behind a dispatch gate on the draw kernel of batch seq + 1
+// when that has been enqueued (gate_epoch > 0): the draw's 4096 one-wave workgroups are a dependent chain each
+// and must all be resident to finish in one pass, so they are placed first and the pipeline takes what is left
+// of the CUs; launched together, the pipeline's workgroups would take the LDS and the draw would run in rounds.
+static int loop_enqueue_tail(sv_loop* L, int64_t seq, uint64_t gate_epoch) {
+    const sv_loop_params& q = L->prm;
+    const size_t s = (size_t)(seq % q.slots), ps = (size_t)((seq + q.slots - 1) % q.slots);
+    sv_batch* b = L->slot[s];
+    hipStream_t st = b->stream;
+    auto begin = [&](int stage) -> hipError_t {
+        if (seq > 0 && ps != s) {
+            hipError_t e = hipStreamWaitEvent(st, L->t1[ps][stage], 0);
+            if (e != hipSuccess) return e;
+        }
+        return hipEventRecord(L->t0[s][stage], st);
+    };
+    auto end = [&](int stage) { return hipEventRecord(L->t1[s][stage], st); };
+    if (gate_epoch) HIP_TRY(launch_loop_gate(L->gate.as<uint64_t>(), gate_epoch, 50.0, st));
+    // the pipeline with every frame's own plane (stereovision.py:97-113)
+    HIP_TRY(begin(kLsPipeline));
+    if (int rc = sv_batch_pipeline_planes(b, &L->cam, q.point_thr, q.hist_thr, 0, 0)) return rc;
+    HIP_TRY(end(kLsPipeline));
+    // road raster + non-zero walk (+ imageRoadMap) (stereovision.py:131-156)
+    HIP_TRY(begin(kLsRoad));
+    if (q.road) {
+        if (int rc = sv_batch_road_raster(b, 0)) return rc;
+    }
+    HIP_TRY(end(kLsRoad));
+    if (L->pending == seq) L->pending = -1;
+    return SV_OK;
+}
+
+static int loop_flush(sv_loop* L) {
+    if (L->pending < 0) return SV_OK;
+    HIP_TRY(hipSetDevice(L->device));
+    return loop_enqueue_tail(L, L->pending, 0);
+}
+
+// Enqueue order of sv_loop_submit(k), slot s = k % slots, the previous batch k - 1 on slot ps:
+//   slot s:  input(k) -> pre-pass(k) -> maskpoints(k)   [the host reads k's counts: they size the draw launch]
+//   slot s:  draw(k)  (after batch k - 1's evaluation: a frame's evaluation needs a whole CU's LDS)
+//   slot ps: gate(draw(k) resident) -> pipeline(k - 1) -> road(k - 1)
+//   slot s:  evaluation(k)  (after road(k - 1): beside pre-pass(k + 1) and maskpoints(k + 1), which use no LDS)
+// so batch k's pipeline and road pass are enqueued by the next submit (or by sv_loop_wait / _timeline).
 int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     if (!L) return fail(SV_E_ARG, "sv_loop_submit: null loop");
     if (first_frame_id < 0) return fail(SV_E_ARG, "sv_loop_submit: first_frame_id >= 0");
@@ -2218,6 +2281,9 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     sv_batch* b = L->slot[s];
     hipStream_t st = b->stream;
     HIP_TRY(hipSetDevice(L->device));
+    if (q.slots == 1) {   // one slot: nothing to overlap, the previous batch's tail first
+        if (int rc = loop_flush(L)) return rc;
+    }
     if (seq == 0) HIP_TRY(hipEventRecord(L->epoch, st));
     auto begin = [&](int stage) -> hipError_t {
         if (seq > 0 && ps != s) {   // the same stage of the batch before, on the other slot's stream
@@ -2252,21 +2318,24 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     HIP_TRY(begin(kLsMaskpoints));
     if (int rc = batch_ransac_prepare(b, &L->cam, q.trials, q.k)) return rc;
     HIP_TRY(end(kLsMaskpoints));
-    // RANSAC (stereovision.py:94): frame g draws after random.seed(seed_base + g). The host waits here for this
-    // batch's counts; the previous batch's stages are all enqueued already.
-    HIP_TRY(begin(kLsRansac));
-    if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k, st)) return rc;
-    HIP_TRY(end(kLsRansac));
-    // the pipeline with every frame's own plane (stereovision.py:97-113)
-    HIP_TRY(begin(kLsPipeline));
-    if (int rc = sv_batch_pipeline_planes(b, &L->cam, q.point_thr, q.hist_thr, 0, 0)) return rc;
-    HIP_TRY(end(kLsPipeline));
-    // road raster + non-zero walk (+ imageRoadMap) (stereovision.py:131-156)
-    HIP_TRY(begin(kLsRoad));
-    if (q.road) {
-        if (int rc = sv_batch_road_raster(b, 0)) return rc;
+    // RANSAC draw (stereovision.py:94): frame g draws after random.seed(seed_base + g); the host waits here for this
+    // batch's counts, with the previous batch's evaluation already enqueued
+    if (seq > 0 && ps != s) HIP_TRY(hipStreamWaitEvent(st, L->t1[ps][kLsEval], 0));
+    HIP_TRY(begin(kLsDraw));
+    if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k, st, 1,
+                                     L->gate.as<uint64_t>(), (uint64_t)seq + 1))
+        return rc;
+    HIP_TRY(end(kLsDraw));
+    // the previous batch's pipeline and road pass, gated on this draw's dispatch
+    if (L->pending >= 0) {
+        if (int rc = loop_enqueue_tail(L, L->pending, (uint64_t)seq + 1)) return rc;
     }
-    HIP_TRY(end(kLsRoad));
+    // RANSAC evaluation, after the previous batch's road pass
+    if (seq > 0 && ps != s) HIP_TRY(hipStreamWaitEvent(st, L->t1[ps][kLsRoad], 0));
+    HIP_TRY(begin(kLsEval));
+    if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k, st, 2)) return rc;
+    HIP_TRY(end(kLsEval));
+    L->pending = seq;
     L->slot_seq[s] = seq;
     L->slot_first[s] = first_frame_id;
     L->next = seq + 1;
@@ -2287,6 +2356,7 @@ static int loop_slot_of(sv_loop* L, int64_t seq, size_t* out) {
 int sv_loop_wait(sv_loop* L, int64_t seq) {
     size_t s;
     if (int rc = loop_slot_of(L, seq, &s)) return rc;
+    if (int rc = loop_flush(L)) return rc;
     HIP_TRY(hipSetDevice(L->device));
     HIP_TRY(hipEventSynchronize(L->t1[s][kLsRoad]));
     return SV_OK;
@@ -2305,6 +2375,7 @@ int sv_loop_timeline(sv_loop* L, int64_t seq, double* out) {
     size_t s;
     if (!out) return fail(SV_E_ARG, "sv_loop_timeline: null out");
     if (int rc = loop_slot_of(L, seq, &s)) return rc;
+    if (int rc = loop_flush(L)) return rc;
     HIP_TRY(hipSetDevice(L->device));
     HIP_TRY(hipEventSynchronize(L->t1[s][kLsRoad]));
     for (int st = 0; st < kLsCount; ++st) {

@@ -158,12 +158,16 @@ struct RansacScratch {
 };
 size_t ransac_sidx_bytes(int64_t max_n, int frames, int trials, int k);
 // max_n: the largest frame's point count; max_pool_n: the largest count that takes random.sample's pool
-// branch (n <= setsize(k)), 0 if none (both size the draw kernel's LDS). trials <= 4096.
+// branch (n <= setsize(k)), 0 if none (both size the draw kernel's LDS). trials <= 4096. phases: 1 = the draw
+// kernel, 2 = the evaluation kernel, 3 = both (in that order; the frame loop runs them as separate stages).
 hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H, int W, int64_t cap, const KParams& cp,
                                const int64_t* counts, int64_t max_n, int64_t max_pool_n, uint64_t seed_base,
                                int64_t first_frame, int frames, int trials, int k, const RansacScratch& rs, double* abc,
                                double* err, int32_t* trial, uint32_t* flags, int32_t* trace, int trace_trials,
-                               int ablate, hipStream_t s);
+                               int ablate, int phases, uint64_t* started, uint64_t epoch, hipStream_t s);
+// the frame loop's dispatch gate: returns once *flag >= epoch (the draw kernel's last workgroup, launched with
+// started = flag, is resident) or after max_ms of wall clock
+hipError_t launch_loop_gate(const uint64_t* flag, uint64_t epoch, double max_ms, hipStream_t s);
 // out[i] = plane_fields of abc[3i..3i+2] (trial[i] < 0, or trial NULL and a NaN plane: valid = 0);
 // trial may be NULL (a device plane, e.g. the RCCL broadcast buffer).
 hipError_t launch_frame_planes(const double* abc, const int32_t* trial, int frames, const KParams& p, double thr,

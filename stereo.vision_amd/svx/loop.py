@@ -6,12 +6,14 @@ in batches and every batch runs the non-cv2 stages of that function:
     input -> pre-pass (fillDisparity / fillAltDisparity, carmask)      stereovision.py:53-76
           -> maskpoints (masked step-2 projection)                      stereovision.py:74-85
           -> RANSAC(maskpoints, 600), frame g seeded with seed_base + g stereovision.py:94
+             (two stages: the draw replay, the evaluation)
           -> the pipeline with each frame's own plane                   stereovision.py:97-113
           -> road raster + non-zero walk (+ imageRoadMap)               stereovision.py:131-156
 
 FrameLoop keeps `slots` batches in flight, one HIP stream each; a stage of batch k waits for the same stage of
-batch k - 1 (a device event), so with two slots batch k + 1's RANSAC — one wave's dependent draw chain per frame,
-the HBM nearly idle — runs beside batch k's HBM-bound pipeline and road pass. The previous cleaned frame of
+batch k - 1 (a device event), and the RANSAC evaluation of batch k for batch k - 1's road pass, so with two slots
+batch k + 1's draw — one wave's dependent chain per frame, the HBM nearly idle — runs beside batch k's HBM-bound
+pipeline and road pass, and batch k + 1's evaluation (a CU's LDS per frame) beside batch k + 2's pre-pass. The previous cleaned frame of
 fillDisparity is carried from batch to batch on the device: a sequence of batches gives exactly the results of
 one long batch (tests/test_gpu_loop.py checks every frame against tests/golden/plane_digests.npz).
 
@@ -29,7 +31,7 @@ import numpy as np
 from . import _abi
 from .batch import CAMERA, Batch
 
-STAGES = ("input", "prepass", "maskpoints", "ransac", "pipeline", "road")
+STAGES = ("input", "prepass", "maskpoints", "draw", "eval", "pipeline", "road")
 _SOURCES = {"caller": 0, "synth": 1}
 _PREPASS = {"none": 0, "previous": 1, "mean": 2}
 _ROAD = {"none": 0, "walk": 1, "map": 2}

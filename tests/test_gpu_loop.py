@@ -65,7 +65,7 @@ def test_two_batches_in_flight_every_frame(gold, mask, slots):
             assert check_batch(b, first, gold[first:first + 2048]) == [], (slots, seq)
         tl = loop.timeline(seqs[-1])
         prev_end = 0.0
-        for name in ("input", "prepass", "maskpoints", "ransac", "pipeline", "road"):
+        for name in ("input", "prepass", "maskpoints", "draw", "eval", "pipeline", "road"):
             a, z = tl[name]
             assert prev_end - 1e-3 <= a <= z, (name, tl)
             prev_end = z
