@@ -457,6 +457,28 @@ def extras(b, args, with_cpu, first=0):
     if not args.no_parity:
         pc, pm = check_plane_parity(b, first)
         ex["_planes_parity"] = [pc, pm]
+    # the road pass of these points two ways: from the points (road_kernel: 8 B a point read) and from the
+    # bitmap the resident pipeline writes as it makes them (sv_batch_road_bits: pass 2 marks the pixels, 68 KB a
+    # frame; road_rowscan + road_rows kernels, one wave a row), with the pipeline's own time in both modes
+    n2p = int(b.read_counts()[:, 2].sum())
+    road_pts = _timed(b, lambda: b.road_raster(sync=False), 3, ramp_ms=args.ramp_ms / 3)
+    b.road_bits(True)
+    b.pipeline_planes(sync=True)
+    _timed(b, lambda: b.pipeline_planes(sync=False), 5, reset=True, ramp_ms=args.ramp_ms / 3)
+    kb_ms, kb_n = b.timing("pipeline")
+    road_bits = _timed(b, lambda: b.road_raster(sync=False), 3, ramp_ms=args.ramp_ms / 3)
+    b.road_bits(False)
+    b.pipeline_planes(sync=True)
+    px_all = b.frames * H * W
+    ex["road_from_bitmap"] = {
+        "road_ms_per_batch": round(road_bits, 3), "road_from_points_ms_per_batch": round(road_pts, 3),
+        "pipeline_with_bitmap_gpu_ms_per_call": round(kb_ms / max(kb_n, 1), 4),
+        "pipeline_gpu_ms_per_call": ex["pipeline_frame_planes"]["gpu_ms_per_call"],
+        "points": n2p, "bytes_from_bitmap": 4 * 32 * H * b.frames + px_all + 8 * n2p,
+        "bytes_from_points": 8 * n2p + px_all + 8 * n2p,
+        "note": "per-frame-plane points; bytes count one walk entry per point (an upper bound); the bitmap is "
+                "written by the pipeline (+0.28 GB per 4096 frames, counted in its time above)",
+        "kernels": "road_rowscan_kernel + road_rows_kernel (from the bitmap) vs road_kernel (from the points)"}
 
     fmod = types.SimpleNamespace(camera_focal_length_px=399.9745178222656, stereo_camera_baseline_m=0.2090607502,
                                  image_centre_w=474.5, image_centre_h=262.0, carmask=mask)

@@ -271,6 +271,12 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
  * the 544 x 1024 imgL; the rest of imgL is unpainted, as the pipeline's points
  * never leave the disparity's own grid). Read-back: H x W x 3 u8. */
 int sv_batch_road_map(sv_batch* b, int enable);
+/* With enable != 0, later frame-resident pipeline calls on 1024-wide frames at step 1 also write a bitmap of
+ * the pixels their int32 points mark (pass 2 marks them as it makes the points; 68 KB a frame), and the next
+ * sv_batch_road_raster builds the images, walks and imageRoadMap from it — one wave a row — instead of
+ * re-reading the points (8 B each). The outputs are the same either way; other shapes and the tiled kernels
+ * keep the points path. */
+int sv_batch_road_bits(sv_batch* b, int enable);
 int sv_batch_read_road_map(sv_batch* b, int frame, uint8_t* out);
 
 /* Batched RANSAC (stereovision.py:84-94 for every frame):

@@ -317,6 +317,127 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
     if (tid == 0) nzcount[frame] = running;
 }
 
+// ---------------------------------------------------------------------------
+// The road pass from the pipeline's bitmap (PipeBuffers::rbits: the resident pipeline marks every int32 point's
+// pixel, numpy's -1 wrap included, as it makes the points; 1024-wide frames). The image, the walk and the paint
+// are then functions of 68 KB a frame instead of the 8 B a point the road_kernel reads, and the rows are
+// independent: one wave a row.
+//  * road_rowscan_kernel — one workgroup a frame: each row's non-zero count (popcount of its 32 words), an
+//                          exclusive scan over the rows -> the walk index of the row's first pixel; the frame's
+//                          total -> nzcount.
+//  * road_rows_kernel    — one wave a row: the row's bytes (0 / 255, 16 pixels a lane, one 16-byte store), its
+//                          walk entries [x, y] in raster order (a wave scan orders the lanes, the x are staged in
+//                          LDS in output order, then written as coalesced 8-byte pairs), and on request the
+//                          imageRoadMap row (the BGR row with [0, 255, 0] at every marked pixel).
+// ---------------------------------------------------------------------------
+constexpr int kRbWords = 32;   // words a row: 1024 pixels
+
+__global__ __launch_bounds__(256) void road_rowscan_kernel(const uint32_t* __restrict__ bits, int H,
+                                                           int32_t* __restrict__ roff, int64_t* __restrict__ nzcount) {
+    __shared__ uint32_t wtot[4];
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int frame = blockIdx.x;
+    const uint4* fb = reinterpret_cast<const uint4*>(bits + (int64_t)frame * H * kRbWords);
+    int32_t* fo = roff + (int64_t)frame * H;
+    constexpr int R = 4;   // rows a thread (H <= 1024)
+    uint32_t cnt[R], tot = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = tid * R + r;
+        uint32_t c = 0;
+        if (row < H) {
+#pragma unroll
+            for (int q = 0; q < kRbWords / 4; ++q) {
+                const uint4 w = fb[row * (kRbWords / 4) + q];
+                c += __builtin_popcount(w.x) + __builtin_popcount(w.y) + __builtin_popcount(w.z) +
+                     __builtin_popcount(w.w);
+            }
+        }
+        cnt[r] = c;
+        tot += c;
+    }
+    const uint32_t inc = wave_incl_scan(tot);
+    if (lane == 63) wtot[wave] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        wbase += w < wave ? wtot[w] : 0u;
+        all += wtot[w];
+    }
+    uint32_t run = wbase + inc - tot;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = tid * R + r;
+        if (row < H) fo[row] = (int32_t)run;
+        run += cnt[r];
+    }
+    if (tid == 0) nzcount[frame] = all;
+}
+
+__global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restrict__ bits, int H,
+                                                        const int32_t* __restrict__ roff, int64_t cap,
+                                                        uint8_t* __restrict__ img, int32_t* __restrict__ nzout,
+                                                        const uint8_t* __restrict__ bgr, uint8_t* __restrict__ paint) {
+    __shared__ uint16_t sx[4][kRbWords * 32];   // a wave's row: its walk's x in output order
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int frame = blockIdx.y, y = blockIdx.x * 4 + wave;
+    if (y >= H) return;   // (whole waves; no block barrier below)
+    const int64_t row = (int64_t)frame * H + y;
+    const uint32_t word = bits[row * kRbWords + (lane >> 1)];
+    const uint32_t b16 = (lane & 1) ? word >> 16 : word & 0xFFFFu;   // pixels 16 lane .. 16 lane + 15
+    uint32_t q[4];   // bit k of a nibble -> byte k = 0xFF (v_perm selector 0x0D; 0x0C gives 0x00)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t nib = (b16 >> (4 * i)) & 0xFu;
+        q[i] = __builtin_amdgcn_perm(0u, 0u, ((__umul24(nib, 0x00204081u) & 0x01010101u) + 0x0C0C0C0Cu));
+    }
+    __builtin_nontemporal_store((v4i){(int)q[0], (int)q[1], (int)q[2], (int)q[3]},
+                                reinterpret_cast<v4i*>(img + row * (kRbWords * 32) + 16 * lane));
+    // the walk: [x, y] of the row's marked pixels, in order, from the row's first index
+    const uint32_t cnt = __builtin_popcount(b16);
+    const uint32_t inc = wave_incl_scan(cnt);
+    const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+    uint32_t m = b16, o = inc - cnt;
+    while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1;
+        sx[wave][o++] = (uint16_t)(16 * lane + b);
+    }
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its LDS writes land before its reads
+    v2i* dst = reinterpret_cast<v2i*>(nzout) + (int64_t)frame * cap + roff[row];
+    for (uint32_t j = lane; j < total; j += kWave) __builtin_nontemporal_store((v2i){(int)sx[wave][j], y}, dst + j);
+    if (paint) {   // imageRoadMap (stereovision.py:131-133): the lane's 16 pixels, 48 bytes
+        const uint4* src = reinterpret_cast<const uint4*>(bgr + row * (kRbWords * 32) * 3 + 48 * lane);
+        uint4 v[3] = {src[0], src[1], src[2]};
+        uint8_t* px = reinterpret_cast<uint8_t*>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if ((b16 >> k) & 1u) {
+                px[3 * k] = 0;
+                px[3 * k + 1] = 255;
+                px[3 * k + 2] = 0;
+            }
+        uint4* out = reinterpret_cast<uint4*>(paint + row * (kRbWords * 32) * 3 + 48 * lane);
+        out[0] = v[0];
+        out[1] = v[1];
+        out[2] = v[2];
+    }
+}
+
+hipError_t launch_road_bits(const uint32_t* bits, int frames, int H, int W, int32_t* roff, int64_t cap,
+                            uint8_t* img, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr, uint8_t* paint,
+                            hipStream_t s) {
+    if (frames <= 0) return hipSuccess;
+    if (W != kRbWords * 32 || H <= 0 || H > 1024 || (paint && !bgr)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(road_rowscan_kernel, dim3(frames), dim3(256), 0, s, bits, H, roff, nzcount);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(road_rows_kernel, dim3((H + 3) / 4, frames), dim3(256), 0, s, bits, H, roff, cap, img, nzout,
+                       bgr, paint);
+    return hipGetLastError();
+}
+
 hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* counts, int64_t cap, uint8_t* img,
                        int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr,
                        uint8_t* paint, hipStream_t s) {

@@ -597,7 +597,55 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
 // pass 2 of one chunk: keep2, block scan, descriptor scatter, then the
 // chunk's whole output groups. Two barriers. Loads chunk c + 1 into r before
 // the stores (PF).
-template <int STEP, int QP, bool LC, bool PF, class SH>
+// The road bitmap's marks of one lane (RB: LC, 1024-wide rows): its 16 points are 16 consecutive x = x0 + k of row
+// gy (x0 = 16 lane), each marking pixel (x0 + k - dx, gy - dy) (generatePointsAsImage, functions.py:339-344).
+// Relative to x0 - 1 a kept point sets bit k + 1 - dx of row gy - dy's 17-bit window; the window is bits 15..31
+// of word x0 / 32 (x0 % 32 == 16) or bit 31 of the word before and bits 0..15 (x0 % 32 == 0). Wave w holds one
+// row, but row gy - 1 also gets the marks of row gy's wave, so the words are OR-ed (ds_or, no return).
+template <class SH>
+__device__ __forceinline__ void rb_mark(SH& sh, uint32_t keep, uint32_t bxm, uint32_t bym, int gy, int x0, int Wu) {
+    if (!keep) return;
+    const uint32_t kb1 = keep & bym, kb0 = keep & ~bym;
+    const uint32_t m0 = ((kb0 & ~bxm) << 1) | (kb0 & bxm);   // row gy
+    const uint32_t m1 = ((kb1 & ~bxm) << 1) | (kb1 & bxm);   // row gy - 1
+    const int w = x0 >> 5;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t m = h ? m1 : m0;
+        if (!m) continue;
+        const int y = gy - h;
+        uint32_t* row = y < 0 ? sh.rwrap : sh.rring + 32 * (y & 7);   // y = -1: numpy's last row
+        if (x0 & 16) {
+            atomicOr(row + w, m << 15);
+        } else {
+            atomicOr(row + w, m >> 1);
+            if (m & 1u) {   // x0 - 1: the word before, or (x0 = 0) numpy's last column
+                const int xl = w > 0 ? x0 - 1 : Wu - 1;
+                atomicOr(row + (xl >> 5), 1u << (xl & 31));
+            }
+        }
+    }
+}
+
+// Write the road bitmap's rows [*rflushed, upto) to out (frame's rows x 32 words) and clear their ring slots. Each
+// thread owns one (slot, word) of the ring for the whole frame (t = 32 * slot + word), so no barrier is needed
+// between a flush and the next one; marks reach a slot only in a chunk whose barriers order them after its clear.
+// (upto - *rflushed <= 8.)
+template <class SH>
+__device__ __forceinline__ void rb_flush(SH& sh, uint32_t* out, int& rflushed, int upto, int H) {
+    const int t = threadIdx.x, slot = t >> 5, word = t & 31;
+    // the row in [rflushed, upto) that this thread's slot holds, if any
+    const int y = rflushed + ((slot - rflushed) & 7);
+    if (y < upto) {
+        uint32_t v = sh.rring[t];
+        if (y == H - 1) v |= sh.rwrap[word];
+        out[32 * y + word] = v;
+        sh.rring[t] = 0u;
+    }
+    rflushed = upto;
+}
+
+template <int STEP, int QP, bool LC, bool PF, bool RB, class SH>
 __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool more, const uint32_t* hist,
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
                                          const uint8_t* fdisp, const uint8_t* fbgr, const RLean& L,
@@ -678,6 +726,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
     uint32_t olc = running + (uint32_t)excl;   // LC: the lane's outputs are one run
     // LC, narrow: the lane's one row's transposed dy word (bit dd = the dy bit of d = dlo + dd)
     const uint32_t tyl = (LC && narrow) ? dl[kRTyOff + (((uint32_t)max(r.g.gy[0], 0) * STEP) & 31u)] : 0u;
+    uint32_t bxm = 0u, bym = 0u;   // RB: the lane's delta bits, bit 4 i + k
 #pragma unroll
     for (int i = 0; i < QPL; ++i) {
         uint32_t o = LC ? olc : rowbase + (uint32_t)((excl >> (16 * i)) & 0xFFFF);
@@ -719,8 +768,16 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
             *(bit ? &sh.stage[o & (stage_of<QP>() - 1)] : sh.dump + tid) =
                 rdesc(dv[k], gy, (uint32_t)(4 * r.g.q[i] + k), bx[k], by[k]);
             o += bit;
+            if constexpr (RB) {
+                bxm |= bx[k] << (4 * i + k);
+                bym |= by[k] << (4 * i + k);
+            }
         }
         olc = o;
+    }
+    if constexpr (RB) {   // LC, step 1: the lane's 16 points are x0 .. x0 + 15 of row gy
+        static_assert(!RB || (LC && STEP == 1 && QPL == 4), "the road bitmap needs lane-contiguous step-1 quads");
+        rb_mark(sh, keep, bxm, bym, r.g.gy[0], 4 * r.g.q[0], bf.rb_Wu);
     }
     if (PF && more) p2_load<STEP, QP, LC>(r, c + 1, tid, fdisp, sh.crange, bf, p, true, next_run, fkb);   // in flight before the stores
     __syncthreads();
@@ -754,6 +811,10 @@ struct FusedShared {
     alignas(16) uint32_t crange[maxchunks_of<QP>() * 4];
     uint32_t dlt[kRDeltaWords];   // pass 2: the chunk's delta words (scatter lookups)
     uint32_t cany[8];             // per chunk: can the frame's plane keep any of its grid points
+    // pass 2 with the road bitmap (RB): image rows being marked, row y in slot y & 7 (32 words of 32 pixels);
+    // marks for row -1 (numpy's last row) wait in rwrap until row H - 1 is written
+    uint32_t rring[8 * 32];
+    uint32_t rwrap[32];
 };
 static_assert(sizeof(FusedShared<4>) <= 32768, "5 workgroups per CU (160 KiB LDS), as many as 93 VGPRs allow");
 
@@ -830,7 +891,7 @@ __device__ __forceinline__ void frame_pass1(int frame, FusedShared<QP>& sh, cons
     __syncthreads();   // histogram, dirty bits, counts complete
 }
 
-template <int STEP, int QP, bool LC, bool PF>
+template <int STEP, int QP, bool LC, bool PF, bool RB>
 __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, const PipeBuffers& bf,
                                             const RLean& L, const FramePlane* Lp,
                                             const RParams& p) {
@@ -854,6 +915,15 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
         return c + 1 == n2 || (cr.x | cr.y | cr.z | cr.w) != 0u;
     };
     const uint16_t* fkb = bf.kbits + (int64_t)frame * p.nchunks * 256;
+    // RB: the road bitmap's rows, written as they become final (chunk c + 1 can still mark row 4 (c + 1) - 1)
+    uint32_t* frb = RB ? bf.rbits + (int64_t)frame * bf.rb_H * 32 : nullptr;
+    int rflushed = 0;
+    if constexpr (RB) {
+        sh.rring[tid] = 0u;
+        if (tid < 32) sh.rwrap[tid] = 0u;
+        __syncthreads();
+    }
+    constexpr int RPC = RB ? 4 : 1;   // RB: grid rows per chunk (1024 quads of 256 a row)
     P2Regs<STEP, QP, LC> r2;
     r2.staged = false;
     if (PF && n2 > 0) p2_load<STEP, QP, LC>(r2, 0, tid, fdisp, sh.crange, bf, p, false, run(0), fkb);
@@ -861,11 +931,19 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
         if (!PF) p2_load<STEP, QP, LC>(r2, c, tid, fdisp, sh.crange, bf, p, c > 0, run(c), fkb);
         if (!run(c)) {   // uniform; c + 1 < n2 here
             if (PF) p2_load<STEP, QP, LC>(r2, c + 1, tid, fdisp, sh.crange, bf, p, true, run(c + 1), fkb);
+            if constexpr (RB) rb_flush(sh, frb, rflushed, RPC * (c + 1) - 1, bf.rb_H);
             continue;
         }
-        p2_chunk<STEP, QP, LC, PF>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oY, oZ,
-                               oPx, oPy,
-                               running, flushed, c + 1 < n2 && run(c + 1), fkb, p);
+        p2_chunk<STEP, QP, LC, PF, RB>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oY,
+                                       oZ, oPx, oPy,
+                                       running, flushed, c + 1 < n2 && run(c + 1), fkb, p);
+        if constexpr (RB) {   // after the chunk's last barrier: its marks are in the ring
+            if (c + 1 < n2) {
+                rb_flush(sh, frb, rflushed, RPC * (c + 1) - 1, bf.rb_H);
+            } else {   // the frame's last chunk: every remaining row, row H - 1 with the wrapped marks
+                while (rflushed < bf.rb_H) rb_flush(sh, frb, rflushed, min(rflushed + 8, bf.rb_H), bf.rb_H);
+            }
+        }
     }
     if (tid == 0) bf.counts[4 * (int64_t)frame + 2] = running;
 }
@@ -874,7 +952,7 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
 // One workgroup = one frame: pass 1 over all chunks, then pass 2 (grid = frames).
 // The frame's plane: bf.planes[frame * bf.plane_stride] (device memory).
 // ---------------------------------------------------------------------------
-template <int STEP, int QP, bool LC, bool PF, bool PF1>
+template <int STEP, int QP, bool LC, bool PF, bool PF1, bool RB>
 __device__ __forceinline__ void fused_body(const PipeBuffers& bf, const RParams& p,
                                            FusedShared<QP>& sh) {
     const int tid = threadIdx.x;
@@ -892,13 +970,13 @@ __device__ __forceinline__ void fused_body(const PipeBuffers& bf, const RParams&
         cn[0] = (int64_t)sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
         cn[1] = (int64_t)sh.red[4] + sh.red[5] + sh.red[6] + sh.red[7];
     }
-    frame_pass2<STEP, QP, LC, PF>(frame, sh, bf, L, Lp, p);
+    frame_pass2<STEP, QP, LC, PF, RB>(frame, sh, bf, L, Lp, p);
 }
 
-template <int STEP, int QP, bool LC, bool PF, bool PF1 = false>
+template <int STEP, int QP, bool LC, bool PF, bool PF1 = false, bool RB = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void resident_fused_kernel(PipeBuffers bf, RParams p) {
     __shared__ FusedShared<QP> sh;
-    fused_body<STEP, QP, LC, PF, PF1>(bf, p, sh);
+    fused_body<STEP, QP, LC, PF, PF1, RB>(bf, p, sh);
 }
 
 bool resident_supported(const KParams& p) {   // frame_quads <= 2^20: every QP's chunk count fits its dirty bits
@@ -912,6 +990,11 @@ static bool resident_lane_quads(const KParams& kp) {
     const char* v = svx_knob("SVX_RES_LC");   // read per call (tools/prof.py ab --env)
     const bool on = !(v && v[0] == '0');
     return on && kp.step == 1 && kp.Q % 4 == 0 && kp.W % 16 == 0 && kp.frame_px % 16 == 0;
+}
+
+bool resident_road_bits_supported(const KParams& p) {   // 1024-wide rows: 4 grid rows a chunk, 32 words a row
+    return resident_supported(p) && p.step == 1 && p.W == 1024 && p.Q == 256 && p.H <= 1024 && p.Hg >= 1 &&
+           resident_lane_quads(p);
 }
 
 static RParams resident_params(const KParams& kp, int qpl) {
@@ -955,7 +1038,13 @@ hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, int
     if (frames <= 0) return hipSuccess;
     if (!resident_supported(kp) || !b.planes) return hipErrorInvalidValue;
     const dim3 grid(frames), block(256);
-    if (kp.step == 1 && resident_lane_quads(kp)) {
+    if (b.rbits) {   // the road bitmap too (resident_road_bits_supported)
+        if (!resident_road_bits_supported(kp) || !resident_lane_quads(kp) || b.rb_H != kp.H) return hipErrorInvalidValue;
+        const RParams p = resident_params(kp, 4);
+        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true, true, true>), grid, block, 0, s, b, p);
+        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true, false, true>), grid, block, 0, s, b, p);
+        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, false, false, true>), grid, block, 0, s, b, p);
+    } else if (kp.step == 1 && resident_lane_quads(kp)) {
         const RParams p = resident_params(kp, 4);
         if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true, true>), grid, block, 0, s, b, p);
         else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true>), grid, block, 0, s, b, p);

@@ -267,6 +267,9 @@ struct sv_batch {
     DevBuf road, nz, nzcount;   // road images (frames x H x W), their non-zero walks (frames x cap x 2)
     bool nz_fresh = false;      // nz holds the walk of the current road images (road_kernel wrote both)
     DevBuf rmap;                // imageRoadMap (stereovision.py:131-133): frames x H x W x 3, on request
+    bool road_bits = false;     // the resident pipeline also writes the road bitmap (sv_batch_road_bits)
+    bool rbits_fresh = false;   // rbits holds the bitmap of the current pipeline points
+    DevBuf rbits, roff;         // the bitmap (frames x H x 32 words); the road pass's per-row walk offsets
     bool want_rmap = false, rmap_fresh = false;
     DevBuf mpts, rres;          // one frame's maskpoints as fp64 (read-back scratch); counts + batched RANSAC results
     DevBuf prev0buf, rdbuf;     // the host prev0 of sv_batch_prepass; sv_batch_read_disp's masked frame (batch-owned:
@@ -543,7 +546,7 @@ int sv_batch_destroy(sv_batch* b) {
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppx, &b->ppy, &b->ctrl, &b->masks,
                       &b->carmask, &b->road, &b->rmap, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtab, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
-                      &b->glut, &b->ghist, &b->sgflags, &b->prev0buf, &b->rdbuf})
+                      &b->glut, &b->ghist, &b->sgflags, &b->prev0buf, &b->rdbuf, &b->rbits, &b->roff})
         if (x->p) (void)hipFree(x->p);
     if (b->hcnt) (void)hipHostFree(b->hcnt);
     if (b->cnt_ev) (void)hipEventDestroy(b->cnt_ev);
@@ -843,6 +846,14 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
         HIP_TRY(launch_store_plane(fp, b->dplane.as<FramePlane>(), b->stream));
         bf.planes = b->dplane.as<FramePlane>();
         bf.plane_stride = 0;
+    }
+    b->rbits_fresh = false;
+    if (mode >= 2 && b->road_bits && resident_road_bits_supported(p)) {   // the road bitmap too (sv_batch_road_bits)
+        HIP_TRY(b->rbits.ensure(sizeof(uint32_t) * 32 * (size_t)b->H * b->frames));
+        bf.rbits = b->rbits.as<uint32_t>();
+        bf.rb_H = b->H;
+        bf.rb_Wu = b->Wu;
+        b->rbits_fresh = true;
     }
     if (mode == 2 && !b->pipe_placed && b->out_planes && b->frames >= 1024) {   // outside the timed region
         b->pipe_placed = true;
@@ -1324,9 +1335,16 @@ int sv_batch_road_raster(sv_batch* b, int sync) {
             HIP_TRY(b->rmap.ensure(px * 3 * b->frames));
             paint = b->rmap.as<uint8_t>();
         }
-        HIP_TRY(launch_road(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), b->counts, (int64_t)b->cap,
-                            b->road.as<uint8_t>(), b->frames, b->H, b->W, b->Wu, b->nz.as<int32_t>(),
-                            b->nzcount.as<int64_t>(), b->bgr.as<uint8_t>(), paint, b->stream));
+        if (b->rbits_fresh) {   // from the pipeline's bitmap (68 KB a frame) instead of its points (8 B a point)
+            HIP_TRY(b->roff.ensure(sizeof(int32_t) * (size_t)b->H * b->frames));
+            HIP_TRY(launch_road_bits(b->rbits.as<uint32_t>(), b->frames, b->H, b->W, b->roff.as<int32_t>(),
+                                     (int64_t)b->cap, b->road.as<uint8_t>(), b->nz.as<int32_t>(),
+                                     b->nzcount.as<int64_t>(), b->bgr.as<uint8_t>(), paint, b->stream));
+        } else {
+            HIP_TRY(launch_road(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), b->counts, (int64_t)b->cap,
+                                b->road.as<uint8_t>(), b->frames, b->H, b->W, b->Wu, b->nz.as<int32_t>(),
+                                b->nzcount.as<int64_t>(), b->bgr.as<uint8_t>(), paint, b->stream));
+        }
         b->rmap_fresh = paint != nullptr;
     } else {
         HIP_TRY(launch_raster(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), 1, b->counts, 4, 2, (int64_t)b->cap,
@@ -1349,6 +1367,12 @@ int sv_batch_nonzero(sv_batch* b, int sync) {
     HIP_TRY(launch_nonzero(b->road.as<uint8_t>(), b->frames, (int64_t)b->H * b->W, b->W, b->nz.as<int32_t>(),
                            (int64_t)b->cap, b->nzcount.as<int64_t>(), b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
+    return SV_OK;
+}
+
+int sv_batch_road_bits(sv_batch* b, int enable) {
+    if (!b) return fail(SV_E_ARG, "null batch");
+    b->road_bits = enable != 0;
     return SV_OK;
 }
 
@@ -2188,6 +2212,7 @@ int sv_loop_create(int device, const sv_loop_params* prm, const sv_camera* cam, 
         if (rc == SV_OK) L->slot[(size_t)i]->timing = false;
         if (rc == SV_OK && carmask) rc = sv_batch_set_mask(L->slot[(size_t)i], carmask);
         if (rc == SV_OK && q.road == 2) rc = sv_batch_road_map(L->slot[(size_t)i], 1);
+        if (rc == SV_OK && q.road) rc = sv_batch_road_bits(L->slot[(size_t)i], 1);
     }
     hipError_t e = hipSuccess;
     if (rc == SV_OK) {

@@ -56,6 +56,11 @@ struct PipeBuffers {
     int64_t cap;         // points per frame (Ng)
     const FramePlane* planes = nullptr;   // device planes: frame f uses planes[f * plane_stride] (else the KParams plane)
     int plane_stride = 1;                 // 0: one device plane for every frame (a broadcast plane)
+    // optional (resident kernel, 1024-wide frames at step 1): a bitmap of the pixels the int32 points mark
+    // (generatePointsAsImage's road image, numpy's -1 wrap included), frames x rb_H rows x 32 words, written by
+    // pass 2 as it makes the points; the road pass then reads 68 KB a frame instead of the points
+    uint32_t* rbits = nullptr;
+    int rb_H = 0, rb_Wu = 0;              // the image rows and the frame's own width (x = -1 wraps to rb_Wu - 1)
 };
 int pipeline_tiles_per_frame(const KParams& p);
 // The whole chain for frames [0, frames) in chunks: chunks + 2 fused stage
@@ -74,6 +79,8 @@ bool resident_supported(const KParams& p);
 // next chunk before issuing this chunk's stores (costs registers).
 hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, int frames,
                                     bool prefetch, hipStream_t s, bool prefetch1 = false);
+// b.rbits can be filled: W == 1024 at step 1 with lane-contiguous quads (4 grid rows a chunk, 32 words a row)
+bool resident_road_bits_supported(const KParams& p);
 // *dst = v on stream s (the resident kernel reads its planes from device memory).
 hipError_t launch_store_plane(const FramePlane& v, FramePlane* dst, hipStream_t s);
 
@@ -104,6 +111,12 @@ hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* coun
                        int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr,
                        uint8_t* paint, hipStream_t s);
 // img frames x px (px % 4 == 0, rows of W <= 4096 pixels)
+// The road pass from the resident pipeline's bitmap (PipeBuffers::rbits; W == 1024, H <= 1024): images, walks
+// (roff: frames x H scratch, the walk index of each row's first pixel) and, when paint != nullptr, the
+// imageRoadMap copies of bgr.
+hipError_t launch_road_bits(const uint32_t* bits, int frames, int H, int W, int32_t* roff, int64_t cap,
+                            uint8_t* img, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr, uint8_t* paint,
+                            hipStream_t s);
 hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
                           hipStream_t s);
 

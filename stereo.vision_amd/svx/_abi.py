@@ -63,6 +63,7 @@ SIGNATURES = {
     "sv_batch_nonzero": [P, I],
     "sv_batch_read_road": [P, I, P, P, I64, PI64],
     "sv_batch_road_map": [P, I],
+    "sv_batch_road_bits": [P, I],
     "sv_batch_read_road_map": [P, I, P],
     "sv_point_errors": [P, I64, I64, P, P],
     "sv_hue_histogram": [P, I64, I64, P, P, P],

@@ -232,6 +232,11 @@ class Batch:
         planePoints) in every later road_raster() pass."""
         _abi.call("sv_batch_road_map", self._h, int(bool(enable)))
 
+    def road_bits(self, enable=True):
+        """Later resident pipeline calls (1024-wide frames, step 1) also write the bitmap of their points' pixels,
+        and road_raster() builds its outputs from it instead of re-reading the points (sv_batch_road_bits)."""
+        _abi.call("sv_batch_road_bits", self._h, int(bool(enable)))
+
     def read_road_map(self, frame):
         out = np.empty((self.H, self.W, 3), np.uint8)
         _abi.call("sv_batch_read_road_map", self._h, frame, _abi.ptr(out))

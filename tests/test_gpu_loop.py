@@ -59,10 +59,16 @@ def test_two_batches_in_flight_every_frame(gold, mask, slots):
         if slots == 1:   # one slot: the first batch's results are gone once the second is submitted
             with pytest.raises(Exception):
                 loop.batch(seqs[0])
+        import oracle
         for seq in held:
             loop.wait(seq)
             b, first = loop.batch(seq)
             assert check_batch(b, first, gold[first:first + 2048]) == [], (slots, seq)
+            for f in (0, 1, 1000, 2047):   # the road pass (from the pipeline's bitmap) against the pinned points
+                _, pts = b.read_points(f)
+                rimg = oracle.road_raster(pts)
+                img, walk = b.read_road(f, walk=True)
+                assert np.array_equal(img, rimg) and np.array_equal(walk, oracle.nonzero_points(rimg)), (seq, f)
         tl = loop.timeline(seqs[-1])
         prev_end = 0.0
         for name in ("input", "prepass", "maskpoints", "draw", "eval", "pipeline", "road"):

@@ -149,10 +149,16 @@ def test_road_raster_reference_fixture(svx_mod, golden):
 
 
 @pytest.mark.parametrize("step", [1, 2])
-def test_batch_road_raster_and_walk(svx_mod, step):
+@pytest.mark.parametrize("bits", [False, True])
+def test_batch_road_raster_and_walk(svx_mod, step, bits):
+    """bits: the resident pipeline writes the road bitmap and the road pass reads it (sv_batch_road_bits; step 1,
+    1024-wide frames; at step 2 the points path runs either way)."""
     frames, first = 5, 321
     with svx_mod.batch.Batch(frames, step=step, with_bgr=True, with_points=True) as b:
         b.synth(first)
+        if bits:
+            b.pipeline_mode("resident")
+            b.road_bits(True)
         b.pipeline()
         b.road_raster()
         b.nonzero()
@@ -166,7 +172,8 @@ def test_batch_road_raster_and_walk(svx_mod, step):
 
 
 @pytest.mark.parametrize("step", [1, 2])
-def test_batch_road_edge_frames(svx_mod, step):
+@pytest.mark.parametrize("bits", [False, True])
+def test_batch_road_edge_frames(svx_mod, step, bits):
     """The fused road pass (bands of rows in LDS, a cursor over the raster-ordered points) on frames with no
     point, every grid point, points on a few scattered rows only, and random disparity: image and walk equal
     the oracle's generatePointsAsImage and its raster-order walk."""
@@ -185,6 +192,9 @@ def test_batch_road_edge_frames(svx_mod, step):
     with svx_mod.batch.Batch(len(frames), H=H, W=W, step=step, with_bgr=True, with_points=True) as b:
         for f, d in enumerate(frames):
             b.upload(f, d, bgr)
+        if bits:
+            b.pipeline_mode("resident")
+            b.road_bits(True)
         b.pipeline(**kw)
         b.road_map(True)
         b.road_raster()
