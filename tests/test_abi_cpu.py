@@ -192,3 +192,26 @@ def test_hue_keys_match_reference_strings():
     fx = json.load(open(os.path.join(GOLDEN, "stages.json")))
     seen = {key for c in fx["crops"].values() for key, _ in c["hist_items"] + c["default_hist_items"]}
     assert seen <= set(keys) and len(seen) > 900
+
+
+def test_loop_params_layout_matches_header(tmp_path):
+    """svx._abi.LoopParams (ctypes) has the size and field offsets of include/svx.h's sv_loop_params (checked by
+    compiling the header with the host C compiler)."""
+    import ctypes
+    import shutil
+    import subprocess
+
+    from svx import _abi
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no host C compiler")
+    fields = [f for f, _ in _abi.LoopParams._fields_]
+    src = tmp_path / "lp.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "svx.h"\nint main(void){printf("%zu'
+                   + "".join(" %zu" for _ in fields) + '\\n", sizeof(sv_loop_params)'
+                   + "".join(f", offsetof(sv_loop_params, {f})" for f in fields) + ");return 0;}\n")
+    exe = tmp_path / "lp"
+    subprocess.check_call([cc, "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)])
+    got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    want = [ctypes.sizeof(_abi.LoopParams)] + [getattr(_abi.LoopParams, f).offset for f in fields]
+    assert got == want
