@@ -326,9 +326,9 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
 //                          exclusive scan over the rows -> the walk index of the row's first pixel; the frame's
 //                          total -> nzcount.
 //  * road_rows_kernel    — one wave a row: the row's bytes (0 / 255, 16 pixels a lane, one 16-byte store), its
-//                          walk entries [x, y] in raster order (a wave scan orders the lanes, the x are staged in
-//                          LDS in output order, then written as coalesced 8-byte pairs), and on request the
-//                          imageRoadMap row (the BGR row with [0, 255, 0] at every marked pixel).
+//                          walk entries [x, y] in raster order (64 pixels a pass, ranked by v_mbcnt, each pass
+//                          one coalesced run of 8-byte pairs), and on request the imageRoadMap row (the BGR row
+//                          with [0, 255, 0] at every marked pixel).
 // ---------------------------------------------------------------------------
 constexpr int kRbWords = 32;   // words a row: 1024 pixels
 
@@ -375,16 +375,21 @@ __global__ __launch_bounds__(256) void road_rowscan_kernel(const uint32_t* __res
     if (tid == 0) nzcount[frame] = all;
 }
 
+template <bool NT>
 __global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restrict__ bits, int H,
                                                         const int32_t* __restrict__ roff, int64_t cap,
                                                         uint8_t* __restrict__ img, int32_t* __restrict__ nzout,
                                                         const uint8_t* __restrict__ bgr, uint8_t* __restrict__ paint) {
-    __shared__ uint16_t sx[4][kRbWords * 32];   // a wave's row: its walk's x in output order
-    const int lane = lane_id(), wave = threadIdx.x >> 6;
-    const int frame = blockIdx.y, y = blockIdx.x * 4 + wave;
-    if (y >= H) return;   // (whole waves; no block barrier below)
+    const int lane = lane_id();
+    const int frame = blockIdx.y, y = blockIdx.x * 4 + wave_uniform_id();
+    if (y >= H) return;
     const int64_t row = (int64_t)frame * H + y;
-    const uint32_t word = bits[row * kRbWords + (lane >> 1)];
+    const uint32_t* rw = bits + row * kRbWords;   // the row's 32 words (wave-uniform address)
+    uint32_t ws[kRbWords];   // all of them in SGPRs before the first store (scalar loads in flight together)
+#pragma unroll
+    for (int i = 0; i < kRbWords; ++i) ws[i] = rw[i];
+    const int32_t first = roff[row];
+    const uint32_t word = rw[lane >> 1];
     const uint32_t b16 = (lane & 1) ? word >> 16 : word & 0xFFFFu;   // pixels 16 lane .. 16 lane + 15
     uint32_t q[4];   // bit k of a nibble -> byte k = 0xFF (v_perm selector 0x0D; 0x0C gives 0x00)
 #pragma unroll
@@ -394,19 +399,25 @@ __global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restri
     }
     __builtin_nontemporal_store((v4i){(int)q[0], (int)q[1], (int)q[2], (int)q[3]},
                                 reinterpret_cast<v4i*>(img + row * (kRbWords * 32) + 16 * lane));
-    // the walk: [x, y] of the row's marked pixels, in order, from the row's first index
-    const uint32_t cnt = __builtin_popcount(b16);
-    const uint32_t inc = wave_incl_scan(cnt);
-    const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
-    uint32_t m = b16, o = inc - cnt;
-    while (m) {
-        const int b = __builtin_ctz(m);
-        m &= m - 1;
-        sx[wave][o++] = (uint16_t)(16 * lane + b);
+    // the walk: [x, y] of the row's marked pixels in x order, from the row's first index. Pass i covers pixels
+    // 64 i .. 64 i + 63, lane l pixel 64 i + l: its bit is bit l of words 2i, 2i+1 (scalar loads, the same for
+    // the whole wave), its rank among the pass's marked pixels one v_mbcnt pair, and the pass's entries one
+    // contiguous run after the previous passes' (s_bcnt1): sixteen coalesced stores, no loop, no LDS.
+    v2i* dst = reinterpret_cast<v2i*>(nzout) + (int64_t)frame * cap + first;
+    uint32_t base = 0;
+#pragma unroll
+    for (int i = 0; i < kRbWords / 2; ++i) {
+        const uint32_t lo = ws[2 * i], hi = ws[2 * i + 1];
+        const uint32_t mine = lane < 32 ? lo >> lane : hi >> (lane - 32);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+        if (mine & 1u) {
+            if (NT)
+                __builtin_nontemporal_store((v2i){64 * i + lane, y}, dst + base + rank);
+            else
+                dst[base + rank] = (v2i){64 * i + lane, y};
+        }
+        base += __builtin_popcount(lo) + __builtin_popcount(hi);
     }
-    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its LDS writes land before its reads
-    v2i* dst = reinterpret_cast<v2i*>(nzout) + (int64_t)frame * cap + roff[row];
-    for (uint32_t j = lane; j < total; j += kWave) __builtin_nontemporal_store((v2i){(int)sx[wave][j], y}, dst + j);
     if (paint) {   // imageRoadMap (stereovision.py:131-133): the lane's 16 pixels, 48 bytes
         const uint4* src = reinterpret_cast<const uint4*>(bgr + row * (kRbWords * 32) * 3 + 48 * lane);
         uint4 v[3] = {src[0], src[1], src[2]};
@@ -433,8 +444,14 @@ hipError_t launch_road_bits(const uint32_t* bits, int frames, int H, int W, int3
     hipLaunchKernelGGL(road_rowscan_kernel, dim3(frames), dim3(256), 0, s, bits, H, roff, nzcount);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(road_rows_kernel, dim3((H + 3) / 4, frames), dim3(256), 0, s, bits, H, roff, cap, img, nzout,
-                       bgr, paint);
+    // SVX_ROAD_NT=0 (diagnostic build): the walk's entries as ordinary stores, merged in L2 before HBM
+    const char* nt = svx_knob("SVX_ROAD_NT");
+    if (nt && nt[0] == '0')
+        hipLaunchKernelGGL(road_rows_kernel<false>, dim3((H + 3) / 4, frames), dim3(256), 0, s, bits, H, roff, cap, img,
+                           nzout, bgr, paint);
+    else
+        hipLaunchKernelGGL(road_rows_kernel<true>, dim3((H + 3) / 4, frames), dim3(256), 0, s, bits, H, roff, cap, img,
+                           nzout, bgr, paint);
     return hipGetLastError();
 }
 

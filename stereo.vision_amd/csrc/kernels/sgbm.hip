@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "../svx_device.h"
@@ -60,12 +61,17 @@ __device__ __forceinline__ int wave_min_i32(int v) {
 // start has p0 = p1 = pmin = 0; d = -1 and d = 128 read MAX_COST. Returns the
 // untruncated L values (for the sums) and updates the state with the int16
 // truncations OpenCV stores.
+// Range: min(...) <= delta, so L <= C <= 32767 always; an L leaves int16 only below -32768, and the walk keeps
+// the running minimum of its untruncated L (one v_min3 a step) and tests it once at the path's end.
 struct PathState {
     int p0 = 0, p1 = 0, pmin = 0;
+    int lmin = 0;
+    __device__ bool ovf() const { return lmin < kInt16Min; }
 };
 
-__device__ __forceinline__ void path_step(int c0, int c1, PathState& s, int P1, int P2, int& L0, int& L1,
-                                          bool& ovf) {
+// A step in two halves, so that a caller with a second wave minimum to take (the row walk's winner) can run
+// both DPP scans interleaved: path_l gives L and min(L0, L1) of the lane, path_commit takes the wave's min.
+__device__ __forceinline__ int path_l(int c0, int c1, const PathState& s, int P1, int P2, int& L0, int& L1) {
     const int delta = s.pmin + P2;
     const int left = __builtin_amdgcn_update_dpp(kMaxCost, s.p1, 0x138, 0xf, 0xf, false);   // wave_shr:1, d0 - 1
     const int right = __builtin_amdgcn_update_dpp(kMaxCost, s.p0, 0x130, 0xf, 0xf, false);  // wave_shl:1, d1 + 1
@@ -73,11 +79,97 @@ __device__ __forceinline__ void path_step(int c0, int c1, PathState& s, int P1, 
     const int m1 = min(min(s.p1, delta), min(s.p0, right) + P1);
     L0 = c0 + m0 - delta;
     L1 = c1 + m1 - delta;
-    const int wm = wave_min_i32(min(L0, L1));
-    ovf = ovf || out16(L0) || out16(L1);
+    return min(L0, L1);
+}
+__device__ __forceinline__ void path_commit(PathState& s, int L0, int L1, int lm, int wm) {
+    s.lmin = min(s.lmin, lm);
     s.p0 = (int)(int16_t)L0;
     s.p1 = (int)(int16_t)L1;
     s.pmin = (int)(int16_t)wm;
+}
+__device__ __forceinline__ void path_step(int c0, int c1, PathState& s, int P1, int P2, int& L0, int& L1) {
+    const int lm = path_l(c0, c1, s, P1, P2, L0, L1);
+    path_commit(s, L0, L1, lm, wave_min_i32(lm));
+}
+
+// The same step on both disparities at once (v_pk_* 16-bit pairs), for the q-volume walks (0 <= P1, P2 <= 15).
+// p holds the stored (int16) L pair. Every term of min(...) that the 32-bit form can take above 32767 (delta,
+// N + P1) only meets min() beside p <= 32767, so saturating it changes nothing; q = delta - m is in [0, P2] and
+// so exact in 16-bit wrapping arithmetic, and L = C - q wraps exactly as OpenCV's int16 store truncates. An L
+// below -32768 is the one range error: then its truncation is C - q + 65536 > C, and sat(L - C) = 32767 > 0,
+// where a good step gives -q <= 0 — the walk keeps the running max of that difference.
+typedef short pk16 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pk16 as_pk(uint32_t v) { return __builtin_bit_cast(pk16, v); }
+__device__ __forceinline__ uint32_t pk_bits(pk16 v) { return __builtin_bit_cast(uint32_t, v); }
+struct PathPk {
+    uint32_t p = 0;
+    int pmin = 0;
+    pk16 acc = {-32768, -32768};
+    __device__ bool ovf() const { return max((int)acc.x, (int)acc.y) > 0; }
+};
+__device__ __forceinline__ uint32_t pk_l(uint32_t c, const PathPk& s, int P1, int P2, uint32_t& q, int& lm) {
+    const int delta = s.pmin + P2;
+    const short ds = (short)min(delta, kMaxCost), dw = (short)delta;
+    const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(0x7FFF7FFF, (int)s.p, 0x138, 0xf, 0xf, false);  // lane - 1
+    const uint32_t sl = (uint32_t)__builtin_amdgcn_update_dpp(0x7FFF7FFF, (int)s.p, 0x130, 0xf, 0xf, false);  // lane + 1
+    const pk16 lft = as_pk(__builtin_amdgcn_alignbit(s.p, sh, 16));   // (d0 - 1, d1 - 1) = (sh.hi, p.lo)
+    const pk16 rgt = as_pk(__builtin_amdgcn_alignbit(sl, s.p, 16));   // (d0 + 1, d1 + 1) = (p.hi, sl.lo)
+    const pk16 n1 = __builtin_elementwise_add_sat(__builtin_elementwise_min(lft, rgt), (pk16){(short)P1, (short)P1});
+    const pk16 m = __builtin_elementwise_min(__builtin_elementwise_min(as_pk(s.p), (pk16){ds, ds}), n1);
+    const pk16 qq = (pk16){dw, dw} - m;
+    const pk16 L = as_pk(c) - qq;
+    q = pk_bits(qq);
+    lm = min((int)L.x, (int)L.y);
+    return pk_bits(L);
+}
+__device__ __forceinline__ void pk_commit(PathPk& s, uint32_t c, uint32_t L, int wm) {
+    s.acc = __builtin_elementwise_max(s.acc, __builtin_elementwise_sub_sat(as_pk(L), as_pk(c)));
+    s.p = L;
+    s.pmin = wm;
+}
+__device__ __forceinline__ uint32_t pk_step(uint32_t c, PathPk& s, int P1, int P2, uint32_t& q) {
+    int lm;
+    const uint32_t L = pk_l(c, s, P1, P2, q, lm);
+    pk_commit(s, c, L, wave_min_i32(lm));
+    return L;
+}
+// both q of a lane (each 0 .. 15, in bits 0-3 and 16-19) as one byte, d0 in the low nibble
+__device__ __forceinline__ uint8_t q_byte_pk(uint32_t q) { return (uint8_t)(q | (q >> 12)); }
+
+// A wave-uniform buffer resource over a path's cells: an access is then the lane's byte offset (a loop-invariant
+// VGPR) + the step's 32-bit SGPR offset, with no per-access VALU address arithmetic (a global access with a
+// 64-bit per-lane address costs a v_lshl_add_u64 each). aux 2: non-temporal.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)min(bytes, (size_t)0x7FFFFFFF),
+                                             0x00020000);
+}
+__device__ __forceinline__ uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, bool nt = false) {
+    return nt ? __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 2) : __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+__device__ __forceinline__ uint32_t bld8(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, bool nt = false) {
+    return nt ? __builtin_amdgcn_raw_buffer_load_b8(r, voff, soff, 2) : __builtin_amdgcn_raw_buffer_load_b8(r, voff, soff, 0);
+}
+__device__ __forceinline__ void bst32(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, 0);
+}
+__device__ __forceinline__ void bst8(uint8_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b8(v, r, voff, soff, 0);
+}
+
+// two wave minimums, their DPP steps interleaved (each step's input was written two instructions earlier)
+__device__ __forceinline__ void wave_min2_i32(int a, int b, int& ra, int& rb) {
+#define SVX_MIN2_STEP(ctl, rm)                                                                 \
+    a = min(a, __builtin_amdgcn_update_dpp(0x7fffffff, a, ctl, rm, 0xf, false));               \
+    b = min(b, __builtin_amdgcn_update_dpp(0x7fffffff, b, ctl, rm, 0xf, false))
+    SVX_MIN2_STEP(0x111, 0xf);
+    SVX_MIN2_STEP(0x112, 0xf);
+    SVX_MIN2_STEP(0x114, 0xf);
+    SVX_MIN2_STEP(0x118, 0xf);
+    SVX_MIN2_STEP(0x142, 0xa);
+    SVX_MIN2_STEP(0x143, 0xc);
+#undef SVX_MIN2_STEP
+    ra = __builtin_amdgcn_readlane(a, 63);
+    rb = __builtin_amdgcn_readlane(b, 63);
 }
 
 // A path's L minus the cost it adds, as OpenCV computes it, is min(...) - delta
@@ -193,12 +285,15 @@ __device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cas
 struct BtFeat {
     uint32_t v, lo, hi;   // value, half-neighbour min, max: channel 0 | channel 1 << 16
 };
+// max(u - v1, v0 - u, 0) = max(sat(u - v1), sat(v0 - u)) with unsigned saturating subtractions (the features
+// are 0 .. 255): v_pk_sub_u16 clamp twice and a v_pk_max_u16 per direction.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t bt_cost2(const BtFeat& a, const BtFeat& b) {
-    const s16x2 z = {0, 0};
-    const s16x2 u = as_s16x2(a.v), u0 = as_s16x2(a.lo), u1 = as_s16x2(a.hi);
-    const s16x2 v = as_s16x2(b.v), v0 = as_s16x2(b.lo), v1 = as_s16x2(b.hi);
-    const s16x2 c0 = __builtin_elementwise_max(__builtin_elementwise_max(u - v1, z), v0 - u);
-    const s16x2 c1 = __builtin_elementwise_max(__builtin_elementwise_max(v - u1, z), u0 - v);
+    const u16x2 u = as_u16x2(a.v), u0 = as_u16x2(a.lo), u1 = as_u16x2(a.hi);
+    const u16x2 v = as_u16x2(b.v), v0 = as_u16x2(b.lo), v1 = as_u16x2(b.hi);
+    const u16x2 c0 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(u, v1), __builtin_elementwise_sub_sat(v0, u));
+    const u16x2 c1 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, u1), __builtin_elementwise_sub_sat(u0, v));
     const uint32_t c = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(c0, c1));
     return (c & 0xFFFF) + (c >> 18);   // channel 0 + (channel 1 >> 2); both in 0 .. 255
 }
@@ -282,7 +377,7 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
     }
     __syncthreads();
 
-    const int lane = lane_id(), wave = tid >> 6;
+    const int lane = lane_id(), wave = wave_uniform_id();
     const int n = k.width1;
     const int seg = (n + 3) / 4;
     const int xs = wave * seg, xe = min(n, xs + seg);
@@ -311,13 +406,13 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
     int jn = min(xs + SW2C, n - 1);   // the last column computed; ring[RS - 1] holds its cost
     uint32_t vlast = ring[RS - 1];
     BtFeat acur = feat(W + jn + kSgD - d0), aprev = feat(W + jn + kSgD - d0 - 1);   // A_jn, A_{jn - 1}
-    uint32_t* out = hvol + ((size_t)f * H + y) * n * 64 + lane;
+    uint32_t* out = hvol + ((size_t)f * H + y) * n * 64;   // wave-uniform row; + the lane per store
     for (int x0 = xs; x0 < xe; x0 += RS) {
 #pragma unroll
         for (int u = 0; u < RS; ++u) {
             const int xi = x0 + u;
             if (xi >= xe) break;
-            out[(size_t)xi * 64] = sum;   // (non-temporal stores: no faster)
+            (out + (size_t)xi * 64)[(uint32_t)lane] = sum;   // (non-temporal stores: no faster)
             // step xi adds column xi + 1 + SW2 (clamped: past the last column it is the last column again)
             if (jn < n - 1) {
                 ++jn;
@@ -351,26 +446,26 @@ __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint3
     const int wpb = blockDim.x >> 6;
     const int cols_blocks = (k.width1 + wpb - 1) / wpb;
     const int f = blockIdx.x / cols_blocks;
-    const int xi = (blockIdx.x - f * cols_blocks) * wpb + (threadIdx.x >> 6);
+    const int xi = (blockIdx.x - f * cols_blocks) * wpb + wave_uniform_id();
     if (f >= frames || xi >= k.width1) return;
-    const int lane = lane_id(), H = k.H, SH2 = k.SH2;
+    const uint32_t lane = lane_id();
+    const int H = k.H, SH2 = k.SH2;
     const size_t rs = (size_t)k.width1 * 64;
-    const size_t base = (size_t)f * H * rs + (size_t)xi * 64 + lane;
+    const size_t base = (size_t)f * H * rs + (size_t)xi * 64;   // wave-uniform: the column's cell at row 0
     const uint32_t* hb = hvol + base;
     int c0 = 0, c1 = 0;
     for (int kk = 0; kk <= SH2; ++kk) {
-        const uint32_t h = hb[(size_t)min(kk, H - 1) * rs];
+        const uint32_t h = (hb + (size_t)min(kk, H - 1) * rs)[lane];
         const int sc = kk == 0 ? SH2 + 1 : 1;
         c0 += lo16(h) * sc;
         c1 += hi16(h) * sc;
     }
-    PathState st;
-    bool ovf = false;
+    std::conditional_t<DQ, PathPk, PathState> st;
     const bool upd_col = xi > 0;
     // step y adds row y + SH2 and drops row y - SH2 - 1 (OpenCV's rules, below)
     const auto load = [&](int y, uint32_t& a, uint32_t& r) {
-        a = hb[(size_t)min(y + SH2, H - 1) * rs];
-        r = hb[(size_t)min(max(y - SH2 - 1, 0), H - 1) * rs];
+        a = (hb + (size_t)min(y + SH2, H - 1) * rs)[lane];
+        r = (hb + (size_t)min(max(y - SH2 - 1, 0), H - 1) * rs)[lane];
     };
     uint32_t ca[U], cr[U];
 #pragma unroll
@@ -388,13 +483,18 @@ __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint3
                 c1 += hi16(ca[u]) - hi16(cr[u]);
             }
             const int cw0 = (int)(int16_t)c0, cw1 = (int)(int16_t)c1;
-            cvol[base + (size_t)y * rs] = pack16(cw0, cw1);
-            int L0, L1;
-            path_step(cw0, cw1, st, k.P1, k.P2, L0, L1, ovf);
-            if constexpr (DQ)
-                q2vol[base + (size_t)y * rs] = q_byte(cw0, cw1, L0, L1);
-            else
-                l2vol[base + (size_t)y * rs] = pack16(L0, L1);
+            const size_t o = base + (size_t)y * rs;
+            const uint32_t cw = pack16(cw0, cw1);
+            (cvol + o)[lane] = cw;
+            if constexpr (DQ) {
+                uint32_t q;
+                pk_step(cw, st, k.P1, k.P2, q);
+                (q2vol + o)[lane] = q_byte_pk(q);
+            } else {
+                int L0, L1;
+                path_step(cw0, cw1, st, k.P1, k.P2, L0, L1);
+                (l2vol + o)[lane] = pack16(L0, L1);
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -402,7 +502,7 @@ __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint3
             cr[u] = nr[u];
         }
     }
-    if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
+    if (__any(st.ovf()) && lane == 0) atomicOr(flags + f, 1u);
 }
 
 // The same walk for a compile-time half window (the reference's block 21: SH2 = 10) with each horizontal sum
@@ -419,18 +519,22 @@ __global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const 
     const int wpb = blockDim.x >> 6;
     const int cols_blocks = (k.width1 + wpb - 1) / wpb;
     const int f = blockIdx.x / cols_blocks;
-    const int xi = (blockIdx.x - f * cols_blocks) * wpb + (threadIdx.x >> 6);
+    const int xi = (blockIdx.x - f * cols_blocks) * wpb + wave_uniform_id();
     if (f >= frames || xi >= k.width1) return;
-    const int lane = lane_id(), H = k.H;
+    const uint32_t lane = lane_id();
+    const int H = k.H;
     const size_t rs = (size_t)k.width1 * 64;
-    const size_t base = (size_t)f * H * rs + (size_t)xi * 64 + lane;
-    const uint32_t* hb = hvol + base;
+    const size_t base = (size_t)f * H * rs + (size_t)xi * 64;   // wave-uniform: the column's cell at row 0
+    const uint32_t rs32 = (uint32_t)rs;   // the column's cells are y * rs on: < 2^31 bytes a frame
+    const __amdgpu_buffer_rsrc_t rh = wave_rsrc(hvol + base, (size_t)H * rs * 4),
+                                 rcv = wave_rsrc(cvol + base, (size_t)H * rs * 4), rq2 = wave_rsrc(q2vol + base, (size_t)H * rs);
+    const auto hrow = [&](int r) { return bld32(rh, lane * 4, (uint32_t)min(r, H - 1) * rs32 * 4); };
     // drop[u]: the row step y0 + u subtracts (block y0 = 0: rows max(u - SH2 - 1, 0), read with the first window)
     uint32_t drop[RS];
     int c0 = 0, c1 = 0;
 #pragma unroll
     for (int kk = 0; kk <= SH2C; ++kk) {
-        const uint32_t h = hb[(size_t)min(kk, H - 1) * rs];
+        const uint32_t h = hrow(kk);
         const int sc = kk == 0 ? SH2C + 1 : 1;
         c0 += lo16(h) * sc;
         c1 += hi16(h) * sc;
@@ -441,16 +545,15 @@ __global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const 
             drop[kk + SH2C + 1] = h;                           // step kk + SH2 + 1 drops row kk
         }   // row SH2 is step RS's drop: step 0 stores it (drop[0] = its added row, SH2)
     }
-    PathState st;
-    bool ovf = false;
+    std::conditional_t<DQ, PathPk, PathState> st;
     const bool upd_col = xi > 0;
     uint32_t add[RS];   // the rows steps y0 .. y0 + RS - 1 add (y + SH2, clamped)
 #pragma unroll
-    for (int u = 0; u < RS; ++u) add[u] = hb[(size_t)min(u + SH2C, H - 1) * rs];
+    for (int u = 0; u < RS; ++u) add[u] = hrow(u + SH2C);
     for (int y0 = 0; y0 < H; y0 += RS) {
         uint32_t nadd[RS];
 #pragma unroll
-        for (int u = 0; u < RS; ++u) nadd[u] = hb[(size_t)min(y0 + RS + u + SH2C, H - 1) * rs];
+        for (int u = 0; u < RS; ++u) nadd[u] = hrow(y0 + RS + u + SH2C);
 #pragma unroll
         for (int u = 0; u < RS; ++u) {
             const int y = y0 + u;
@@ -461,18 +564,22 @@ __global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const 
             }
             drop[u] = add[u];   // step y + RS drops row y + SH2
             const int cw0 = (int)(int16_t)c0, cw1 = (int)(int16_t)c1;
-            cvol[base + (size_t)y * rs] = pack16(cw0, cw1);
-            int L0, L1;
-            path_step(cw0, cw1, st, k.P1, k.P2, L0, L1, ovf);
-            if constexpr (DQ)
-                q2vol[base + (size_t)y * rs] = q_byte(cw0, cw1, L0, L1);
-            else
-                l2vol[base + (size_t)y * rs] = pack16(L0, L1);
+            const uint32_t cw = pack16(cw0, cw1);
+            bst32(cw, rcv, lane * 4, (uint32_t)y * rs32 * 4);
+            if constexpr (DQ) {
+                uint32_t q;
+                pk_step(cw, st, k.P1, k.P2, q);
+                bst8(q_byte_pk(q), rq2, lane, (uint32_t)y * rs32);
+            } else {
+                int L0, L1;
+                path_step(cw0, cw1, st, k.P1, k.P2, L0, L1);
+                (l2vol + base + (size_t)y * rs)[lane] = pack16(L0, L1);
+            }
         }
 #pragma unroll
         for (int u = 0; u < RS; ++u) add[u] = nadd[u];
     }
-    if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
+    if (__any(st.ovf()) && lane == 0) atomicOr(flags + f, 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -486,7 +593,7 @@ __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t*
     const int wpb = blockDim.x >> 6;
     const int npaths = k.width1 + k.H - 1;   // per direction
     const int per_frame = 2 * npaths;
-    const int gw = blockIdx.x * wpb + (threadIdx.x >> 6);
+    const int gw = blockIdx.x * wpb + wave_uniform_id();
     const int f = gw / per_frame;
     if (f >= frames) return;
     int p = gw - f * per_frame;
@@ -500,38 +607,46 @@ __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t*
         xi = dir ? k.width1 - 1 : 0;
         y = p - k.width1 + 1;
     }
-    // the path: cells (xi + t * dx, y + t), t < len
+    // the path: cells (xi + t * dx, y + t), t < len; every address below is a wave-uniform cell + the lane
     const int len = min(k.H - y, dir ? xi + 1 : k.width1 - xi);
-    const int lane = lane_id();
+    const uint32_t lane = lane_id();
     const size_t rs = (size_t)k.width1 * 64;
-    const size_t a0 = (size_t)f * k.H * rs + (size_t)y * rs + (size_t)xi * 64 + lane;
+    const size_t a0 = (size_t)f * k.H * rs + (size_t)y * rs + (size_t)xi * 64;
     const size_t step = dir ? rs - 64 : rs + 64;
     uint32_t* out = dir ? l3vol : l1vol;
     uint8_t* qout = dir ? q3vol : q1vol;
-    PathState st;
-    bool ovf = false;
+    // the path's cells from its first: t * step cells on, at most a frame's volume (< 2^31 bytes)
+    const size_t span = (size_t)(len - 1) * step + 64;
+    const __amdgpu_buffer_rsrc_t rc = wave_rsrc(cvol + a0, span * 4), rq = wave_rsrc(qout + a0, span);
+    const uint32_t st32 = (uint32_t)step;
+    const auto cell = [&](int t) { return bld32(rc, lane * 4, (uint32_t)min(t, len - 1) * st32 * 4); };
+    std::conditional_t<DQ, PathPk, PathState> st;
     uint32_t cc[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) cc[u] = cvol[a0 + (size_t)min(u, len - 1) * step];
+    for (int u = 0; u < U; ++u) cc[u] = cell(u);
     for (int t0 = 0; t0 < len; t0 += U) {
         uint32_t nc[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) nc[u] = cvol[a0 + (size_t)min(t0 + U + u, len - 1) * step];
+        for (int u = 0; u < U; ++u) nc[u] = cell(t0 + U + u);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int t = t0 + u;
             if (t >= len) break;
-            int L0, L1;
-            path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1, ovf);
-            if constexpr (DQ)
-                qout[a0 + (size_t)t * step] = q_byte(lo16(cc[u]), hi16(cc[u]), L0, L1);
-            else
-                out[a0 + (size_t)t * step] = pack16(L0, L1);
+            const size_t o = a0 + (size_t)t * step;
+            if constexpr (DQ) {
+                uint32_t q;
+                pk_step(cc[u], st, k.P1, k.P2, q);
+                bst8(q_byte_pk(q), rq, lane, (uint32_t)t * st32);
+            } else {
+                int L0, L1;
+                path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1);
+                (out + o)[lane] = pack16(L0, L1);
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) cc[u] = nc[u];
     }
-    if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
+    if (__any(st.ovf()) && lane == 0) atomicOr(flags + f, 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -539,6 +654,11 @@ __global__ __launch_bounds__(256) void sgbm_diag_kernel(SgbmK k, const uint32_t*
 // ---------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ T ld_nt(const T* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
+
+// LDS per wave: the right view's best cost per column as one word, (minS + 32768) << 16 | (0xFFFF - xi) — the
+// reference's "if (disp2cost[x2] > minS)" in decreasing x is the minimum of that key (the smaller cost, then
+// the larger xi, i.e. the pixel visited first), so the updates need no order and no read — then disp1 (int16).
+__host__ __device__ constexpr size_t sgbm_row_lds_per_wave(int W) { return ((size_t)6 * W + 3) & ~(size_t)3; }
 
 template <int U, bool NT, bool DQ>
 __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* __restrict__ cvol,
@@ -548,39 +668,44 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
                                                          const uint8_t* __restrict__ q2vol,
                                                          const uint8_t* __restrict__ q3vol, int16_t* __restrict__ d16,
                                                          uint32_t* __restrict__ flags, int frames) {
-    extern __shared__ int16_t rsm[];
-    const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
+    extern __shared__ uint32_t rsm32[];
+    const int wpb = blockDim.x >> 6, wave = wave_uniform_id();
     const int gw = blockIdx.x * wpb + wave;
     const int f = gw / k.H, y = gw - f * k.H;
     if (f >= frames) return;
-    const int W = k.W, lane = lane_id();
-    int16_t* disp1 = rsm + wave * 3 * W;
-    int16_t* disp2 = disp1 + W;
-    int16_t* d2cost = disp2 + W;
+    const int W = k.W;
+    const uint32_t lane = lane_id();
+    uint32_t* d2key = rsm32 + wave * (sgbm_row_lds_per_wave(W) / 4);
+    int16_t* disp1 = reinterpret_cast<int16_t*>(d2key + W);
     const int INVALID = -kSgScale;   // (minD - 1) * 16, minD = 0
     for (int x = lane; x < W; x += 64) {
         disp1[x] = (int16_t)INVALID;
-        disp2[x] = (int16_t)INVALID;
-        d2cost[x] = (int16_t)kMaxCost;
+        d2key[x] = ~0u;
     }
     wave_lds_sync();
     const size_t rs = (size_t)k.width1 * 64;
-    const size_t rb = ((size_t)f * k.H + y) * rs + lane;
-    bool ovf = false;
+    const size_t rb = ((size_t)f * k.H + y) * rs;   // wave-uniform: the row's first cell
     const int n = k.width1;
+    // the cell of column xi in a volume: a wave-uniform address + the lane (DQ: buffer resources over the row)
+    const auto at = [&](auto* vol, int xi) { return vol + rb + (size_t)xi * 64; };
+    const __amdgpu_buffer_rsrc_t rc = wave_rsrc(cvol + rb, rs * 4), rq0 = wave_rsrc(q0vol + rb, rs),
+                                 rq1 = wave_rsrc(q1vol + rb, rs), rq2 = wave_rsrc(q2vol + rb, rs),
+                                 rq3 = wave_rsrc(q3vol + rb, rs);
+    std::conditional_t<DQ, PathPk, PathState> sa, sb;
     // pass A: x ascending, direction (-1, 0); P = sat16(L0 + L1 + L2 + L3) replaces L1.
     // DQ: pass A stores only its own q (q0 = C - L0) and pass B forms P = sat16(4 C - (q0 + q1 + q2 + q3))
     // from the four q bytes: C is read twice, the other directions once, as 64 B a cell.
     {
-        PathState st;
         uint32_t cc[U], ca[U], cb[U], ce[U];
         const auto load = [&](int xi, uint32_t& c, uint32_t& a, uint32_t& b, uint32_t& e) {
-            const size_t o = rb + (size_t)min(xi, n - 1) * 64;
-            c = cvol[o];
-            if constexpr (!DQ) {
-                a = ld_nt(l1p + o, NT);
-                b = ld_nt(l2vol + o, NT);
-                e = ld_nt(l3vol + o, NT);
+            xi = min(xi, n - 1);
+            if constexpr (DQ) {
+                c = bld32(rc, lane * 4, (uint32_t)xi * 256);
+            } else {
+                c = at(cvol, xi)[lane];
+                a = ld_nt(at(l1p, xi) + lane, NT);
+                b = ld_nt(at(l2vol, xi) + lane, NT);
+                e = ld_nt(at(l3vol, xi) + lane, NT);
             }
         };
 #pragma unroll
@@ -593,17 +718,19 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
             for (int u = 0; u < U; ++u) {
                 const int xi = x0 + u;
                 if (xi >= n) break;
-                int L0, L1;
-                path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1, ovf);
                 if constexpr (DQ) {
-                    q0vol[rb + (size_t)xi * 64] = q_byte(lo16(cc[u]), hi16(cc[u]), L0, L1);
+                    uint32_t q;
+                    pk_step(cc[u], sa, k.P1, k.P2, q);
+                    bst8(q_byte_pk(q), rq0, lane, (uint32_t)xi * 64);
                 } else {
+                    int L0, L1;
+                    path_step(lo16(cc[u]), hi16(cc[u]), sa, k.P1, k.P2, L0, L1);
                     const uint32_t pv = pack16(sat16(L0 + lo16(ca[u]) + lo16(cb[u]) + lo16(ce[u])),
                                                sat16(L1 + hi16(ca[u]) + hi16(cb[u]) + hi16(ce[u])));
                     if (NT)
-                        __builtin_nontemporal_store(pv, l1p + rb + (size_t)xi * 64);
+                        __builtin_nontemporal_store(pv, at(l1p, xi) + lane);
                     else
-                        l1p[rb + (size_t)xi * 64] = pv;
+                        at(l1p, xi)[lane] = pv;
                 }
             }
 #pragma unroll
@@ -615,21 +742,25 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
             }
         }
     }
-    // pass B: x descending, direction (+1, 0), S = sat16(P + L), winner per pixel
+    // pass B: x descending, direction (+1, 0), S = sat16(P + L), winner per pixel. The winner and its
+    // neighbours' costs are wave-uniform; step u of a group of U parks them in lane u and the
+    // group's subpixel divisions and LDS updates run once, lanes 0 .. U-1 side by side, after its U steps.
     {
-        PathState st;
         const int d0 = 2 * lane;
         uint32_t cc[U], cp[U];
         // step j visits xi = n - 1 - j (pass A's P of every cell is stored before these loads;
         // DQ: pp = the four q bytes, q0 | q1 << 8 | q2 << 16 | q3 << 24)
         const auto load = [&](int j, uint32_t& c, uint32_t& pp) {
-            const size_t o = rb + (size_t)max(n - 1 - j, 0) * 64;
-            c = ld_nt(cvol + o, NT);
-            if constexpr (DQ)
-                pp = (uint32_t)ld_nt(q0vol + o, NT) | (uint32_t)ld_nt(q1vol + o, NT) << 8 |
-                     (uint32_t)ld_nt(q2vol + o, NT) << 16 | (uint32_t)ld_nt(q3vol + o, NT) << 24;
-            else
-                pp = ld_nt(l1p + o, NT);
+            const int xi = max(n - 1 - j, 0);
+            if constexpr (DQ) {
+                const uint32_t so = (uint32_t)xi * 64;
+                c = bld32(rc, lane * 4, so * 4, NT);
+                pp = bld8(rq0, lane, so, NT) | bld8(rq1, lane, so, NT) << 8 | bld8(rq2, lane, so, NT) << 16 |
+                     bld8(rq3, lane, so, NT) << 24;
+            } else {
+                c = ld_nt(at(cvol, xi) + lane, NT);
+                pp = ld_nt(at(l1p, xi) + lane, NT);
+            }
         };
 #pragma unroll
         for (int u = 0; u < U; ++u) load(u, cc[u], cp[u]);
@@ -637,23 +768,34 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
             uint32_t nc[U], np[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) load(j0 + U + u, nc[u], np[u]);
+            int gkey = -1, gnum = 0, gdv = 1;   // lane u: step u's kmin (-1: no pixel written), subpixel terms
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int xi = n - 1 - (j0 + u);
                 if (xi < 0) break;
-                int L0, L1;
-                path_step(lo16(cc[u]), hi16(cc[u]), st, k.P1, k.P2, L0, L1, ovf);
+                int L0, L1, lm;
+                uint32_t Lpk = 0;
                 int P0, P1;
                 if constexpr (DQ) {   // the byte sums of the low and the high nibbles (v_sad_u8 against 0)
+                    uint32_t q;
+                    Lpk = pk_l(cc[u], sb, k.P1, k.P2, q, lm);
+                    L0 = lo16(Lpk);
+                    L1 = hi16(Lpk);
                     P0 = sat16(4 * lo16(cc[u]) - (int)__builtin_amdgcn_sad_u8(cp[u] & 0x0F0F0F0Fu, 0u, 0u));
                     P1 = sat16(4 * hi16(cc[u]) - (int)__builtin_amdgcn_sad_u8((cp[u] >> 4) & 0x0F0F0F0Fu, 0u, 0u));
                 } else {
+                    lm = path_l(lo16(cc[u]), hi16(cc[u]), sb, k.P1, k.P2, L0, L1);
                     P0 = lo16(cp[u]);
                     P1 = hi16(cp[u]);
                 }
                 const int S0 = sat16(P0 + L0), S1 = sat16(P1 + L1);
                 const int key = min(((S0 + 32768) << 7) | d0, ((S1 + 32768) << 7) | (d0 + 1));
-                const int kmin = wave_min_i32(key);
+                int wm, kmin;
+                wave_min2_i32(lm, key, wm, kmin);
+                if constexpr (DQ)
+                    pk_commit(sb, cc[u], Lpk, wm);
+                else
+                    path_commit(sb, L0, L1, lm, wm);
                 const int minS = (kmin >> 7) - 32768, best = kmin & 127;
                 if (k.uniq > 0) {
                     const bool bad = (S0 * (100 - k.uniq) < minS * 100 && abs(best - d0) > 1) ||
@@ -665,24 +807,28 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
                     // pixel gets (-1) * 16 = INVALID; disp2 is not touched (its cost test is strict too)
                     continue;
                 }
-                const uint32_t spk = pack16(S0, S1);
-                int dd = best * kSgScale;
+                int num = 0, dv = 1;   // dd = best * 16 + num / dv (C division)
                 if (best > 0 && best < kSgD - 1) {
+                    const uint32_t spk = pack16(S0, S1);
                     const uint32_t wm = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best - 1) >> 1);
                     const uint32_t wp = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best + 1) >> 1);
                     const int Sm = (best - 1) & 1 ? hi16(wm) : lo16(wm);
                     const int Sp = (best + 1) & 1 ? hi16(wp) : lo16(wp);
                     const int den = max(Sm + Sp - 2 * minS, 1);
-                    dd = best * kSgScale + ((Sm - Sp) * kSgScale + den) / (den * 2);
+                    num = (Sm - Sp) * kSgScale + den;
+                    dv = den * 2;
                 }
-                if (lane == 0) {
-                    const int x2 = xi + k.minX1 - best;
-                    if (d2cost[x2] > minS) {
-                        d2cost[x2] = (int16_t)minS;
-                        disp2[x2] = (int16_t)best;
-                    }
-                    disp1[xi + k.minX1] = (int16_t)dd;
+                if (lane == (uint32_t)u) {   // one v_cndmask each: the lane masks are loop invariants
+                    gkey = kmin;
+                    gnum = num;
+                    gdv = dv;
                 }
+            }
+            if (gkey >= 0) {   // lanes 0 .. U-1 whose step wrote a pixel
+                const int xi = n - 1 - (j0 + (int)lane);
+                const int best = gkey & 127, minS = (gkey >> 7) - 32768;
+                disp1[xi + k.minX1] = (int16_t)(best * kSgScale + gnum / gdv);
+                atomicMin(d2key + (xi + k.minX1 - best), (uint32_t)(minS + 32768) << 16 | (0xFFFFu - (uint32_t)xi));
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -691,21 +837,27 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
             }
         }
     }
-    wave_lds_sync();   // lane 0's LDS writes before the check reads them
-    // left-right check -> the int16 result row
+    wave_lds_sync();   // the group updates before the check reads them
+    // left-right check -> the int16 result row; disp2 of column x from its key: -1 when never set, else
+    // the best of the pixel xi that set it, xi + minX1 - x
+    const auto disp2 = [&](int x) {
+        const uint32_t kk = d2key[x];
+        return kk == ~0u ? -1 : (int)(0xFFFFu - (kk & 0xFFFFu)) + k.minX1 - x;
+    };
     int16_t* orow = d16 + (size_t)f * k.frame_px + (size_t)y * W;
     for (int x = lane; x < W; x += 64) {
         int v = disp1[x];
         if (v != INVALID) {
             const int _d = v >> 4, d_ = (v + kSgScale - 1) >> 4;
             const int _x = x - _d, x_ = x - d_;
-            if (0 <= _x && _x < W && disp2[_x] >= 0 && abs(disp2[_x] - _d) > k.d12 && 0 <= x_ && x_ < W &&
-                disp2[x_] >= 0 && abs(disp2[x_] - d_) > k.d12)
-                v = INVALID;
+            if (0 <= _x && _x < W && 0 <= x_ && x_ < W) {
+                const int a = disp2(_x), b = disp2(x_);
+                if (a >= 0 && abs(a - _d) > k.d12 && b >= 0 && abs(b - d_) > k.d12) v = INVALID;
+            }
         }
         orow[x] = (int16_t)v;
     }
-    if (__any(ovf) && lane == 0) atomicOr(flags + f, 1u);
+    if (__any(sa.ovf() || sb.ovf()) && lane == 0) atomicOr(flags + f, 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -1065,7 +1217,7 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
     }
     const int cb = (k.width1 + 3) / 4;
     const int paths = 2 * (k.width1 + H - 1) * frames;
-    const size_t lds4 = sizeof(int16_t) * 3 * (size_t)k.W * 4;
+    const size_t lds4 = sgbm_row_lds_per_wave(k.W) * 4;
     const int pf = sgbm_prefetch();
     // the register-ring vertical walk for the reference's block 21 (SVX_SGBM_VRING=0: the generic walk)
     const char* vr = svx_knob("SVX_SGBM_VRING");
@@ -1077,7 +1229,7 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
     // the q-byte volumes of the four directions the row walk sums (P2 <= 15; SVX_SGBM_DQ=0: int16 L volumes and
     // P, A/B): four volumes of 64 B a cell in the space of the fourth int16 volume
     const char* dqv = svx_knob("SVX_SGBM_DQ");
-    const bool dq = k.P2 <= 15 && !(dqv && dqv[0] == '0');
+    const bool dq = k.P1 >= 0 && k.P2 <= 15 && !(dqv && dqv[0] == '0');
     const size_t qb = (size_t)frames * H * k.width1 * 64;
     uint8_t* q0 = reinterpret_cast<uint8_t*>(s.l3);
     uint8_t* q1 = q0 + qb;

@@ -281,6 +281,9 @@ __device__ __forceinline__ int hue_bin_fast(uint32_t col, bool& near) {
 // Wave / block helpers (wave64).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+// The wave's index in its workgroup, as a value the compiler knows is wave-uniform: addresses built from it stay
+// in SGPRs, so a per-lane access is one scalar base + the lane's VGPR offset (no 64-bit VALU address arithmetic).
+__device__ __forceinline__ int wave_uniform_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 // Inclusive wave64 scan of an operation with identity 0 (add, unsigned max, ...)
 // in six DPP steps: row_shr 1/2/4/8 (Hillis-Steele inside each 16-lane row),
