@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void road_rowscan_kernel(const uint32_t* __res
     if (tid == 0) nzcount[frame] = all;
 }
 
-template <bool NT>
+template <bool NT, bool NTI>
 __global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restrict__ bits, int H,
                                                         const int32_t* __restrict__ roff, int64_t cap,
                                                         uint8_t* __restrict__ img, int32_t* __restrict__ nzout,
@@ -397,8 +397,11 @@ __global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restri
         const uint32_t nib = (b16 >> (4 * i)) & 0xFu;
         q[i] = __builtin_amdgcn_perm(0u, 0u, ((__umul24(nib, 0x00204081u) & 0x01010101u) + 0x0C0C0C0Cu));
     }
-    __builtin_nontemporal_store((v4i){(int)q[0], (int)q[1], (int)q[2], (int)q[3]},
-                                reinterpret_cast<v4i*>(img + row * (kRbWords * 32) + 16 * lane));
+    v4i* irow = reinterpret_cast<v4i*>(img + row * (kRbWords * 32) + 16 * lane);
+    if (NTI)
+        __builtin_nontemporal_store((v4i){(int)q[0], (int)q[1], (int)q[2], (int)q[3]}, irow);
+    else
+        *irow = (v4i){(int)q[0], (int)q[1], (int)q[2], (int)q[3]};
     // the walk: [x, y] of the row's marked pixels in x order, from the row's first index. Pass i covers pixels
     // 64 i .. 64 i + 63, lane l pixel 64 i + l: its bit is bit l of words 2i, 2i+1 (scalar loads, the same for
     // the whole wave), its rank among the pass's marked pixels one v_mbcnt pair, and the pass's entries one
@@ -444,14 +447,23 @@ hipError_t launch_road_bits(const uint32_t* bits, int frames, int H, int W, int3
     hipLaunchKernelGGL(road_rowscan_kernel, dim3(frames), dim3(256), 0, s, bits, H, roff, nzcount);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // SVX_ROAD_NT=0 (diagnostic build): the walk's entries as ordinary stores, merged in L2 before HBM
+    // The walk's entries as ordinary stores: a pass's run starts at any 8-byte offset, and the partial lines at
+    // its ends merge with the neighbouring passes' in L2 before they reach HBM; written non-temporal each partial
+    // line went out on its own: 2.46 vs 2.99 ms per 4096 frames (profiles/r04/ab_road_walk_nt.txt); the image
+    // rows too (2.40 vs 2.41-2.49 ms, profiles/r04/ab_road_img_nt.txt). A/B (diagnostic build): SVX_ROAD_NT=1 /
+    // SVX_ROAD_IMG_NT=1 make the walk / image stores non-temporal.
     const char* nt = svx_knob("SVX_ROAD_NT");
-    if (nt && nt[0] == '0')
-        hipLaunchKernelGGL(road_rows_kernel<false>, dim3((H + 3) / 4, frames), dim3(256), 0, s, bits, H, roff, cap, img,
-                           nzout, bgr, paint);
+    const char* nti = svx_knob("SVX_ROAD_IMG_NT");
+    const bool wnt = nt && nt[0] == '1', int_ = nti && nti[0] == '1';
+    const dim3 g((H + 3) / 4, frames);
+    if (wnt && int_)
+        hipLaunchKernelGGL((road_rows_kernel<true, true>), g, dim3(256), 0, s, bits, H, roff, cap, img, nzout, bgr, paint);
+    else if (wnt)
+        hipLaunchKernelGGL((road_rows_kernel<true, false>), g, dim3(256), 0, s, bits, H, roff, cap, img, nzout, bgr, paint);
+    else if (int_)
+        hipLaunchKernelGGL((road_rows_kernel<false, true>), g, dim3(256), 0, s, bits, H, roff, cap, img, nzout, bgr, paint);
     else
-        hipLaunchKernelGGL(road_rows_kernel<true>, dim3((H + 3) / 4, frames), dim3(256), 0, s, bits, H, roff, cap, img,
-                           nzout, bgr, paint);
+        hipLaunchKernelGGL((road_rows_kernel<false, false>), g, dim3(256), 0, s, bits, H, roff, cap, img, nzout, bgr, paint);
     return hipGetLastError();
 }
 

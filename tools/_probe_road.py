@@ -21,5 +21,5 @@ with sb.Batch(F, step=1, with_bgr=True, with_points=True) as b:
             b.road_raster(sync=False)
         b.sync()
         res.append((time.perf_counter() - t0) / 5 * 1e3)
-    print(f"road from bitmap NT={os.environ.get('SVX_ROAD_NT', '1')}: min {min(res):.3f} median "
+    print(f"road from bitmap NT={os.environ.get('SVX_ROAD_NT', '0')} IMG_NT={os.environ.get('SVX_ROAD_IMG_NT', '0')}: min {min(res):.3f} median "
           f"{sorted(res)[2]:.3f} ms per {F} frames", flush=True)
