@@ -609,7 +609,7 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
                                                          IdxT* __restrict__ sidx, double* __restrict__ tri,
                                                          int32_t* __restrict__ fstat, int32_t* __restrict__ trace,
                                                          int trace_trials, int bitmap_words, int ablate,
-                                                         uint64_t* __restrict__ started, uint64_t epoch) {
+                                                         uint64_t* __restrict__ started, uint64_t epoch, int nframes) {
     // the frame loop's dispatch signal: the last workgroup of the grid is placed after every other one, so once it
     // runs, every frame's wave is resident and another stream's kernel may take the rest of the CUs (loop_gate)
     if (started && blockIdx.x == gridDim.x - 1 && lane_id() == 0)
@@ -626,7 +626,9 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
     sh.dummy = dummy;
     sh.ablate = ablate;
     const int lane = lane_id();
-    const int frame = blockIdx.x;
+    // one frame a wave, or (the frame loop, gridDim.x < nframes) a wave's frames one after the other: fewer
+    // waves resident at once hold less LDS beside the other batch's pipeline
+    for (int frame = blockIdx.x; frame < nframes; frame += gridDim.x) {
     const int64_t n64 = counts[frame];
     const uint32_t* fpk = packed + (int64_t)frame * cap;
     if (n64 < k || trials <= 0) {   // every trial's random.sample raises: (None, None)
@@ -634,7 +636,7 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
             fstat[2 * frame] = 0;
             fstat[2 * frame + 1] = 0;
         }
-        return;
+        continue;
     }
     const uint32_t n = (uint32_t)n64;
     const int kb = 32 - __builtin_clz(n);
@@ -693,6 +695,8 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
     if (lane == 0) {
         fstat[2 * frame] = status;   // 1: the reference would never return; 2: draw budget
         fstat[2 * frame + 1] = s;    // trials drawn (the failing one excluded)
+    }
+    __syncthreads();   // (one wave) the next frame re-seeds mt and clears the bitmap
     }
 }
 
@@ -1067,15 +1071,21 @@ static hipError_t launch_ransac_typed(const uint32_t* packed, const RbTables& tb
                                       int trace_trials, int ablate, int phases, uint64_t* started, uint64_t epoch,
                                       hipStream_t s) {
     IdxT* sidx = reinterpret_cast<IdxT*>(rs.sidx);
+    // frames a draw wave walks: 1, or in the frame loop (started: the draw runs beside another batch's pipeline)
+    // SVX_DRAW_FPW (diagnostic build, A/B)
+    int fpw = 1;
+    if (started)
+        if (const char* e = svx_knob("SVX_DRAW_FPW")) fpw = std::max(1, std::atoi(e));
+    const int grid = (frames + fpw - 1) / fpw;
     if (!(phases & 1)) {
     } else if (trace)
-        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, true>), dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words,
+        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, true>), dim3(grid), dim3(64), sizeof(uint32_t) * (size_t)words,
                            s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace,
-                           trace_trials, (int)words, ablate, started, epoch);
+                           trace_trials, (int)words, ablate, started, epoch, frames);
     else
-        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, false>), dim3(frames), dim3(64), sizeof(uint32_t) * (size_t)words,
+        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, false>), dim3(grid), dim3(64), sizeof(uint32_t) * (size_t)words,
                            s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat,
-                           nullptr, 0, (int)words, ablate, started, epoch);
+                           nullptr, 0, (int)words, ablate, started, epoch, frames);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !(phases & 2)) return e;
     if (ablate & (8 | 16)) ablate |= 1;   // DIAGNOSTIC: no samples / planes drawn -> no evaluation of them

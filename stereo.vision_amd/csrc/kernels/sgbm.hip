@@ -1002,15 +1002,17 @@ __global__ __launch_bounds__(256) void sgbm_cc_union_kernel(SgbmK k, const int16
 // Component sizes: one wave per row; each run adds its length at its root,
 // lanes sharing the wave's running root are summed first (large regions touch
 // one address once per row, not once per run).
+// Each run's end lane also points the run's first pixel straight at the root (a final value: every union is
+// done, and readers following par see an ancestor or the root either way), so sgbm_out's finds take ~2 hops.
 __global__ __launch_bounds__(256) void sgbm_cc_count_kernel(SgbmK k, const int16_t* __restrict__ d16,
-                                                              const int32_t* __restrict__ parent,
+                                                              int32_t* __restrict__ parent,
                                                               int32_t* __restrict__ size, int frames) {
     const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int f = gw / k.H, y = gw - f * k.H;
     if (f >= frames) return;
     const int lane = lane_id(), W = k.W;
     const int16_t* d = d16 + (size_t)f * k.frame_px + (size_t)y * W;
-    const int32_t* par = parent + (size_t)f * k.frame_px;
+    int32_t* par = parent + (size_t)f * k.frame_px;
     int32_t* sz = size + (size_t)f * k.frame_px;
     int carry = 0, acc_root = -1, acc = 0;
     for (int x0 = 0; x0 < W; x0 += 64) {
@@ -1023,6 +1025,7 @@ __global__ __launch_bounds__(256) void sgbm_cc_count_kernel(SgbmK k, const int16
         carry = __builtin_amdgcn_readlane(s, 63);
         const bool end = in && v != k.new_val && !cc_link(v, vr, k);
         const int root = end ? cc_root(par, y * W + s) : -1;
+        if (end && root != y * W + s) __hip_atomic_store(par + y * W + s, root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int len = x - s + 1;
         const bool mine = end && root == acc_root;
         int add = mine ? len : 0;

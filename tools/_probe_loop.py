@@ -15,7 +15,10 @@ def show(loop, seqs):
         tl = loop.timeline(q)
         print(f"  batch {q}: " + "  ".join(f"{n[:4]} {tl[n][0]:8.2f}-{tl[n][1]:8.2f}" for n in STAGES), flush=True)
 
+ONLY = os.environ.get("PROBE_ONLY")   # e.g. "caller2": that configuration alone, nothing after it
 for source, slots in (("caller", 2), ("caller", 1), ("synth", 2)):
+    if ONLY and ONLY != f"{source}{slots}":
+        continue
     with FrameLoop(F, slots=slots, source=source, carmask=mask) as loop:
         for i in range(6):
             if i == 2:
@@ -29,6 +32,8 @@ for source, slots in (("caller", 2), ("caller", 1), ("synth", 2)):
         print(f"source={source} slots={slots}: {dt:.2f} ms/batch", flush=True)
         show(loop, range(s - slots + 1, s + 1))
 
+if ONLY:
+    sys.exit(0)
 # the batched RANSAC alone (maskpoints + draw + eval), 4096 carmask frames
 with sb.Batch(F, step=1, with_bgr=True, with_points=True) as rb:
     rb.synth(0); rb.set_mask(mask); rb.prepass("previous")
