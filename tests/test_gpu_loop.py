@@ -98,16 +98,20 @@ def test_eight_batches_every_frame(gold, mask):
         assert check_batch(b, first, gold[first:first + frames]) == [], prev
 
 
-def test_caller_filled_batches_equal_one_batch(mask):
+@pytest.mark.parametrize("H,W,step", [(544, 1024, 1), (544, 1024, 2), (390, 889, 1)])
+def test_caller_filled_batches_equal_one_batch(mask, H, W, step):
     """source="caller": frames uploaded into the acquired slot (svx.loop.FrameLoop.acquire). Three batches of 4
     frames give, frame for frame, what one 12-frame batch gives with the same pre-pass, RANSAC and pipeline
-    (the carry is the previous batch's last cleaned frame), and the imageRoadMap / road walk are produced."""
+    (the carry is the previous batch's last cleaned frame), and the imageRoadMap / road walk are produced; at
+    the reference's step 2 and on the cropped 390 x 889 frames too (the tiled pipeline and the road from the
+    points)."""
     import oracle
     from svx import batch
     from svx.loop import FrameLoop
     ids = list(range(300, 312))
-    frames = [oracle.synth_frame(g) for g in ids]
-    with batch.Batch(12, step=1, with_bgr=True, with_points=True) as one:
+    frames = [tuple(np.ascontiguousarray(a[:H, :W]) for a in oracle.synth_frame(g)) for g in ids]
+    mask = np.ascontiguousarray(mask[:H, :W])
+    with batch.Batch(12, H=H, W=W, step=step, with_bgr=True, with_points=True) as one:
         for f, (d, c) in enumerate(frames):
             one.upload(f, d, c)
         one.set_mask(mask)
@@ -120,7 +124,7 @@ def test_caller_filled_batches_equal_one_batch(mask):
         want_r = [one.read_ransac(f) for f in range(12)]
         want_road = [one.read_road(f, walk=True) for f in range(12)]
         want_map = [one.read_road_map(f) for f in (0, 11)]
-    with FrameLoop(4, slots=2, source="caller", seed_base=7, road="map", carmask=mask) as loop:
+    with FrameLoop(4, H=H, W=W, step=step, slots=2, source="caller", seed_base=7, road="map", carmask=mask) as loop:
         for i in range(3):
             b = loop.acquire()
             for f in range(4):
@@ -140,3 +144,34 @@ def test_caller_filled_batches_equal_one_batch(mask):
         b, first = loop.batch(seq)
         assert np.array_equal(b.digest("pipeline"), want[8:12])
         assert np.array_equal(b.read_road_map(3), want_map[1])
+
+
+def test_step2_resident_batches_equal_one_batch(mask):
+    """Two 1024-frame batches at the reference's step 2 (the resident pipeline, road from its points: the
+    bitmap is step-1 only) equal one 2048-frame batch frame for frame: RANSAC, pipeline digests, road."""
+    from svx import batch
+    from svx.loop import FrameLoop
+    n = 1024
+    with batch.Batch(2 * n, step=2, with_bgr=True, with_points=True) as one:
+        one.synth(0)
+        one.set_mask(mask)
+        one.prepass("previous")
+        one.ransac(seed_base=0, trials=600)
+        one.pipeline_planes()
+        one.road_raster()
+        want = one.digest("pipeline")
+        probe = (0, 1, n - 1, n, n + 1, 2 * n - 1)
+        want_r = {f: one.read_ransac(f) for f in probe}
+        want_road = {f: one.read_road(f, walk=True) for f in probe}
+    with FrameLoop(n, step=2, slots=2, carmask=mask) as loop:
+        seqs = [loop.submit(0), loop.submit(n)]
+        for seq in seqs:
+            loop.wait(seq)
+            b, first = loop.batch(seq)
+            assert np.array_equal(b.digest("pipeline"), want[first:first + n]), seq
+            for f in probe:
+                if first <= f < first + n:
+                    r = b.read_ransac(f - first)
+                    assert r["trial"] == want_r[f]["trial"] and r["err"] == want_r[f]["err"], f
+                    img, walk = b.read_road(f - first, walk=True)
+                    assert np.array_equal(img, want_road[f][0]) and np.array_equal(walk, want_road[f][1]), f
