@@ -1197,7 +1197,10 @@ static int sgbm_prefetch() {
 }
 
 bool sgbm_supported(const SgbmK& k) {
-    return k.width1 > k.SW2 && k.W <= 2048 && k.H >= 1 && k.SW2 >= 0 && k.SW2 <= 31;
+    // the walks address a frame's volume through buffer resources with 32-bit byte offsets (wave_rsrc): a frame's
+    // int16 volume, diagonal stride included, stays below 2^31 bytes
+    const size_t frame_vol = (size_t)(k.H + 1) * ((size_t)k.width1 * 64 + 64) * sizeof(uint32_t);
+    return k.width1 > k.SW2 && k.W <= 2048 && k.H >= 1 && k.SW2 >= 0 && k.SW2 <= 31 && frame_vol < 0x7FFFFFFFu;
 }
 
 size_t sgbm_volume_bytes(const SgbmK& k) { return (size_t)k.H * k.width1 * kSgD * sizeof(int16_t); }
