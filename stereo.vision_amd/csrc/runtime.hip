@@ -2181,6 +2181,7 @@ int sv_loop_destroy(sv_loop* L) {
             if (e) (void)hipEventDestroy(e);
     if (L->epoch) (void)hipEventDestroy(L->epoch);
     if (L->carry.p) (void)hipFree(L->carry.p);
+    if (L->gate.p) (void)hipFree(L->gate.p);
     for (sv_batch* b : L->slot) sv_batch_destroy(b);
     delete L;
     return SV_OK;
