@@ -582,7 +582,10 @@ def sgbm_extra(sb, device, with_cpu, frames=128, chunk=128):
              "us_per_frame": round(k_ms / max(k_n, 1) / frames * 1e3, 1),
              "frame0_matches_oracle": bool(np.array_equal(b.read_disp(0), ref)),
              "kernels": "sgbm_hsum + sgbm_vertical + sgbm_diag + sgbm_row + sgbm_median3 + cc_rows/union/count + out",
-             "parity": "unpinned vs OpenCV (absent); bit-exact vs oracle/sgbm_oracle.c"}
+             "parity": "unpinned vs OpenCV (absent); bit-exact vs oracle/sgbm_oracle.c",
+             "placement": dict(b.placement("sgbm"), note="sgbm_place: on the batch's first SGBM call up to 2 "
+                               "contiguous sets of the four cost volumes, the first chunk's compute timed on each, "
+                               "the fastest kept (outside the timed region; DESIGN §7.4)")}
         if with_cpu:
             r["cpu_restatement_ms_per_frame"] = round(cpu_ms, 1)
             r["cpu_note"] = "oracle/sgbm_oracle.c, 1 thread, scalar C (not OpenCV's SIMD build)"

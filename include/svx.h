@@ -348,10 +348,11 @@ int sv_batch_last_ms(sv_batch* b, int which, float* ms);
  * Synchronises the batch stream. */
 int sv_batch_timing(sv_batch* b, int which, double* total_ms, int64_t* count);
 int sv_batch_timing_reset(sv_batch* b);
-/* The output-plane placement probe of a large batch's first call (which: 0 = K1's X/Y/Z planes, k1_place;
- * 1 = the resident pipeline's five output planes, pipe_place): up to 3 sets of planes are allocated and one call
- * is timed on each (the pipeline: the faster of two passes); the fastest set is kept. ms[0..n-1] = each set's
- * timed call, *kept = the kept set's index (-1 when no probe ran: small batch, too little free memory). */
+/* The placement probe of a large batch's first call (which: 0 = K1's X/Y/Z planes, k1_place; 1 = the resident
+ * pipeline's five output planes, pipe_place; 2 = the SGBM cost volumes, sgbm_place): up to 3 (SGBM: 2) sets are
+ * allocated and one call is timed on each (the pipeline: the faster of two passes; SGBM: the first chunk's
+ * compute, the second of two runs); the fastest set is kept. ms[0..n-1] = each set's timed call, *kept = the
+ * kept set's index (-1 when no probe ran: small batch or chunk, too little free memory). */
 int sv_batch_placement(sv_batch* b, int which, float* ms, int cap, int* n, int* kept);
 
 /* Read back. */

@@ -16,7 +16,7 @@
 //                   (P = sat16), then the (+1,0) path, S = sat16(P + L),
 //                   winner, subpixel, disp2 and the left-right check -> int16
 //   cc_* kernels    filterSpeckles as union-find connected components
-//   out_kernel      speckle decision + TOZERO + scaling -> u8 (and int16)
+//   out_rows_kernel speckle decision + TOZERO + scaling -> u8 (and int16), one wave a row
 // Volumes are [frame][y][x][d] int16 (one 256-byte line per cell, lane l
 // holding d = 2l, 2l+1), so every path step is one coalesced 4-byte load or
 // store per lane. Exactness rules: see oracle/sgbm_oracle.c (same semantics).
@@ -289,13 +289,21 @@ struct BtFeat {
 // are 0 .. 255): v_pk_sub_u16 clamp twice and a v_pk_max_u16 per direction.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
-__device__ __forceinline__ uint32_t bt_cost2(const BtFeat& a, const BtFeat& b) {
+// both channels' costs (channel 0 in the low half, channel 1 in the high)
+__device__ __forceinline__ uint32_t bt_cost_ch(const BtFeat& a, const BtFeat& b) {
     const u16x2 u = as_u16x2(a.v), u0 = as_u16x2(a.lo), u1 = as_u16x2(a.hi);
     const u16x2 v = as_u16x2(b.v), v0 = as_u16x2(b.lo), v1 = as_u16x2(b.hi);
     const u16x2 c0 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(u, v1), __builtin_elementwise_sub_sat(v0, u));
     const u16x2 c1 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, u1), __builtin_elementwise_sub_sat(u0, v));
-    const uint32_t c = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(c0, c1));
-    return (c & 0xFFFF) + (c >> 18);   // channel 0 + (channel 1 >> 2); both in 0 .. 255
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(c0, c1));
+}
+// two pixels' costs as a pair: (c0(a) + c1(a) >> 2) | (c0(b) + c1(b) >> 2) << 16, with the channels regrouped
+// by two v_perm so that the shift and the sum are one packed operation each for both
+__device__ __forceinline__ uint32_t bt_cost_pair(const BtFeat& l, const BtFeat& a, const BtFeat& b) {
+    const uint32_t ca = bt_cost_ch(l, a), cb = bt_cost_ch(l, b);
+    const u16x2 ch0 = as_u16x2(__builtin_amdgcn_perm(cb, ca, 0x05040100u));   // (ca.lo, cb.lo)
+    const u16x2 ch1 = as_u16x2(__builtin_amdgcn_perm(cb, ca, 0x07060302u));   // (ca.hi, cb.hi)
+    return __builtin_bit_cast(uint32_t, ch0 + (ch1 >> (u16x2){2, 2}));
 }
 
 template <int SW2C>
@@ -389,7 +397,7 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
     };
     // cost pair (d0, d0 + 1) from the left features at x and the right ones at x - d0 (a) and x - d0 - 1 (b)
     const auto cost = [](const BtFeat& l, const BtFeat& a, const BtFeat& b) -> uint32_t {
-        return bt_cost2(l, a) | bt_cost2(l, b) << 16;
+        return bt_cost_pair(l, a, b);
     };
     const auto pix = [&](int j) -> uint32_t {
         j = min(max(j, 0), n - 1);
@@ -407,6 +415,12 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
     uint32_t vlast = ring[RS - 1];
     BtFeat acur = feat(W + jn + kSgD - d0), aprev = feat(W + jn + kSgD - d0 - 1);   // A_jn, A_{jn - 1}
     uint32_t* out = hvol + ((size_t)f * H + y) * n * 64;   // wave-uniform row; + the lane per store
+    // The main loop's feature reads at column x are the same for every lane; with x wave-uniform the compiler
+    // copies the SGPR address into a VGPR for each of the four reads. An opaque zero added once keeps x in a
+    // VGPR, stepped by one add per column.
+    int vzero;
+    __asm__("v_mov_b32 %0, 0" : "=v"(vzero));
+    int xv = jn + kSgD + vzero;
     for (int x0 = xs; x0 < xe; x0 += RS) {
 #pragma unroll
         for (int u = 0; u < RS; ++u) {
@@ -416,7 +430,7 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
             // step xi adds column xi + 1 + SW2 (clamped: past the last column it is the last column again)
             if (jn < n - 1) {
                 ++jn;
-                const int x = jn + kSgD;
+                const int x = ++xv;   // jn + kSgD
                 const BtFeat rn = feat(W + x);   // lane 0's A_jn
                 BtFeat anew;                     // wave_shr:1 of A_{jn - 2}
                 anew.v = __builtin_amdgcn_update_dpp((int)rn.v, (int)aprev.v, 0x138, 0xf, 0xf, false);
@@ -876,9 +890,9 @@ __device__ __forceinline__ int cc_find(int32_t* par, int x) {
     return x;
 }
 
-// Read-only find for the counting pass: that pass stores every pixel's root
-// into par[p], and a halving write from another thread's find could replace
-// such a root with a mere ancestor after it was stored.
+// Read-only find for the counting pass: once every union is done no path needs halving, and the counting
+// pass's only writes are final roots into run starts (an earlier version stored every pixel's root while other
+// threads' halving finds ran: a halving write could replace such a root with a mere ancestor).
 __device__ __forceinline__ int cc_root(const int32_t* par, int x) {
     int p = __atomic_load_n(par + x, __ATOMIC_RELAXED);
     while (p != x) {
@@ -1049,23 +1063,42 @@ __global__ __launch_bounds__(256) void sgbm_cc_count_kernel(SgbmK k, const int16
     if (lane == 0 && acc_root >= 0 && acc) atomicAdd(sz + acc_root, acc);
 }
 
-__global__ __launch_bounds__(256) void sgbm_out_kernel(SgbmK k, const int16_t* __restrict__ d16,
-                                                         const int32_t* __restrict__ parent,
-                                                         const int32_t* __restrict__ size, uint8_t* __restrict__ out,
-                                                         int16_t* __restrict__ filt, int frames) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t f = i / k.frame_px;
+// The speckle decision row by row (one wave a row, as the counting pass): a pixel's run start comes from the
+// same segmented scan, its root is par[run start] (the counting pass pointed every run start at its root) and
+// the root's size decides — two loads per run (the same address across the run's lanes), no per-pixel find.
+__global__ __launch_bounds__(256) void sgbm_out_rows_kernel(SgbmK k, const int16_t* __restrict__ d16,
+                                                            const int32_t* __restrict__ parent,
+                                                            const int32_t* __restrict__ size,
+                                                            uint8_t* __restrict__ out, int16_t* __restrict__ filt,
+                                                            int frames) {
+    const int gw = blockIdx.x * (blockDim.x >> 6) + wave_uniform_id();
+    const int f = gw / k.H, y = gw - f * k.H;
     if (f >= frames) return;
-    const int p = (int)(i - f * k.frame_px);
-    int v = d16[f * k.frame_px + p];
-    if (v != k.new_val && size[f * k.frame_px + cc_root(parent + f * k.frame_px, p)] <= k.max_size) v = k.new_val;
-    if (filt) filt[f * k.frame_px + p] = (int16_t)v;
-    if (!out) return;
-    const int y = p / k.W, x = p - y * k.W;
-    const int oy = y, ox = x - k.out_c0;
-    if (oy >= k.out_rows || ox < 0 || ox >= k.out_cols) return;
-    const int q = v > 0 ? v >> 4 : 0;   // TOZERO, then (d / 16.).astype(uint8)
-    out[f * (int64_t)k.out_rows * k.out_stride + (int64_t)oy * k.out_stride + ox] = (uint8_t)(int)((double)q * k.scale);
+    const int lane = lane_id(), W = k.W;
+    const int16_t* d = d16 + (size_t)f * k.frame_px + (size_t)y * W;
+    const int32_t* par = parent + (size_t)f * k.frame_px;
+    const int32_t* sz = size + (size_t)f * k.frame_px;
+    int carry = 0;
+    for (int x0 = 0; x0 < W; x0 += 64) {
+        const int x = x0 + lane;
+        const bool in = x < W;
+        int v = in ? d[x] : k.new_val;
+        const int vl = in && x > 0 ? d[x - 1] : k.new_val;
+        const int s = cc_run_start(in && !(x > 0 && cc_link(v, vl, k)), x, carry);
+        carry = __builtin_amdgcn_readlane(s, 63);
+        if (!in) continue;
+        if (v != k.new_val) {
+            const int root = __atomic_load_n(par + y * W + s, __ATOMIC_RELAXED);
+            if (sz[root] <= k.max_size) v = k.new_val;
+        }
+        const int p = y * W + x;
+        if (filt) filt[(size_t)f * k.frame_px + p] = (int16_t)v;
+        if (!out) continue;
+        const int ox = x - k.out_c0;
+        if (y >= k.out_rows || ox < 0 || ox >= k.out_cols) continue;
+        const int q = v > 0 ? v >> 4 : 0;   // TOZERO, then (d / 16.).astype(uint8)
+        out[f * (int64_t)k.out_rows * k.out_stride + (int64_t)y * k.out_stride + ox] = (uint8_t)(int)((double)q * k.scale);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1283,7 +1316,8 @@ hipError_t launch_speckle_scale(const SgbmK& k, int frames, const SgbmScratch& s
     hipError_t e = hipMemsetAsync(s.size, 0, sizeof(int32_t) * n, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(sgbm_cc_count_kernel, dim3(rows), dim3(256), 0, st, k, s.d16, s.parent, s.size, frames);
-    hipLaunchKernelGGL(sgbm_out_kernel, dim3(g), dim3(256), 0, st, k, s.d16, s.parent, s.size, out, filt, frames);
+    hipLaunchKernelGGL(sgbm_out_rows_kernel, dim3(rows), dim3(256), 0, st, k, s.d16, s.parent, s.size, out, filt,
+                       frames);
     return hipGetLastError();
 }
 

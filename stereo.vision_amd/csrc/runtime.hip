@@ -89,10 +89,23 @@ struct DevBuf {
 struct SgbmBufs {
     DevBuf vol[4], raw, d16, par, size, flags;
     int frames = 0;
+    bool placed = false;   // the volumes came from sgbm_place (re-placed when they have to grow)
+    hipError_t ensure_rest(const SgbmK& k, int n) {   // the per-pixel scratch (the volumes: sgbm_place)
+        const size_t px = (size_t)k.frame_px * n;
+        hipError_t e = raw.ensure(px * sizeof(int16_t));
+        if (e == hipSuccess) e = d16.ensure(px * sizeof(int16_t));
+        if (e == hipSuccess) e = par.ensure(px * sizeof(int32_t));
+        if (e == hipSuccess) e = size.ensure(px * sizeof(int32_t));
+        if (e == hipSuccess) e = flags.ensure(sizeof(uint32_t) * n);
+        return e;
+    }
     hipError_t ensure(const SgbmK& k, int n) {
         const size_t vb = sgbm_volume_bytes(k) * n, px = (size_t)k.frame_px * n;
         hipError_t e = hipSuccess;
-        for (int i = 0; i < 4 && e == hipSuccess; ++i) e = vol[i].ensure(vb);
+        // the cost volumes physically contiguous: 32.37 vs 33.09 ms per 128 frames over five alternating
+        // processes with every large buffer contiguous (profiles/r04/ab_sgbm_contig.txt); the walks stream them
+        // (sgbm_place allocates them first for a large chunk and keeps the faster of two sets)
+        for (int i = 0; i < 4 && e == hipSuccess; ++i) e = vol[i].ensure(vb, true);
         if (e == hipSuccess) e = raw.ensure(px * sizeof(int16_t));
         if (e == hipSuccess) e = d16.ensure(px * sizeof(int16_t));
         if (e == hipSuccess) e = par.ensure(px * sizeof(int32_t));
@@ -310,8 +323,8 @@ struct sv_batch {
     size_t pool_next = 0;
     // the placement probes of the first K1 / resident pipeline call (k1_place / pipe_place): each set's timed
     // call (ms), how many sets were tried and which one was kept (-1: no probe ran)
-    float place_ms[2][8] = {};
-    int place_n[2] = {0, 0}, place_kept[2] = {-1, -1};
+    float place_ms[3][8] = {};
+    int place_n[3] = {0, 0, 0}, place_kept[3] = {-1, -1, -1};
     bool timing = true;        // record per-launch timing events (off for a frame loop's slots: they run unbounded)
     hipError_t timed_event(int* idx) {
         if (!timing) {
@@ -933,7 +946,7 @@ int sv_batch_read_frame_plane(sv_batch* b, int frame, double* out4) {
 }
 
 int sv_batch_placement(sv_batch* b, int which, float* ms, int cap, int* n, int* kept) {
-    if (!b || which < 0 || which > 1 || !n || !kept || cap < 0 || (cap > 0 && !ms))
+    if (!b || which < 0 || which > 2 || !n || !kept || cap < 0 || (cap > 0 && !ms))
         return fail(SV_E_ARG, "sv_batch_placement: bad arguments");
     *n = b->place_n[which];
     *kept = b->place_kept[which];
@@ -2085,6 +2098,74 @@ int sv_batch_preprocess(sv_batch* b, const uint8_t* lut, int sync) {
     return SV_OK;
 }
 
+// The cost volumes, placed (as K1's planes, k1_place): where the four streamed volumes land moves the walks by
+// up to 7 % from one allocation to the next (30.9-33.1 ms per 128 frames over five processes of the same build,
+// profiles/r04/ab_sgbm_volcontig.txt). A chunk of >= 64 frames allocates up to SVX_SGBM_TRIES (default 2)
+// contiguous sets (all held until the end, at most 3/4 of the free memory), runs the first chunk's SGBM on each
+// (the second of two runs timed) and keeps the fastest; the results are the same on every set.
+static int sgbm_place(sv_batch* b, const SgbmK& k, int chunk, const uint8_t* left, const uint8_t* right) {
+    int tries = 2;
+    if (const char* e = svx_knob("SVX_SGBM_TRIES")) tries = std::max(1, std::atoi(e));
+    const size_t vb = sgbm_volume_bytes(k) * (size_t)chunk, set_b = 4 * (vb + vb / 4);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+    for (DevBuf& v : b->sg.vol) {   // the old volumes go (a new size)
+        if (v.p) (void)hipFree(v.p);
+        v.p = nullptr;
+        v.bytes = 0;
+    }
+    if (chunk < 64) tries = 1;
+    else tries = (int)std::min<size_t>((size_t)tries, std::max<size_t>(1, free_b / 4 * 3 / set_b));
+    std::vector<std::array<DevBuf, 4>> sets((size_t)tries);
+    int best = -1;
+    float best_ms = 0.f;
+    for (int t = 0; t < tries; ++t) {
+        auto& c = sets[(size_t)t];
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < 4 && e == hipSuccess; ++i) e = c[i].ensure(vb, true);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        if (tries > 1) {
+            for (int i = 0; i < 4; ++i) b->sg.vol[i] = c[i];   // (borrowed: the set's owner is `sets`)
+            SgbmScratch sc = b->sg.scratch();
+            sc.flags = b->sgflags.as<uint32_t>();
+            float ms = 0.f;
+            for (int rep = 0; rep < 2 && e == hipSuccess; ++rep) {   // the second run is timed
+                e = hipEventRecord(b->ev[0], b->stream);
+                if (e == hipSuccess) e = launch_sgbm_compute(k, left, right, chunk, sc, b->stream);
+                if (e == hipSuccess) e = hipEventRecord(b->ev[1], b->stream);
+                if (e == hipSuccess) e = hipEventSynchronize(b->ev[1]);
+                if (e == hipSuccess) e = hipEventElapsedTime(&ms, b->ev[0], b->ev[1]);
+            }
+            if (e != hipSuccess) break;
+            if (t < 8) {
+                b->place_ms[2][t] = ms;
+                b->place_n[2] = t + 1;
+            }
+            if (best < 0 || ms < best_ms) {
+                best = t;
+                best_ms = ms;
+            }
+        } else {
+            best = t;
+        }
+    }
+    for (DevBuf& v : b->sg.vol) v = DevBuf{};
+    int rc = SV_OK;
+    if (best < 0) rc = fail(SV_E_HIP, "SGBM volumes: allocation failed (%zu bytes each)", vb);
+    b->place_kept[2] = tries > 1 ? best : -1;
+    for (int t = 0; t < (int)sets.size(); ++t)
+        for (int i = 0; i < 4; ++i) {
+            DevBuf& x = sets[(size_t)t][i];
+            if (t == best) b->sg.vol[i] = x;
+            else if (x.p) (void)hipFree(x.p);
+        }
+    b->sg.placed = rc == SV_OK;
+    return rc;
+}
+
 int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int chunk) {
     if (!b) return fail(SV_E_ARG, "null batch");
     if (!b->pairL.p || !b->pairR.p) return fail(SV_E_STATE, "no stereo pairs (sv_batch_synth_pair / upload_pair)");
@@ -2112,10 +2193,14 @@ int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int
         while (chunk > 1 && (size_t)chunk * per > budget) chunk = chunk * 3 / 4;
     }
     chunk = std::min(chunk, b->frames);
-    HIP_TRY(b->sg.ensure(k, chunk));
     // the range flags of every frame of the batch, checked once after the last chunk (no host sync between chunks)
     HIP_TRY(b->sgflags.ensure(sizeof(uint32_t) * b->frames));
     const size_t px = (size_t)k.frame_px, opx = (size_t)b->H * b->W;
+    if (b->sg.vol[0].bytes < sgbm_volume_bytes(k) * (size_t)chunk) {
+        HIP_TRY(b->sg.ensure_rest(k, chunk));
+        if (int rc = sgbm_place(b, k, chunk, b->pairL.as<uint8_t>(), b->pairR.as<uint8_t>())) return rc;
+    }
+    HIP_TRY(b->sg.ensure(k, chunk));
     int t0, t1;
     HIP_TRY(hipEventRecord(b->ev[4], b->stream));
     HIP_TRY(b->timed_event(&t0));

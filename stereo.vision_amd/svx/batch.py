@@ -207,12 +207,13 @@ class Batch:
         return float(tot.value), int(cnt.value)
 
     def placement(self, which="project"):
-        """The first large call's output-plane placement probe: {"tried_ms": [...], "kept": index or None}
-        (which = "project" for K1's planes, "pipeline" for the resident pipeline's; sv_batch_placement)."""
+        """The first large call's placement probe: {"tried_ms": [...], "kept": index or None} (which = "project"
+        for K1's planes, "pipeline" for the resident pipeline's output planes, "sgbm" for the SGBM cost volumes;
+        sv_batch_placement)."""
         ms = (ctypes.c_float * 8)()
         n, kept = ctypes.c_int(0), ctypes.c_int(-1)
-        _abi.call("sv_batch_placement", self._h, 0 if which == "project" else 1, ms, 8, ctypes.byref(n),
-                  ctypes.byref(kept))
+        _abi.call("sv_batch_placement", self._h, {"project": 0, "pipeline": 1, "sgbm": 2}[which], ms, 8,
+                  ctypes.byref(n), ctypes.byref(kept))
         return {"tried_ms": [round(float(ms[i]), 4) for i in range(n.value)],
                 "kept": kept.value if kept.value >= 0 else None}
 
