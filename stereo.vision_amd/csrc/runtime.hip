@@ -55,12 +55,13 @@ struct DevBuf {
     // hipMalloc's pages, where K1's planes land decides how its three store streams spread over the HBM
     // channels: K1 took 4.35-5.0 ms from one allocation to the next, 4.23-4.34 ms contiguous.
     // SVX_CONTIG: 0 = never, 2 = every large buffer (A/B).
-    hipError_t ensure(size_t n, bool contiguous = false, int tag = 0) {
+    // exact: no 1/4 growth slack (the SGBM volumes, 16 GB each at 128 frames, whose size follows the chunk)
+    hipError_t ensure(size_t n, bool contiguous = false, int tag = 0, bool exact = false) {
         if (n <= bytes) return hipSuccess;
         if (p) (void)hipFree(p);
         p = nullptr;
         bytes = 0;
-        size_t want = n < 4096 ? 4096 : n + n / 4;
+        size_t want = n < 4096 ? 4096 : exact ? n : n + n / 4;
         hipError_t e = hipErrorUnknown;
         static const int mode = [] {
             const char* v = svx_knob("SVX_CONTIG");
@@ -105,7 +106,7 @@ struct SgbmBufs {
         // the cost volumes physically contiguous: 32.37 vs 33.09 ms per 128 frames over five alternating
         // processes with every large buffer contiguous (profiles/r04/ab_sgbm_contig.txt); the walks stream them
         // (sgbm_place allocates them first for a large chunk and keeps the faster of two sets)
-        for (int i = 0; i < 4 && e == hipSuccess; ++i) e = vol[i].ensure(vb, true);
+        for (int i = 0; i < 4 && e == hipSuccess; ++i) e = vol[i].ensure(vb, true, 0, true);
         if (e == hipSuccess) e = raw.ensure(px * sizeof(int16_t));
         if (e == hipSuccess) e = d16.ensure(px * sizeof(int16_t));
         if (e == hipSuccess) e = par.ensure(px * sizeof(int32_t));
@@ -2101,12 +2102,12 @@ int sv_batch_preprocess(sv_batch* b, const uint8_t* lut, int sync) {
 // The cost volumes, placed (as K1's planes, k1_place): where the four streamed volumes land moves the walks by
 // up to 7 % from one allocation to the next (30.9-33.1 ms per 128 frames over five processes of the same build,
 // profiles/r04/ab_sgbm_volcontig.txt). A chunk of >= 64 frames allocates up to SVX_SGBM_TRIES (default 2)
-// contiguous sets (all held until the end, at most 3/4 of the free memory), runs the first chunk's SGBM on each
+// contiguous sets (all held until the end, at most 7/8 of the free memory), runs the first chunk's SGBM on each
 // (the second of two runs timed) and keeps the fastest; the results are the same on every set.
 static int sgbm_place(sv_batch* b, const SgbmK& k, int chunk, const uint8_t* left, const uint8_t* right) {
     int tries = 2;
     if (const char* e = svx_knob("SVX_SGBM_TRIES")) tries = std::max(1, std::atoi(e));
-    const size_t vb = sgbm_volume_bytes(k) * (size_t)chunk, set_b = 4 * (vb + vb / 4);
+    const size_t vb = sgbm_volume_bytes(k) * (size_t)chunk, set_b = 4 * vb;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     for (DevBuf& v : b->sg.vol) {   // the old volumes go (a new size)
@@ -2115,14 +2116,14 @@ static int sgbm_place(sv_batch* b, const SgbmK& k, int chunk, const uint8_t* lef
         v.bytes = 0;
     }
     if (chunk < 64) tries = 1;
-    else tries = (int)std::min<size_t>((size_t)tries, std::max<size_t>(1, free_b / 4 * 3 / set_b));
+    else tries = (int)std::min<size_t>((size_t)tries, std::max<size_t>(1, free_b / 8 * 7 / set_b));
     std::vector<std::array<DevBuf, 4>> sets((size_t)tries);
     int best = -1;
     float best_ms = 0.f;
     for (int t = 0; t < tries; ++t) {
         auto& c = sets[(size_t)t];
         hipError_t e = hipSuccess;
-        for (int i = 0; i < 4 && e == hipSuccess; ++i) e = c[i].ensure(vb, true);
+        for (int i = 0; i < 4 && e == hipSuccess; ++i) e = c[i].ensure(vb, true, 0, true);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             break;
