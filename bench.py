@@ -392,9 +392,10 @@ def extras(b, args, with_cpu, first=0):
     px = b.frames * H * W
     n2 = int(b.read_counts()[:, 2].sum())
     ms = _timed(b, lambda: (b.road_raster(sync=False), b.nonzero(sync=False)), 3, ramp_ms=args.ramp_ms / 3)
-    # one pass (road_kernel): the points in (8 B each), the images out once, 8 B per non-zero pixel out (at most
-    # one per point: counted as one per point, so approx_GBps is an upper bound)
-    byts = 8 * n2 + px + 8 * n2
+    # one pass (road_kernel): the points in (8 B each), the images out once, 4 B per non-zero pixel out (the walk's
+    # packed x | y << 16 entries, widened to int32 pairs on read-back; at most one per point: counted as one per
+    # point, so approx_GBps is an upper bound)
+    byts = 8 * n2 + px + 4 * n2
     ex["road_raster_nonzero"] = {"ms_per_batch": round(ms, 3), "approx_GBps": round(byts / ms / 1e6, 1),
                                  "points": n2, "kernels": "road_kernel (raster + non-zero walk in one pass)"}
     mask = carmask()
@@ -474,9 +475,10 @@ def extras(b, args, with_cpu, first=0):
         "road_ms_per_batch": round(road_bits, 3), "road_from_points_ms_per_batch": round(road_pts, 3),
         "pipeline_with_bitmap_gpu_ms_per_call": round(kb_ms / max(kb_n, 1), 4),
         "pipeline_gpu_ms_per_call": ex["pipeline_frame_planes"]["gpu_ms_per_call"],
-        "points": n2p, "bytes_from_bitmap": 4 * 32 * H * b.frames + px_all + 8 * n2p,
-        "bytes_from_points": 8 * n2p + px_all + 8 * n2p,
-        "note": "per-frame-plane points; bytes count one walk entry per point (an upper bound); the bitmap is "
+        "points": n2p, "bytes_from_bitmap": 4 * 32 * H * b.frames + px_all + 4 * n2p,
+        "bytes_from_points": 8 * n2p + px_all + 4 * n2p,
+        "note": "per-frame-plane points; bytes count one 4-byte walk entry (x | y << 16) per point (an upper "
+                "bound); the bitmap is "
                 "written by the pipeline (+0.28 GB per 4096 frames, counted in its time above)",
         "kernels": "road_rowscan_kernel + road_rows_kernel (from the bitmap) vs road_kernel (from the points)"}
 

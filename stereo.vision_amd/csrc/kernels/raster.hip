@@ -59,6 +59,12 @@ struct NonzeroShared {
 // block scan orders them, lanes put the pixel indices into LDS in output order,
 // then the whole chunk's [j, i] pairs are written contiguously (coalesced,
 // non-temporal: written once, read by the caller later).
+// A batch's walk entry (PK): x | y << 16 in one word (x < 4096, y < 65536), widened to the reference's [x, y]
+// int32 pair when read back (sv_batch_read_road): the walk is written once and only the host reads it, so it
+// moves 4 B per non-zero pixel instead of 8. The drop-in (sv_nonzero_points, any height) writes int32 pairs.
+__device__ __forceinline__ uint32_t walk_pk(int x, int y) { return (uint32_t)x | ((uint32_t)y << 16); }
+
+template <bool PK>
 __global__ __launch_bounds__(256) void nonzero_kernel(const uint8_t* __restrict__ img, int64_t frame_px, int W,
                                                       uint64_t W_m40, int32_t* __restrict__ out, int64_t cap,
                                                       int64_t* __restrict__ counts) {
@@ -107,11 +113,20 @@ __global__ __launch_bounds__(256) void nonzero_kernel(const uint8_t* __restrict_
             sh.stage[o++] = p0 + (uint32_t)b;
         }
         __syncthreads();   // sh.wtot is rewritten next chunk; sh.stage is complete
-        v2i* dst = reinterpret_cast<v2i*>(fo + running);
-        for (uint32_t j = tid; j < tot; j += 256) {
-            const uint32_t p = sh.stage[j];
-            const int y = fastdiv40((int)p, W_m40);
-            __builtin_nontemporal_store((v2i){(int)(p - (uint32_t)y * (uint32_t)W), y}, dst + j);
+        if (PK) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(out) + (int64_t)frame * cap + running;
+            for (uint32_t j = tid; j < tot; j += 256) {
+                const uint32_t p = sh.stage[j];
+                const int y = fastdiv40((int)p, W_m40);
+                dst[j] = walk_pk((int)(p - (uint32_t)y * (uint32_t)W), y);
+            }
+        } else {
+            v2i* dst = reinterpret_cast<v2i*>(fo + running);
+            for (uint32_t j = tid; j < tot; j += 256) {
+                const uint32_t p = sh.stage[j];
+                const int y = fastdiv40((int)p, W_m40);
+                __builtin_nontemporal_store((v2i){(int)(p - (uint32_t)y * (uint32_t)W), y}, dst + j);
+            }
         }
         running += tot;
     }
@@ -165,7 +180,7 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
     const int32_t* fx = px + (int64_t)frame * cap;
     const int32_t* fy = py + (int64_t)frame * cap;
     uint8_t* fimg = img + (int64_t)frame * H * W;
-    int2* fo = reinterpret_cast<int2*>(nzout) + (int64_t)frame * cap;
+    uint32_t* fo = reinterpret_cast<uint32_t*>(nzout) + (int64_t)frame * cap;
     if (tid < 128) sh.wrap[tid] = 0;
     // this lane's kRoadPts consecutive points of the 256 * kRoadPts-point chunk at i0 (qy = -2: past the
     // list): one 16-byte load per plane when the planes are 16-byte aligned (vec), 4-byte loads at the list's end
@@ -293,23 +308,11 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
                 sh.stage[o++] = p0 + (uint32_t)b;
             }
             __syncthreads();   // sh.wtot is rewritten next chunk; sh.stage is complete
-            v2i* dst = reinterpret_cast<v2i*>(fo + running);
-            const auto xy = [&](uint32_t p) {
+            uint32_t* dst = fo + running;   // packed entries (walk_pk), ordinary stores (partial lines merge in L2)
+            for (uint32_t j = tid; j < tot; j += 256) {
+                const uint32_t p = sh.stage[j];
                 const int y = fastdiv40((int)p, W_m40);
-                return (v2i){(int)(p - (uint32_t)y * (uint32_t)W), y};
-            };
-            if (vec) {   // two outputs a lane, 16-byte stores: output `running` alone when it is odd, the last alone when left over
-                const uint32_t lead = (running & 1u) && tot > 0 ? 1u : 0u;
-                const uint32_t pairs = (tot - lead) / 2;
-                if (lead && tid == 0) __builtin_nontemporal_store(xy(sh.stage[0]), dst);
-                for (uint32_t m = tid; m < pairs; m += 256) {
-                    const uint32_t j = lead + 2 * m;
-                    const v2i a = xy(sh.stage[j]), b2 = xy(sh.stage[j + 1]);
-                    __builtin_nontemporal_store((v4i){a.x, a.y, b2.x, b2.y}, reinterpret_cast<v4i*>(dst + j));
-                }
-                if (((tot - lead) & 1u) && tid == 0) __builtin_nontemporal_store(xy(sh.stage[tot - 1]), dst + tot - 1);
-            } else {
-                for (uint32_t j = tid; j < tot; j += 256) __builtin_nontemporal_store(xy(sh.stage[j]), dst + j);
+                dst[j] = walk_pk((int)(p - (uint32_t)y * (uint32_t)W), y);
             }
             running += tot;
         }
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restri
     // 64 i .. 64 i + 63, lane l pixel 64 i + l: its bit is bit l of words 2i, 2i+1 (scalar loads, the same for
     // the whole wave), its rank among the pass's marked pixels one v_mbcnt pair, and the pass's entries one
     // contiguous run after the previous passes' (s_bcnt1): sixteen coalesced stores, no loop, no LDS.
-    v2i* dst = reinterpret_cast<v2i*>(nzout) + (int64_t)frame * cap + first;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(nzout) + (int64_t)frame * cap + first;   // packed (walk_pk)
     uint32_t base = 0;
 #pragma unroll
     for (int i = 0; i < kRbWords / 2; ++i) {
@@ -415,9 +418,9 @@ __global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restri
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
         if (mine & 1u) {
             if (NT)
-                __builtin_nontemporal_store((v2i){64 * i + lane, y}, dst + base + rank);
+                __builtin_nontemporal_store(walk_pk(64 * i + lane, y), dst + base + rank);
             else
-                dst[base + rank] = (v2i){64 * i + lane, y};
+                dst[base + rank] = walk_pk(64 * i + lane, y);
         }
         base += __builtin_popcount(lo) + __builtin_popcount(hi);
     }
@@ -481,19 +484,22 @@ hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* coun
     const uint64_t m40 = (((uint64_t)1 << 40) + (uint64_t)W - 1) / (uint64_t)W;
     // vec: the point planes and the walk's output 16-byte aligned at every frame (cap % 4 == 0), so a lane takes
     // its 4 points with one load per plane and writes two walk outputs with one store
-    const bool vec = cap % 4 == 0 && ((reinterpret_cast<uintptr_t>(px) | reinterpret_cast<uintptr_t>(py) |
-                                       reinterpret_cast<uintptr_t>(nzout)) & 15u) == 0;
+    if (H > 65536) return hipErrorInvalidValue;   // packed walk entries: y < 65536
+    const bool vec = cap % 4 == 0 && ((reinterpret_cast<uintptr_t>(px) | reinterpret_cast<uintptr_t>(py)) & 15u) == 0;
     hipLaunchKernelGGL(road_kernel, dim3(frames), dim3(256), dyn, s, px, py, counts, cap, img, H, W, Wu, R, m40, nzout,
                        nzcount, bgr, paint, vec);
     return hipGetLastError();
 }
 
 hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
-                          hipStream_t s) {
+                          bool packed, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
-    if (px % 4 || px >= (1ll << 28) || W <= 0 || W > 4096) return hipErrorInvalidValue;
+    if (px % 4 || px >= (1ll << 28) || W <= 0 || W > 4096 || (packed && px / W > 65536)) return hipErrorInvalidValue;
     const uint64_t m40 = (((uint64_t)1 << 40) + (uint64_t)W - 1) / (uint64_t)W;
-    hipLaunchKernelGGL(nonzero_kernel, dim3(frames), dim3(256), 0, s, img, px, W, m40, out, cap, counts);
+    if (packed)
+        hipLaunchKernelGGL(nonzero_kernel<true>, dim3(frames), dim3(256), 0, s, img, px, W, m40, out, cap, counts);
+    else
+        hipLaunchKernelGGL(nonzero_kernel<false>, dim3(frames), dim3(256), 0, s, img, px, W, m40, out, cap, counts);
     return hipGetLastError();
 }
 

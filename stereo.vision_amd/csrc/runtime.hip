@@ -1318,7 +1318,7 @@ int sv_nonzero_points(const uint8_t* img, int H, int W, int32_t* out, int64_t ca
     HIP_TRY(hipMemcpyAsync(d->aux.p, img, (size_t)px, hipMemcpyHostToDevice, s));
     HIP_TRY(d->xy.ensure(sizeof(int32_t) * 2 * (size_t)px + 64));
     int64_t* cnt = reinterpret_cast<int64_t*>(d->xy.as<char>() + sizeof(int32_t) * 2 * (size_t)px);
-    HIP_TRY(launch_nonzero(d->aux.as<uint8_t>(), 1, padded, W, d->xy.as<int32_t>(), px, cnt, s));
+    HIP_TRY(launch_nonzero(d->aux.as<uint8_t>(), 1, padded, W, d->xy.as<int32_t>(), px, cnt, false, s));
     int64_t n = 0;
     HIP_TRY(hipMemcpyAsync(&n, cnt, sizeof n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -1337,7 +1337,7 @@ int sv_batch_road_raster(sv_batch* b, int sync) {
     HIP_TRY(hipSetDevice(b->device));
     const size_t px = (size_t)b->H * b->W;
     HIP_TRY(b->road.ensure(px * b->frames));
-    HIP_TRY(b->nz.ensure(sizeof(int32_t) * 2 * b->cap * b->frames));
+    HIP_TRY(b->nz.ensure(sizeof(uint32_t) * b->cap * b->frames));   // packed entries x | y << 16 (walk_pk)
     HIP_TRY(b->nzcount.ensure(sizeof(int64_t) * b->frames));
     // the images and their non-zero walks in one pass (road_kernel); SVX_ROAD_FUSED=0: raster, then the walk
     const char* v = svx_knob("SVX_ROAD_FUSED");
@@ -1376,10 +1376,10 @@ int sv_batch_nonzero(sv_batch* b, int sync) {
         if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
         return SV_OK;
     }
-    HIP_TRY(b->nz.ensure(sizeof(int32_t) * 2 * b->cap * b->frames));
+    HIP_TRY(b->nz.ensure(sizeof(uint32_t) * b->cap * b->frames));   // packed entries x | y << 16 (walk_pk)
     HIP_TRY(b->nzcount.ensure(sizeof(int64_t) * b->frames));
     HIP_TRY(launch_nonzero(b->road.as<uint8_t>(), b->frames, (int64_t)b->H * b->W, b->W, b->nz.as<int32_t>(),
-                           (int64_t)b->cap, b->nzcount.as<int64_t>(), b->stream));
+                           (int64_t)b->cap, b->nzcount.as<int64_t>(), true, b->stream));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }
@@ -1423,9 +1423,15 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
         HIP_TRY(hipMemcpy(&k, b->nzcount.as<int64_t>() + frame, sizeof k, hipMemcpyDeviceToHost));
         *n = k;
         if (k > cap) return fail(SV_E_CAP, "capacity %lld < %lld", (long long)cap, (long long)k);
-        if (k && nzpts)
-            HIP_TRY(hipMemcpy(nzpts, b->nz.as<int32_t>() + 2 * b->cap * frame, sizeof(int32_t) * 2 * k,
+        if (k && nzpts) {   // the packed entries (x | y << 16) widened to the reference's [x, y] int32 pairs
+            std::vector<uint32_t> pk((size_t)k);
+            HIP_TRY(hipMemcpy(pk.data(), b->nz.as<uint32_t>() + b->cap * frame, sizeof(uint32_t) * k,
                               hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < k; ++i) {
+                nzpts[2 * i] = (int32_t)(pk[(size_t)i] & 0xFFFFu);
+                nzpts[2 * i + 1] = (int32_t)(pk[(size_t)i] >> 16);
+            }
+        }
     }
     return SV_OK;
 }

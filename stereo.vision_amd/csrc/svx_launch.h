@@ -117,7 +117,7 @@ hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* coun
 hipError_t launch_road_bits(const uint32_t* bits, int frames, int H, int W, int32_t* roff, int64_t cap,
                             uint8_t* img, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr, uint8_t* paint,
                             hipStream_t s);
-hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts,
+hipError_t launch_nonzero(const uint8_t* img, int frames, int64_t px, int W, int32_t* out, int64_t cap, int64_t* counts, bool packed,
                           hipStream_t s);
 
 // kernels/ransac.hip -------------------------------------------------------
