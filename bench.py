@@ -444,12 +444,15 @@ def extras(b, args, with_cpu, first=0):
     ms = _timed(b, lambda: b.pipeline_planes(sync=False), 5, reset=True, ramp_ms=args.ramp_ms)
     k_ms, k_n = b.timing("pipeline")
     kept = int(b.read_counts()[:, 2].sum())
-    fp_bytes = 4 * b.Ng * b.frames + 20 * kept + 4096 * b.frames   # the config-4 accounting, this call's points
+    fp_bytes = 4 * b.Ng * b.frames + 16 * kept + 4096 * b.frames   # the config-4 accounting, this call's points
     fp_s = k_ms / max(k_n, 1) / 1e3
     ex["pipeline_frame_planes"] = {"ms_per_batch": round(ms, 3), "gpu_ms_per_call": round(fp_s * 1e3, 4),
                                    "frames": b.frames, "kept_points": kept,
                                    "algorithmic_bytes_per_call": fp_bytes,
                                    "frac": round(fp_bytes / fp_s / 1e9 / PEAK_HBM_GBS, 4) if fp_s > 0 else None,
+                                   "survey_bytes_per_call": fp_bytes + 4 * kept,
+                                   "frac_at_survey_bytes": round((fp_bytes + 4 * kept) / fp_s / 1e9 / PEAK_HBM_GBS, 4)
+                                   if fp_s > 0 else None,
                                    "workload": "the prepass-cleaned frames (fill previous + carmask), each with its "
                                                "own RANSAC plane (threshold 0.05, hist thr 10)",
                                    "traffic": pipeline_traffic(args.traffic_planes, b.frames, args.step),
@@ -796,7 +799,8 @@ def main(argv=None):
         counts_local = np.sum([b.read_counts().sum(axis=0) for b in batches], axis=0).astype(np.float64)
         counts = ctrl.sum(counts_local)
         kept2_gpu0 = int(batches[0].read_counts()[:, 2].sum())
-        pbytes = 4 * ng * frames_gpu + 20 * kept2_gpu0 + 4096 * frames_gpu
+        pbytes = 4 * ng * frames_gpu + 16 * kept2_gpu0 + 4096 * frames_gpu
+        survey_bytes = pbytes + 4 * kept2_gpu0   # SURVEY 8d's 20 B per kept point (int32 x and y stored apart)
         out["pipeline"] = {
             "workload": "configs[3]/[4]: same batch, plane threshold 0.05 + hue histogram (thr 10) "
                         "+ ordered compaction + int32 back-projection",
@@ -805,10 +809,15 @@ def main(argv=None):
             "achieved_GBps": round(pbytes / p_avg_s / 1e9, 1),
             "frac": round(pbytes / p_avg_s / 1e9 / PEAK_HBM_GBS, 4),
             "algorithmic_bytes_per_call": pbytes,
-            "bytes_note": "algorithmic = SURVEY 8d config 4 per GPU: 4 B read per grid point (disparity + BGR) + 20 B "
-                          "per kept point + 4 KB histogram per frame; the resident kernel does not read the BGR (nor, "
-                          "in pass 2, the disparity) of chunks the plane rules out, so it moves fewer bytes "
-                          "(traffic = PMC bytes per call, frac_of_traffic = traffic / time / peak)",
+            "bytes_note": "algorithmic = SURVEY 8d config 4 per GPU with the outputs as stored: 4 B read per grid point "
+                          "(disparity + BGR) + 16 B per kept point (fp32 X, Y, Z + the int32 (x, y) back-projection as "
+                          "int16 halves of one word, lossless: -1 <= x, y < 32768, widened on read-back; SURVEY counts "
+                          "20 B: survey_bytes_per_call, frac_at_survey_bytes) + 4 KB histogram per frame; the resident "
+                          "kernel does not read the BGR (nor, in pass 2, the disparity) of chunks the plane rules out, "
+                          "so it moves fewer bytes (traffic = PMC bytes per call, frac_of_traffic = traffic / time / "
+                          "peak)",
+            "survey_bytes_per_call": survey_bytes,
+            "frac_at_survey_bytes": round(survey_bytes / p_avg_s / 1e9 / PEAK_HBM_GBS, 4),
             "counts_total": {"valid": int(counts[0]), "kept": int(counts[1]), "kept2": int(counts[2])},
             "plane_broadcast": comm_note or {
                 "ranks": "RCCL ncclBroadcast into device memory every step (sv_comm_broadcast_plane_dev)",

@@ -70,8 +70,7 @@ __global__ __launch_bounds__(256) void digest_pipe_kernel(const uint8_t* __restr
                                                           const float* __restrict__ ox,
                                                           const float* __restrict__ oy,
                                                           const float* __restrict__ oz, int64_t ofs,
-                                                          const int32_t* __restrict__ ppx,
-                                                          const int32_t* __restrict__ ppy, int64_t cap, KParams p,
+                                                          const uint32_t* __restrict__ ppxy, int64_t cap, KParams p,
                                                           uint64_t* __restrict__ out) {
     __shared__ uint64_t red[4][4];
     const int frame = blockIdx.x, tid = threadIdx.x;
@@ -80,8 +79,7 @@ __global__ __launch_bounds__(256) void digest_pipe_kernel(const uint8_t* __restr
     const float* oX = ox + (int64_t)frame * ofs;
     const float* oY = oy + (int64_t)frame * ofs;
     const float* oZ = oz + (int64_t)frame * ofs;
-    const int32_t* oPx = ppx + (int64_t)frame * cap;
-    const int32_t* oPy = ppy + (int64_t)frame * cap;
+    const uint32_t* oPxy = ppxy + (int64_t)frame * cap;
     uint64_t acc[4] = {disp_hash_part(reinterpret_cast<const uint32_t*>(fd), p.frame_px / 4), 0, 0, 0};
     for (int k = tid; k < 1000; k += 256)
         acc[1] += dmix64(((uint64_t)(k + 65536) << 32) | hist[(int64_t)frame * kBins + k]);
@@ -104,8 +102,8 @@ __global__ __launch_bounds__(256) void digest_pipe_kernel(const uint8_t* __restr
             const double Y64 = (((double)y - p.ch) * Z64) / p.f;
             ok = ok && close_rel(X, X64) && close_rel(Y, Y64) && close_rel(Z, Z64);
         }
-        const uint32_t px = (uint32_t)oPx[i], py = (uint32_t)oPy[i];
-        const uint64_t a = ((uint64_t)(x | (y << 12) | (d << 24)) << 32) | (uint64_t)((px & 0xFFFFu) | ((py & 0xFFFFu) << 16));
+        // the planePoints entry: (x & 0xFFFF) | (y & 0xFFFF) << 16 of the int32 pair, i.e. the stored pp_pack word
+        const uint64_t a = ((uint64_t)(x | (y << 12) | (d << 24)) << 32) | (uint64_t)oPxy[i];
         acc[2] += dmix64(a ^ dmix64((uint64_t)i));
         acc[3] += ok ? 0u : 1u;
     }
@@ -174,7 +172,7 @@ hipError_t launch_digest_pipe(const KParams& p, const uint8_t* disp, const uint3
                               const PipeBuffers& bf, int frames, uint64_t* out, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
     hipLaunchKernelGGL(digest_pipe_kernel, dim3(frames), dim3(256), 0, s, disp, hist, counts, bf.ox, bf.oy, bf.oz,
-                       bf.ofs, bf.px, bf.py, bf.cap, p, out);
+                       bf.ofs, bf.pxy, bf.cap, p, out);
     return hipGetLastError();
 }
 

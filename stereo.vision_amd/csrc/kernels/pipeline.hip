@@ -381,10 +381,9 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
     float* oX = bf.ox + (int64_t)frame * bf.ofs + g0;
     float* oY = bf.oy + (int64_t)frame * bf.ofs + g0;
     float* oZ = bf.oz + (int64_t)frame * bf.ofs + g0;
-    int32_t* oPx = bf.px + (int64_t)frame * bf.cap + g0;
-    int32_t* oPy = bf.py + (int64_t)frame * bf.cap + g0;
+    uint32_t* oPxy = bf.pxy + (int64_t)frame * bf.cap + g0;
     // Groups of 4 outputs at 16-byte-aligned slots: lane l of a wave stores the
-    // X, Y, Z, x, y of group m0 + l, so every store instruction covers 1 KiB
+    // X, Y, Z, (x, y) of group m0 + l, so every store instruction covers 1 KiB
     // contiguous of its plane.
     const uint32_t groups = (end + 3) >> 2;
     for (uint32_t m0 = tid & ~63u; m0 < groups; m0 += 256) {   // uniform per wave
@@ -423,8 +422,9 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
             __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + 4 * m));
             __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + 4 * m));
             __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + 4 * m));
-            __builtin_nontemporal_store((v4i){PX[0], PX[1], PX[2], PX[3]}, reinterpret_cast<v4i*>(oPx + 4 * m));
-            __builtin_nontemporal_store((v4i){PY[0], PY[1], PY[2], PY[3]}, reinterpret_cast<v4i*>(oPy + 4 * m));
+            __builtin_nontemporal_store((v4i){(int)pp_pack(PX[0], PY[0]), (int)pp_pack(PX[1], PY[1]),
+                                         (int)pp_pack(PX[2], PY[2]), (int)pp_pack(PX[3], PY[3])},
+                                        reinterpret_cast<v4i*>(oPxy + 4 * m));
         } else {                // the tile's first / last group
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -432,8 +432,7 @@ __device__ __forceinline__ void compact_tile(const PipeBuffers& bf, int frame, i
                 oX[4 * m + e] = X[e];
                 oY[4 * m + e] = Y[e];
                 oZ[4 * m + e] = Z[e];
-                oPx[4 * m + e] = PX[e];
-                oPy[4 * m + e] = PY[e];
+                oPxy[4 * m + e] = pp_pack(PX[e], PY[e]);
             }
         }
     }

@@ -20,8 +20,8 @@ namespace svx {
 typedef int v2i __attribute__((ext_vector_type(2)));
 typedef int v4i __attribute__((ext_vector_type(4)));
 
-// point i of frame f: x = px[(f cap + i) * ps], y = py[(f cap + i) * ps] (ps = 1: the pipeline's two planes;
-// ps = 2: interleaved (x, y) pairs); counts[frame * cstride + cidx] = points of the frame
+// point i of frame f: x = px[(f cap + i) * ps], y = py[(f cap + i) * ps] (ps = 2: interleaved (x, y) pairs); ps = 0:
+// px holds the batch's pp_pack words (x and y as int16 halves); counts[frame * cstride + cidx] = points of the frame
 __global__ __launch_bounds__(256) void raster_kernel(const int32_t* __restrict__ px, const int32_t* __restrict__ py,
                                                      int ps, const int64_t* __restrict__ counts, int cstride, int cidx,
                                                      int64_t cap, uint8_t* __restrict__ img, int H, int W, int Wu) {
@@ -30,7 +30,15 @@ __global__ __launch_bounds__(256) void raster_kernel(const int32_t* __restrict__
     const int64_t f0 = (int64_t)frame * cap;
     uint8_t* fi = img + (int64_t)frame * H * W;
     for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const int qx = px[(f0 + i) * ps], qy = py[(f0 + i) * ps];
+        int qx, qy;
+        if (ps == 0) {   // pp_pack words (a batch's planePoints)
+            const uint32_t w = (uint32_t)px[f0 + i];
+            qx = pp_x(w);
+            qy = pp_y(w);
+        } else {
+            qx = px[(f0 + i) * ps];
+            qy = py[(f0 + i) * ps];
+        }
         const int x = qx < 0 ? qx + Wu : qx, y = qy < 0 ? qy + H : qy;
         fi[(int64_t)y * W + x] = 255;
     }
@@ -164,7 +172,7 @@ struct RoadShared {
 // marked — generatePointsAsImage and the paint index the same [y][x] with the
 // same wrap, so the band in LDS is exactly the paint mask (3 B read + 3 B
 // written per pixel, 8 bytes a lane).
-__global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ px, const int32_t* __restrict__ py,
+__global__ __launch_bounds__(256) void road_kernel(const uint32_t* __restrict__ pxy,
                                                    const int64_t* __restrict__ counts, int64_t cap,
                                                    uint8_t* __restrict__ img, int H, int W, int Wu, int R,
                                                    uint64_t W_m40, int32_t* __restrict__ nzout,
@@ -177,27 +185,30 @@ __global__ __launch_bounds__(256) void road_kernel(const int32_t* __restrict__ p
     const int frame = blockIdx.x;
     int64_t n = counts[4 * (int64_t)frame + 2];
     n = n < 0 ? 0 : (n > cap ? cap : n);
-    const int32_t* fx = px + (int64_t)frame * cap;
-    const int32_t* fy = py + (int64_t)frame * cap;
+    const uint32_t* fxy = pxy + (int64_t)frame * cap;
     uint8_t* fimg = img + (int64_t)frame * H * W;
     uint32_t* fo = reinterpret_cast<uint32_t*>(nzout) + (int64_t)frame * cap;
     if (tid < 128) sh.wrap[tid] = 0;
     // this lane's kRoadPts consecutive points of the 256 * kRoadPts-point chunk at i0 (qy = -2: past the
-    // list): one 16-byte load per plane when the planes are 16-byte aligned (vec), 4-byte loads at the list's end
-    static_assert(kRoadPts == 4, "one int4 of x and one of y per lane");
+    // list): one 16-byte load of pp_pack words when the plane is 16-byte aligned (vec), 4-byte loads at the end
+    static_assert(kRoadPts == 4, "one uint4 of packed points per lane");
     const auto load = [&](int64_t i0, int (&qx)[kRoadPts], int (&qy)[kRoadPts]) {
         const int64_t i = i0 + kRoadPts * tid;
         if (vec && i + kRoadPts <= n) {
-            const int4 vx = *reinterpret_cast<const int4*>(fx + i);
-            const int4 vy = *reinterpret_cast<const int4*>(fy + i);
-            qx[0] = vx.x, qx[1] = vx.y, qx[2] = vx.z, qx[3] = vx.w;
-            qy[0] = vy.x, qy[1] = vy.y, qy[2] = vy.z, qy[3] = vy.w;
+            const uint4 v = *reinterpret_cast<const uint4*>(fxy + i);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int t = 0; t < kRoadPts; ++t) {
+                qx[t] = pp_x(w[t]);
+                qy[t] = pp_y(w[t]);
+            }
         } else {
 #pragma unroll
             for (int t = 0; t < kRoadPts; ++t) {
                 const bool ok = i + t < n;
-                qx[t] = ok ? fx[i + t] : 0;
-                qy[t] = ok ? fy[i + t] : -2;
+                const uint32_t w = ok ? fxy[i + t] : 0u;
+                qx[t] = ok ? pp_x(w) : 0;
+                qy[t] = ok ? pp_y(w) : -2;
             }
         }
     };
@@ -470,7 +481,7 @@ hipError_t launch_road_bits(const uint32_t* bits, int frames, int H, int W, int3
     return hipGetLastError();
 }
 
-hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* counts, int64_t cap, uint8_t* img,
+hipError_t launch_road(const uint32_t* pxy, const int64_t* counts, int64_t cap, uint8_t* img,
                        int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr,
                        uint8_t* paint, hipStream_t s) {
     if (frames <= 0) return hipSuccess;
@@ -485,8 +496,8 @@ hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* coun
     // vec: the point planes and the walk's output 16-byte aligned at every frame (cap % 4 == 0), so a lane takes
     // its 4 points with one load per plane and writes two walk outputs with one store
     if (H > 65536) return hipErrorInvalidValue;   // packed walk entries: y < 65536
-    const bool vec = cap % 4 == 0 && ((reinterpret_cast<uintptr_t>(px) | reinterpret_cast<uintptr_t>(py)) & 15u) == 0;
-    hipLaunchKernelGGL(road_kernel, dim3(frames), dim3(256), dyn, s, px, py, counts, cap, img, H, W, Wu, R, m40, nzout,
+    const bool vec = cap % 4 == 0 && (reinterpret_cast<uintptr_t>(pxy) & 15u) == 0;
+    hipLaunchKernelGGL(road_kernel, dim3(frames), dim3(256), dyn, s, pxy, counts, cap, img, H, W, Wu, R, m40, nzout,
                        nzcount, bgr, paint, vec);
     return hipGetLastError();
 }

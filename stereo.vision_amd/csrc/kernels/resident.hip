@@ -4,7 +4,7 @@
 // < point_thr (functions.py:300-323); hist = hue-bin counts over keep1
 // (functions.py:215-226); keep2 = keep1 & hist[bin] > hist_thr
 // (functions.py:228-230); the keep2 points in raster order as fp32 X, Y, Z +
-// int32 (x, y) back-projection (functions.py:201-209, stereovision.py:112).
+// the int32 (x, y) back-projection (functions.py:201-209, stereovision.py:112) as int16 halves of one word.
 //
 // keep1 is evaluated per grid point from the frame's plane (FramePlane: the
 // per-call plane, the frame's own RANSAC plane, or a plane broadcast into
@@ -548,7 +548,7 @@ __device__ __forceinline__ uint32_t rdesc(uint32_t d, uint32_t gy, uint32_t gx, 
 // only LDS.
 template <int STEP, int QP, bool LC>
 __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint32_t b, float* oX, float* oY,
-                                         float* oZ, int32_t* oPx, int32_t* oPy, const RParams& p) {
+                                         float* oZ, uint32_t* oPxy, const RParams& p) {
     constexpr uint32_t SM = stage_of<QP>() - 1;
     const uint32_t first = a & ~3u;
     const uint32_t groups = (b - first + 3) >> 2;
@@ -578,8 +578,9 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
             __builtin_nontemporal_store((v4f){X[0], X[1], X[2], X[3]}, reinterpret_cast<v4f*>(oX + g));
             __builtin_nontemporal_store((v4f){Y[0], Y[1], Y[2], Y[3]}, reinterpret_cast<v4f*>(oY + g));
             __builtin_nontemporal_store((v4f){Z[0], Z[1], Z[2], Z[3]}, reinterpret_cast<v4f*>(oZ + g));
-            __builtin_nontemporal_store((v4i){PX[0], PX[1], PX[2], PX[3]}, reinterpret_cast<v4i*>(oPx + g));
-            __builtin_nontemporal_store((v4i){PY[0], PY[1], PY[2], PY[3]}, reinterpret_cast<v4i*>(oPy + g));
+            __builtin_nontemporal_store((v4i){(int)pp_pack(PX[0], PY[0]), (int)pp_pack(PX[1], PY[1]),
+                                         (int)pp_pack(PX[2], PY[2]), (int)pp_pack(PX[3], PY[3])},
+                                        reinterpret_cast<v4i*>(oPxy + g));
         } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -587,8 +588,7 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
                 oX[g + e] = X[e];
                 oY[g + e] = Y[e];
                 oZ[g + e] = Z[e];
-                oPx[g + e] = PX[e];
-                oPy[g + e] = PY[e];
+                oPxy[g + e] = pp_pack(PX[e], PY[e]);
             }
         }
     }
@@ -650,7 +650,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
                                          const uint32_t* dirty, SH& sh, uint32_t* wstage,
                                          const uint8_t* fdisp, const uint8_t* fbgr, const RLean& L,
                                          const FramePlane* Lp, const PipeBuffers& bf, float* oX, float* oY,
-                                         float* oZ, int32_t* oPx, int32_t* oPy,
+                                         float* oZ, uint32_t* oPxy,
                                          uint32_t& running, uint32_t& flushed, bool next_run, const uint16_t* fkb,
                                          const RParams& p) {
     constexpr int QPL = RCfg<STEP, QP, LC>::QPL;
@@ -714,7 +714,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
                                 (uint32_t)((tot >> 32) & 0xFFFF) + (uint32_t)((tot >> 48) & 0xFFFF);
     if (tid < (int)(running - flushed)) sh.stage[(flushed + tid) & (stage_of<QP>() - 1)] = sh.red[tid];   // the tail
     if (T > (uint32_t)stage_of<QP>() - (running - flushed)) {   // uniform
-        p2_write<STEP, QP, LC>(sh.stage, flushed, running, oX, oY, oZ, oPx, oPy, p);
+        p2_write<STEP, QP, LC>(sh.stage, flushed, running, oX, oY, oZ, oPxy, p);
         flushed = running;
         // the scatter below wraps onto the slots just written out: every wave must have read them first
         // (without this barrier the other waves' scatter raced wave 0's read of the tail)
@@ -789,7 +789,7 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
     // chunk's dirty path may reuse sh.stage before its scatter restores them
     if (tid < (int)(running - upto)) sh.red[tid] = sh.stage[(upto + tid) & (stage_of<QP>() - 1)];
     if (upto > flushed) {
-        p2_write<STEP, QP, LC>(sh.stage, flushed, upto, oX, oY, oZ, oPx, oPy, p);
+        p2_write<STEP, QP, LC>(sh.stage, flushed, upto, oX, oY, oZ, oPxy, p);
         flushed = upto;
     }
 }
@@ -903,8 +903,7 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
     float* oX = bf.ox + (int64_t)frame * bf.ofs;
     float* oY = bf.oy + (int64_t)frame * bf.ofs;
     float* oZ = bf.oz + (int64_t)frame * bf.ofs;
-    int32_t* oPx = bf.px + (int64_t)frame * bf.cap;
-    int32_t* oPy = bf.py + (int64_t)frame * bf.cap;
+    uint32_t* oPxy = bf.pxy + (int64_t)frame * bf.cap;
     uint32_t running = 0, flushed = 0;
     const int n2 = (p.ablate & 256) ? 0 : p.nchunks;
     // a chunk in which pass 1 kept no point (its keep1 range is 0 in every wave;
@@ -935,7 +934,7 @@ __device__ __forceinline__ void frame_pass2(int frame, FusedShared<QP>& sh, cons
             continue;
         }
         p2_chunk<STEP, QP, LC, PF, RB>(r2, c, c + 1 < n2, sh.hist, sh.dirty, sh, wstage, fdisp, fbgr, L, Lp, bf, oX, oY,
-                                       oZ, oPx, oPy,
+                                       oZ, oPxy,
                                        running, flushed, c + 1 < n2 && run(c + 1), fkb, p);
         if constexpr (RB) {   // after the chunk's last barrier: its marks are in the ring
             if (c + 1 < n2) {

@@ -273,7 +273,7 @@ struct sv_batch {
                                      // and two streams on one queue run in order, so no stream is made unused
     std::vector<hipEvent_t> sync_ev; // pipeline hand-offs between A and B (timing disabled)
     DevBuf disp, bgr, X, Y, Z, xyz, ctrl, masks;
-    DevBuf ppx, ppy;            // the pipeline's int32 (x, y): two planes of frames x cap
+    DevBuf ppxy;                // the pipeline's planePoints: one pp_pack word (x, y as int16 halves) a point
     DevBuf oxb, oyb, ozb;       // pipeline X, Y, Z: three planes of frames x cap (default; SoA in xyz: A/B)
     bool out_planes = false;
     bool pipe_placed = false;   // the resident pipeline's outputs were placed (pipe_place)
@@ -359,8 +359,7 @@ static hipError_t ensure_points(sv_batch* b) {
     } else {
         e = b->xyz.ensure(3 * plane, false, 4);
     }
-    if (e == hipSuccess) e = b->ppx.ensure(plane, false, 4);
-    if (e == hipSuccess) e = b->ppy.ensure(plane, false, 4);
+    if (e == hipSuccess) e = b->ppxy.ensure(plane, false, 4);
     return e;
 }
 
@@ -376,8 +375,7 @@ static void point_planes(const sv_batch* b, PipeBuffers& bf) {
         bf.oz = bf.oy + b->cap;
         bf.ofs = 3 * (int64_t)b->cap;
     }
-    bf.px = b->ppx.as<int32_t>();
-    bf.py = b->ppy.as<int32_t>();
+    bf.pxy = b->ppxy.as<uint32_t>();
     bf.cap = (int64_t)b->cap;
 }
 
@@ -557,7 +555,7 @@ int sv_batch_destroy(sv_batch* b) {
     if (!b) return SV_OK;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
-    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppx, &b->ppy, &b->ctrl, &b->masks,
+    for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppxy, &b->ctrl, &b->masks,
                       &b->carmask, &b->road, &b->rmap, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtab, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
                       &b->glut, &b->ghist, &b->sgflags, &b->prev0buf, &b->rdbuf, &b->rbits, &b->roff})
@@ -584,7 +582,7 @@ int sv_batch_info(const sv_batch* b, int64_t* o) {
     o[1] = b->kp.Wg;
     o[2] = b->kp.pitch;
     o[3] = b->Ng;
-    o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->oxb.bytes * 3 + b->ppx.bytes * 2 +
+    o[4] = (int64_t)(b->disp.bytes + b->bgr.bytes + b->X.bytes * 3 + b->xyz.bytes + b->oxb.bytes * 3 + b->ppxy.bytes +
                      b->ctrl.bytes);
     o[5] = b->frames;
     o[6] = b->H;
@@ -743,7 +741,7 @@ RansacRes ransac_res(sv_batch* b) {
 }  // namespace
 
 // planes: device planes, frame f uses planes[f * plane_stride] (NULL: the host plane)
-// The pipeline's five output planes, placed like K1's (k1_place): where they land moves the resident pipeline
+// The pipeline's four output planes (X, Y, Z, planePoints), placed like K1's (k1_place): where they land moves the resident pipeline
 // by up to 8 % (5.85-5.96 ms, one placement in four 6.36-6.46 ms). On a large batch's first resident call,
 // up to two more sets are allocated beside the current one (at most half the free memory), one call is timed
 // on each (all held), and the fastest set is kept. SVX_PIPE_TRIES=1 turns it off.
@@ -751,13 +749,13 @@ static hipError_t pipe_place(sv_batch* b, const KParams& p, PipeBuffers bf, hipS
     int tries = 3;
     if (const char* e = svx_knob("SVX_PIPE_TRIES")) tries = std::max(1, std::atoi(e));
     const size_t plane = sizeof(float) * b->cap * (size_t)b->frames;
-    const size_t set_b = 5 * (plane + plane / 4);
+    const size_t set_b = 4 * (plane + plane / 4);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     tries = (int)std::min<size_t>((size_t)tries, 1 + free_b / 2 / set_b);
     if (tries <= 1) return hipSuccess;
-    std::vector<std::array<DevBuf, 5>> sets((size_t)tries);
-    sets[0] = {b->oxb, b->oyb, b->ozb, b->ppx, b->ppy};
+    std::vector<std::array<DevBuf, 4>> sets((size_t)tries);
+    sets[0] = {b->oxb, b->oyb, b->ozb, b->ppxy};
     std::vector<float> set_ms((size_t)tries, 0.f);
     int placed = tries;   // sets allocated
     hipError_t e = hipSuccess;
@@ -767,10 +765,10 @@ static hipError_t pipe_place(sv_batch* b, const KParams& p, PipeBuffers bf, hipS
     for (int pass = 0; pass < 2 && e == hipSuccess; ++pass) {
         for (int t = 0; t < placed && e == hipSuccess; ++t) {
             auto& c = sets[(size_t)t];
-            for (int k = 0; k < 5 && e == hipSuccess && t > 0 && pass == 0; ++k) e = c[k].ensure(plane, false, 4);
+            for (int k = 0; k < 4 && e == hipSuccess && t > 0 && pass == 0; ++k) e = c[k].ensure(plane, false, 4);
             if (e != hipSuccess) {   // out of memory: place among the sets held so far
                 (void)hipGetLastError();
-                for (int k = 0; k < 5; ++k)
+                for (int k = 0; k < 4; ++k)
                     if (c[k].p) {
                         (void)hipFree(c[k].p);
                         c[k] = DevBuf();
@@ -783,8 +781,7 @@ static hipError_t pipe_place(sv_batch* b, const KParams& p, PipeBuffers bf, hipS
             bf.oy = c[1].as<float>();
             bf.oz = c[2].as<float>();
             bf.ofs = (int64_t)b->cap;
-            bf.px = c[3].as<int32_t>();
-            bf.py = c[4].as<int32_t>();
+            bf.pxy = c[3].as<uint32_t>();
             float ms = 0.f;
             for (int rep = pass == 0 ? 0 : 1; rep < 2 && e == hipSuccess; ++rep) {   // the last call is timed
                 e = hipEventRecord(b->ev[0], s);
@@ -805,10 +802,10 @@ static hipError_t pipe_place(sv_batch* b, const KParams& p, PipeBuffers bf, hipS
     for (int t = 0; t < b->place_n[1]; ++t) b->place_ms[1][t] = set_ms[(size_t)t];
     b->place_kept[1] = best;
     for (int t = 0; t < (int)sets.size(); ++t)
-        for (int k = 0; k < 5; ++k) {
+        for (int k = 0; k < 4; ++k) {
             DevBuf& x = sets[(size_t)t][k];
             if (t == best) {
-                DevBuf* dst[5] = {&b->oxb, &b->oyb, &b->ozb, &b->ppx, &b->ppy};
+                DevBuf* dst[4] = {&b->oxb, &b->oyb, &b->ozb, &b->ppxy};
                 *dst[k] = x;
             } else if (x.p && (t != 0 || best != 0)) {
                 (void)hipFree(x.p);
@@ -1043,7 +1040,7 @@ int sv_batch_read_hist(sv_batch* b, int frame, uint32_t* hist) {
 }
 
 int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64_t cap, int64_t* n) {
-    if (!b || !n || frame < 0 || frame >= b->frames || !b->ppx.p) return fail(SV_E_ARG, "bad args");
+    if (!b || !n || frame < 0 || frame >= b->frames || !b->ppxy.p) return fail(SV_E_ARG, "bad args");
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
     int64_t c[4];
@@ -1061,13 +1058,12 @@ int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64
         for (size_t i = 0; i < np; ++i)
             for (int k = 0; k < 3; ++k) xyz[3 * i + k] = soa[k * np + i];
     }
-    if (pts && np) {   // device layout: x and y planes; the caller gets (x, y) pairs
-        std::vector<int32_t> pl(2 * np);
-        HIP_TRY(hipMemcpy(pl.data(), b->ppx.as<int32_t>() + cap_f * frame, 4 * np, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(pl.data() + np, b->ppy.as<int32_t>() + cap_f * frame, 4 * np, hipMemcpyDeviceToHost));
+    if (pts && np) {   // device layout: one pp_pack word a point; the caller gets the int32 (x, y) pairs
+        std::vector<uint32_t> pl(np);
+        HIP_TRY(hipMemcpy(pl.data(), b->ppxy.as<uint32_t>() + cap_f * frame, 4 * np, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < np; ++i) {
-            pts[2 * i] = pl[i];
-            pts[2 * i + 1] = pl[np + i];
+            pts[2 * i] = pp_x(pl[i]);
+            pts[2 * i + 1] = pp_y(pl[i]);
         }
     }
     return SV_OK;
@@ -1076,7 +1072,7 @@ int sv_batch_read_points(sv_batch* b, int frame, float* xyz, int32_t* pts, int64
 int sv_batch_digest(sv_batch* b, const sv_camera* cam, int which, uint64_t* out) {
     if (!b || !cam || !out || which < 0 || which > 1) return fail(SV_E_ARG, "sv_batch_digest: bad args");
     if (which == 0 && !b->Z.p) return fail(SV_E_STATE, "sv_batch_digest: nothing projected");
-    if (which == 1 && !b->ppx.p) return fail(SV_E_STATE, "sv_batch_digest: no pipeline outputs");
+    if (which == 1 && !b->ppxy.p) return fail(SV_E_STATE, "sv_batch_digest: no pipeline outputs");
     if ((b->kp.frame_px % 4) != 0) return fail(SV_E_ARG, "sv_batch_digest: H * W must be a multiple of 4");
     HIP_TRY(hipSetDevice(b->device));
     KParams p = make_params(b->H, b->W, b->step, *cam, b->Wu);
@@ -1333,7 +1329,7 @@ int sv_nonzero_points(const uint8_t* img, int H, int W, int32_t* out, int64_t ca
 
 int sv_batch_road_raster(sv_batch* b, int sync) {
     if (!b) return fail(SV_E_ARG, "null batch");
-    if (!b->ppx.p) return fail(SV_E_STATE, "no pipeline points (create the batch with points and run the pipeline)");
+    if (!b->ppxy.p) return fail(SV_E_STATE, "no pipeline points (create the batch with points and run the pipeline)");
     HIP_TRY(hipSetDevice(b->device));
     const size_t px = (size_t)b->H * b->W;
     HIP_TRY(b->road.ensure(px * b->frames));
@@ -1355,13 +1351,13 @@ int sv_batch_road_raster(sv_batch* b, int sync) {
                                      (int64_t)b->cap, b->road.as<uint8_t>(), b->nz.as<int32_t>(),
                                      b->nzcount.as<int64_t>(), b->bgr.as<uint8_t>(), paint, b->stream));
         } else {
-            HIP_TRY(launch_road(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), b->counts, (int64_t)b->cap,
+            HIP_TRY(launch_road(b->ppxy.as<uint32_t>(), b->counts, (int64_t)b->cap,
                                 b->road.as<uint8_t>(), b->frames, b->H, b->W, b->Wu, b->nz.as<int32_t>(),
                                 b->nzcount.as<int64_t>(), b->bgr.as<uint8_t>(), paint, b->stream));
         }
         b->rmap_fresh = paint != nullptr;
     } else {
-        HIP_TRY(launch_raster(b->ppx.as<int32_t>(), b->ppy.as<int32_t>(), 1, b->counts, 4, 2, (int64_t)b->cap,
+        HIP_TRY(launch_raster(b->ppxy.as<int32_t>(), nullptr, 0, b->counts, 4, 2, (int64_t)b->cap,
                               b->road.as<uint8_t>(), b->frames, b->H, b->W, b->Wu, b->stream));
     }
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));

@@ -284,6 +284,11 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 // The wave's index in its workgroup, as a value the compiler knows is wave-uniform: addresses built from it stay
 // in SGPRs, so a per-lane access is one scalar base + the lane's VGPR offset (no 64-bit VALU address arithmetic).
 __device__ __forceinline__ int wave_uniform_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+// A planePoints entry (functions.py:201-209 + stereovision.py:112's int32 cast) as one word: x and y as int16
+// halves (-1 <= x < W, -1 <= y < H, both < 32768), widened back to the reference's int32 pair on read-back.
+__host__ __device__ __forceinline__ uint32_t pp_pack(int x, int y) { return (uint32_t)(uint16_t)x | ((uint32_t)(uint16_t)y << 16); }
+__host__ __device__ __forceinline__ int pp_x(uint32_t w) { return (int)(int16_t)(uint16_t)(w & 0xFFFFu); }
+__host__ __device__ __forceinline__ int pp_y(uint32_t w) { return (int)(int16_t)(uint16_t)(w >> 16); }
 
 // Inclusive wave64 scan of an operation with identity 0 (add, unsigned max, ...)
 // in six DPP steps: row_shr 1/2/4/8 (Hillis-Steele inside each 16-lane row),

@@ -45,8 +45,8 @@ struct PipeBuffers {
     float* oy;           //   (ofs = cap), or SoA per frame (ofs = 3 cap, oy = ox + cap, oz = ox + 2 cap)
     float* oz;
     int64_t ofs;
-    int32_t* px;         // the int32 back-projection (planePoints): x and y as two planes of frames x cap
-    int32_t* py;         //   (frame f's at f * cap)
+    uint32_t* pxy;       // the back-projection (planePoints): one word a point, pp_pack(x, y), frames x cap
+                         //   (frame f's at f * cap; widened to int32 pairs on read-back)
     const uint32_t* dxbits;
     const uint32_t* dybits;
     // the same bits transposed: word j of coordinate c holds d = 32 j .. 32 j + 31 (bit d mod 32), as
@@ -100,14 +100,15 @@ hipError_t launch_mask(const uint8_t* disp, uint8_t* out, const uint8_t* mask_ff
 // Road raster (points -> 255 on a zeroed image) and the raster-order non-zero walk.
 // counts: NULL -> cap points per frame, else counts[frame * cstride + cidx].
 // images of H rows at stride W; Wu = the image width (numpy's negative-index wrap). Point i of frame f:
-// (px[(f cap + i) ps], py[(f cap + i) ps]): ps = 1 for two planes, 2 for interleaved (x, y) pairs.
+// (px[(f cap + i) ps], py[(f cap + i) ps]): ps = 2 for interleaved (x, y) pairs; ps = 0: px holds pp_pack words
+// (a batch's planePoints), py unused.
 hipError_t launch_raster(const int32_t* px, const int32_t* py, int ps, const int64_t* counts, int cstride, int cidx,
                          int64_t cap, uint8_t* img, int frames, int H, int W, int Wu, hipStream_t s);
 // The batch's road images and walks in one pass (road_kernel): the pipeline's points (two planes, frame f's
 // counts[4f + 2] points at f * cap, in the pipeline's raster order) -> img (frames x H x W, W % 8 == 0) and the
 // raster-order [j, i] of every non-zero pixel (frames x cap pairs) + nzcount[frame]; with paint != nullptr also
 // imageRoadMap (stereovision.py:131-133): bgr (frames x H x W x 3) with [0, 255, 0] at the marked pixels -> paint.
-hipError_t launch_road(const int32_t* px, const int32_t* py, const int64_t* counts, int64_t cap, uint8_t* img,
+hipError_t launch_road(const uint32_t* pxy, const int64_t* counts, int64_t cap, uint8_t* img,
                        int frames, int H, int W, int Wu, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr,
                        uint8_t* paint, hipStream_t s);
 // img frames x px (px % 4 == 0, rows of W <= 4096 pixels)
