@@ -2444,8 +2444,13 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     if (L->pending >= 0) {
         if (int rc = loop_enqueue_tail(L, L->pending, (uint64_t)seq + 1)) return rc;
     }
-    // RANSAC evaluation, after the previous batch's road pass
-    if (seq > 0 && ps != s) HIP_TRY(hipStreamWaitEvent(st, L->t1[ps][kLsRoad], 0));
+    // RANSAC evaluation, after the previous batch's road pass (SVX_LOOP_EVAL_AFTER=pipeline, diagnostic build:
+    // after its pipeline, beside the road pass)
+    {
+        const char* ea = svx_knob("SVX_LOOP_EVAL_AFTER");
+        const int dep = ea && ea[0] == 'p' ? kLsPipeline : kLsRoad;
+        if (seq > 0 && ps != s) HIP_TRY(hipStreamWaitEvent(st, L->t1[ps][dep], 0));
+    }
     HIP_TRY(begin(kLsEval));
     if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k, st, 2)) return rc;
     HIP_TRY(end(kLsEval));
