@@ -306,7 +306,11 @@ __device__ __forceinline__ uint32_t bt_cost_pair(const BtFeat& l, const BtFeat& 
     return __builtin_bit_cast(uint32_t, ch0 + (ch1 >> (u16x2){2, 2}));
 }
 
-template <int SW2C>
+// ABL (diagnostic build only, results invalid): the same stores with no arithmetic, to find what bounds the
+// kernel — 1 the staging and then each wave's quarter of the row written with constants, 2 the staging and then
+// the four waves' stores interleaved by column (the workgroup writes 1 KB contiguous a step), 3 the stores of 1
+// without the staging
+template <int SW2C, int ABL = 0>
 __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint8_t* __restrict__ left,
                                                                const uint8_t* __restrict__ right,
                                                                uint32_t* __restrict__ hvol, int frames) {
@@ -315,6 +319,14 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
     const int W = k.W, H = k.H;
     const int f = blockIdx.x / H, y = blockIdx.x - f * H;
     if (f >= frames) return;
+    if constexpr (ABL != 0) {
+        if (ABL == 3) {
+            const int n = k.width1, seg = (n + 3) / 4, lane = lane_id(), wave = wave_uniform_id();
+            uint32_t* out = hvol + ((size_t)f * H + y) * n * 64;
+            for (int xi = wave * seg; xi < min(n, wave * seg + seg); ++xi) (out + (size_t)xi * 64)[(uint32_t)lane] = lane;
+            return;
+        }
+    }
     uint2* featA = reinterpret_cast<uint2*>(smem);             // [img][W] (value, min)
     uint32_t* featB = reinterpret_cast<uint32_t*>(featA + 2 * W);   // [img][W] max
     uint8_t* raw = reinterpret_cast<uint8_t*>(smem);           // [img][row above, row, row below][W], dead before
@@ -389,6 +401,15 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
     const int n = k.width1;
     const int seg = (n + 3) / 4;
     const int xs = wave * seg, xe = min(n, xs + seg);
+    if constexpr (ABL == 1 || ABL == 2) {
+        uint32_t* out = hvol + ((size_t)f * H + y) * n * 64;
+        const uint32_t v = featB[lane];   // keeps the staging live
+        if (ABL == 1)
+            for (int xi = xs; xi < xe; ++xi) (out + (size_t)xi * 64)[(uint32_t)lane] = v;
+        else
+            for (int xi = wave; xi < n; xi += 4) (out + (size_t)xi * 64)[(uint32_t)lane] = v;
+        return;
+    }
     if (xs >= xe) return;
     const int d0 = 2 * lane;
     const auto feat = [&](int i) -> BtFeat {
@@ -421,27 +442,42 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
     int vzero;
     __asm__("v_mov_b32 %0, 0" : "=v"(vzero));
     int xv = jn + kSgD + vzero;
-    for (int x0 = xs; x0 < xe; x0 += RS) {
+    const auto step = [&]() {   // adds column jn + 1 (jn < n - 1)
+        ++jn;
+        const int x = ++xv;   // jn + kSgD
+        const BtFeat rn = feat(W + x);   // lane 0's A_jn
+        BtFeat anew;                     // wave_shr:1 of A_{jn - 2}
+        anew.v = __builtin_amdgcn_update_dpp((int)rn.v, (int)aprev.v, 0x138, 0xf, 0xf, false);
+        anew.lo = __builtin_amdgcn_update_dpp((int)rn.lo, (int)aprev.lo, 0x138, 0xf, 0xf, false);
+        anew.hi = __builtin_amdgcn_update_dpp((int)rn.hi, (int)aprev.hi, 0x138, 0xf, 0xf, false);
+        vlast = cost(feat(x), anew, acur);
+        aprev = acur;
+        acur = anew;
+    };
+    int x0 = xs;
+    // whole blocks of RS columns that each store and each add a column: no condition in the unrolled block, so
+    // the ring index is a compile-time register and the next columns' LDS reads can be issued early
+    for (; x0 + RS <= xe && jn + RS <= n - 1; x0 += RS) {
+#pragma unroll
+        for (int u = 0; u < RS; ++u) {
+            (out + (size_t)(x0 + u) * 64)[(uint32_t)lane] = sum;
+            step();
+            sum = (sum + vlast) - ring[u];
+            ring[u] = vlast;
+        }
+    }
+    // the rest (the row's last columns), the ring's phase unchanged
+    for (; x0 < xe; x0 += RS) {
 #pragma unroll
         for (int u = 0; u < RS; ++u) {
             const int xi = x0 + u;
-            if (xi >= xe) break;
-            (out + (size_t)xi * 64)[(uint32_t)lane] = sum;   // (non-temporal stores: no faster)
-            // step xi adds column xi + 1 + SW2 (clamped: past the last column it is the last column again)
-            if (jn < n - 1) {
-                ++jn;
-                const int x = ++xv;   // jn + kSgD
-                const BtFeat rn = feat(W + x);   // lane 0's A_jn
-                BtFeat anew;                     // wave_shr:1 of A_{jn - 2}
-                anew.v = __builtin_amdgcn_update_dpp((int)rn.v, (int)aprev.v, 0x138, 0xf, 0xf, false);
-                anew.lo = __builtin_amdgcn_update_dpp((int)rn.lo, (int)aprev.lo, 0x138, 0xf, 0xf, false);
-                anew.hi = __builtin_amdgcn_update_dpp((int)rn.hi, (int)aprev.hi, 0x138, 0xf, 0xf, false);
-                vlast = cost(feat(x), anew, acur);
-                aprev = acur;
-                acur = anew;
+            if (xi < xe) {
+                (out + (size_t)xi * 64)[(uint32_t)lane] = sum;   // (non-temporal stores: no faster)
+                // step xi adds column xi + 1 + SW2 (clamped: past the last column it is the last column again)
+                if (jn < n - 1) step();
+                sum = (sum + vlast) - ring[u];
+                ring[u] = vlast;
             }
-            sum = (sum + vlast) - ring[u];
-            ring[u] = vlast;
         }
     }
 }
@@ -564,35 +600,40 @@ __global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const 
     uint32_t add[RS];   // the rows steps y0 .. y0 + RS - 1 add (y + SH2, clamped)
 #pragma unroll
     for (int u = 0; u < RS; ++u) add[u] = hrow(u + SH2C);
-    for (int y0 = 0; y0 < H; y0 += RS) {
+    const auto vstep = [&](int u, int y) {
+        if (y > 0 && upd_col && y + SH2C < H) {
+            c0 += lo16(add[u]) - lo16(drop[u]);
+            c1 += hi16(add[u]) - hi16(drop[u]);
+        }
+        drop[u] = add[u];   // step y + RS drops row y + SH2
+        const int cw0 = (int)(int16_t)c0, cw1 = (int)(int16_t)c1;
+        const uint32_t cw = pack16(cw0, cw1);
+        bst32(cw, rcv, lane * 4, (uint32_t)y * rs32 * 4);
+        if constexpr (DQ) {
+            uint32_t q;
+            pk_step(cw, st, k.P1, k.P2, q);
+            bst8(q_byte_pk(q), rq2, lane, (uint32_t)y * rs32);
+        } else {
+            int L0, L1;
+            path_step(cw0, cw1, st, k.P1, k.P2, L0, L1);
+            (l2vol + base + (size_t)y * rs)[lane] = pack16(L0, L1);
+        }
+    };
+    // whole blocks (no exit inside the unrolled block, so both rings stay compile-time registers), the next
+    // block's rows in flight; then the last, partial block
+    int y0 = 0;
+    for (; y0 + RS <= H; y0 += RS) {
         uint32_t nadd[RS];
 #pragma unroll
         for (int u = 0; u < RS; ++u) nadd[u] = hrow(y0 + RS + u + SH2C);
 #pragma unroll
-        for (int u = 0; u < RS; ++u) {
-            const int y = y0 + u;
-            if (y >= H) break;
-            if (y > 0 && upd_col && y + SH2C < H) {
-                c0 += lo16(add[u]) - lo16(drop[u]);
-                c1 += hi16(add[u]) - hi16(drop[u]);
-            }
-            drop[u] = add[u];   // step y + RS drops row y + SH2
-            const int cw0 = (int)(int16_t)c0, cw1 = (int)(int16_t)c1;
-            const uint32_t cw = pack16(cw0, cw1);
-            bst32(cw, rcv, lane * 4, (uint32_t)y * rs32 * 4);
-            if constexpr (DQ) {
-                uint32_t q;
-                pk_step(cw, st, k.P1, k.P2, q);
-                bst8(q_byte_pk(q), rq2, lane, (uint32_t)y * rs32);
-            } else {
-                int L0, L1;
-                path_step(cw0, cw1, st, k.P1, k.P2, L0, L1);
-                (l2vol + base + (size_t)y * rs)[lane] = pack16(L0, L1);
-            }
-        }
+        for (int u = 0; u < RS; ++u) vstep(u, y0 + u);
 #pragma unroll
         for (int u = 0; u < RS; ++u) add[u] = nadd[u];
     }
+#pragma unroll
+    for (int u = 0; u < RS; ++u)
+        if (y0 + u < H) vstep(u, y0 + u);
     if (__any(st.ovf()) && lane == 0) atomicOr(flags + f, 1u);
 }
 
@@ -1247,9 +1288,27 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
     // (the register-ring walk for the reference's block 21: features (24 W bytes, the staged rows (6 W) under
     // them) + byte values (4 W); SVX_SGBM_HRING=0: the generic kernel)
     const char* hr = svx_knob("SVX_SGBM_HRING");
+#ifdef SVX_DIAG
+    const char* ha = svx_knob("SVX_SGBM_HSUM_ABLATE");
+    const int habl = ha && *ha ? std::atoi(ha) : 0;
+#else
+    constexpr int habl = 0;
+#endif
     if (k.SW2 == 10 && !(hr && hr[0] == '0')) {
-        hipLaunchKernelGGL(sgbm_hsum_ring_kernel<10>, dim3(frames * H), dim3(256), 28 * (size_t)k.W, st, k, left,
-                           right, s.hl1, frames);
+        if (habl == 0)
+            hipLaunchKernelGGL(sgbm_hsum_ring_kernel<10>, dim3(frames * H), dim3(256), 28 * (size_t)k.W, st, k, left,
+                               right, s.hl1, frames);
+#ifdef SVX_DIAG
+        else if (habl == 1)
+            hipLaunchKernelGGL((sgbm_hsum_ring_kernel<10, 1>), dim3(frames * H), dim3(256), 28 * (size_t)k.W, st, k,
+                               left, right, s.hl1, frames);
+        else if (habl == 2)
+            hipLaunchKernelGGL((sgbm_hsum_ring_kernel<10, 2>), dim3(frames * H), dim3(256), 28 * (size_t)k.W, st, k,
+                               left, right, s.hl1, frames);
+        else
+            hipLaunchKernelGGL((sgbm_hsum_ring_kernel<10, 3>), dim3(frames * H), dim3(256), 28 * (size_t)k.W, st, k,
+                               left, right, s.hl1, frames);
+#endif
     } else {
         const size_t lds1 = sizeof(uint32_t) * (5 * (size_t)k.W + 4 * (2 * k.SW2 + 1) * 64);
         hipLaunchKernelGGL(sgbm_hsum_kernel, dim3(frames * H), dim3(256), lds1, st, k, left, right, s.hl1, frames);
