@@ -458,9 +458,10 @@ __global__ __launch_bounds__(256) void sgbm_hsum_ring_kernel(SgbmK k, const uint
     // whole blocks of RS columns that each store and each add a column: no condition in the unrolled block, so
     // the ring index is a compile-time register and the next columns' LDS reads can be issued early
     for (; x0 + RS <= xe && jn + RS <= n - 1; x0 += RS) {
+        uint32_t* ob = out + (size_t)x0 * 64 + lane;   // the block's first cell: immediate offsets per step
 #pragma unroll
         for (int u = 0; u < RS; ++u) {
-            (out + (size_t)(x0 + u) * 64)[(uint32_t)lane] = sum;
+            ob[u * 64] = sum;
             step();
             sum = (sum + vlast) - ring[u];
             ring[u] = vlast;
