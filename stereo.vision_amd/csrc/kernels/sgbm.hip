@@ -886,18 +886,18 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
                 else
                     path_commit(sb, L0, L1, lm, wm);
                 const int minS = (kmin >> 7) - 32768, best = kmin & 127;
+                // a flag rather than `continue`: an exit from the unrolled step makes the compiler dispatch
+                // each step's end through a state register (several scalar instructions and branches a step)
+                // every S saturated: OpenCV's strict "<" never fires, bestDisp stays -1 and the pixel gets
+                // (-1) * 16 = INVALID; disp2 is not touched (its cost test is strict too)
+                bool write = minS != kMaxCost;
                 if (k.uniq > 0) {
                     const bool bad = (S0 * (100 - k.uniq) < minS * 100 && abs(best - d0) > 1) ||
                                      (S1 * (100 - k.uniq) < minS * 100 && abs(best - d0 - 1) > 1);
-                    if (__any(bad)) continue;
-                }
-                if (minS == kMaxCost) {
-                    // every S saturated: OpenCV's strict "<" never fires, bestDisp stays -1 and the
-                    // pixel gets (-1) * 16 = INVALID; disp2 is not touched (its cost test is strict too)
-                    continue;
+                    if (__any(bad)) write = false;
                 }
                 int num = 0, dv = 1;   // dd = best * 16 + num / dv (C division)
-                if (best > 0 && best < kSgD - 1) {
+                if (write && best > 0 && best < kSgD - 1) {
                     const uint32_t spk = pack16(S0, S1);
                     const uint32_t wm = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best - 1) >> 1);
                     const uint32_t wp = (uint32_t)__builtin_amdgcn_readlane((int)spk, (best + 1) >> 1);
@@ -907,7 +907,7 @@ __global__ __launch_bounds__(256) void sgbm_row_kernel(SgbmK k, const uint32_t* 
                     num = (Sm - Sp) * kSgScale + den;
                     dv = den * 2;
                 }
-                if (lane == (uint32_t)u) {   // one v_cndmask each: the lane masks are loop invariants
+                if (write && lane == (uint32_t)u) {   // one v_cndmask each: the lane masks are loop invariants
                     gkey = kmin;
                     gnum = num;
                     gdv = dv;

@@ -1,12 +1,12 @@
 #!/bin/bash
 # Row-walk probe: per-kernel times of the SGBM stage under two libraries (the product and an A/B build
 # compiled with -DSVX_ROW_ABLATE=1/2/3: the walk's loads and stores without pass A's / pass B's / both passes'
-# path steps; results invalid).
+# path steps; results invalid). VARIANTS="prod x y" compares tools/_ab/libsvx_x.so ... instead.
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
 for pass in 1 2; do
-  for v in prod abl1 abl2 abl3; do
-    if [ $v = prod ]; then L=$R/stereo.vision_amd/svx/_lib/libsvx.so; else L=$R/tools/_ab/libsvx_row_$v.so; fi
+  for v in ${VARIANTS:-prod abl1 abl2 abl3}; do
+    if [ $v = prod ]; then L=$R/stereo.vision_amd/svx/_lib/libsvx.so; else L=$R/tools/_ab/libsvx_$v.so; fi
     rm -rf "$R/gpurun_out/row_${v}_$pass"
     SVX_LIB=$L timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/row_${v}_$pass" -- python3 "$R/tools/prof.py" workload --what sgbm --frames 128 --reps 3 > "$R/gpurun_out/row_${v}_$pass.log" 2>&1 || { tail -20 "$R/gpurun_out/row_${v}_$pass.log"; exit 1; }
     python3 - "$R/gpurun_out/row_${v}_$pass" "$v" <<'PY'
