@@ -560,6 +560,9 @@ __global__ __launch_bounds__(256) void sgbm_vertical_kernel(SgbmK k, const uint3
 // read once: the row a step drops (max(y - SH2 - 1, 0)) is the row added RS = 2 SH2 + 1 steps before it, or
 // one of rows 0 .. SH2 read for the first window, so the walk keeps the next RS drops in registers (a ring
 // indexed by the unrolled step) and loads only the added rows, the next block's in flight.
+#ifndef SVX_VRING_ABLATE
+#define SVX_VRING_ABLATE 0
+#endif
 template <int SH2C, bool DQ>
 __global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const uint32_t* __restrict__ hvol,
                                                                    uint32_t* __restrict__ cvol,
@@ -611,9 +614,13 @@ __global__ __launch_bounds__(256) void sgbm_vertical_ring_kernel(SgbmK k, const 
         const uint32_t cw = pack16(cw0, cw1);
         bst32(cw, rcv, lane * 4, (uint32_t)y * rs32 * 4);
         if constexpr (DQ) {
+#if SVX_VRING_ABLATE   // A/B builds only (results invalid): the loads and stores without the path step
+            bst8(cw, rq2, lane, (uint32_t)y * rs32);
+#else
             uint32_t q;
             pk_step(cw, st, k.P1, k.P2, q);
             bst8(q_byte_pk(q), rq2, lane, (uint32_t)y * rs32);
+#endif
         } else {
             int L0, L1;
             path_step(cw0, cw1, st, k.P1, k.P2, L0, L1);
