@@ -1014,10 +1014,10 @@ __device__ __forceinline__ int med3_i(int a, int b, int c) { return max(min(a, b
 __global__ __launch_bounds__(256) void sgbm_median3_kernel(int H, int W, int64_t frame_px,
                                                              const int16_t* __restrict__ raw,
                                                              int16_t* __restrict__ out, int frames) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t f = i / frame_px;
-    if (f >= frames) return;
-    const int p = (int)(i - f * frame_px);
+    const int64_t f = blockIdx.y;   // grid (pixels of a frame, frames): no 64-bit division per pixel
+    const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (f >= frames || p >= frame_px) return;
+    const int64_t i = f * frame_px + p;
     const int y = p / W, x = p - y * W;
     const int16_t* d = raw + f * frame_px;
     const int16_t* r0 = d + (size_t)max(y - 1, 0) * W;
@@ -1079,10 +1079,9 @@ __global__ __launch_bounds__(256) void sgbm_cc_rows_kernel(SgbmK k, const int16_
 // are in the same runs as p / q and linked themselves (that union covered it).
 __global__ __launch_bounds__(256) void sgbm_cc_union_kernel(SgbmK k, const int16_t* __restrict__ d16,
                                                               int32_t* __restrict__ parent, int frames) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t f = i / k.frame_px;
-    if (f >= frames) return;
-    const int p = (int)(i - f * k.frame_px);
+    const int64_t f = blockIdx.y;   // grid (pixels of a frame, frames): no 64-bit division per pixel
+    const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (f >= frames || p >= k.frame_px) return;
     const int y = p / k.W, x = p - y * k.W;
     if (y + 1 >= k.H) return;
     const int16_t* d = d16 + f * k.frame_px;
@@ -1399,20 +1398,21 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
         SVX_SGBM_WALKS(8, false);
     }
 #undef SVX_SGBM_WALKS
-    // StereoSGBM::compute's medianBlur(disp, disp, 3): raw -> d16
-    const int64_t n = (int64_t)frames * k.frame_px;
-    hipLaunchKernelGGL(sgbm_median3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, k.H, k.W,
-                       k.frame_px, s.raw, s.d16, frames);
+    // StereoSGBM::compute's medianBlur(disp, disp, 3): raw -> d16 (grid: a frame's pixels x frames)
+    if (frames > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sgbm_median3_kernel, dim3((unsigned)((k.frame_px + 255) / 256), (unsigned)frames), dim3(256), 0,
+                       st, k.H, k.W, k.frame_px, s.raw, s.d16, frames);
     return hipGetLastError();
 }
 
 hipError_t launch_speckle_scale(const SgbmK& k, int frames, const SgbmScratch& s, uint8_t* out, int16_t* filt,
                                 hipStream_t st) {
     const int64_t n = (int64_t)frames * k.frame_px;
-    const unsigned g = (unsigned)((n + 255) / 256);
+    if (frames > 65535) return hipErrorInvalidValue;   // the pixel kernels' grid: a frame's pixels x frames
     const unsigned rows = (unsigned)((frames * k.H + 3) / 4);   // one wave per row
     hipLaunchKernelGGL(sgbm_cc_rows_kernel, dim3(rows), dim3(256), 0, st, k, s.d16, s.parent, frames);
-    hipLaunchKernelGGL(sgbm_cc_union_kernel, dim3(g), dim3(256), 0, st, k, s.d16, s.parent, frames);
+    hipLaunchKernelGGL(sgbm_cc_union_kernel, dim3((unsigned)((k.frame_px + 255) / 256), (unsigned)frames), dim3(256), 0,
+                       st, k, s.d16, s.parent, frames);
     hipError_t e = hipMemsetAsync(s.size, 0, sizeof(int32_t) * n, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(sgbm_cc_count_kernel, dim3(rows), dim3(256), 0, st, k, s.d16, s.parent, s.size, frames);

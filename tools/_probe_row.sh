@@ -14,7 +14,7 @@ import csv, glob, sys
 for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         n = r["Name"]
-        if "sgbm_row" in n or "sgbm_diag" in n or "sgbm_vertical" in n or "sgbm_hsum" in n:
+        if "sgbm" in n:
             print(f"{sys.argv[2]} {n.split('(svx::SgbmK')[0].replace('void svx::(anonymous namespace)::','')} calls={r['Calls']} avg_ms={float(r['AverageNs'])/1e6:.3f}")
 PY
   done
