@@ -143,16 +143,16 @@ def carmask():
 
 
 def cpu_baseline(budget_s):
-    """configs[0]: stereovision.py:84-113 for synthetic frame 0 at step 2 on ONE pinned host core, per stage,
-    through the reference's loops as written (oracle/cpu_literal.py: functions.py:178-323 and its RANSAC,
-    :240-298) — `value` is that literal loop's projection rate — and beside it through the hoisted port
-    (oracle/cpu_loop.py + oracle/ransac.py: the same arithmetic with loop invariants hoisted); then a bounded
-    step-1 projection sample (the headline workload's unit)."""
+    """configs[0]: stereovision.py:84-113 for synthetic frame 0 at step 2 on ONE pinned host core, per stage, through
+    the CPU port (oracle/cpu_loop.py + oracle/ransac.py: a nested-loop restatement of functions.py:178-323 and its
+    RANSAC, :240-298, with the reference's numpy-scalar fp64 semantics, pinned to the reference-run fixtures in
+    tests/golden/) — `value` is the port's projectDisparityTo3d rate — then a bounded step-1 projection sample (the
+    headline workload's unit). The reference's own Python never runs on the GPU box."""
     import random
     import warnings
 
     import oracle
-    from oracle import cpu_literal, cpu_loop
+    from oracle import cpu_loop
     from oracle import ransac as oransac
     try:
         cpu = sorted(os.sched_getaffinity(0))[0]
@@ -175,90 +175,85 @@ def cpu_baseline(budget_s):
         out = fn()
         return out, (time.perf_counter() - t) * 1e3
 
-    def literal_run():
-        L = cpu_literal
+    def port_run():
         s = {}
-        points, s["a1_project_rgb"] = stage(lambda: L.project(disp, 128, bgr))            # stereovision.py:84
-        mpts, s["a1_project_masked"] = stage(lambda: L.project(mdisp, 128))               # :85
+        points, s["a1_project_rgb"] = stage(lambda: cpu_loop.project(disp, bgr, 2))      # stereovision.py:84
+        mpts, s["a1_project_masked"] = stage(lambda: cpu_loop.project(mdisp, None, 2))   # :85
         random.seed(0)
-        (_, abc), s["ransac_600"] = stage(lambda: L.ransac(mpts, 600))                    # :94
+        (abc, _), s["ransac_600"] = stage(lambda: oransac.ransac(np.asarray(mpts), 600))  # :94
         abc = abc if abc is not None else abc_syn
-        diffs, s["a2_point_errors"] = stage(lambda: L.point_errors(abc, points))          # :97
-        kept, s["a3_planar_threshold"] = stage(lambda: L.plane_keep(points, diffs, 0.05))  # :100
-        hist, s["a5_colour_histogram"] = stage(lambda: L.colour_hist(kept))               # :103
-        kept2, s["a6_histogram_filter"] = stage(lambda: L.hist_keep(kept, hist, 10))      # :106
+        dist, s["a2_point_errors"] = stage(lambda: cpu_loop.point_errors(abc, points))     # :97
+        kept, s["a3_planar_threshold"] = stage(lambda: cpu_loop.plane_keep(points, dist, 0.05))   # :100
+        hist, s["a5_colour_histogram"] = stage(lambda: cpu_loop.colour_hist(kept))        # :103
+        kept2, s["a6_histogram_filter"] = stage(lambda: cpu_loop.hist_keep(kept, hist, 10))   # :106
         _, s["a7_a8_backproject_int32"] = stage(                                          # :111-113
-            lambda: np.array(L.backproject(kept2), np.int32).reshape((-1, 1, 2)))
-        return s
-
-    def hoisted_run():
-        s = {}
-        points, s["a1_project_rgb"] = stage(lambda: cpu_loop.project(disp, bgr, 2))
-        mpts, s["a1_project_masked"] = stage(lambda: cpu_loop.project(mdisp, None, 2))
-        random.seed(0)
-        (abc, _), s["ransac_600"] = stage(lambda: oransac.ransac(np.asarray(mpts), 600))
-        abc = abc if abc is not None else abc_syn
-        dist, s["a2_point_errors"] = stage(lambda: cpu_loop.point_errors(abc, points))
-        kept, s["a3_planar_threshold"] = stage(lambda: cpu_loop.plane_keep(points, dist, 0.05))
-        hist, s["a5_colour_histogram"] = stage(lambda: cpu_loop.colour_hist(kept))
-        kept2, s["a6_histogram_filter"] = stage(lambda: cpu_loop.hist_keep(kept, hist, 10))
-        _, s["a7_a8_backproject_int32"] = stage(
             lambda: np.array(cpu_loop.backproject(kept2), np.int32).reshape((-1, 1, 2)))
         return s
 
-    def medians(run, share):
-        reps, st = 0, {}
-        t_all = time.perf_counter()
-        state = random.getstate()
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore", DeprecationWarning)   # functions.py:307's sqrt of (1,)-arrays
-            while True:
-                for k, v in run().items():
-                    st.setdefault(k, []).append(v)
-                reps += 1
-                if (reps >= 2 and time.perf_counter() - t_all >= budget_s * share) or reps >= 3:
-                    break
-        random.setstate(state)
-        med = {k: round(float(np.median(v)), 1) for k, v in st.items()}
-        return med, reps
-
-    lit, lit_reps = medians(literal_run, 0.45)
-    hst, hst_reps = medians(hoisted_run, 0.25)
-    # bounded step-1 projection sample (hoisted port: the reference hard-codes step 2)
+    reps, st = 0, {}
+    t_all = time.perf_counter()
+    state = random.getstate()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", DeprecationWarning)
+        while True:
+            for k, v in port_run().items():
+                st.setdefault(k, []).append(v)
+            reps += 1
+            if (reps >= 2 and time.perf_counter() - t_all >= budget_s * 0.6) or reps >= 5:
+                break
+    random.setstate(state)
+    med = {k: round(float(np.median(v)), 1) for k, v in st.items()}
+    # bounded step-1 projection sample (the reference hard-codes step 2)
     t1, frames1, pts1 = time.perf_counter(), 0, 0
-    while frames1 == 0 or time.perf_counter() - t1 < budget_s * 0.3:
+    while frames1 == 0 or time.perf_counter() - t1 < budget_s * 0.4:
         d1, _ = oracle.synth_frame(frames1)
         cpu_loop.project(d1, None, step=1)
         pts1 += (H - 1) * (W - 1)
         frames1 += 1
     s1 = time.perf_counter() - t1
-    return {"value": round(ng2 / lit["a1_project_rgb"] / 1e3, 4), "unit": "Mpoints/s", "cores": 1, "kind": "port",
-            "port": "literal: oracle/cpu_literal.py, functions.py:178-323 and :240-298 as written (disparity[y,x] "
-                    "twice, f*B per point, len(rgb) and three rgb[y,x,c] per point, module globals per use), "
-                    "pinned to tests/golden/ like the hoisted port",
+    return {"value": round(ng2 / med["a1_project_rgb"] / 1e3, 4), "unit": "Mpoints/s", "cores": 1, "kind": "port",
+            "port": "oracle/cpu_loop.py + oracle/ransac.py: nested-loop restatement of functions.py:178-323 and "
+                    ":240-298 (numpy-scalar fp64 semantics), pinned to the reference-run fixtures in tests/golden/",
             "sample": f"configs[0]: synthetic frame 0, step 2 ({ng2} grid points), stereovision.py:84-113 per stage, "
-                      f"median of {lit_reps} runs on one pinned core; value = grid points / the literal "
+                      f"median of {reps} runs on one pinned core; value = grid points / the port's "
                       f"projectDisparityTo3d time",
-            "config1_stage_ms": lit, "config1_chain_ms_per_frame": round(sum(lit.values()), 1),
-            "hoisted_port": {"config1_stage_ms": hst, "config1_chain_ms_per_frame": round(sum(hst.values()), 1),
-                             "value": round(ng2 / hst["a1_project_rgb"] / 1e3, 4), "runs": hst_reps,
-                             "what": "oracle/cpu_loop.py + oracle/ransac.py: the same arithmetic, loop invariants "
-                                     "hoisted, vectorised RANSAC scoring"},
+            "config1_stage_ms": med, "config1_chain_ms_per_frame": round(sum(med.values()), 1),
             "step1_projection": {"Mpoints_per_s": round(pts1 / s1 / 1e6, 4), "frames": frames1,
-                                 "seconds": round(s1, 1), "port": "hoisted"},
+                                 "seconds": round(s1, 1)},
             "cpu": model, "cpu_index": cpu}
 
 
-def pipeline_traffic(path, frames, step):
-    """PMC HBM bytes per pipeline call (tools/traffic.py output), if measured at this workload."""
+def kernel_source_id(kind):
+    """sha256 (16 hex) of the sources that define a timed kernel (kind "k1" or "pipeline"): a PMC profile records
+    it (tools/prof.py traffic_json) beside the kernel's name, and bench.py uses the profile only when both match."""
+    import hashlib
+    csrc = os.path.join(REPO, "stereo.vision_amd", "csrc")
+    files = {"k1": ["kernels/project.hip"], "pipeline": ["kernels/resident.hip", "kernels/tables.hip"]}[kind]
+    h = hashlib.sha256()
+    for f in files + ["svx_device.h", "svx_launch.h"]:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def profile_traffic(path, frames, step, kernel, kind):
+    """PMC HBM bytes per launch (k1) or per call (pipeline) from a traffic JSON (tools/prof.py pmc --traffic), and
+    why it was not used if it was not: only a profile of this workload, of the same kernel instance (`kernel`, the
+    name the batch reports for its timed launch) built from the same sources (kernel_source_id) counts."""
     try:
         with open(path) as fh:
             tj = json.load(fh)
-    except (OSError, ValueError):
-        return None
+    except (OSError, ValueError) as e:
+        return None, f"no traffic profile ({type(e).__name__}: {os.path.relpath(path, REPO)})"
     if tj.get("frames") != frames or tj.get("step") != step:
-        return None
-    return tj.get("pipeline_hbm_bytes_per_call")
+        return None, f"profile is of {tj.get('frames')} frames step {tj.get('step')}, not {frames} step {step}"
+    names = [tj.get("k1_kernel")] if kind == "k1" else list(tj.get("pipeline_kernels", {}))
+    if kernel not in names:
+        return None, f"profile measured {names}, the timed kernel is {kernel}"
+    src, have = kernel_source_id(kind), tj.get("source_ids", {}).get(kind)
+    if have != src:
+        return None, f"profile built from sources {have}, the timed kernel from {src}"
+    return tj.get("k1_hbm_bytes_per_launch" if kind == "k1" else "pipeline_hbm_bytes_per_call"), None
 
 
 def ramp(fn, syncs, ms):
@@ -455,9 +450,15 @@ def extras(b, args, with_cpu, first=0):
                                    if fp_s > 0 else None,
                                    "workload": "the prepass-cleaned frames (fill previous + carmask), each with its "
                                                "own RANSAC plane (threshold 0.05, hist thr 10)",
-                                   "traffic": pipeline_traffic(args.traffic_planes, b.frames, args.step),
                                    "kernels": "frame_planes_kernel + resident_fused_kernel (each frame's plane)"
-                                   if b.frames >= 512 else "frame_planes_kernel + tiled kernels"}
+                                   if b.frames >= 512 else "frame_planes_kernel + tiled kernels",
+                                   "kernel": b.kernel_name("pipeline")}
+    fp_tr, fp_why = profile_traffic(args.traffic_planes, b.frames, args.step, b.kernel_name("pipeline"), "pipeline")
+    ex["pipeline_frame_planes"]["traffic"] = fp_tr
+    if fp_tr:
+        ex["pipeline_frame_planes"]["frac_of_traffic"] = round(fp_tr / fp_s / 1e9 / PEAK_HBM_GBS, 4)
+    else:
+        ex["pipeline_frame_planes"]["traffic_note"] = fp_why
     if not args.no_parity:
         pc, pm = check_plane_parity(b, first)
         ex["_planes_parity"] = [pc, pm]
@@ -723,15 +724,8 @@ def main(argv=None):
     bytes_launch = K1_BYTES_PER_POINT * ng * batches[0].frames
     achieved = bytes_launch / k_avg_s / 1e9
 
-    traffic = None
-    if os.path.exists(args.traffic):
-        try:
-            with open(args.traffic) as fh:
-                tj = json.load(fh)
-            if tj.get("frames") == batches[0].frames and tj.get("step") == args.step:
-                traffic = tj.get("k1_hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    k1_name = batches[0].kernel_name("project")
+    traffic, traffic_why = profile_traffic(args.traffic, batches[0].frames, args.step, k1_name, "k1")
 
     frames_gpu = batches[0].frames
     global_frames = int(ctrl.sum([sum(b.frames for b in batches)])[0])
@@ -752,7 +746,7 @@ def main(argv=None):
                    "parallelism": f"frame-sharded x{pl['n_gpus']} (no data-path collective); {par}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                     "kernel": "project_dense_kernel", "kernel_ms": round(k_avg_s * 1e3, 4),
+                     "kernel": k1_name, "kernel_ms": round(k_avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_point": K1_BYTES_PER_POINT,
                      "placement": dict(batches[0].placement("project"),
@@ -760,6 +754,8 @@ def main(argv=None):
                                             "X/Y/Z planes, one K1 launch timed on each, the fastest kept "
                                             "(outside the timed region; DESIGN §4)")},
     }
+    if traffic_why:
+        out["roofline"]["traffic_note"] = traffic_why
     parity = {}
     if not args.no_parity:
         c, m = check_parity(batches, shards, "dense", args.step)
@@ -814,8 +810,10 @@ def main(argv=None):
                           "int16 halves of one word, lossless: -1 <= x, y < 32768, widened on read-back; SURVEY counts "
                           "20 B: survey_bytes_per_call, frac_at_survey_bytes) + 4 KB histogram per frame; the resident "
                           "kernel does not read the BGR (nor, in pass 2, the disparity) of chunks the plane rules out, "
-                          "so it moves fewer bytes (traffic = PMC bytes per call, frac_of_traffic = traffic / time / "
-                          "peak)",
+                          "so it moves fewer bytes (traffic = PMC bytes per call of the timed kernel instance, "
+                          "frac_of_traffic = traffic / time / peak; null with traffic_note when no profile of that "
+                          "instance and its sources is committed). frac_at_survey_bytes is an EFFECTIVE rate: it credits "
+                          "4 B per kept point that SURVEY counts and the kernel does not store; frac is the real one",
             "survey_bytes_per_call": survey_bytes,
             "frac_at_survey_bytes": round(survey_bytes / p_avg_s / 1e9 / PEAK_HBM_GBS, 4),
             "counts_total": {"valid": int(counts[0]), "kept": int(counts[1]), "kept2": int(counts[2])},
@@ -830,10 +828,14 @@ def main(argv=None):
                                    "planes and up to two more, each timed (the faster of two passes), the fastest "
                                    "kept (outside the timed region; DESIGN §4.1)"),
         }
-        ptraffic = pipeline_traffic(args.traffic_pipeline, frames_gpu, args.step)
+        pname = batches[0].kernel_name("pipeline")
+        out["pipeline"]["kernel"] = pname
+        ptraffic, pwhy = profile_traffic(args.traffic_pipeline, frames_gpu, args.step, pname, "pipeline")
+        out["pipeline"]["traffic"] = ptraffic
         if ptraffic:
-            out["pipeline"]["traffic"] = ptraffic
             out["pipeline"]["frac_of_traffic"] = round(ptraffic / p_avg_s / 1e9 / PEAK_HBM_GBS, 4)
+        else:
+            out["pipeline"]["traffic_note"] = pwhy
         if not args.no_parity:
             c, m = check_parity(batches, shards, "pipeline", args.step)
             parity["pipeline"] = [c, m]

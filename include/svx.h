@@ -349,11 +349,16 @@ int sv_batch_last_ms(sv_batch* b, int which, float* ms);
 int sv_batch_timing(sv_batch* b, int which, double* total_ms, int64_t* count);
 int sv_batch_timing_reset(sv_batch* b);
 /* The placement probe of a large batch's first call (which: 0 = K1's X/Y/Z planes, k1_place; 1 = the resident
- * pipeline's five output planes, pipe_place; 2 = the SGBM cost volumes, sgbm_place): up to 3 (SGBM: 2) sets are
+ * pipeline's four output planes (X, Y, Z and the packed planePoints word), pipe_place; 2 = the SGBM cost volumes, sgbm_place): up to 3 (SGBM: 2) sets are
  * allocated and one call is timed on each (the pipeline: the faster of two passes; SGBM: the first chunk's
  * compute, the second of two runs); the fastest set is kept. ms[0..n-1] = each set's timed call, *kept = the
  * kept set's index (-1 when no probe ran: small batch or chunk, too little free memory). */
 int sv_batch_placement(sv_batch* b, int which, float* ms, int cap, int* n, int* kept);
+/* The kernel instance the last sv_batch_project (which 0) / sv_batch_pipeline* (1) call launched, as rocprofv3
+ * names it (e.g. "svx::resident_fused_kernel<1, 4, true, true, true, false>"; the tiled pipeline's two kernels;
+ * 2: "sgbm stage"), NUL-terminated into buf[cap]: a PMC profile of that name is the timed kernel's. SV_E_STATE
+ * before the first call. */
+int sv_batch_kernel_name(sv_batch* b, int which, char* buf, int cap);
 
 /* Read back. */
 int sv_batch_read_dense(sv_batch* b, int frame, float* X, float* Y, float* Z);
@@ -394,11 +399,13 @@ int sv_loop_destroy(sv_loop* L);
  * source 0 the caller uploads its frames (or runs sv_batch_sgbm on it) before submitting. */
 int sv_loop_acquire(sv_loop* L, sv_batch** out);
 /* Enqueue one batch (global frame ids first_frame_id..) through every stage; returns its sequence number. The
- * host waits inside only for this batch's maskpoint counts (they size the RANSAC launch), never for a stage of
- * the batch before. */
+ * host waits inside for this batch's maskpoint counts (they size the RANSAC launch). That copy is enqueued on the
+ * slot's stream behind the slot's own earlier work: with two slots, behind batch k - 2's pipeline and road pass,
+ * and (a cross-stream wait) behind batch k - 1's pre-pass; so a submit returns once those have run. Batch k's own
+ * pipeline and road pass are enqueued by the next submit (or by sv_loop_wait / _batch / _timeline). */
 int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq);
 /* Wait for batch seq's last stage. sv_loop_batch: the batch holding seq's results (sv_batch_read_* work on it)
- * until batch seq + slots is acquired or submitted. sv_loop_timeline: the start and end of each of the seven
+ * until batch seq + slots is acquired or submitted; it enqueues seq's pending stages and waits for them first. sv_loop_timeline: the start and end of each of the seven
  * stages (input, pre-pass, maskpoints, RANSAC draw, RANSAC evaluation, pipeline, road) in ms since the loop's
  * first submit, 14 doubles. */
 int sv_loop_wait(sv_loop* L, int64_t seq);

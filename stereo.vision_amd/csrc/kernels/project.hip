@@ -162,40 +162,67 @@ __global__ __launch_bounds__(256) void project_dense_kernel(const uint8_t* __res
     }
 }
 
+// the instance's name as rocprofv3 prints it (kname of launch_project_dense)
+template <int STEP, bool NT, int QPL, int TAG>
+static const char* dense_name() {
+    static const char* const n[2][2][5][2] = {
+        {{{}, {"svx::project_dense_kernel<1, false, 1, 0>", "svx::project_dense_kernel<1, false, 1, 1>"},
+          {"svx::project_dense_kernel<1, false, 2, 0>"}, {}, {"svx::project_dense_kernel<1, false, 4, 0>"}},
+         {{}, {"svx::project_dense_kernel<1, true, 1, 0>", "svx::project_dense_kernel<1, true, 1, 1>"},
+          {"svx::project_dense_kernel<1, true, 2, 0>"}, {}, {"svx::project_dense_kernel<1, true, 4, 0>"}}},
+        {{{}, {"svx::project_dense_kernel<2, false, 1, 0>", "svx::project_dense_kernel<2, false, 1, 1>"},
+          {"svx::project_dense_kernel<2, false, 2, 0>"}, {}, {"svx::project_dense_kernel<2, false, 4, 0>"}},
+         {{}, {"svx::project_dense_kernel<2, true, 1, 0>", "svx::project_dense_kernel<2, true, 1, 1>"},
+          {"svx::project_dense_kernel<2, true, 2, 0>"}, {}, {"svx::project_dense_kernel<2, true, 4, 0>"}}}};
+    return n[STEP - 1][NT ? 1 : 0][QPL][TAG];
+}
+
 template <int STEP, bool NT>
-static void launch_dense_qpl(int qpl, dim3 block, const uint8_t* disp, float* X, float* Y, float* Z,
-                             uint32_t t, const KParams& p, hipStream_t s) {
+static const char* launch_dense_qpl(int qpl, dim3 block, const uint8_t* disp, float* X, float* Y, float* Z,
+                                    uint32_t t, const KParams& p, hipStream_t s) {
     const uint32_t per = 256u * (uint32_t)qpl;
     const dim3 grid((t + per - 1) / per);
     switch (qpl) {
-        case 2: hipLaunchKernelGGL((project_dense_kernel<STEP, NT, 2>), grid, block, 0, s, disp, X, Y, Z, t, p); break;
-        case 4: hipLaunchKernelGGL((project_dense_kernel<STEP, NT, 4>), grid, block, 0, s, disp, X, Y, Z, t, p); break;
-        default: hipLaunchKernelGGL((project_dense_kernel<STEP, NT, 1>), grid, block, 0, s, disp, X, Y, Z, t, p); break;
+        case 2:
+            hipLaunchKernelGGL((project_dense_kernel<STEP, NT, 2>), grid, block, 0, s, disp, X, Y, Z, t, p);
+            return dense_name<STEP, NT, 2, 0>();
+        case 4:
+            hipLaunchKernelGGL((project_dense_kernel<STEP, NT, 4>), grid, block, 0, s, disp, X, Y, Z, t, p);
+            return dense_name<STEP, NT, 4, 0>();
+        default:
+            hipLaunchKernelGGL((project_dense_kernel<STEP, NT, 1>), grid, block, 0, s, disp, X, Y, Z, t, p);
+            return dense_name<STEP, NT, 1, 0>();
     }
 }
 
 hipError_t launch_project_dense(const KParams& p, const uint8_t* disp, float* X, float* Y, float* Z,
-                                int frames, int qpl, int nontemporal, hipStream_t s) {
+                                int frames, int qpl, int nontemporal, hipStream_t s, const char** kname) {
     const uint64_t total = (uint64_t)frames * (uint64_t)p.frame_quads;
     if (total >= (1ull << 32)) return hipErrorInvalidValue;
     const dim3 block(256);
     const uint32_t t = (uint32_t)total;
+    const char* name = nullptr;
     if (nontemporal == 2) {   // the same K1, one quad per lane, as a separately named instance
         const dim3 grid((t + 255) / 256);
-        if (p.step == 1) hipLaunchKernelGGL((project_dense_kernel<1, true, 1, 1>), grid, block, 0, s, disp, X, Y, Z, t, p);
-        else if (p.step == 2) hipLaunchKernelGGL((project_dense_kernel<2, true, 1, 1>), grid, block, 0, s, disp, X, Y, Z, t, p);
-        else return hipErrorInvalidValue;
-        return hipGetLastError();
-    }
-    if (p.step == 1) {
-        if (nontemporal) launch_dense_qpl<1, true>(qpl, block, disp, X, Y, Z, t, p, s);
-        else launch_dense_qpl<1, false>(qpl, block, disp, X, Y, Z, t, p, s);
+        if (p.step == 1) {
+            hipLaunchKernelGGL((project_dense_kernel<1, true, 1, 1>), grid, block, 0, s, disp, X, Y, Z, t, p);
+            name = dense_name<1, true, 1, 1>();
+        } else if (p.step == 2) {
+            hipLaunchKernelGGL((project_dense_kernel<2, true, 1, 1>), grid, block, 0, s, disp, X, Y, Z, t, p);
+            name = dense_name<2, true, 1, 1>();
+        } else {
+            return hipErrorInvalidValue;
+        }
+    } else if (p.step == 1) {
+        name = nontemporal ? launch_dense_qpl<1, true>(qpl, block, disp, X, Y, Z, t, p, s)
+                           : launch_dense_qpl<1, false>(qpl, block, disp, X, Y, Z, t, p, s);
     } else if (p.step == 2) {
-        if (nontemporal) launch_dense_qpl<2, true>(qpl, block, disp, X, Y, Z, t, p, s);
-        else launch_dense_qpl<2, false>(qpl, block, disp, X, Y, Z, t, p, s);
+        name = nontemporal ? launch_dense_qpl<2, true>(qpl, block, disp, X, Y, Z, t, p, s)
+                           : launch_dense_qpl<2, false>(qpl, block, disp, X, Y, Z, t, p, s);
     } else {
         return hipErrorInvalidValue;
     }
+    if (kname) *kname = name;
     return hipGetLastError();
 }
 

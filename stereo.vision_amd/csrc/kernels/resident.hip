@@ -1031,34 +1031,43 @@ hipError_t launch_store_plane(const FramePlane& v, FramePlane* dst, hipStream_t 
     return hipGetLastError();
 }
 
-// b.planes must be set (device planes; one for every frame with plane_stride 0).
+// b.planes must be set (device planes; one for every frame with plane_stride 0). kname (nullable): the
+// launched instance's name as rocprofv3 prints it, so a PMC profile can be matched to the kernel that was timed.
 hipError_t launch_pipeline_resident(const KParams& kp, const PipeBuffers& b, int frames,
-                                    bool prefetch, hipStream_t s, bool prefetch1) {
+                                    bool prefetch, hipStream_t s, bool prefetch1, const char** kname) {
     if (frames <= 0) return hipSuccess;
     if (!resident_supported(kp) || !b.planes) return hipErrorInvalidValue;
     const dim3 grid(frames), block(256);
+    const char* name = nullptr;
+#define SVX_RESIDENT(ST, QP, LC, PF, PF1, RB, SIG)                                                          \
+    do {                                                                                                    \
+        hipLaunchKernelGGL((resident_fused_kernel<ST, QP, LC, PF, PF1, RB>), grid, block, 0, s, b, p);    \
+        name = "svx::resident_fused_kernel<" SIG ">";                                                       \
+    } while (0)
     if (b.rbits) {   // the road bitmap too (resident_road_bits_supported)
         if (!resident_road_bits_supported(kp) || !resident_lane_quads(kp) || b.rb_H != kp.H) return hipErrorInvalidValue;
         const RParams p = resident_params(kp, 4);
-        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true, true, true>), grid, block, 0, s, b, p);
-        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true, false, true>), grid, block, 0, s, b, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, false, false, true>), grid, block, 0, s, b, p);
+        if (prefetch1) SVX_RESIDENT(1, 4, true, true, true, true, "1, 4, true, true, true, true");
+        else if (prefetch) SVX_RESIDENT(1, 4, true, true, false, true, "1, 4, true, true, false, true");
+        else SVX_RESIDENT(1, 4, true, false, false, true, "1, 4, true, false, false, true");
     } else if (kp.step == 1 && resident_lane_quads(kp)) {
         const RParams p = resident_params(kp, 4);
-        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true, true>), grid, block, 0, s, b, p);
-        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, true>), grid, block, 0, s, b, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, true, false>), grid, block, 0, s, b, p);
+        if (prefetch1) SVX_RESIDENT(1, 4, true, true, true, false, "1, 4, true, true, true, false");
+        else if (prefetch) SVX_RESIDENT(1, 4, true, true, false, false, "1, 4, true, true, false, false");
+        else SVX_RESIDENT(1, 4, true, false, false, false, "1, 4, true, false, false, false");
     } else if (kp.step == 1) {
         const RParams p = resident_params(kp, 4);
-        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<1, 4, false, true, true>), grid, block, 0, s, b, p);
-        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<1, 4, false, true>), grid, block, 0, s, b, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<1, 4, false, false>), grid, block, 0, s, b, p);
+        if (prefetch1) SVX_RESIDENT(1, 4, false, true, true, false, "1, 4, false, true, true, false");
+        else if (prefetch) SVX_RESIDENT(1, 4, false, true, false, false, "1, 4, false, true, false, false");
+        else SVX_RESIDENT(1, 4, false, false, false, false, "1, 4, false, false, false, false");
     } else {
         const RParams p = resident_params(kp, 2);
-        if (prefetch1) hipLaunchKernelGGL((resident_fused_kernel<2, 2, false, true, true>), grid, block, 0, s, b, p);
-        else if (prefetch) hipLaunchKernelGGL((resident_fused_kernel<2, 2, false, true>), grid, block, 0, s, b, p);
-        else hipLaunchKernelGGL((resident_fused_kernel<2, 2, false, false>), grid, block, 0, s, b, p);
+        if (prefetch1) SVX_RESIDENT(2, 2, false, true, true, false, "2, 2, false, true, true, false");
+        else if (prefetch) SVX_RESIDENT(2, 2, false, true, false, false, "2, 2, false, true, false, false");
+        else SVX_RESIDENT(2, 2, false, false, false, false, "2, 2, false, false, false, false");
     }
+#undef SVX_RESIDENT
+    if (kname) *kname = name;
     return hipGetLastError();
 }
 

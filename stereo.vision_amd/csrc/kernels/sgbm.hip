@@ -1194,10 +1194,15 @@ __global__ void lut_kernel(const uint8_t* __restrict__ in, int64_t n, const uint
         out[i] = t[in[i]];
 }
 
+// lut (nullable): preProcessImages' gamma table (functions.py:81-87) applied to each channel as it is read, so
+// the BGR pairs themselves are never rewritten (cv2.LUT returns a new image)
 __global__ __launch_bounds__(256) void grey_hist_kernel(const uint8_t* __restrict__ bgr, int64_t px, int frames,
-                                                          uint8_t* __restrict__ grey, uint32_t* __restrict__ hist) {
+                                                          uint8_t* __restrict__ grey, uint32_t* __restrict__ hist,
+                                                          const uint8_t* __restrict__ lut) {
     __shared__ uint32_t h[256];
+    __shared__ uint8_t t[256];
     h[threadIdx.x] = 0;
+    t[threadIdx.x] = lut ? lut[threadIdx.x] : (uint8_t)threadIdx.x;
     __syncthreads();
     const int64_t per = (px + gridDim.x - 1) / gridDim.x;   // gridDim.x blocks per frame in y
     const int f = blockIdx.y;
@@ -1205,7 +1210,7 @@ __global__ __launch_bounds__(256) void grey_hist_kernel(const uint8_t* __restric
     const uint8_t* src = bgr + (size_t)f * px * 3;
     for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
         const uint8_t* c = src + 3 * p;
-        const int g = (c[0] * 1868 + c[1] * 9617 + c[2] * 4899 + (1 << 13)) >> 14;
+        const int g = (t[c[0]] * 1868 + t[c[1]] * 9617 + t[c[2]] * 4899 + (1 << 13)) >> 14;
         grey[(size_t)f * px + p] = (uint8_t)g;
         atomicAdd(&h[g], 1u);
     }
@@ -1278,11 +1283,15 @@ __global__ void synth_bgr_pair_kernel(uint8_t* __restrict__ left, uint8_t* __res
 }
 
 __global__ __launch_bounds__(256) void copy_bgr_region_kernel(const uint8_t* __restrict__ src, int Hp, int Wp,
-                                                              uint8_t* __restrict__ dst, int H, int W, int Wu) {
+                                                              uint8_t* __restrict__ dst, int H, int W, int Wu,
+                                                              const uint8_t* __restrict__ lut) {
+    __shared__ uint8_t t[256];
+    t[threadIdx.x] = lut ? lut[threadIdx.x] : (uint8_t)threadIdx.x;
+    __syncthreads();
     const int row = blockIdx.x, f = blockIdx.y;   // row < H <= Hp
     const uint8_t* s = src + ((int64_t)f * Hp + row) * Wp * 3;
     uint8_t* d = dst + ((int64_t)f * H + row) * W * 3;
-    for (int b = threadIdx.x; b < 3 * Wu; b += blockDim.x) d[b] = s[b];
+    for (int b = threadIdx.x; b < 3 * Wu; b += blockDim.x) d[b] = t[s[b]];
 }
 
 }  // namespace
@@ -1296,11 +1305,11 @@ hipError_t launch_synth_bgr_pair(uint8_t* left, uint8_t* right, int H, int W, in
 }
 
 hipError_t launch_copy_bgr_region(const uint8_t* src, int Hp, int Wp, uint8_t* dst, int H, int W, int Wu, int frames,
-                                  hipStream_t s) {
+                                  hipStream_t s, const uint8_t* lut) {
     if (frames <= 0 || H <= 0) return hipSuccess;
     if (H > Hp || Wu > Wp || Wu > W) return hipErrorInvalidValue;
     hipLaunchKernelGGL(copy_bgr_region_kernel, dim3((unsigned)H, (unsigned)frames), dim3(256), 0, s, src, Hp, Wp, dst,
-                       H, W, Wu);
+                       H, W, Wu, lut);
     return hipGetLastError();
 }
 
@@ -1429,11 +1438,11 @@ hipError_t launch_lut(const uint8_t* in, int64_t n, const uint8_t* lut, uint8_t*
 }
 
 hipError_t launch_grey_equalize(const uint8_t* bgr, int64_t px, int frames, uint8_t* grey, uint32_t* hist,
-                                hipStream_t s) {
+                                hipStream_t s, const uint8_t* lut) {
     hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * 256 * frames, s);
     if (e != hipSuccess) return e;
     const unsigned bx = (unsigned)std::min<int64_t>((px + 4095) / 4096, 256);
-    hipLaunchKernelGGL(grey_hist_kernel, dim3(bx, frames), dim3(256), 0, s, bgr, px, frames, grey, hist);
+    hipLaunchKernelGGL(grey_hist_kernel, dim3(bx, frames), dim3(256), 0, s, bgr, px, frames, grey, hist, lut);
     hipLaunchKernelGGL(equalize_kernel, dim3(bx, frames), dim3(256), 0, s, grey, px, hist);
     return hipGetLastError();
 }

@@ -326,6 +326,8 @@ struct sv_batch {
     // call (ms), how many sets were tried and which one was kept (-1: no probe ran)
     float place_ms[3][8] = {};
     int place_n[3] = {0, 0, 0}, place_kept[3] = {-1, -1, -1};
+    // the kernel instance the last timed call of each kind launched (rocprofv3's name; sv_batch_kernel_name)
+    const char* kname[3] = {nullptr, nullptr, nullptr};
     bool timing = true;        // record per-launch timing events (off for a frame loop's slots: they run unbounded)
     hipError_t timed_event(int* idx) {
         if (!timing) {
@@ -711,7 +713,7 @@ int sv_batch_project(sv_batch* b, const sv_camera* cam, int sync) {
     HIP_TRY(hipEventRecord(b->ev[0], b->stream));
     HIP_TRY(b->timed_event(&t0));
     HIP_TRY(launch_project_dense(p, b->disp.as<uint8_t>(), b->X.as<float>(), b->Y.as<float>(), b->Z.as<float>(),
-                                 b->frames, b->qpl, b->nontemporal, b->stream));
+                                 b->frames, b->qpl, b->nontemporal, b->stream, &b->kname[0]));
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[1], b->stream));
     if (t0 >= 0) b->pending[0].push_back({t0, t1});
@@ -875,8 +877,9 @@ static int batch_pipeline_impl(sv_batch* b, const sv_camera* cam, const sv_plane
     HIP_TRY(hipEventRecord(b->ev[2], b->stream));
     HIP_TRY(b->timed_event(&t0));
     if (mode >= 2) {   // every output word (hist, counts, points) is rewritten: no memset, no host sync
-        HIP_TRY(launch_pipeline_resident(p, bf, b->frames, mode != 3, b->stream, mode == 2));
+        HIP_TRY(launch_pipeline_resident(p, bf, b->frames, mode != 3, b->stream, mode == 2, &b->kname[1]));
     } else {
+        b->kname[1] = "svx::stage_kernel + svx::offsets_kernel";
         const int nchunks = (b->frames + chunk - 1) / chunk;
         while ((int)b->sync_ev.size() < 2 * nchunks) {
             hipEvent_t e;
@@ -949,6 +952,14 @@ int sv_batch_placement(sv_batch* b, int which, float* ms, int cap, int* n, int* 
     *n = b->place_n[which];
     *kept = b->place_kept[which];
     for (int t = 0; t < std::min(cap, *n); ++t) ms[t] = b->place_ms[which][t];
+    return SV_OK;
+}
+
+int sv_batch_kernel_name(sv_batch* b, int which, char* buf, int cap) {
+    if (!b || which < 0 || which > 2 || !buf || cap <= 0) return fail(SV_E_ARG, "sv_batch_kernel_name: bad arguments");
+    const char* n = which == 2 ? (b->have_ms[2] ? "sgbm stage" : nullptr) : b->kname[which];
+    if (!n) return fail(SV_E_STATE, "no kernel of this kind launched yet");
+    std::snprintf(buf, (size_t)cap, "%s", n);
     return SV_OK;
 }
 
@@ -2083,20 +2094,19 @@ int sv_batch_preprocess(sv_batch* b, const uint8_t* lut, int sync) {
     HIP_TRY(b->pairL.ensure((size_t)px * b->frames));
     HIP_TRY(b->pairR.ensure((size_t)px * b->frames));
     HIP_TRY(hipMemcpyAsync(b->glut.p, lut, 256, hipMemcpyHostToDevice, b->stream));
-    const int64_t n3 = px * 3 * b->frames;
-    // preProcessImages: the gamma table on both images (in place), functions.py:81-87
-    HIP_TRY(launch_lut(b->bgrL.as<uint8_t>(), n3, b->glut.as<uint8_t>(), b->bgrL.as<uint8_t>(), b->stream));
-    HIP_TRY(launch_lut(b->bgrR.as<uint8_t>(), n3, b->glut.as<uint8_t>(), b->bgrR.as<uint8_t>(), b->stream));
+    // preProcessImages' gamma table (functions.py:81-87) is applied as the pairs are read: cv2.LUT returns new
+    // images, so the stored pairs stay the raw ones and every call corrects them exactly once (stereovision.py:44)
+    const uint8_t* lut_d = b->glut.as<uint8_t>();
     // greyscale: BGR2GRAY + equalizeHist of both, functions.py:89-97 -> the SGBM pairs
     HIP_TRY(launch_grey_equalize(b->bgrL.as<uint8_t>(), px, b->frames, b->pairL.as<uint8_t>(),
-                                 b->ghist.as<uint32_t>(), b->stream));
+                                 b->ghist.as<uint32_t>(), b->stream, lut_d));
     HIP_TRY(launch_grey_equalize(b->bgrR.as<uint8_t>(), px, b->frames, b->pairR.as<uint8_t>(),
-                                 b->ghist.as<uint32_t>(), b->stream));
+                                 b->ghist.as<uint32_t>(), b->stream, lut_d));
     // the pipeline's colours: projectDisparityTo3d(disparity, 128, imgL) reads the gamma-corrected left image at
     // the disparity's own (y, x) (stereovision.py:44, :84), the top-left H x W of it when the disparity is cropped
     if (b->with_bgr)
         HIP_TRY(launch_copy_bgr_region(b->bgrL.as<uint8_t>(), H, W, b->bgr.as<uint8_t>(), b->H, b->W, b->Wu, b->frames,
-                                       b->stream));
+                                       b->stream, lut_d));
     if (sync) HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
 }
@@ -2247,7 +2257,10 @@ struct sv_loop {
     std::vector<int64_t> slot_seq, slot_first;
     std::vector<std::array<hipEvent_t, kLsCount>> t0, t1;   // per slot: start / end of each stage (its last batch)
     hipEvent_t epoch = nullptr;
-    DevBuf carry;              // the previous batch's last cleaned frame (fillDisparity's previousDisparity)
+    // the previous batch's last cleaned frame (fillDisparity's previousDisparity), double-buffered: a submit reads
+    // carry[cur] and writes carry[cur ^ 1], and only a submit that enqueued every stage makes its write current
+    DevBuf carry[2];
+    int carry_cur = 0;
     bool carry_valid = false;
     DevBuf gate;               // uint64: the last draw kernel whose grid is resident (its epoch = seq + 1)
     int64_t next = 0;          // sequence number of the next submitted batch
@@ -2268,7 +2281,8 @@ int sv_loop_destroy(sv_loop* L) {
         for (auto& e : a)
             if (e) (void)hipEventDestroy(e);
     if (L->epoch) (void)hipEventDestroy(L->epoch);
-    if (L->carry.p) (void)hipFree(L->carry.p);
+    for (DevBuf& c : L->carry)
+        if (c.p) (void)hipFree(c.p);
     if (L->gate.p) (void)hipFree(L->gate.p);
     for (sv_batch* b : L->slot) sv_batch_destroy(b);
     delete L;
@@ -2284,6 +2298,13 @@ int sv_loop_create(int device, const sv_loop_params* prm, const sv_camera* cam, 
         q.prepass > 2 || q.road < 0 || q.road > 2 || (q.step != 1 && q.step != 2) || q.trials < 0 || q.k < 1)
         return fail(SV_E_ARG, "sv_loop_create: bad parameters (frames >= 1, 1 <= slots <= 8, source 0/1, prepass "
                               "0..2, road 0..2, step 1/2, trials >= 0, k >= 1)");
+    // what a submit would only find out after enqueueing the input and pre-pass stages (the RANSAC and synthetic
+    // input limits of batch_ransac_prepare / sv_batch_synth)
+    if (q.trials > 4096 || q.k > 1024) return fail(SV_E_ARG, "sv_loop_create: RANSAC trials <= 4096, k <= 1024");
+    if (q.H > 4096 || q.W > 4096) return fail(SV_E_ARG, "sv_loop_create: frames up to 4096 x 4096");
+    if ((int64_t)grid_len(q.H, 2) * grid_len(q.W, 2) > 163840)
+        return fail(SV_E_ARG, "sv_loop_create: more than 163,840 step-2 grid points per frame (RANSAC)");
+    if (q.source == 1 && q.W % 8) return fail(SV_E_ARG, "sv_loop_create: synthetic frames need W %% 8 == 0 (W=%d)", q.W);
     sv_loop* L = new sv_loop;
     L->device = device;
     L->prm = q;
@@ -2312,7 +2333,8 @@ int sv_loop_create(int device, const sv_loop_params* prm, const sv_camera* cam, 
                 if (e == hipSuccess) e = hipEventCreate(&L->t1[(size_t)i][st]);
             }
         if (e == hipSuccess) e = hipEventCreate(&L->epoch);
-        if (e == hipSuccess) e = L->carry.ensure((size_t)L->slot[0]->H * L->slot[0]->W);
+        for (DevBuf& c : L->carry)
+            if (e == hipSuccess) e = c.ensure((size_t)L->slot[0]->H * L->slot[0]->W);
         if (e == hipSuccess) e = L->gate.ensure(sizeof(uint64_t));
         if (e == hipSuccess) e = hipMemset(L->gate.p, 0, sizeof(uint64_t));
         if (e != hipSuccess) rc = fail(SV_E_HIP, "sv_loop_create: %s", hipGetErrorString(e));
@@ -2416,15 +2438,15 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     HIP_TRY(end(kLsInput));
     // pre-pass (stereovision.py:53-76): frame 0 cleaned with the previous batch's last cleaned frame
     HIP_TRY(begin(kLsPrepass));
+    bool carried = false;
     if (q.prepass) {
-        if (int rc = batch_prepass_impl(b, q.prepass, q.prepass == 1 && L->carry_valid ? L->carry.as<uint8_t>()
-                                                                                       : nullptr))
-            return rc;
+        const uint8_t* prev = q.prepass == 1 && L->carry_valid ? L->carry[L->carry_cur].as<uint8_t>() : nullptr;
+        if (int rc = batch_prepass_impl(b, q.prepass, prev)) return rc;
         if (q.prepass == 1) {
             const size_t px = (size_t)b->H * b->W;
-            HIP_TRY(hipMemcpyAsync(L->carry.p, b->disp.as<uint8_t>() + px * (b->frames - 1), px,
+            HIP_TRY(hipMemcpyAsync(L->carry[L->carry_cur ^ 1].p, b->disp.as<uint8_t>() + px * (b->frames - 1), px,
                                    hipMemcpyDeviceToDevice, st));
-            L->carry_valid = true;
+            carried = true;
         }
     }
     HIP_TRY(end(kLsPrepass));
@@ -2454,6 +2476,10 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     HIP_TRY(begin(kLsEval));
     if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k, st, 2)) return rc;
     HIP_TRY(end(kLsEval));
+    if (carried) {   // every stage enqueued: this batch's last cleaned frame is the next batch's previous one
+        L->carry_cur ^= 1;
+        L->carry_valid = true;
+    }
     L->pending = seq;
     L->slot_seq[s] = seq;
     L->slot_first[s] = first_frame_id;
@@ -2485,6 +2511,13 @@ int sv_loop_batch(sv_loop* L, int64_t seq, sv_batch** out, int64_t* first_frame_
     size_t s;
     if (!out) return fail(SV_E_ARG, "sv_loop_batch: null out");
     if (int rc = loop_slot_of(L, seq, &s)) return rc;
+    // the batch's pipeline and road pass may not be enqueued yet (the next submit enqueues them): enqueue them and
+    // wait for them, so that sv_batch_read_* of the returned batch never mixes this batch's RANSAC with the points
+    // and road images of the batch the slot held before
+    if (L->pending == seq)
+        if (int rc = loop_flush(L)) return rc;
+    HIP_TRY(hipSetDevice(L->device));
+    HIP_TRY(hipEventSynchronize(L->t1[s][kLsRoad]));
     *out = L->slot[s];
     if (first_frame_id) *first_frame_id = L->slot_first[s];
     return SV_OK;

@@ -11,8 +11,9 @@ namespace svx {
 hipError_t launch_synth(const KParams& p, uint8_t* disp, uint8_t* bgr, int frames,
                         int64_t first_frame, hipStream_t s);
 // K1: dense fp32 projection over frames * Hg * Q quads; qpl = quads per lane (1, 2, 4).
+// kname (nullable): the launched instance's name as rocprofv3 prints it.
 hipError_t launch_project_dense(const KParams& p, const uint8_t* disp, float* X, float* Y, float* Z,
-                                int frames, int qpl, int nontemporal, hipStream_t s);
+                                int frames, int qpl, int nontemporal, hipStream_t s, const char** kname = nullptr);
 // Drop-in projection: fp64 XYZ, compacted in raster order (any H, W, step).
 hipError_t launch_project_compact_f64(const KParams& p, const uint8_t* disp, int64_t ld_disp,
                                       const uint8_t* bgr, int64_t ld_bgr, double* xyz, uint8_t* rgb,
@@ -77,8 +78,10 @@ hipError_t launch_pipeline(const KParams& p, const PipeBuffers& b, int frames, i
 bool resident_supported(const KParams& p);
 // One workgroup per frame (pass 1 then pass 2); prefetch = pass 2 loads the
 // next chunk before issuing this chunk's stores (costs registers).
+// kname (nullable): the launched instance's name as rocprofv3 prints it.
 hipError_t launch_pipeline_resident(const KParams& p, const PipeBuffers& b, int frames,
-                                    bool prefetch, hipStream_t s, bool prefetch1 = false);
+                                    bool prefetch, hipStream_t s, bool prefetch1 = false,
+                                    const char** kname = nullptr);
 // b.rbits can be filled: W == 1024 at step 1 with lane-contiguous quads (4 grid rows a chunk, 32 words a row)
 bool resident_road_bits_supported(const KParams& p);
 // *dst = v on stream s (the resident kernel reads its planes from device memory).

@@ -42,17 +42,19 @@ hipError_t launch_sgbm_compute(const SgbmK& k, const uint8_t* left, const uint8_
 hipError_t launch_speckle_scale(const SgbmK& k, int frames, const SgbmScratch& s, uint8_t* out, int16_t* filt,
                                 hipStream_t st);
 hipError_t launch_lut(const uint8_t* in, int64_t n, const uint8_t* lut, uint8_t* out, hipStream_t s);
-// BGR2GRAY + equalizeHist of `frames` images of px pixels; hist: frames x 256 scratch.
+// BGR2GRAY + equalizeHist of `frames` images of px pixels; hist: frames x 256 scratch; lut (nullable): a table
+// applied to every channel as it is read (the gamma of preProcessImages; the input is not rewritten).
 hipError_t launch_grey_equalize(const uint8_t* bgr, int64_t px, int frames, uint8_t* grey, uint32_t* hist,
-                                hipStream_t s);
+                                hipStream_t s, const uint8_t* lut = nullptr);
 hipError_t launch_synth_pair(uint8_t* left, uint8_t* right, int H, int W, int frames, int64_t first, hipStream_t s);
 // Synthetic BGR pairs: the synthetic pair's texture with a per-source-pixel channel jitter (so left (y, x) and
 // right (y, x - D) carry the same colour), frames x H x W x 3 each.
 hipError_t launch_synth_bgr_pair(uint8_t* left, uint8_t* right, int H, int W, int frames, int64_t first,
                                  hipStream_t s);
-// dst rows (frames x H rows of Wu * 3 bytes at a stride of W * 3) from the top-left of src frames of Hp x Wp x 3
+// dst rows (frames x H rows of Wu * 3 bytes at a stride of W * 3) from the top-left of src frames of Hp x Wp x 3,
+// through lut (nullable) byte by byte
 hipError_t launch_copy_bgr_region(const uint8_t* src, int Hp, int Wp, uint8_t* dst, int H, int W, int Wu, int frames,
-                                  hipStream_t s);
+                                  hipStream_t s, const uint8_t* lut = nullptr);
 
 // Synthetic rectified pair (numpy twin: oracle/sgbm.py synth_pair): texture
 // T(frame, y, u) from the splitmix64 finaliser; row y's true disparity is the

@@ -168,9 +168,11 @@ class Batch:
         _abi.call("sv_batch_synth_bgr_pair", self._h, int(first_frame_id))
 
     def preprocess(self, gamma=1.4, sync=True):
-        """stereovision.py:44-46 on the BGR pairs: preProcessImages (gamma, in
-        place), greyscale (-> the SGBM pairs) and the corrected left image's
-        colours into the batch (with_bgr)."""
+        """stereovision.py:44-46 on the BGR pairs: preProcessImages (gamma,
+        applied as the pairs are read: the stored pairs stay raw, so every call
+        corrects them once, as cv2.LUT returns new images), greyscale (-> the
+        SGBM pairs) and the corrected left image's colours into the batch
+        (with_bgr)."""
         from .disparity import gamma_table
         lut = np.ascontiguousarray(gamma_table(gamma), np.uint8)
         _abi.call("sv_batch_preprocess", self._h, _abi.ptr(lut), int(bool(sync)))
@@ -216,6 +218,13 @@ class Batch:
                   ctypes.byref(n), ctypes.byref(kept))
         return {"tried_ms": [round(float(ms[i]), 4) for i in range(n.value)],
                 "kept": kept.value if kept.value >= 0 else None}
+
+    def kernel_name(self, which="project"):
+        """The kernel instance the last project / pipeline call launched, as rocprofv3 names it
+        (sv_batch_kernel_name): a PMC profile under that name measured the kernel this batch timed."""
+        buf = ctypes.create_string_buffer(256)
+        _abi.call("sv_batch_kernel_name", self._h, _WHICH[which], buf, 256)
+        return buf.value.decode()
 
     def reset_timing(self):
         _abi.call("sv_batch_timing_reset", self._h)

@@ -25,6 +25,7 @@ one long batch (tests/test_gpu_loop.py checks every frame against tests/golden/p
     b, first = loop.batch(seq)               # a Batch: read_points / read_road / read_ransac / digest ...
 """
 import ctypes
+import weakref
 
 import numpy as np
 
@@ -54,9 +55,12 @@ class FrameLoop:
         _abi.call("sv_loop_create", device, ctypes.byref(prm), ctypes.byref(camera or CAMERA), _abi.ptr(m),
                   ctypes.byref(h))
         self._h = h
+        self._views = weakref.WeakSet()   # the Batch views handed out: invalidated by close()
 
     def _view(self, handle):
-        return Batch._view(handle, self.frames, self.H, self.W, self.step, self.device)
+        v = Batch._view(handle, self.frames, self.H, self.W, self.step, self.device)
+        self._views.add(v)
+        return v
 
     def acquire(self):
         """The Batch the next submit() runs (source="caller": fill it first, e.g. upload() or sgbm())."""
@@ -88,6 +92,10 @@ class FrameLoop:
 
     def close(self):
         if self._h:
+            # a view the caller kept must not reach the destroyed slots: its handle becomes NULL, so a later call
+            # on it raises SvxError ("null batch") instead of touching freed memory
+            for v in list(getattr(self, "_views", ())):
+                v._h = None
             _abi.call("sv_loop_destroy", self._h)
             self._h = None
 

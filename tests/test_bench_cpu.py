@@ -109,3 +109,46 @@ def test_strong_scaling_shards(n):
     assert bench.parse(["--global-frames", str(total)]).global_frames == total
     with pytest.raises(SystemExit):
         bench.shards_of(bench.plan(8, {}), 4096, 4)
+
+
+def _traffic_file(tmp_path, **kw):
+    import json
+    tj = {"frames": 4096, "step": 1, "pipeline_kernels": {
+        "svx::frame_planes_kernel": {"launches": 1, "fetch_bytes_total": 1.0, "write_bytes_total": 2.0},
+        "svx::resident_fused_kernel<1, 4, true, true, true, false>": {
+            "launches": 1, "fetch_bytes_total": 9e9, "write_bytes_total": 18e9}},
+        "pipeline_hbm_bytes_per_call": 27e9, "source_ids": {"pipeline": bench.kernel_source_id("pipeline")}}
+    tj.update(kw)
+    p = tmp_path / "traffic.json"
+    p.write_text(json.dumps(tj))
+    return str(p)
+
+
+def test_profile_traffic_only_for_the_timed_kernel(tmp_path):
+    """bench.py reports PMC traffic only for a profile of the same kernel instance built from the same sources
+    (a stale profile of another instance or of older sources gives null and the reason)."""
+    name = "svx::resident_fused_kernel<1, 4, true, true, true, false>"
+    p = _traffic_file(tmp_path)
+    assert bench.profile_traffic(p, 4096, 1, name, "pipeline") == (27e9, None)
+    # another instance (round 3's five-parameter kernel): null, with the reason
+    v, why = bench.profile_traffic(p, 4096, 1, "svx::resident_fused_kernel<1, 4, true, true, true>", "pipeline")
+    assert v is None and "timed kernel" in why
+    # the same name from other sources
+    v, why = bench.profile_traffic(_traffic_file(tmp_path, source_ids={"pipeline": "0" * 16}), 4096, 1, name,
+                                   "pipeline")
+    assert v is None and "sources" in why
+    # another workload, a missing file
+    v, why = bench.profile_traffic(p, 2048, 1, name, "pipeline")
+    assert v is None and "2048" in why
+    v, why = bench.profile_traffic(str(tmp_path / "none.json"), 4096, 1, name, "pipeline")
+    assert v is None and why
+
+
+def test_committed_profiles_name_their_kernel():
+    """Every committed traffic profile bench.py reads names its kernel instance and the sources it measured."""
+    import json
+    for f, key in (("traffic.json", "k1_kernel"), ("traffic_pipeline.json", "pipeline_kernels"),
+                   ("traffic_planes.json", "pipeline_kernels")):
+        tj = json.load(open(os.path.join(REPO, "profiles", f)))
+        assert tj.get(key), f
+        assert tj.get("source_ids"), f

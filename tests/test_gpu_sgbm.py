@@ -229,6 +229,24 @@ def test_batch_bgr_front_end(sv, crop):
         assert b.read_disp(0)[300:].any()
 
 
+def test_batch_preprocess_leaves_pairs_raw(sv):
+    """preprocess() corrects the stored pairs as it reads them: a second call
+    gives the same SGBM pairs, disparity and colours as the first (the
+    reference corrects each pair once, stereovision.py:44)."""
+    with sv.batch.Batch(2, 96, 320, step=1, with_bgr=True, with_points=True) as b:
+        b.synth_bgr_pair(3)
+        plane = (0.0, 0.0, 0.01)
+        runs = []
+        for _ in range(3):
+            b.preprocess(1.4)
+            b.sgbm()
+            b.pipeline(plane=plane, point_thr=1e9, hist_thr=2)
+            runs.append((b.read_disp(0), b.read_disp(1), b.read_counts(), b.read_hist(0), b.read_points(1)[1]))
+        for r in runs[1:]:
+            for a, c in zip(runs[0], r):
+                assert np.array_equal(a, c)
+
+
 def test_dropin_installed_module(sv):
     """functions.disparity / greyscale / preProcessImages patched into a module
     object; a stereoProcessor with OpenCV's getters is honoured."""

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
-from oracle import cpu_literal, cpu_loop
+from oracle import cpu_loop
 from oracle import synth as osynth
 from conftest import sparse_frame
 
@@ -121,39 +121,14 @@ def test_cpu_loop_port_matches_reference_sparse(golden):
         assert type(rows[0][3]) is np.uint8 and type(rows[0][0]) is np.float64
 
 
-def test_cpu_literal_matches_reference_crops(golden):
-    """oracle/cpu_literal.py (functions.py:178-323 as written: the config-1 CPU baseline) against the
-    reference-run fixtures, bit for bit, like the hoisted port above."""
-    c = golden.crops
-    for k in range(3):
-        rows, kept, kept2, pp, hist = cpu_literal.chain(c[f"c{k}_disp"], c[f"c{k}_bgr"], c[f"c{k}_abc"])
-        xyz = np.array([r[:3] for r in rows], np.float64)
-        assert np.array_equal(xyz.view(np.uint64), c[f"c{k}_xyz"].view(np.uint64))
-        assert len(kept) == len(c[f"c{k}_keep_idx"])
-        assert np.array_equal(pp, c[f"c{k}_plane_points"])
-        h = np.zeros(1024, np.uint32)
-        for key, v in hist.items():
-            h[cpu_loop.key_to_bin(key)] = v
-        assert np.array_equal(h, c[f"c{k}_hist"])
-
-
-def test_cpu_literal_matches_reference_sparse(golden):
-    abc = np.array(golden.meta["plane_abc"])
-    for k in range(3):
-        disp, bgr = sparse_frame(golden, k)
-        rows, kept, kept2, pp, hist = cpu_literal.chain(disp, bgr, abc)
-        assert np.array_equal(pp, golden.sparse[f"f{k}_plane_points"])
-        assert type(rows[0][3]) is np.uint8 and type(rows[0][0]) is np.float64
-
-
-def test_cpu_literal_frame0_digest(golden):
-    """The literal loop on synthetic frame 0 (the bench's config-1 input) gives the reference's XYZ digest,
+def test_cpu_loop_frame0_digest(golden):
+    """The CPU port on synthetic frame 0 (the bench's config-1 input) gives the reference's XYZ digest,
     counts and planePoints digest (tests/golden/digests.json)."""
     import hashlib
 
     import oracle
     disp, bgr = oracle.synth_frame(0)
-    rows, kept, kept2, pp, _ = cpu_literal.chain(disp, bgr, oracle.synthetic_plane())
+    rows, kept, kept2, pp, _ = cpu_loop.chain(disp, bgr, oracle.synthetic_plane())
     xyz = np.array([r[:3] for r in rows], np.float64)
     assert hashlib.sha256(xyz.tobytes()).hexdigest()[:16] == "4e8146c117e8d5f0"
     assert (len(rows), len(kept), len(kept2)) == (74200, 69341, 63826)

@@ -49,28 +49,6 @@ def test_oracle_matches_reference(cases):
         random.setstate(saved)
 
 
-def test_literal_ransac_matches_reference(cases):
-    """oracle/cpu_literal.ransac (functions.py:240-298 as written, the config-1 baseline's RANSAC) gives the
-    reference's plane bits and leaves the reference's `random` state, on every fixture case."""
-    import warnings
-
-    from oracle import cpu_literal
-    saved = random.getstate()
-    try:
-        for key, ref in FIX.items():
-            name, seed = key.split("/")
-            pts = [list(r) for r in np.asarray(cases[name])]
-            pts = [[np.float64(v) for v in r] for r in pts]
-            random.seed(int(seed))
-            with warnings.catch_warnings():
-                warnings.simplefilter("ignore", DeprecationWarning)
-                _, abc = cpu_literal.ransac(pts, ref["trials"])
-            assert (None if abc is None else bits(abc)) == ref["abc_bits"], key
-            assert state_digest() == ref["state_after"], key
-    finally:
-        random.setstate(saved)
-
-
 def _draw(state, pts, trials, k):
     from svx import _abi
     words = np.array(state[1], dtype=np.uint32)

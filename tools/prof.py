@@ -231,6 +231,13 @@ def traffic_json(root, frames, step):
     v = _load_pmc(root)
     out = {"frames": frames, "step": step, "source": root,
            "correction": "fetched = 2 x FETCH_SIZE (gfx950, calibrated on K1's loads); written = WRITE_SIZE"}
+    # the sources the profiled kernels were built from: bench.py uses a profile only for the same instance name
+    # AND the same sources (bench.kernel_source_id)
+    import bench
+    kinds = {"k1": "project_dense_kernel", "pipeline": "resident_fused_kernel"}
+    for kind, pat in kinds.items():
+        if any(pat in k for k in v):
+            out.setdefault("source_ids", {})[kind] = bench.kernel_source_id(kind)
     for k, cs in v.items():
         if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
