@@ -224,16 +224,15 @@ def cpu_baseline(budget_s):
 
 
 def kernel_source_id(kind):
-    """sha256 (16 hex) of the sources that define a timed kernel (kind "k1" or "pipeline"): a PMC profile records
-    it (tools/prof.py traffic_json) beside the kernel's name, and bench.py uses the profile only when both match."""
-    import hashlib
-    csrc = os.path.join(REPO, "stereo.vision_amd", "csrc")
-    files = {"k1": ["kernels/project.hip"], "pipeline": ["kernels/resident.hip", "kernels/tables.hip"]}[kind]
-    h = hashlib.sha256()
-    for f in files + ["svx_device.h", "svx_launch.h"]:
-        with open(os.path.join(csrc, f), "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+    """The library's build-time id of the sources that define a timed kernel (kind "k1" or "pipeline";
+    sv_source_id): a PMC profile records it (tools/prof.py traffic_json, from the library it profiled) beside the
+    kernel's name, and bench.py uses the profile only when both match the library it timed."""
+    import ctypes
+
+    from svx import _abi
+    buf = ctypes.create_string_buffer(64)
+    _abi.call("sv_source_id", {"k1": 0, "pipeline": 1}[kind], buf, 64)
+    return buf.value.decode()
 
 
 def profile_traffic(path, frames, step, kernel, kind):

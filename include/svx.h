@@ -292,10 +292,15 @@ int sv_batch_read_road_map(sv_batch* b, int frame, uint8_t* out);
  * numpy's rounding — LAPACK dgesv + dot, gemv, pairwise mean — so abc, err and
  * trial equal the reference's bit for bit; 8: every triple drawn in 65,536 attempts was collinear
  * — the reference never returns there — trial = -1; 16: more than 2^28
- * draws in one frame, trial = -1). Step-2 grids of
- * <= 163,840 points, frames up to 4096 x 4096; 1 <= k <= 1024. The call
- * waits for the maskpoints counts (one small read-back: the largest frame
- * sizes the RANSAC kernel's LDS); `sync` then applies to the RANSAC kernel. */
+ * draws in one frame, trial = -1; 32: a frame above the launch's size bound,
+ * trial = -1 — cannot happen while the bound holds). Step-2 grids of
+ * <= 163,840 points, frames up to 4096 x 4096; 1 <= k <= 1024. The kernels'
+ * LDS is sized for the largest frame: with a mask set (the reference always
+ * masks, stereovision.py:74-85) from the mask's own step-2 points, an upper
+ * bound of every frame's count, so the call enqueues everything without a
+ * host wait; without a mask (or a mask too large for 8 KiB of sample LDS) it
+ * waits for the maskpoints counts (one small read-back). `sync` then applies
+ * to the RANSAC kernels. */
 int sv_batch_ransac(sv_batch* b, const sv_camera* cam, uint64_t seed_base, int64_t first_frame, int trials, int k,
                     int sync);
 int sv_batch_read_ransac(sv_batch* b, int frame, double* abc, double* err, int32_t* trial, uint32_t* flags);
@@ -359,6 +364,10 @@ int sv_batch_placement(sv_batch* b, int which, float* ms, int cap, int* n, int* 
  * 2: "sgbm stage"), NUL-terminated into buf[cap]: a PMC profile of that name is the timed kernel's. SV_E_STATE
  * before the first call. */
 int sv_batch_kernel_name(sv_batch* b, int which, char* buf, int cap);
+/* sha256 (16 hex) of the sources this library's K1 (which 0: kernels/project.hip + the device headers) or resident
+ * pipeline (1: kernels/resident.hip, kernels/tables.hip + the device headers) was compiled from, fixed at build time:
+ * a PMC profile records it, and a profile counts for the timed kernel only when the ids agree. */
+int sv_source_id(int which, char* buf, int cap);
 
 /* Read back. */
 int sv_batch_read_dense(sv_batch* b, int frame, float* X, float* Y, float* Z);
@@ -398,11 +407,12 @@ int sv_loop_destroy(sv_loop* L);
 /* The batch the next sv_loop_submit runs (waits on the host until its slot's previous batch is done): with
  * source 0 the caller uploads its frames (or runs sv_batch_sgbm on it) before submitting. */
 int sv_loop_acquire(sv_loop* L, sv_batch** out);
-/* Enqueue one batch (global frame ids first_frame_id..) through every stage; returns its sequence number. The
- * host waits inside for this batch's maskpoint counts (they size the RANSAC launch). That copy is enqueued on the
- * slot's stream behind the slot's own earlier work: with two slots, behind batch k - 2's pipeline and road pass,
- * and (a cross-stream wait) behind batch k - 1's pre-pass; so a submit returns once those have run. Batch k's own
- * pipeline and road pass are enqueued by the next submit (or by sv_loop_wait / _batch / _timeline). */
+/* Enqueue one batch (global frame ids first_frame_id..) through every stage; returns its sequence number. With a
+ * carmask the host waits for nothing (the mask's step-2 points bound every frame's maskpoints count and size the
+ * RANSAC launches); without one it waits for this batch's maskpoint counts, whose copy is enqueued on the slot's
+ * stream behind the slot's earlier work (with two slots: batch k - 2's pipeline and road pass, and batch k - 1's
+ * pre-pass). Batch k's own pipeline and road pass are enqueued by the next submit (or by sv_loop_wait / _batch /
+ * _timeline). */
 int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq);
 /* Wait for batch seq's last stage. sv_loop_batch: the batch holding seq's results (sv_batch_read_* work on it)
  * until batch seq + slots is acquired or submitted; it enqueues seq's pending stages and waits for them first. sv_loop_timeline: the start and end of each of the seven

@@ -216,7 +216,7 @@ constexpr int kRBMaxAttempts = 1 << 16;
 // frame (240k trials of 600) the frame stops with flag 16, so no input can keep
 // a wave spinning
 constexpr uint32_t kRBMaxDraws = 1u << 28;
-// the pool branch's list shares the bitmap: n <= setsize(k <= 1024) = 21 + 4096 = 4117 < 5120 words
+// the pool branch's list (<= k words) shares the bitmap's words
 
 // LDS of one frame: a fixed part (static) and, in dynamic LDS sized by the
 // launch for the batch's largest frame, the sample bitmap (set branch) or the
@@ -226,7 +226,7 @@ template <class IdxT>
 struct RansacShared {
     uint32_t* mt;
     uint32_t* bitmap;                         // set branch: selected indices of the current sample
-    int32_t* pool;                            // pool branch: the shrinking list (same words)
+    uint32_t* pool_list;                      // pool branch: the virtual pool's entries (same words, <= k)
     int k;
     uint32_t* dummy;                          // claims of rejected draws (one word a lane)
     int ablate;                               // DIAGNOSTIC (SVX_RANSAC_ABLATE, diag build)
@@ -472,22 +472,58 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
     rb_wave_lds_sync();
 }
 
-// wave 0, lane 0 drives: random.sample(range(n), k), pool branch (n <= setsize)
+// wave 0: random.sample(range(n), k), pool branch (n <= setsize), over a virtual pool. CPython keeps
+// pool = list(range(n)) and per pick i takes j = randbelow(n - i), selects pool[j] and moves pool[n - i - 1] into
+// slot j. Here the pool is V(x) = x unless the frame's LDS list holds an entry x | V(x) << 16 (n <= 4117 < 2^16):
+// a pick reads V(j) and V(n - i - 1) from one scan of the list by the whole wave (four entries a lane per 16-byte
+// read) and adds or replaces the entry of j, so the list holds at most k entries — k words of LDS instead of n,
+// which is what lets the launch size the LDS without the frames' counts (positions >= n - i are never read again:
+// the entry of n - i - 1 may stay).
 template <class IdxT, bool TR>
 __device__ void rb_sample_pool(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, int k, IdxT* idx, int32_t* tr) {
     const int lane = lane_id();
-    for (uint32_t q = lane; q < n; q += kWave) sh.pool[q] = (int32_t)q;
-    rb_wave_lds_sync();
+    uint32_t* ml = sh.pool_list;
+    uint32_t cnt = 0;   // list entries (uniform)
     for (int i = 0; i < k && st.pos < kRBMaxDraws; ++i) {
         const uint32_t bound = n - (uint32_t)i;
         const int kb = 32 - __builtin_clz(bound);
         uint32_t j = 0;
         rb_draw_below(sh, st, bound, kb, 1, &j);
-        if (lane == 0) {
-            idx[i] = (IdxT)sh.pool[j];
-            if (TR && tr) tr[i] = sh.pool[j];
-            sh.pool[j] = sh.pool[n - i - 1];
+        const uint32_t lk = bound - 1u;   // the last live position
+        int pj = -1;                      // this lane's entry position of j, of lk (at most one lane each)
+        uint32_t vj = 0u, vl = 0u;
+        bool hl = false;
+        for (uint32_t b = 0; b < cnt; b += 4u * kWave) {   // uniform
+            const uint32_t e0 = b + 4u * (uint32_t)lane;
+            if (e0 < cnt) {
+                const uint4 w = *reinterpret_cast<const uint4*>(ml + e0);
+                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const bool live = e0 + (uint32_t)t < cnt;
+                    const uint32_t key = ww[t] & 0xFFFFu;
+                    if (live && key == j) {
+                        pj = (int)(e0 + (uint32_t)t);
+                        vj = ww[t] >> 16;
+                    }
+                    if (live && key == lk) {
+                        hl = true;
+                        vl = ww[t] >> 16;
+                    }
+                }
+            }
         }
+        const uint64_t mj = rb_ballot(pj >= 0), ml_ = rb_ballot(hl);
+        const int posj = mj ? __builtin_amdgcn_readlane(pj, (int)__builtin_ctzll(mj)) : -1;
+        const uint32_t valj = mj ? (uint32_t)__builtin_amdgcn_readlane((int)vj, (int)__builtin_ctzll(mj)) : j;
+        const uint32_t vall = ml_ ? (uint32_t)__builtin_amdgcn_readlane((int)vl, (int)__builtin_ctzll(ml_)) : lk;
+        if (lane == 0) {
+            idx[i] = (IdxT)valj;
+            if (TR && tr) tr[i] = (int32_t)valj;
+            ml[posj >= 0 ? (uint32_t)posj : cnt] = j | (vall << 16);
+        }
+        cnt += posj >= 0 ? 0u : 1u;
+        rb_wave_lds_sync();   // the next pick's scan reads lane 0's entry
     }
     rb_wave_lds_sync();   // idx (and the trace) read by every lane next
 }
@@ -621,7 +657,7 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
     RansacShared<IdxT> sh;
     sh.mt = mt;
     sh.bitmap = rb_dyn;
-    sh.pool = reinterpret_cast<int32_t*>(rb_dyn);
+    sh.pool_list = rb_dyn;
     sh.k = k;
     sh.dummy = dummy;
     sh.ablate = ablate;
@@ -641,6 +677,15 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
     const uint32_t n = (uint32_t)n64;
     const int kb = 32 - __builtin_clz(n);
     const bool pool = (int64_t)n <= ransac_setsize(k);
+    // the launch sized the sample LDS from an upper bound of the counts; a frame above it (only if the bound's
+    // premise broke) stops with status 3 rather than write past its LDS
+    if (pool ? k > bitmap_words : (int64_t)(n + 31) / 32 > bitmap_words) {
+        if (lane == 0) {
+            fstat[2 * frame] = 3;
+            fstat[2 * frame + 1] = 0;
+        }
+        continue;
+    }
     for (int q = lane; q < bitmap_words; q += 64) sh.bitmap[q] = 0;
     if (lane == 0) rb_seed(sh.mt, seed_base + (uint64_t)(first_frame + frame));
     __syncthreads();   // one wave: orders lane 0's seeding before every lane's reads
@@ -841,6 +886,15 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
     const int status = fstat[2 * frame], T = fstat[2 * frame + 1];
     const uint32_t* fpk = packed + (int64_t)frame * cap;
     const uint32_t* P = fpk;
+    if (LDS_PTS && n64 > lds_pts_words) {   // above the launch's LDS bound (only if its premise broke): flag 32
+        if (tid == 0) {
+            out_trial[frame] = -1;
+            out_flags[frame] = 32;
+            out_err[frame] = 0.0;
+            out_abc[3 * frame] = out_abc[3 * frame + 1] = out_abc[3 * frame + 2] = 0.0;
+        }
+        return;
+    }
     if constexpr (LDS_PTS) {
         for (int64_t q = tid; q < n64; q += kRBEvalThreads) ev_dyn[q] = fpk[q];
         P = ev_dyn;
@@ -1049,9 +1103,9 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
         }
     }
     if (tid == 0) {
-        if (status) {   // 1: the reference would never return; 2: draw budget
+        if (status) {   // 1: the reference would never return; 2: draw budget; 3: above the launch's LDS bound
             best_t = -1;
-            flags |= status == 1 ? 8u : 16u;
+            flags |= status == 1 ? 8u : status == 2 ? 16u : 32u;
         }
         if (best_t >= 0 && second <= best * (1.0 + 1e-9)) flags |= 4u;   // near-tie
         out_trial[frame] = best_t;
@@ -1124,9 +1178,9 @@ hipError_t launch_ransac_batch(const uint32_t* packed, const double* tab, int H,
     if (frames <= 0) return hipSuccess;
     if (k < 1 || k > kRBMaxK || trials > kRBMaxTrials || cap > (int64_t)kRBBitmapWords * 32 || max_n > cap)
         return hipErrorInvalidValue;
-    // draw-kernel LDS: the set branch's bitmap (n bits) or the pool branch's list (n words), for the largest frame
+    // draw-kernel LDS: the set branch's bitmap (n bits) for the largest frame, or the pool branch's list (k words)
     int64_t words = (max_n + 31) / 32;
-    if (max_pool_n > words) words = max_pool_n;
+    if (max_pool_n > 0 && k > words) words = k;
     if (words < 1) words = 1;
     words = (words + 3) & ~3ll;   // the bitmap is cleared 4 words a store
     // the samples as u16 indices when every frame has < 65536 points

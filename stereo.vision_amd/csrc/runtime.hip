@@ -304,8 +304,10 @@ struct sv_batch {
     DevBuf sgflags;             // SGBM range flags, one word per frame of the batch
     int64_t mcap = 0;
     int64_t rmax_n = 0, rmax_pool_n = 0;   // the last RANSAC draw launch's largest frame (they size the eval too)
+    int64_t rbound = -1;        // the last prepare's device-side bound of the counts (-1: the counts are read back)
     int trace_trials = 0, trace_k = 0, traced_trials = 0;   // requested; k and trials of the recorded trace
     bool have_mask = false;
+    int64_t mask_n2 = 0;        // the mask's points on the step-2 grid (an upper bound of every frame's maskpoints)
     // pipeline control block (one memset per call): hist | counts | err
     uint32_t* hist = nullptr;
     int64_t* counts = nullptr;
@@ -955,6 +957,16 @@ int sv_batch_placement(sv_batch* b, int which, float* ms, int cap, int* n, int* 
     return SV_OK;
 }
 
+int sv_source_id(int which, char* buf, int cap) {
+#ifndef SVX_SRCID_K1
+#define SVX_SRCID_K1 "unknown"
+#define SVX_SRCID_PIPE "unknown"
+#endif
+    if (which < 0 || which > 1 || !buf || cap <= 0) return fail(SV_E_ARG, "sv_source_id: bad arguments");
+    std::snprintf(buf, (size_t)cap, "%s", which == 0 ? SVX_SRCID_K1 : SVX_SRCID_PIPE);
+    return SV_OK;
+}
+
 int sv_batch_kernel_name(sv_batch* b, int which, char* buf, int cap) {
     if (!b || which < 0 || which > 2 || !buf || cap <= 0) return fail(SV_E_ARG, "sv_batch_kernel_name: bad arguments");
     const char* n = which == 2 ? (b->have_ms[2] ? "sgbm stage" : nullptr) : b->kname[which];
@@ -1222,6 +1234,12 @@ int sv_batch_set_mask(sv_batch* b, const uint8_t* mask) {
     HIP_TRY(launch_mask_bytes(grey, b->carmask.as<uint8_t>(), px, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     b->have_mask = true;
+    // the mask's points on maskpoints' step-2 grid (range(0, H-1, 2) x range(0, W-1, 2)): no frame's masked point
+    // count can exceed it, so it sizes the batched RANSAC's launches without reading the counts back (batch_ransac_*)
+    int64_t n2 = 0;
+    for (int y = 0; y < b->H - 1; y += 2)
+        for (int x = 0; x < b->Wu - 1; x += 2) n2 += mask[(int64_t)y * b->Wu + x] != 0;
+    b->mask_n2 = n2;
     return SV_OK;
 }
 
@@ -1460,6 +1478,16 @@ static int ransac_ablate() {
 // one read-back: phase 1 enqueues the step-2 tables, maskpoints and the copy of the per-frame counts into pinned
 // host memory (+ an event); phase 2 waits for that event — the largest frame sizes the draw kernel's LDS (bitmap /
 // pool list) and the sample index width — and enqueues the draw and evaluation kernels.
+// An upper bound of every frame's maskpoints count that sizes the RANSAC launches with no read-back, or -1: the
+// mask's step-2 grid points when a mask is set and they keep the draw kernel's sample LDS (a bitmap of n bits, or
+// the pool branch's k-entry list) within 8 KiB and the sample indices 16-bit; otherwise the counts are read.
+static int64_t ransac_device_bound(const sv_batch* b, int k) {
+    if (!b->have_mask) return -1;
+    const int64_t n = std::min(b->mask_n2, b->mcap);
+    const int64_t words = std::max<int64_t>((n + 31) / 32, k);
+    return (words <= 2048 && n <= 65535) ? n : -1;
+}
+
 static int batch_ransac_prepare(sv_batch* b, const sv_camera* cam, int trials, int k) {
     if (!b || !cam || trials < 0 || k < 1 || k > 1024)
         return fail(SV_E_ARG, "sv_batch_ransac: bad arguments (1 <= k <= 1024, trials >= 0)");
@@ -1486,8 +1514,13 @@ static int batch_ransac_prepare(sv_batch* b, const sv_camera* cam, int trials, i
     const uint8_t* mff = b->have_mask ? b->carmask.as<uint8_t>() : nullptr;
     HIP_TRY(launch_maskpoints(b->disp.as<uint8_t>(), mff, b->frames, b->H, b->W, p, b->mpk.as<uint32_t>(), mcap,
                               r.mcount, b->stream));
-    HIP_TRY(hipMemcpyAsync(b->hcnt, r.mcount, sizeof(int64_t) * F, hipMemcpyDeviceToHost, b->stream));
-    HIP_TRY(hipEventRecord(b->cnt_ev, b->stream));
+    // the launches are sized from an upper bound of every frame's count when one is small enough (the mask's grid
+    // points: ransac_device_bound), else from the counts read back (the host waits for them in the launch)
+    b->rbound = ransac_device_bound(b, k);
+    if (b->rbound < 0) {
+        HIP_TRY(hipMemcpyAsync(b->hcnt, r.mcount, sizeof(int64_t) * F, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipEventRecord(b->cnt_ev, b->stream));
+    }
     return SV_OK;
 }
 
@@ -1513,8 +1546,12 @@ static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_
         b->trace_k = k;
         b->traced_trials = trace ? b->trace_trials : 0;   // what rtrace holds now (sv_batch_read_ransac_trace)
     }
-    // the largest frame sizes the kernel's LDS (bitmap / pool list): the counts phase 1 copied back
-    if (phases & 1) {
+    // the largest frame sizes the kernel's LDS (bitmap / pool list): the device bound of batch_ransac_prepare, or
+    // the counts phase 1 copied back
+    if ((phases & 1) && b->rbound >= 0) {
+        b->rmax_n = b->rbound;
+        b->rmax_pool_n = b->rbound >= k ? std::min<int64_t>(b->rbound, ransac_setsize(k)) : 0;
+    } else if (phases & 1) {
         HIP_TRY(hipEventSynchronize(b->cnt_ev));
         int64_t max_n = 0, max_pool_n = 0;
         const int64_t setsize = ransac_setsize(k);
@@ -2403,7 +2440,8 @@ static int loop_flush(sv_loop* L) {
 }
 
 // Enqueue order of sv_loop_submit(k), slot s = k % slots, the previous batch k - 1 on slot ps:
-//   slot s:  input(k) -> pre-pass(k) -> maskpoints(k)   [the host reads k's counts: they size the draw launch]
+//   slot s:  input(k) -> pre-pass(k) -> maskpoints(k)   [without a carmask the host reads k's counts: they size
+//            the draw launch; with one, the mask's step-2 points bound them and nothing is read]
 //   slot s:  draw(k)  (after batch k - 1's evaluation: a frame's evaluation needs a whole CU's LDS)
 //   slot ps: gate(draw(k) resident) -> pipeline(k - 1) -> road(k - 1)
 //   slot s:  evaluation(k)  (after road(k - 1): beside pre-pass(k + 1) and maskpoints(k + 1), which use no LDS)
@@ -2454,8 +2492,9 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     HIP_TRY(begin(kLsMaskpoints));
     if (int rc = batch_ransac_prepare(b, &L->cam, q.trials, q.k)) return rc;
     HIP_TRY(end(kLsMaskpoints));
-    // RANSAC draw (stereovision.py:94): frame g draws after random.seed(seed_base + g); the host waits here for this
-    // batch's counts, with the previous batch's evaluation already enqueued
+    // RANSAC draw (stereovision.py:94): frame g draws after random.seed(seed_base + g); sized from the carmask's
+    // bound of the counts (no host wait; without a mask the host waits here for this batch's counts, with the
+    // previous batch's evaluation already enqueued)
     if (seq > 0 && ps != s) HIP_TRY(hipStreamWaitEvent(st, L->t1[ps][kLsEval], 0));
     HIP_TRY(begin(kLsDraw));
     if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k, st, 1,

@@ -106,6 +106,7 @@ SIGNATURES = {
     "sv_batch_timing_reset": [P],
     "sv_batch_placement": [P, I, PF, I, ctypes.POINTER(I), ctypes.POINTER(I)],
     "sv_batch_kernel_name": [P, I, P, I],
+    "sv_source_id": [I, P, I],
     "sv_batch_read_dense": [P, I, P, P, P],
     "sv_batch_read_counts": [P, P],
     "sv_batch_read_hist": [P, I, P],

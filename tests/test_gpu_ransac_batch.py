@@ -160,6 +160,41 @@ def test_batch_sample_branches(svb, ns, k, seed_base):
             _check(b.read_ransac(f), *ref, what=f"n={n} k={k}")
 
 
+@pytest.mark.parametrize("ns,k,seed_base", [
+    ((3000, 4117, 4118, 20000), 600, 9),     # pool branch (virtual pool), set branch
+    ((599, 600, 601, 4500), 600, 2**33 + 1),
+    ((20, 21, 22, 300), 5, 13),
+])
+def test_batch_sample_branches_mask_bound(svb, ns, k, seed_base):
+    """With a mask set, the launches are sized from the mask's step-2 points (an upper bound of every frame's
+    count) instead of the counts read back; both random.sample branches must still replay CPython exactly. The
+    mask keeps grid rows < 120 (61,440 step-2 points: 1,920 bitmap words, 16-bit sample indices) and every
+    point of these frames lies there."""
+    trials = 25
+    mask = np.zeros((H, W), np.uint8)
+    mask[:240, :] = 255
+    with svb.Batch(len(ns), H=H, W=W, step=2, with_bgr=False) as b:
+        for f, n in enumerate(ns):
+            d = _sparse_frame(n, 300 + n + f)
+            hit = d[240:] != 0
+            if hit.any():   # move the points below the masked rows up into them (same count, distinct cells)
+                rng = np.random.default_rng(n + f)
+                free = np.flatnonzero(d[0:240:2, 0:1023:2] == 0)
+                cells = rng.choice(free, int(hit.sum()), replace=False)
+                vals = d[240:][hit]
+                d[240:] = 0
+                d[2 * (cells // 512), 2 * (cells % 512)] = vals
+            assert (d[0:543:2, 0:1023:2] != 0).sum() == n
+            b.upload(f, d)
+        b.set_mask(mask)
+        b.ransac(seed_base=seed_base, trials=trials, k=k)
+        for f, n in enumerate(ns):
+            pts = b.read_maskpoints(f)
+            assert len(pts) == n
+            ref = _oracle_frame(pts, trials, seed_base + f, k=k)
+            _check(b.read_ransac(f), *ref, what=f"mask bound n={n} k={k}")
+
+
 def _lines_frame(rows, n_per_row, n_rest, seed):
     """n_rest random step-2 points plus n_per_row points on each given grid row at one disparity (50): every
     triple drawn from one row is collinear (same Y and Z)."""

@@ -31,11 +31,13 @@
 //           grid barrier after every round's pass 1 and after its pass 2 (so the whole chip reads, then writes);
 //           35 mode 34 with pass 2 as K = 64 (all re-reads, then all writes); 36 mode 34 with only the barrier
 //           after pass 1
-// argv: frames (4096), outputs per frame (277200), 1 = output planes physically contiguous (0)
+// argv: frames (4096), outputs per frame (277200), 1 = output planes physically contiguous (0);
+//       or: r05 frames kept skip reps (the round-5 probe of the 16-B layout, shape16_kernel)
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/_sol_pipe tools/sol_pipe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                              \
@@ -265,7 +267,141 @@ __global__ __launch_bounds__(256) void sol_kernel(Args a) {
     if (acc == 0x12345678u) a.sink[f] = acc;   // keeps the loads
 }
 
+// Round 5: the resident kernel's shape at its 16-B layout (three f32 planes X, Y, Z + one packed planePoints
+// word a point, round 4). A frame has `nch` chunks (the kernel's 4096 grid points each: 136 at 1024 x 544); the
+// first `skip` of them are chunks the plane rules out (the rows above the horizon: pass 1 reads their disparity
+// only, pass 2 skips them), the rest hold the frame's `kept` outputs evenly. Pass 1 reads disparity + BGR, pass 2
+// re-reads the disparity and writes its chunk's outputs, K chunks' reads before their writes.
+//   r5 mode 0  K = 1, frame-strided planes (the kernel)          1  K = 1, atomic regions (dense frames)
+//           2  K = whole frame, strided                          3  K = whole frame, atomic regions
+//           4  pass 1 reads only                                 5  pass-2 writes only (strided)
+//           6  mode 0 without the pass-2 disparity re-read       7  writes only, dense frames
+struct Args5 {
+    const uint8_t* disp;
+    const uint8_t* bgr;
+    float* o[4];
+    uint32_t* sink;
+    int64_t px, cap, kept;
+    int nch, skip, mode;
+    unsigned long long* counter;
+};
+
+__global__ __launch_bounds__(256) void shape16_kernel(Args5 a) {
+    const int f = blockIdx.x;
+    const int64_t chunk_px = (a.px + a.nch - 1) / a.nch;   // bytes of disparity a chunk covers
+    const uint4* d = reinterpret_cast<const uint4*>(a.disp + (int64_t)f * a.px);
+    const uint4* c = reinterpret_cast<const uint4*>(a.bgr + (int64_t)f * a.px * 3);
+    uint32_t acc = 0;
+    const int live = a.nch - a.skip;
+    const auto cw0 = [&](int ch) { return (int64_t)ch * chunk_px / 16; };
+    const auto cw1 = [&](int ch) { return min((int64_t)(ch + 1) * chunk_px, a.px) / 16; };
+    if (a.mode != 5 && a.mode != 7) {   // pass 1
+        for (int ch = 0; ch < a.nch; ++ch) {
+            const bool bgr = ch >= a.skip;
+            for (int64_t w = cw0(ch) + threadIdx.x; w < cw1(ch); w += 256) {
+                const uint4 x = d[w];
+                acc ^= x.x ^ x.w;
+                if (bgr) {
+                    const uint4 y0 = c[3 * w], y1 = c[3 * w + 1], y2 = c[3 * w + 2];
+                    acc ^= y0.x ^ y1.y ^ y2.w;
+                }
+            }
+        }
+    }
+    if (a.mode == 4) {
+        if (acc == 0x12345678u) a.sink[f] = acc;
+        return;
+    }
+    __shared__ int64_t base;
+    if (threadIdx.x == 0)
+        base = (a.mode == 1 || a.mode == 3 || a.mode == 7) ? (int64_t)atomicAdd(a.counter, (unsigned long long)a.kept)
+                                                           : (int64_t)f * a.cap;
+    __syncthreads();
+    const int K = (a.mode == 2 || a.mode == 3) ? live : 1;
+    const float v = (float)f;
+    for (int c0 = 0; c0 < live; c0 += K) {
+        if (a.mode != 5 && a.mode != 6 && a.mode != 7)
+            for (int ch = c0; ch < min(c0 + K, live); ++ch)
+                for (int64_t w = cw0(a.skip + ch) + threadIdx.x; w < cw1(a.skip + ch); w += 256) {
+                    const uint4 x = d[w];
+                    acc ^= x.x ^ x.w;
+                }
+        const int64_t g0 = (a.kept / 4 * c0 / live) * 4, g1 = (a.kept / 4 * min(c0 + K, live) / live) * 4;
+        for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
+            const v4f q = {v, v, v, v};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + base + g));
+        }
+    }
+    if (acc == 0x12345678u) a.sink[f] = acc;
+}
+
+static int main_r05(int argc, char** argv) {
+    // argv: r05 frames kept skip_of_136 reps
+    const int frames = argc > 2 ? std::atoi(argv[2]) : 4096;
+    const int64_t kept = argc > 3 ? std::atoll(argv[3]) : 277200;
+    const int skip = argc > 4 ? std::atoi(argv[4]) : 50;
+    const int reps = argc > 5 ? std::atoi(argv[5]) : 5;
+    const int64_t px = 544 * 1024, cap = (555489 + 63) / 64 * 64;
+    Args5 a{};
+    void* p;
+    CK(hipMalloc(&p, frames * px));
+    CK(hipMemset(p, 1, frames * px));
+    a.disp = (const uint8_t*)p;
+    CK(hipMalloc(&p, frames * px * 3));
+    CK(hipMemset(p, 2, frames * px * 3));
+    a.bgr = (const uint8_t*)p;
+    for (int k = 0; k < 4; ++k) {
+        CK(hipMalloc(&p, frames * cap * 4));
+        a.o[k] = (float*)p;
+    }
+    CK(hipMalloc(&p, frames * 4));
+    a.sink = (uint32_t*)p;
+    CK(hipMalloc(&p, 8));
+    a.counter = (unsigned long long*)p;
+    a.px = px;
+    a.cap = cap;
+    a.kept = kept;
+    a.nch = 136;
+    a.skip = skip;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const char* names[] = {"K=1 strided (the kernel's shape)", "K=1 atomic regions", "K=frame strided",
+                           "K=frame atomic regions", "pass 1 reads only", "pass-2 writes only, strided",
+                           "K=1 strided, no pass-2 re-read", "writes only, atomic regions"};
+    const int live = a.nch - skip;
+    for (int round = 0; round < 2; ++round)
+        for (int mode = 0; mode < 8; ++mode) {
+            a.mode = mode;
+            float best = 1e30f, tot = 0.f;
+            CK(hipMemset(a.counter, 0, 8));
+            hipLaunchKernelGGL(shape16_kernel, dim3(frames), dim3(256), 0, 0, a);
+            for (int r = 0; r < reps; ++r) {
+                CK(hipMemset(a.counter, 0, 8));
+                CK(hipEventRecord(e0, 0));
+                hipLaunchKernelGGL(shape16_kernel, dim3(frames), dim3(256), 0, 0, a);
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                best = ms < best ? ms : best;
+                tot += ms;
+            }
+            const double p1 = (mode == 5 || mode == 7) ? 0. : px * frames * (1. + 3. * live / a.nch);
+            const double p2r = (mode <= 3) ? px * frames * (double)live / a.nch : 0.;
+            const double wr = mode == 4 ? 0. : 16. * kept * frames;
+            std::printf("{\"round\": %d, \"r5mode\": %d, \"what\": \"%s\", \"skip\": %d, \"kept\": %lld, "
+                        "\"GB\": %.2f, \"best_ms\": %.3f, \"mean_ms\": %.3f, \"TBps_best\": %.2f}\n",
+                        round, mode, names[mode], skip, (long long)kept, (p1 + p2r + wr) / 1e9, best, tot / reps,
+                        (p1 + p2r + wr) / best / 1e9);
+            std::fflush(stdout);
+        }
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "r05") return main_r05(argc, argv);
     const int frames = argc > 1 ? std::atoi(argv[1]) : 4096;
     const int64_t px = 544 * 1024;
     const int64_t kept = argc > 2 ? std::atoll(argv[2]) : 277200;   // 1.135 G kept points / 4096 frames (the bench pipeline)
