@@ -16,8 +16,8 @@ def show(loop, seqs):
         print(f"  batch {q}: " + "  ".join(f"{n[:4]} {tl[n][0]:8.2f}-{tl[n][1]:8.2f}" for n in STAGES), flush=True)
 
 ONLY = os.environ.get("PROBE_ONLY")   # e.g. "caller2": that configuration alone, nothing after it
-for source, slots in (("caller", 2), ("caller", 1), ("synth", 2)):
-    if ONLY and ONLY != f"{source}{slots}":
+for source, slots in (("caller", 2), ("caller", 1), ("synth", 2), ("caller", 3), ("synth", 3)):
+    if ONLY and f"{source}{slots}" not in ONLY.split(","):
         continue
     with FrameLoop(F, slots=slots, source=source, carmask=mask) as loop:
         for i in range(6):
