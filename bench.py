@@ -501,8 +501,9 @@ def loop_extra(args, device, first, mask):
     """stereovision.py:53-136 minus the cv2 drawing over a SEQUENCE of 4096-frame batches (svx.loop.FrameLoop):
     pre-pass -> maskpoints -> RANSAC(600) -> pipeline with each frame's plane -> road raster + walk, two batches in
     flight on two streams (batch k + 1's RANSAC beside batch k's pipeline and road), against the same loop with
-    one batch at a time. `device_frame_loop` / `_serial`: the frames stay resident in the slots (generated once,
-    as the round-3 device loop ran on a resident batch), so a batch's time is the stages' alone;
+    one batch at a time. `device_frame_loop` / `_serial`: the raw frames stay resident in the slots (generated once;
+    a caller-fed slot keeps the frames written into it and its pre-pass writes the cleaned frames elsewhere, so
+    every batch cleans the same raw frames), so a batch's time is the stages' alone;
     `device_frame_loop_with_input`: every batch first generates its synthetic frames on the device (global ids).
     Steady state: `warm` batches first (buffers, tables, clocks), then `reps` batches timed host-side from the end
     of the last warm-up batch to the end of the last one. Then the parity leg: frames 0..4095 as two 2048-frame
@@ -528,7 +529,8 @@ def loop_extra(args, device, first, mask):
         stage_ms = {name: round(float(np.mean([tl[name][1] - tl[name][0] for tl in tls])), 3) for name in STAGES}
         r = {"ms_per_batch": round(ms, 2), "frames": frames, "frames_per_s": round(frames / ms * 1e3, 1),
              "slots": slots, "batches_timed": reps, "input": "synthetic frames generated per batch on the device"
-             if source == "synth" else "resident frames (generated once per slot)",
+             if source == "synth" else "resident raw frames (generated once per slot and kept; every batch "
+                                       "cleans them again)",
              "stage_ms": stage_ms,
              "stages": ("synthetic input (global ids) -> " if source == "synth" else "") +
                        "prepass(previous+carmask) -> maskpoints -> RANSAC(600, random.seed(g)): draw, eval -> "

@@ -258,6 +258,8 @@ int ensure_tables(Device& d, int H, int W, const sv_camera& cam, hipStream_t s) 
 // ---------------------------------------------------------------------------
 // batch object
 // ---------------------------------------------------------------------------
+struct sv_batch;
+static uint8_t* input_disp(sv_batch* b);
 struct sv_batch {
     int device = 0;
     int frames = 0, H = 0, W = 0, step = 1;
@@ -307,6 +309,11 @@ struct sv_batch {
     int64_t rbound = -1;        // the last prepare's device-side bound of the counts (-1: the counts are read back)
     int trace_trials = 0, trace_k = 0, traced_trials = 0;   // requested; k and trials of the recorded trace
     bool have_mask = false;
+    // keep_input (a caller-fed frame loop slot): the frames written by synth / upload / sgbm go to `raw`, and the
+    // pre-pass reads them there and writes the cleaned frames to `disp`, so resubmitting the slot cleans the same
+    // raw frames again (fillDisparity returns a new array, functions.py:140-147)
+    bool keep_input = false;
+    DevBuf raw;
     int64_t mask_n2 = 0;        // the mask's points on the step-2 grid (an upper bound of every frame's maskpoints)
     // pipeline control block (one memset per call): hist | counts | err
     uint32_t* hist = nullptr;
@@ -346,6 +353,10 @@ struct sv_batch {
         return hipEventRecord(pool[*idx], stream);
     }
 };
+
+// where the batch's frames are written: the raw-input buffer (keep_input) or the disparity the stages read
+static uint8_t* input_disp(sv_batch* b) { return b->keep_input ? b->raw.as<uint8_t>() : b->disp.as<uint8_t>(); }
+
 
 extern "C" {
 
@@ -562,7 +573,7 @@ int sv_batch_destroy(sv_batch* b) {
     for (DevBuf* x : {&b->disp, &b->bgr, &b->X, &b->Y, &b->Z, &b->oxb, &b->oyb, &b->ozb, &b->xyz, &b->ppxy, &b->ctrl, &b->masks,
                       &b->carmask, &b->road, &b->rmap, &b->nz, &b->nzcount, &b->mpts, &b->mpk, &b->rres, &b->rtab, &b->rtrace, &b->fplanes, &b->dplane, &b->abc,
                       &b->pairL, &b->pairR, &b->rsidx, &b->rtri, &b->bgrL, &b->bgrR,
-                      &b->glut, &b->ghist, &b->sgflags, &b->prev0buf, &b->rdbuf, &b->rbits, &b->roff})
+                      &b->glut, &b->ghist, &b->sgflags, &b->prev0buf, &b->rdbuf, &b->rbits, &b->roff, &b->raw})
         if (x->p) (void)hipFree(x->p);
     if (b->hcnt) (void)hipHostFree(b->hcnt);
     if (b->cnt_ev) (void)hipEventDestroy(b->cnt_ev);
@@ -608,7 +619,7 @@ int sv_batch_synth(sv_batch* b, int64_t first_frame_id) {
     if (!b) return fail(SV_E_ARG, "null batch");
     if (b->Wu != b->W) return fail(SV_E_ARG, "synthetic frames need W %% 8 == 0 (W=%d)", b->Wu);
     HIP_TRY(hipSetDevice(b->device));
-    HIP_TRY(launch_synth(b->kp, b->disp.as<uint8_t>(), b->with_bgr ? b->bgr.as<uint8_t>() : nullptr,
+    HIP_TRY(launch_synth(b->kp, input_disp(b), b->with_bgr ? b->bgr.as<uint8_t>() : nullptr,
                          b->frames, first_frame_id, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     return SV_OK;
@@ -619,7 +630,7 @@ int sv_batch_upload(sv_batch* b, int frame, const uint8_t* disp, const uint8_t* 
     if (bgr && !b->with_bgr) return fail(SV_E_ARG, "batch created without bgr");
     HIP_TRY(hipSetDevice(b->device));
     const size_t px = (size_t)b->H * b->W;
-    uint8_t* dd = b->disp.as<uint8_t>() + px * frame;
+    uint8_t* dd = input_disp(b) + px * frame;
     if (b->Wu == b->W) {
         HIP_TRY(hipMemcpyAsync(dd, disp, px, hipMemcpyHostToDevice, b->stream));
     } else {   // rows at the padded stride, pad columns zero (outside every grid)
@@ -1249,10 +1260,13 @@ static int batch_prepass_impl(sv_batch* b, int option, const uint8_t* dprev0) {
     uint8_t* masked = nullptr;
     const uint8_t* mff = nullptr;
     uint8_t* disp = b->disp.as<uint8_t>();
+    const uint8_t* in = input_disp(b);   // keep_input: the raw frames, read here and never written
+    const int64_t px = (int64_t)b->H * b->W;
     if (option == 1) {
-        HIP_TRY(launch_fill_prev(disp, disp, masked, mff, dprev0, b->frames, (int64_t)b->H * b->W, b->stream));
-    } else if (option == 2) {
-        HIP_TRY(launch_fill_mean(disp, masked, mff, b->frames, b->H, b->W, b->Wu, b->stream));
+        HIP_TRY(launch_fill_prev(in, disp, masked, mff, dprev0, b->frames, px, b->stream));
+    } else {
+        if (in != disp) HIP_TRY(hipMemcpyAsync(disp, in, (size_t)px * b->frames, hipMemcpyDeviceToDevice, b->stream));
+        if (option == 2) HIP_TRY(launch_fill_mean(disp, masked, mff, b->frames, b->H, b->W, b->Wu, b->stream));
     }
     return SV_OK;
 }
@@ -2260,7 +2274,7 @@ int sv_batch_sgbm(sv_batch* b, const sv_sgbm_params* prm, int max_disparity, int
         sc.flags = b->sgflags.as<uint32_t>() + f0;
         HIP_TRY(launch_sgbm_compute(k, b->pairL.as<uint8_t>() + px * f0, b->pairR.as<uint8_t>() + px * f0, n, sc,
                                     b->stream));
-        HIP_TRY(launch_speckle_scale(k, n, sc, b->disp.as<uint8_t>() + opx * f0, nullptr, b->stream));
+        HIP_TRY(launch_speckle_scale(k, n, sc, input_disp(b) + opx * f0, nullptr, b->stream));
     }
     HIP_TRY(b->timed_event(&t1));
     HIP_TRY(hipEventRecord(b->ev[5], b->stream));
@@ -2357,6 +2371,12 @@ int sv_loop_create(int device, const sv_loop_params* prm, const sv_camera* cam, 
     for (int i = 0; i < q.slots && rc == SV_OK; ++i) {
         rc = sv_batch_create(device, q.frames, q.H, q.W, q.step, 1, 1, &L->slot[(size_t)i]);
         if (rc == SV_OK) L->slot[(size_t)i]->timing = false;
+        if (rc == SV_OK && q.source == 0) {   // caller-fed: the frames the caller writes stay as written
+            sv_batch* sb = L->slot[(size_t)i];
+            const hipError_t ee = sb->raw.ensure(sb->disp.bytes);
+            if (ee != hipSuccess) rc = fail(SV_E_HIP, "sv_loop_create: %s", hipGetErrorString(ee));
+            else sb->keep_input = true;
+        }
         if (rc == SV_OK && carmask) rc = sv_batch_set_mask(L->slot[(size_t)i], carmask);
         if (rc == SV_OK && q.road == 2) rc = sv_batch_road_map(L->slot[(size_t)i], 1);
         if (rc == SV_OK && q.road) rc = sv_batch_road_bits(L->slot[(size_t)i], 1);
@@ -2471,7 +2491,7 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     HIP_TRY(begin(kLsInput));
     if (q.source == 1) {
         if (b->Wu != b->W) return fail(SV_E_ARG, "synthetic frames need W %% 8 == 0 (W=%d)", b->Wu);
-        HIP_TRY(launch_synth(b->kp, b->disp.as<uint8_t>(), b->bgr.as<uint8_t>(), b->frames, first_frame_id, st));
+        HIP_TRY(launch_synth(b->kp, input_disp(b), b->bgr.as<uint8_t>(), b->frames, first_frame_id, st));
     }
     HIP_TRY(end(kLsInput));
     // pre-pass (stereovision.py:53-76): frame 0 cleaned with the previous batch's last cleaned frame

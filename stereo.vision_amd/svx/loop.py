@@ -63,7 +63,9 @@ class FrameLoop:
         return v
 
     def acquire(self):
-        """The Batch the next submit() runs (source="caller": fill it first, e.g. upload() or sgbm())."""
+        """The Batch the next submit() runs (source="caller": fill it first, e.g. upload() or sgbm(); the slot keeps
+        the frames written into it — the pre-pass writes the cleaned frames elsewhere — so a slot submitted again
+        without refilling processes the same raw frames)."""
         out = ctypes.c_void_p()
         _abi.call("sv_loop_acquire", self._h, ctypes.byref(out))
         return self._view(out.value)

@@ -146,6 +146,32 @@ def test_caller_filled_batches_equal_one_batch(mask, H, W, step):
         assert np.array_equal(b.read_road_map(3), want_map[1])
 
 
+@pytest.mark.parametrize("prepass", ["mean", "none"])
+def test_caller_slot_keeps_its_raw_frames(mask, prepass):
+    """A caller-fed slot keeps the frames the caller wrote: the pre-pass reads them there and writes the cleaned
+    frames elsewhere, so submitting the slot again without refilling it processes the same raw frames (with a
+    per-frame pre-pass, fillAltDisparity or none, the results are identical), and the raw frames are never
+    overwritten by a clean."""
+    import oracle
+    from svx.loop import FrameLoop
+    frames = [oracle.synth_frame(g) for g in range(40, 44)]
+    with FrameLoop(4, slots=1, source="caller", prepass=prepass, seed_base=3, carmask=mask) as loop:
+        b = loop.acquire()
+        for f, (d, c) in enumerate(frames):
+            b.upload(f, d, c)
+        s0 = loop.submit(40)
+        loop.wait(s0)
+        b0, _ = loop.batch(s0)
+        want = b0.digest("pipeline")
+        want_r = [b0.read_ransac(f)["trial"] for f in range(4)]
+        for rep in range(2):
+            loop.acquire()   # not refilled
+            s1 = loop.submit(40)
+            b1, _ = loop.batch(s1)
+            assert np.array_equal(b1.digest("pipeline"), want), rep
+            assert [b1.read_ransac(f)["trial"] for f in range(4)] == want_r, rep
+
+
 def test_step2_resident_batches_equal_one_batch(mask):
     """Two 1024-frame batches at the reference's step 2 (the resident pipeline, road from its points: the
     bitmap is step-1 only) equal one 2048-frame batch frame for frame: RANSAC, pipeline digests, road."""
