@@ -32,7 +32,7 @@ for source, slots in (("caller", 2), ("caller", 1), ("synth", 2), ("caller", 3),
         print(f"source={source} slots={slots}: {dt:.2f} ms/batch", flush=True)
         show(loop, range(s - slots + 1, s + 1))
 
-if ONLY:
+if ONLY and not os.environ.get("PROBE_RANSAC"):
     sys.exit(0)
 # the batched RANSAC alone (maskpoints + draw + eval), 4096 carmask frames
 with sb.Batch(F, step=1, with_bgr=True, with_points=True) as rb:
@@ -43,6 +43,8 @@ with sb.Batch(F, step=1, with_bgr=True, with_points=True) as rb:
         rb.ransac(seed_base=0, trials=600, sync=False)
     rb.sync()
     print(f"ransac alone: {(time.perf_counter() - t0) / 5 * 1e3:.3f} ms", flush=True)
+if ONLY:
+    sys.exit(0)
 
 # two streams, K1 on each: concurrent?
 a = sb.Batch(2048, step=1, with_bgr=False); a.synth(0)
