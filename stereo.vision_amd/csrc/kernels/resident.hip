@@ -508,23 +508,29 @@ __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP, LC>& r, int c, u
         // its own kept points in turn: at most 1/4 of the lanes idle, and no LDS staging writes and reads
         // (16384: DIAGNOSTIC A/B, always stage)
 #pragma unroll
-        for (int b = 0; b < NPL; ++b) {
-            if ((keep >> b) & 1u) {
-                const uint32_t o = atomicAdd(&hist[r_bin_sel(r_col<STEP, QP, LC>(r.cw[b >> 2], b & 3))], 1u);
-                cand |= o < lim;
+        for (int b0 = 0; b0 < NPL; b0 += 4) {
+            uint32_t o[4];
+#pragma unroll
+            for (int b = b0; b < b0 + 4; ++b) {
+                o[b - b0] = lim;
+                if ((keep >> b) & 1u) o[b - b0] = atomicAdd(&hist[r_bin_sel(r_col<STEP, QP, LC>(r.cw[b >> 2], b & 3))], 1u);
             }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cand |= o[k] < lim;
         }
     } else {
         const uint32_t wtotal = r_stage_colours_sel<STEP, QP, LC>(keep, r.cw, wstage, dump, pos0);
-        for (uint32_t j = lane; j < ((p.ablate & 512) ? 0u : wtotal); j += 2 * kWave) {   // two colours in flight
-            const bool v1 = j + kWave < wtotal;
-            const uint32_t c0 = wstage[j];
-            const uint32_t c1 = wstage[v1 ? j + kWave : j];
-            const uint32_t b0 = r_bin_sel(c0), b1 = r_bin_sel(c1);
-            const uint32_t o0 = atomicAdd(&hist[b0], 1u);
-            uint32_t o1 = lim;
-            if (v1) o1 = atomicAdd(&hist[b1], 1u);
-            cand |= (o0 < lim) | (o1 < lim);
+        for (uint32_t j = lane; j < ((p.ablate & 512) ? 0u : wtotal); j += 4 * kWave) {   // four colours in flight
+            uint32_t o[4], cl[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cl[k] = wstage[min(j + k * kWave, wtotal - 1)];   // the reads first
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                o[k] = lim;
+                if (j + k * kWave < wtotal) o[k] = atomicAdd(&hist[r_bin_sel(cl[k])], 1u);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cand |= o[k] < lim;
         }
     }
     if (__ballot(cand) && lane == 0) atomicOr(&dirty[c >> 5], 1u << (c & 31));
