@@ -24,61 +24,69 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+// grid (blocks over a frame's quads, frames): a quad's row and column from one 32-bit multiply-shift (fastdiv40,
+// exact below 2^28 quads a frame), its pixels' counter from one 64-bit base; the row's disparity trend once a quad
 __global__ __launch_bounds__(256) void synth_kernel(uint8_t* __restrict__ disp, uint8_t* __restrict__ bgr,
-                                                    int H, int W, int frames, int64_t first_frame) {
-    const int64_t quads = (int64_t)frames * H * (W / 4);
-    for (int64_t g = blockIdx.x * 256ll + threadIdx.x; g < quads; g += (int64_t)gridDim.x * 256) {
-        const int64_t px0 = g * 4;
-        const int64_t fl = px0 / ((int64_t)H * W);
-        const int64_t rem = px0 - fl * H * W;
-        const int y = (int)(rem / W);
-        const int x0 = (int)(rem - (int64_t)y * W);
-        uint32_t dw = 0;
-        uint32_t c[3] = {0, 0, 0};
-        for (int k = 0; k < 4; ++k) {
-            const uint64_t idx = ((uint64_t)(first_frame + fl) * H + y) * W + (x0 + k);
-            const uint64_t r = mix64(idx + 0x5EED000000000001ull);
-            const uint64_t r2 = mix64(idx + 0x5EED000000000002ull);
+                                                    int H, int W, int frames, int64_t first_frame, uint64_t Wq_m40) {
+    const int Wq = W / 4;
+    const int qf = H * Wq;   // quads a frame
+    for (int f = blockIdx.y; f < frames; f += gridDim.y) {
+        const int64_t fq = (int64_t)f * qf;
+        for (int qi = blockIdx.x * 256 + threadIdx.x; qi < qf; qi += gridDim.x * 256) {
+            const int y = fastdiv40(qi, Wq_m40);
+            const int x0 = 4 * (qi - y * Wq);
+            const uint64_t base = ((uint64_t)(first_frame + f) * H + y) * W + x0;
             // floor((3*(y-200))/5) with Python floor semantics
             const int num = 3 * (y - 200);
-            int t = (num >= 0) ? num / 5 : -((-num + 4) / 5);
-            t += (int)((r >> 8) & 7) - 3;
-            t = t < 0 ? 0 : (t > 254 ? 254 : t);
-            uint32_t d = (uint32_t)(t & ~1);
-            if ((r & 0xFF) < 38) d = 0;
-            dw |= d << (8 * k);
-            uint32_t B, G, R;
-            if (y >= 262) {
-                B = 110 + (uint32_t)(r2 & 3);
-                G = 100 + (uint32_t)((r2 >> 2) & 3);
-                R = 90 + (uint32_t)((r2 >> 4) & 3);
-            } else {
-                B = (uint32_t)(r2 & 255);
-                G = (uint32_t)((r2 >> 8) & 255);
-                R = (uint32_t)((r2 >> 16) & 255);
+            const int trend = (num >= 0) ? num / 5 : -((-num + 4) / 5);
+            uint32_t dw = 0;
+            uint32_t c[3] = {0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t idx = base + k;
+                const uint64_t r = mix64(idx + 0x5EED000000000001ull);
+                const uint64_t r2 = mix64(idx + 0x5EED000000000002ull);
+                int t = trend + (int)((r >> 8) & 7) - 3;
+                t = t < 0 ? 0 : (t > 254 ? 254 : t);
+                uint32_t d = (uint32_t)(t & ~1);
+                if ((r & 0xFF) < 38) d = 0;
+                dw |= d << (8 * k);
+                uint32_t B, G, R;
+                if (y >= 262) {
+                    B = 110 + (uint32_t)(r2 & 3);
+                    G = 100 + (uint32_t)((r2 >> 2) & 3);
+                    R = 90 + (uint32_t)((r2 >> 4) & 3);
+                } else {
+                    B = (uint32_t)(r2 & 255);
+                    G = (uint32_t)((r2 >> 8) & 255);
+                    R = (uint32_t)((r2 >> 16) & 255);
+                }
+                const int o = 3 * k;
+                c[(o + 0) >> 2] |= B << (8 * ((o + 0) & 3));
+                c[(o + 1) >> 2] |= G << (8 * ((o + 1) & 3));
+                c[(o + 2) >> 2] |= R << (8 * ((o + 2) & 3));
             }
-            const int o = 3 * k;
-            c[(o + 0) >> 2] |= B << (8 * ((o + 0) & 3));
-            c[(o + 1) >> 2] |= G << (8 * ((o + 1) & 3));
-            c[(o + 2) >> 2] |= R << (8 * ((o + 2) & 3));
-        }
-        reinterpret_cast<uint32_t*>(disp)[g] = dw;
-        if (bgr) {
-            uint32_t* cb = reinterpret_cast<uint32_t*>(bgr) + 3 * g;
-            cb[0] = c[0];
-            cb[1] = c[1];
-            cb[2] = c[2];
+            reinterpret_cast<uint32_t*>(disp)[fq + qi] = dw;
+            if (bgr) {
+                uint32_t* cb = reinterpret_cast<uint32_t*>(bgr) + 3 * (fq + qi);
+                cb[0] = c[0];
+                cb[1] = c[1];
+                cb[2] = c[2];
+            }
         }
     }
 }
 
 hipError_t launch_synth(const KParams& p, uint8_t* disp, uint8_t* bgr, int frames,
                         int64_t first_frame, hipStream_t s) {
-    const int64_t quads = (int64_t)frames * p.H * (p.W / 4);
-    int64_t blocks = (quads + 255) / 256;
-    if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, s, disp, bgr, p.H, p.W,
-                       frames, first_frame);
+    if (frames <= 0) return hipSuccess;
+    const int64_t qf = (int64_t)p.H * (p.W / 4);
+    if (qf <= 0) return hipSuccess;
+    if (qf >= (1ll << 28) || p.W % 4) return hipErrorInvalidValue;   // fastdiv40's range; whole quads a row
+    const unsigned bx = (unsigned)std::min<int64_t>((qf + 255) / 256, 1024);
+    const unsigned by = (unsigned)std::min(frames, 65535);
+    const uint64_t wq_m40 = ((1ull << 40) + (uint64_t)(p.W / 4) - 1) / (uint64_t)(p.W / 4);
+    hipLaunchKernelGGL(synth_kernel, dim3(bx, by), dim3(256), 0, s, disp, bgr, p.H, p.W, frames, first_frame, wq_m40);
     return hipGetLastError();
 }
 

@@ -870,7 +870,8 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
     double* __restrict__ tri, const int32_t* __restrict__ fstat, double* __restrict__ out_abc,
     double* __restrict__ out_err, int32_t* __restrict__ out_trial, uint32_t* __restrict__ out_flags, int ablate,
     int lds_pts_words) {
-    extern __shared__ uint32_t ev_dyn[];
+    extern __shared__ uint4 ev_dyn4[];   // 16-byte aligned: the points' fill stores 16 bytes a lane
+    uint32_t* ev_dyn = reinterpret_cast<uint32_t*>(ev_dyn4);
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.x;
     const int64_t n64 = counts[frame];
@@ -896,7 +897,28 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
         return;
     }
     if constexpr (LDS_PTS) {
-        for (int64_t q = tid; q < n64; q += kRBEvalThreads) ev_dyn[q] = fpk[q];
+        // 16-byte loads, four in flight a thread (the frame's words start 16-byte aligned when cap % 4 == 0)
+        int64_t done = 0;
+        if ((reinterpret_cast<uintptr_t>(fpk) & 15) == 0) {
+            const uint4* f4 = reinterpret_cast<const uint4*>(fpk);
+            uint4* l4 = reinterpret_cast<uint4*>(ev_dyn);
+            const int64_t n4 = n64 >> 2;
+            for (int64_t b = 0; b < n4; b += 4 * kRBEvalThreads) {
+                uint4 v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int64_t q = b + i * kRBEvalThreads + tid;
+                    v[i] = f4[q < n4 ? q : 0];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int64_t q = b + i * kRBEvalThreads + tid;
+                    if (q < n4) l4[q] = v[i];
+                }
+            }
+            done = n4 << 2;
+        }
+        for (int64_t q = done + tid; q < n64; q += kRBEvalThreads) ev_dyn[q] = fpk[q];
         P = ev_dyn;
     }
     double* scr = reinterpret_cast<double*>(ev_dyn + (LDS_PTS ? lds_pts_words : 0));   // [T][2]
@@ -920,14 +942,17 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
         __syncthreads();   // the records are read by other waves below (same workgroup: same L1)
     }
     // screen every trial in fp32 (one wave a trial): the mean distance from the
-    // packed points and, per point, the bound (|Xa| + |Yb| + |Zc| + 1) 2^-18 / |abc|
-    // on its difference to the fp64 distance. A term's error: fp32 X, Y, Z within
-    // 2^-21 relative, a, b, c rounded to fp32, a product and two fmas, the -1:
-    // <= (T + 1) 2^-20.33 (T = |Xa| + |Yb| + |Zc|); a lane's fp32 sum of <= 10
-    // terms adds <= 9 x 2^-24 of them, <= (T + 1) 2^-20.83 each: together
-    // <= (T + 1) 2^-19.55, under the bound's 2^-18 (computed in fp32 as well: it
-    // is low by at most ~2^-19.3 relative) with a margin of ~2.9x. The lanes'
-    // sums are added in fp64.
+    // packed points and, per point, the bound (T' + 1) 2^-18 / |abc| on its
+    // difference to the fp64 distance, T' = rcp(d) (|cx Ba| + |cy Bb| + |Cc|) (the
+    // term's magnitudes, ~ |Xa| + |Yb| + |Zc|; `point` below). A term's error:
+    // cx, cy (x - cw_hi: exact, or one rounding), Ba, Bb, Cc rounded to fp32 and
+    // the two inner fmas, each <= 2^-24 of the magnitudes: <= 4 x 2^-24 T' d in
+    // the sum; rcp(d) within 1 ulp (2^-23 T'); the last fma 2^-24 (T' + 1):
+    // together <= 7 x 2^-24 (T' + 1). A lane's fp32 sum of <= 10 terms adds
+    // <= 9 x 2^-24 of them: in all <= 16 x 2^-24 (T' + 1) = 2^-20 (T' + 1), under
+    // the bound's 2^-18 (its sum in fp32, low by at most ~2^-20 relative) with a
+    // margin of ~4x. (The reference's own fp64 roundings are ~2^-50 (T + 1).) The
+    // lanes' sums are added in fp64.
     if (!(ablate & 1)) {
         // software-pipelined over the wave's trials: the next trial's indices and
         // record are loaded (global, just written by the draw kernel) while this
@@ -935,18 +960,18 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
         constexpr int NW = kRBEvalThreads / 64;
         // one point's fp32 distance term and bound term, summed per lane in fp32 (at most 10 terms a lane per
         // batch; the batches and the lanes in fp64): the sum's rounding, <= 9 x 2^-24 of the summed terms, stays
-        // inside the bound's margin (see the note at the eval kernel)
-        const auto point = [&](uint32_t u, float a, float b, float c, float fa, float fb, float fc, float& sum,
-                               float& bnd) {
-            const int x = (int)(u & 0xFFF), y = (int)((u >> 12) & 0xFFF);
+        // inside the bound's margin (see the note at the eval kernel). Per trial: Ba = B a, Bb = B b and
+        // Cc = fB c - cw_lo B a - ch_lo B b (fp64, rounded to fp32), so with cx = x - cw_hi, cy = y - ch_hi the term
+        // is |rcp(d) (cx Ba + cy Bb + Cc) - 1| (three fmas) and its bound term rcp(d) (|cx Ba| + |cy Bb| + |Cc|)
+        // (the +1 of every term is added as k at the end). `live` masks the lanes past the sample (no branch).
+        const auto point = [&](uint32_t u, bool live, float Ba, float Bb, float Cc, float& sum, float& bnd) {
+            const float cx = (float)(u & 0xFFF) - cp.cw_hi, cy = (float)((u >> 12) & 0xFFF) - cp.ch_hi;
             const float rr = __builtin_amdgcn_rcpf((float)(u >> 24));
-            const float K = cp.B32 * rr;
-            const float X = centred(x, cp.cw_hi, cp.cw_lo) * K;
-            const float Y = centred(y, cp.ch_hi, cp.ch_lo) * K;
-            const float Z = cp.fB32 * rr;
-            const float dot = __builtin_fmaf(Z, c, __builtin_fmaf(X, a, Y * b));
-            sum += __builtin_fabsf(dot - 1.0f);
-            bnd += __builtin_fmaf(fa, __builtin_fabsf(X), __builtin_fmaf(fb, __builtin_fabsf(Y), fc * Z)) + 1.0f;
+            const float t = __builtin_fmaf(rr, __builtin_fmaf(cx, Ba, __builtin_fmaf(cy, Bb, Cc)), -1.0f);
+            const float q = __builtin_fmaf(__builtin_fabsf(cx), __builtin_fabsf(Ba),
+                                           __builtin_fmaf(__builtin_fabsf(cy), __builtin_fabsf(Bb), __builtin_fabsf(Cc)));
+            sum += live ? __builtin_fabsf(t) : 0.0f;
+            bnd = __builtin_fmaf(rr, live ? q : 0.0f, bnd);
         };
         const auto finish = [&](int t, const double (&rec)[kRBTri], double sum, double bnd) {
 #pragma unroll
@@ -957,17 +982,14 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
             if (lane == 0) {   // the screened mean and its bound; bound -1 marks a singular trial
                 const double d = rec[3];
                 scr[2 * t] = sum / (d * k);
-                scr[2 * t + 1] = rec[4] == 1.0 ? -1.0 : bnd * 0x1p-18 / (d * k);
+                scr[2 * t + 1] = rec[4] == 1.0 ? -1.0 : (bnd + (double)k) * 0x1p-18 / (d * k);
             }
         };
         {
             auto load = [&](int t, uint32_t (&ix)[kRBGather], double (&rec)[kRBTri]) {
                 const IdxT* idx = fidx + (int64_t)t * k;
 #pragma unroll
-                for (int v = 0; v < kRBGather; ++v) {
-                    const int j = lane + kWave * v;
-                    ix[v] = j < k ? (uint32_t)idx[j] : 0u;
-                }
+                for (int v = 0; v < kRBGather; ++v) ix[v] = (uint32_t)idx[min(lane + kWave * v, k - 1)];   // no branch
 #pragma unroll
                 for (int q = 0; q < kRBTri; ++q) rec[q] = ftri[(int64_t)t * kRBTri + q];
             };
@@ -984,25 +1006,21 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
                 if (t + NW < T) load(t + NW, nix, nrec);
                 double sum = 0.0, bnd = 0.0;
                 if (rec[4] != 1.0) {
-                    const float a = (float)rec[0], b = (float)rec[1], c = (float)rec[2];
-                    const float fa = __builtin_fabsf(a), fb = __builtin_fabsf(b), fc = __builtin_fabsf(c);
-                    for (int j0 = lane, g = 0; j0 < k; j0 += kRBGather * kWave, ++g) {
+                    const double Ba64 = cp.B * rec[0], Bb64 = cp.B * rec[1];
+                    const float Ba = (float)Ba64, Bb = (float)Bb64;
+                    const float Cc = (float)(cp.fB * rec[2] - (double)cp.cw_lo * Ba64 - (double)cp.ch_lo * Bb64);
+                    for (int j0 = lane, g = 0; j0 < k + lane; j0 += kRBGather * kWave, ++g) {   // uniform
                         uint32_t u[kRBGather];
                         float s32 = 0.0f, b32 = 0.0f;
                         if (g > 0) {   // k > 640: the rest of the sample (same order as the first batch)
 #pragma unroll
-                            for (int v = 0; v < kRBGather; ++v) {
-                                const int j = j0 + kWave * v;
-                                ix[v] = j < k ? (uint32_t)fidx[(int64_t)t * k + j] : 0u;
-                            }
+                            for (int v = 0; v < kRBGather; ++v)
+                                ix[v] = (uint32_t)fidx[(int64_t)t * k + min(j0 + kWave * v, k - 1)];
                         }
 #pragma unroll
                         for (int v = 0; v < kRBGather; ++v) u[v] = P[ix[v]];
 #pragma unroll
-                        for (int v = 0; v < kRBGather; ++v) {
-                            if (j0 + kWave * v >= k) continue;
-                            point(u[v], a, b, c, fa, fb, fc, s32, b32);
-                        }
+                        for (int v = 0; v < kRBGather; ++v) point(u[v], j0 + kWave * v < k, Ba, Bb, Cc, s32, b32);
                         sum += (double)s32;
                         bnd += (double)b32;
                     }

@@ -389,21 +389,15 @@ __global__ __launch_bounds__(256) void road_rowscan_kernel(const uint32_t* __res
     if (tid == 0) nzcount[frame] = all;
 }
 
+// RPW rows a wave (rows y0, y0 + 4, ...: the workgroup's four waves interleave): the next row's 32 words are
+// loaded (scalar) before this row's stores
 template <bool NT, bool NTI>
-__global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restrict__ bits, int H,
-                                                        const int32_t* __restrict__ roff, int64_t cap,
-                                                        uint8_t* __restrict__ img, int32_t* __restrict__ nzout,
-                                                        const uint8_t* __restrict__ bgr, uint8_t* __restrict__ paint) {
+__device__ __forceinline__ void road_row(const uint32_t (&ws)[kRbWords], uint32_t word, int32_t first, int frame,
+                                         int y, int H,
+                                         int64_t cap, uint8_t* __restrict__ img, int32_t* __restrict__ nzout,
+                                         const uint8_t* __restrict__ bgr, uint8_t* __restrict__ paint) {
     const int lane = lane_id();
-    const int frame = blockIdx.y, y = blockIdx.x * 4 + wave_uniform_id();
-    if (y >= H) return;
     const int64_t row = (int64_t)frame * H + y;
-    const uint32_t* rw = bits + row * kRbWords;   // the row's 32 words (wave-uniform address)
-    uint32_t ws[kRbWords];   // all of them in SGPRs before the first store (scalar loads in flight together)
-#pragma unroll
-    for (int i = 0; i < kRbWords; ++i) ws[i] = rw[i];
-    const int32_t first = roff[row];
-    const uint32_t word = rw[lane >> 1];
     const uint32_t b16 = (lane & 1) ? word >> 16 : word & 0xFFFFu;   // pixels 16 lane .. 16 lane + 15
     uint32_t q[4];   // bit k of a nibble -> byte k = 0xFF (v_perm selector 0x0D; 0x0C gives 0x00)
 #pragma unroll
@@ -453,6 +447,43 @@ __global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restri
     }
 }
 
+template <bool NT, bool NTI, int RPW>
+__global__ __launch_bounds__(256) void road_rows_kernel(const uint32_t* __restrict__ bits, int H,
+                                                        const int32_t* __restrict__ roff, int64_t cap,
+                                                        uint8_t* __restrict__ img, int32_t* __restrict__ nzout,
+                                                        const uint8_t* __restrict__ bgr, uint8_t* __restrict__ paint) {
+    const int frame = blockIdx.y;
+    int y = blockIdx.x * 4 * RPW + wave_uniform_id();
+    if (y >= H) return;
+    const uint32_t* fb = bits + (int64_t)frame * H * kRbWords;   // wave-uniform addresses: scalar loads
+    const int32_t* fo = roff + (int64_t)frame * H;
+    uint32_t ws[kRbWords];   // the row's words in SGPRs before its first store
+#pragma unroll
+    for (int i = 0; i < kRbWords; ++i) ws[i] = fb[y * kRbWords + i];
+    uint32_t word = fb[y * kRbWords + (lane_id() >> 1)];   // the lane's own word (pixels 16 lane ..)
+    int32_t first = fo[y];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int yn = y + 4;
+        uint32_t wn[kRbWords], wordn = 0;
+        int32_t fn = 0;
+        const bool more = r + 1 < RPW && yn < H;   // uniform
+        if (more) {
+#pragma unroll
+            for (int i = 0; i < kRbWords; ++i) wn[i] = fb[yn * kRbWords + i];
+            wordn = fb[yn * kRbWords + (lane_id() >> 1)];
+            fn = fo[yn];
+        }
+        road_row<NT, NTI>(ws, word, first, frame, y, H, cap, img, nzout, bgr, paint);
+        if (!more) break;
+#pragma unroll
+        for (int i = 0; i < kRbWords; ++i) ws[i] = wn[i];
+        word = wordn;
+        first = fn;
+        y = yn;
+    }
+}
+
 hipError_t launch_road_bits(const uint32_t* bits, int frames, int H, int W, int32_t* roff, int64_t cap,
                             uint8_t* img, int32_t* nzout, int64_t* nzcount, const uint8_t* bgr, uint8_t* paint,
                             hipStream_t s) {
@@ -469,15 +500,29 @@ hipError_t launch_road_bits(const uint32_t* bits, int frames, int H, int W, int3
     const char* nt = svx_knob("SVX_ROAD_NT");
     const char* nti = svx_knob("SVX_ROAD_IMG_NT");
     const bool wnt = nt && nt[0] == '1', int_ = nti && nti[0] == '1';
-    const dim3 g((H + 3) / 4, frames);
-    if (wnt && int_)
-        hipLaunchKernelGGL((road_rows_kernel<true, true>), g, dim3(256), 0, s, bits, H, roff, cap, img, nzout, bgr, paint);
-    else if (wnt)
-        hipLaunchKernelGGL((road_rows_kernel<true, false>), g, dim3(256), 0, s, bits, H, roff, cap, img, nzout, bgr, paint);
-    else if (int_)
-        hipLaunchKernelGGL((road_rows_kernel<false, true>), g, dim3(256), 0, s, bits, H, roff, cap, img, nzout, bgr, paint);
-    else
-        hipLaunchKernelGGL((road_rows_kernel<false, false>), g, dim3(256), 0, s, bits, H, roff, cap, img, nzout, bgr, paint);
+    // rows a wave (SVX_ROAD_RPW: DIAGNOSTIC A/B, 1 / 2 / 4)
+    const char* rk = svx_knob("SVX_ROAD_RPW");
+    const int rpw = rk ? std::atoi(rk) : 1;
+#define SVX_ROAD_ROWS(R)                                                                                            \
+    do {                                                                                                            \
+        const dim3 g((H + 4 * (R) - 1) / (4 * (R)), frames);                                                        \
+        if (wnt && int_)                                                                                            \
+            hipLaunchKernelGGL((road_rows_kernel<true, true, R>), g, dim3(256), 0, s, bits, H, roff, cap, img,     \
+                               nzout, bgr, paint);                                                                  \
+        else if (wnt)                                                                                               \
+            hipLaunchKernelGGL((road_rows_kernel<true, false, R>), g, dim3(256), 0, s, bits, H, roff, cap, img,    \
+                               nzout, bgr, paint);                                                                  \
+        else if (int_)                                                                                              \
+            hipLaunchKernelGGL((road_rows_kernel<false, true, R>), g, dim3(256), 0, s, bits, H, roff, cap, img,    \
+                               nzout, bgr, paint);                                                                  \
+        else                                                                                                        \
+            hipLaunchKernelGGL((road_rows_kernel<false, false, R>), g, dim3(256), 0, s, bits, H, roff, cap, img,   \
+                               nzout, bgr, paint);                                                                  \
+    } while (0)
+    if (rpw >= 4) SVX_ROAD_ROWS(4);
+    else if (rpw == 2) SVX_ROAD_ROWS(2);
+    else SVX_ROAD_ROWS(1);
+#undef SVX_ROAD_ROWS
     return hipGetLastError();
 }
 

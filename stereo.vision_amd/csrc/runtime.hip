@@ -1481,8 +1481,7 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 
 // DIAGNOSTIC ONLY (env SVX_RANSAC_ABLATE, diagnostic build, documented in DESIGN.md): 1 skips the trial
 // evaluation, 2 draws only the first two trials (results invalid); 4 evaluates every trial in fp64 (no fp32
-// screen; results valid, for A/B); draw kernel (results invalid): 8 no triple loads / collinearity test /
-// plane solve, 16 no random.sample.
+// screen; results valid, for A/B); draw kernel (results invalid): 8 no collinearity test, 16 no random.sample.
 static int ransac_ablate() {
     const char* e = svx_knob("SVX_RANSAC_ABLATE");
     return e ? std::atoi(e) : 0;

@@ -14,12 +14,18 @@ with sb.Batch(F, step=1, with_bgr=True, with_points=True) as b:
     for _ in range(3):
         b.road_raster(sync=False)
     b.sync()
-    res = []
+    variants = os.environ.get("PROBE_RPW", "1").split(",")   # SVX_ROAD_RPW values, alternated in this process
+    res = {v: [] for v in variants}
     for _ in range(5):
-        t0 = time.perf_counter()
-        for _ in range(5):
+        for v in variants:
+            os.environ["SVX_ROAD_RPW"] = v
             b.road_raster(sync=False)
-        b.sync()
-        res.append((time.perf_counter() - t0) / 5 * 1e3)
-    print(f"road from bitmap NT={os.environ.get('SVX_ROAD_NT', '0')} IMG_NT={os.environ.get('SVX_ROAD_IMG_NT', '0')}: min {min(res):.3f} median "
-          f"{sorted(res)[2]:.3f} ms per {F} frames", flush=True)
+            b.sync()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                b.road_raster(sync=False)
+            b.sync()
+            res[v].append((time.perf_counter() - t0) / 5 * 1e3)
+    for v, r in res.items():
+        print(f"road from bitmap RPW={v} NT={os.environ.get('SVX_ROAD_NT', '0')} IMG_NT={os.environ.get('SVX_ROAD_IMG_NT', '0')}: "
+              f"min {min(r):.3f} median {sorted(r)[2]:.3f} ms per {F} frames", flush=True)

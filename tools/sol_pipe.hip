@@ -276,6 +276,10 @@ __global__ __launch_bounds__(256) void sol_kernel(Args a) {
 //           2  K = whole frame, strided                          3  K = whole frame, atomic regions
 //           4  pass 1 reads only                                 5  pass-2 writes only (strided)
 //           6  mode 0 without the pass-2 disparity re-read       7  writes only, dense frames
+//           8  pass-2 writes only, one AoS plane of 16-B records   9  mode 0 with the AoS records
+//          10  K = 1, the next chunk's pass-2 read issued before this chunk's writes and waited for with
+//              s_waitcnt vmcnt(12) (the writes stay outstanding): is K = 1's cost the loads waiting behind the
+//              stores' acknowledgements (gfx9 counts both in vmcnt)?
 struct Args5 {
     const uint8_t* disp;
     const uint8_t* bgr;
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(256) void shape16_kernel(Args5 a) {
     const int live = a.nch - a.skip;
     const auto cw0 = [&](int ch) { return (int64_t)ch * chunk_px / 16; };
     const auto cw1 = [&](int ch) { return min((int64_t)(ch + 1) * chunk_px, a.px) / 16; };
-    if (a.mode != 5 && a.mode != 7) {   // pass 1
+    if (a.mode != 5 && a.mode != 7 && a.mode != 8) {   // pass 1
         for (int ch = 0; ch < a.nch; ++ch) {
             const bool bgr = ch >= a.skip;
             for (int64_t w = cw0(ch) + threadIdx.x; w < cw1(ch); w += 256) {
@@ -317,20 +321,56 @@ __global__ __launch_bounds__(256) void shape16_kernel(Args5 a) {
         base = (a.mode == 1 || a.mode == 3 || a.mode == 7) ? (int64_t)atomicAdd(a.counter, (unsigned long long)a.kept)
                                                            : (int64_t)f * a.cap;
     __syncthreads();
+    if (a.mode == 10) {   // one 16-byte disparity load a lane a chunk (4096 B = 256 lanes x 16 B)
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const float v = (float)f;
+        u32x4 xn;
+        const u32x4* dv = reinterpret_cast<const u32x4*>(d);
+        const auto ld = [&](int ch) {   // the compiler does not track this load: the waits below are ours
+            u32x4 r;
+            const u32x4* ptr = dv + cw0(a.skip + ch) + threadIdx.x;
+            __asm__ volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(ptr) : "memory");
+            return r;
+        };
+        xn = ld(0);
+        for (int c0 = 0; c0 < live; ++c0) {
+            if (c0 == 0) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else __asm__ volatile("s_waitcnt vmcnt(12)" ::: "memory");   // >= 12 stores of the last chunk a lane
+            const u32x4 x = xn;
+            if (c0 + 1 < live) xn = ld(c0 + 1);
+            acc ^= x.x ^ x.w;
+            const int64_t g0 = (a.kept / 4 * c0 / live) * 4, g1 = (a.kept / 4 * (c0 + 1) / live) * 4;
+            for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
+                const v4f q = {v, v, v, v};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + base + g));
+            }
+        }
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (acc == 0x12345678u) a.sink[f] = acc;
+        return;
+    }
     const int K = (a.mode == 2 || a.mode == 3) ? live : 1;
     const float v = (float)f;
     for (int c0 = 0; c0 < live; c0 += K) {
-        if (a.mode != 5 && a.mode != 6 && a.mode != 7)
+        if (a.mode != 5 && a.mode != 6 && a.mode != 7 && a.mode != 8)
             for (int ch = c0; ch < min(c0 + K, live); ++ch)
                 for (int64_t w = cw0(a.skip + ch) + threadIdx.x; w < cw1(a.skip + ch); w += 256) {
                     const uint4 x = d[w];
                     acc ^= x.x ^ x.w;
                 }
         const int64_t g0 = (a.kept / 4 * c0 / live) * 4, g1 = (a.kept / 4 * min(c0 + K, live) / live) * 4;
-        for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
-            const v4f q = {v, v, v, v};
+        if (a.mode == 8 || a.mode == 9) {   // record g = X, Y, Z, P of output g: 1 KiB contiguous a wave-store
+            for (int64_t g = g0 + threadIdx.x; g < g1; g += 256) {
+                const v4f q = {v, v, v, v};
+                __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[0]) + base + g);
+            }
+        } else {
+            for (int64_t g = g0 + 4 * threadIdx.x; g < g1; g += 1024) {
+                const v4f q = {v, v, v, v};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + base + g));
+                for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + base + g));
+            }
         }
     }
     if (acc == 0x12345678u) a.sink[f] = acc;
@@ -351,8 +391,8 @@ static int main_r05(int argc, char** argv) {
     CK(hipMalloc(&p, frames * px * 3));
     CK(hipMemset(p, 2, frames * px * 3));
     a.bgr = (const uint8_t*)p;
-    for (int k = 0; k < 4; ++k) {
-        CK(hipMalloc(&p, frames * cap * 4));
+    for (int k = 0; k < 4; ++k) {   // plane 0 holds the AoS records too (4 x cap floats)
+        CK(hipMalloc(&p, frames * cap * (k == 0 ? 16 : 4)));
         a.o[k] = (float*)p;
     }
     CK(hipMalloc(&p, frames * 4));
@@ -369,10 +409,12 @@ static int main_r05(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     const char* names[] = {"K=1 strided (the kernel's shape)", "K=1 atomic regions", "K=frame strided",
                            "K=frame atomic regions", "pass 1 reads only", "pass-2 writes only, strided",
-                           "K=1 strided, no pass-2 re-read", "writes only, atomic regions"};
+                           "K=1 strided, no pass-2 re-read", "writes only, atomic regions",
+                           "pass-2 writes only, AoS records", "K=1, AoS records",
+                           "K=1, next read before the writes, vmcnt(12)"};
     const int live = a.nch - skip;
     for (int round = 0; round < 2; ++round)
-        for (int mode = 0; mode < 8; ++mode) {
+        for (int mode = 0; mode < 11; ++mode) {
             a.mode = mode;
             float best = 1e30f, tot = 0.f;
             CK(hipMemset(a.counter, 0, 8));
@@ -388,8 +430,8 @@ static int main_r05(int argc, char** argv) {
                 best = ms < best ? ms : best;
                 tot += ms;
             }
-            const double p1 = (mode == 5 || mode == 7) ? 0. : px * frames * (1. + 3. * live / a.nch);
-            const double p2r = (mode <= 3) ? px * frames * (double)live / a.nch : 0.;
+            const double p1 = (mode == 5 || mode == 7 || mode == 8) ? 0. : px * frames * (1. + 3. * live / a.nch);
+            const double p2r = (mode <= 3 || mode == 9 || mode == 10) ? px * frames * (double)live / a.nch : 0.;
             const double wr = mode == 4 ? 0. : 16. * kept * frames;
             std::printf("{\"round\": %d, \"r5mode\": %d, \"what\": \"%s\", \"skip\": %d, \"kept\": %lld, "
                         "\"GB\": %.2f, \"best_ms\": %.3f, \"mean_ms\": %.3f, \"TBps_best\": %.2f}\n",
