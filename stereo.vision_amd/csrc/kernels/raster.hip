@@ -500,9 +500,10 @@ hipError_t launch_road_bits(const uint32_t* bits, int frames, int H, int W, int3
     const char* nt = svx_knob("SVX_ROAD_NT");
     const char* nti = svx_knob("SVX_ROAD_IMG_NT");
     const bool wnt = nt && nt[0] == '1', int_ = nti && nti[0] == '1';
-    // rows a wave (SVX_ROAD_RPW: DIAGNOSTIC A/B, 1 / 2 / 4)
+    // rows a wave: 2 (SVX_ROAD_RPW, DIAGNOSTIC A/B: 1 / 2 / 4 took 1.557 / 1.422 / 1.498 ms per 4096 frames in one
+    // process, profiles/r05/probe_road_rpw_s8.txt)
     const char* rk = svx_knob("SVX_ROAD_RPW");
-    const int rpw = rk ? std::atoi(rk) : 1;
+    const int rpw = rk ? std::atoi(rk) : 2;
 #define SVX_ROAD_ROWS(R)                                                                                            \
     do {                                                                                                            \
         const dim3 g((H + 4 * (R) - 1) / (4 * (R)), frames);                                                        \

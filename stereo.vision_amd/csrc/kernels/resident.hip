@@ -503,6 +503,24 @@ __device__ __forceinline__ void p1_chunk(const P1Regs<STEP, QP, LC>& r, int c, u
     constexpr int NPL = 4 * RCfg<STEP, QP, LC>::QPL;   // grid points a lane holds
     // density threshold in eighths (DIAGNOSTIC A/B: ablate bits 15-16 pick 6, 4, 5 or 7; release: 6)
     const uint32_t dense8 = (0x7546u >> (4 * ((p.ablate >> 15) & 3))) & 0xFu;
+#ifdef SVX_DIAG
+    // DIAGNOSTIC (diagnostic build only, results invalid): 2 no hue binning; 8 the bins without the atomics; 32
+    // plain adds (no return) on spread bins (lane + 64 b mod 1000) without the bin arithmetic; 64 the real bins with
+    // adds that return nothing (no candidates)
+    if (p.ablate & 2) {
+    } else if (p.ablate & (8 | 32 | 64)) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int b = 0; b < NPL; ++b) {
+            if (!((keep >> b) & 1u)) continue;
+            if (p.ablate & 8) acc += r_bin_sel(r_col<STEP, QP, LC>(r.cw[b >> 2], b & 3));
+            else if (p.ablate & 64) __hip_atomic_fetch_add(&hist[r_bin_sel(r_col<STEP, QP, LC>(r.cw[b >> 2], b & 3))], 1u,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else atomicAdd(&hist[(uint32_t)(lane + 64 * b) % 1000u], 1u);
+        }
+        if (acc == 0xFFFFFFFFu) hist[0] = acc;   // keeps the bins
+    } else
+#endif
     if (!(p.ablate & 16384) && wave_sum((uint32_t)__builtin_popcount(keep)) * 8u >= dense8 * 64u * NPL) {
         // uniform: a dense wave (>= 3/4 of its points kept, the road) bins its colours from registers, each lane
         // its own kept points in turn: at most 1/4 of the lanes idle, and no LDS staging writes and reads
@@ -563,6 +581,18 @@ __device__ __forceinline__ void p2_write(const uint32_t* stage, uint32_t a, uint
         const uint32_t m = m0 + lane;
         if (m >= groups) continue;
         const uint32_t g = first + 4 * m;
+#ifdef SVX_DIAG
+        if (p.ablate & 4096) {   // DIAGNOSTIC (diagnostic build only, results invalid): the stores alone
+            if (g >= a && g + 3 < b) {
+                const v4f z = {0.f, 0.f, 0.f, 0.f};
+                __builtin_nontemporal_store(z, reinterpret_cast<v4f*>(oX + g));
+                __builtin_nontemporal_store(z, reinterpret_cast<v4f*>(oY + g));
+                __builtin_nontemporal_store(z, reinterpret_cast<v4f*>(oZ + g));
+                __builtin_nontemporal_store((v4i){0, 0, 0, 0}, reinterpret_cast<v4i*>(oPxy + g));
+            }
+            continue;
+        }
+#endif
         const uint4 u4 = *reinterpret_cast<const uint4*>(&stage[g & SM]);
         const uint32_t u[4] = {u4.x, u4.y, u4.z, u4.w};
         float X[4], Y[4], Z[4];
@@ -670,7 +700,12 @@ __device__ __forceinline__ void p2_chunk(P2Regs<STEP, QP, LC>& r, int c, bool mo
     if (!r.reuse) p2_stage_deltas<STEP, QP, LC>(r, dl);
     const int dlo = r.dlo;
     const bool narrow = r.narrow;
-    if ((dirty[c >> 5] >> (c & 31)) & 1) {   // uniform: candidate chunk (rare)
+#ifdef SVX_DIAG
+    const bool dirty_c = !(p.ablate & 16) && ((dirty[c >> 5] >> (c & 31)) & 1);   // 16: no chunk re-binned (invalid)
+#else
+    const bool dirty_c = (dirty[c >> 5] >> (c & 31)) & 1;
+#endif
+    if (dirty_c) {   // uniform: candidate chunk (rare)
         uint32_t cw[QPL][RCfg<STEP, QP, LC>::CW];
         r_load_bgr<STEP, QP, LC>(fbgr, r.g, p, cw);
         __syncthreads();   // every wave is done writing the previous chunk: sh.stage is free

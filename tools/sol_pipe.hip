@@ -280,6 +280,10 @@ __global__ __launch_bounds__(256) void sol_kernel(Args a) {
 //          10  K = 1, the next chunk's pass-2 read issued before this chunk's writes and waited for with
 //              s_waitcnt vmcnt(12) (the writes stay outstanding): is K = 1's cost the loads waiting behind the
 //              stores' acknowledgements (gfx9 counts both in vmcnt)?
+//          11  mode 0 with each chunk's outputs starting on a 128-byte line (multiples of 32 outputs, as the
+//              kernel writes them: whole lines, the tail carried)      12  mode 11 without the pass-2 re-read
+//          13  mode 11 at the kernel's occupancy (32 KB of LDS a workgroup: 5 a CU)
+//          14  mode 13 with the kernel's two workgroup barriers a chunk in pass 2 and one a chunk in pass 1
 struct Args5 {
     const uint8_t* disp;
     const uint8_t* bgr;
@@ -299,8 +303,11 @@ __global__ __launch_bounds__(256) void shape16_kernel(Args5 a) {
     const int live = a.nch - a.skip;
     const auto cw0 = [&](int ch) { return (int64_t)ch * chunk_px / 16; };
     const auto cw1 = [&](int ch) { return min((int64_t)(ch + 1) * chunk_px, a.px) / 16; };
+    extern __shared__ uint32_t occ_lds[];   // modes 13, 14: launched with 32 KB (the kernel's occupancy)
+    if ((a.mode == 13 || a.mode == 14) && threadIdx.x == 0) occ_lds[0] = 0u;
     if (a.mode != 5 && a.mode != 7 && a.mode != 8) {   // pass 1
         for (int ch = 0; ch < a.nch; ++ch) {
+            if (a.mode == 14) __syncthreads();
             const bool bgr = ch >= a.skip;
             for (int64_t w = cw0(ch) + threadIdx.x; w < cw1(ch); w += 256) {
                 const uint4 x = d[w];
@@ -353,13 +360,18 @@ __global__ __launch_bounds__(256) void shape16_kernel(Args5 a) {
     const int K = (a.mode == 2 || a.mode == 3) ? live : 1;
     const float v = (float)f;
     for (int c0 = 0; c0 < live; c0 += K) {
-        if (a.mode != 5 && a.mode != 6 && a.mode != 7 && a.mode != 8)
+        if (a.mode != 5 && a.mode != 6 && a.mode != 7 && a.mode != 8 && a.mode != 12)   // (13, 14 read)
             for (int ch = c0; ch < min(c0 + K, live); ++ch)
                 for (int64_t w = cw0(a.skip + ch) + threadIdx.x; w < cw1(a.skip + ch); w += 256) {
                     const uint4 x = d[w];
                     acc ^= x.x ^ x.w;
                 }
-        const int64_t g0 = (a.kept / 4 * c0 / live) * 4, g1 = (a.kept / 4 * min(c0 + K, live) / live) * 4;
+        int64_t g0 = (a.kept / 4 * c0 / live) * 4, g1 = (a.kept / 4 * min(c0 + K, live) / live) * 4;
+        if (a.mode == 14) __syncthreads();
+        if (a.mode >= 11 && a.mode <= 14) {   // whole 128-byte lines a chunk (the last chunk ends at kept)
+            g0 &= ~31ll;
+            g1 = min(c0 + K, live) == live ? a.kept : (g1 & ~31ll);
+        }
         if (a.mode == 8 || a.mode == 9) {   // record g = X, Y, Z, P of output g: 1 KiB contiguous a wave-store
             for (int64_t g = g0 + threadIdx.x; g < g1; g += 256) {
                 const v4f q = {v, v, v, v};
@@ -372,6 +384,7 @@ __global__ __launch_bounds__(256) void shape16_kernel(Args5 a) {
                 for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(a.o[k] + base + g));
             }
         }
+        if (a.mode == 14) __syncthreads();
     }
     if (acc == 0x12345678u) a.sink[f] = acc;
 }
@@ -411,18 +424,21 @@ static int main_r05(int argc, char** argv) {
                            "K=frame atomic regions", "pass 1 reads only", "pass-2 writes only, strided",
                            "K=1 strided, no pass-2 re-read", "writes only, atomic regions",
                            "pass-2 writes only, AoS records", "K=1, AoS records",
-                           "K=1, next read before the writes, vmcnt(12)"};
+                           "K=1, next read before the writes, vmcnt(12)", "K=1, chunks on whole lines",
+                           "K=1, whole lines, no pass-2 re-read", "K=1, whole lines, 5 workgroups a CU",
+                           "K=1, whole lines, 5 a CU, the kernel's barriers"};
     const int live = a.nch - skip;
     for (int round = 0; round < 2; ++round)
-        for (int mode = 0; mode < 11; ++mode) {
+        for (int mode = 0; mode < 15; ++mode) {
             a.mode = mode;
             float best = 1e30f, tot = 0.f;
             CK(hipMemset(a.counter, 0, 8));
-            hipLaunchKernelGGL(shape16_kernel, dim3(frames), dim3(256), 0, 0, a);
+            const size_t lds = (mode == 13 || mode == 14) ? 32768 : 0;
+            hipLaunchKernelGGL(shape16_kernel, dim3(frames), dim3(256), lds, 0, a);
             for (int r = 0; r < reps; ++r) {
                 CK(hipMemset(a.counter, 0, 8));
                 CK(hipEventRecord(e0, 0));
-                hipLaunchKernelGGL(shape16_kernel, dim3(frames), dim3(256), 0, 0, a);
+                hipLaunchKernelGGL(shape16_kernel, dim3(frames), dim3(256), lds, 0, a);
                 CK(hipEventRecord(e1, 0));
                 CK(hipEventSynchronize(e1));
                 float ms;
@@ -431,7 +447,9 @@ static int main_r05(int argc, char** argv) {
                 tot += ms;
             }
             const double p1 = (mode == 5 || mode == 7 || mode == 8) ? 0. : px * frames * (1. + 3. * live / a.nch);
-            const double p2r = (mode <= 3 || mode == 9 || mode == 10) ? px * frames * (double)live / a.nch : 0.;
+            const double p2r = (mode <= 3 || mode == 9 || mode == 10 || mode == 11 || mode == 13 || mode == 14)
+                                   ? px * frames * (double)live / a.nch
+                                                                                    : 0.;
             const double wr = mode == 4 ? 0. : 16. * kept * frames;
             std::printf("{\"round\": %d, \"r5mode\": %d, \"what\": \"%s\", \"skip\": %d, \"kept\": %lld, "
                         "\"GB\": %.2f, \"best_ms\": %.3f, \"mean_ms\": %.3f, \"TBps_best\": %.2f}\n",
