@@ -440,6 +440,14 @@ int sv_delta_tables(int device, int H, int W, const sv_camera* cam, int8_t* dx, 
 /* Regenerate one synthetic frame on the device and copy it back. */
 int sv_synth_frame(int device, int64_t frame_id, int H, int W, uint8_t* disp, uint8_t* bgr);
 
+/* ---- image I/O (host only): PNG ingest of the stereo pairs and masks ---------
+ * Replaces cv2.imread at functions.py:29-34 (the masks) and :52-55 (loadImages)
+ * for 8-bit non-interlaced PNGs; svx.io.imread inflates the IDAT stream (zlib) and
+ * this undoes the scanline filters: `in` holds H rows of 1 filter byte + rowbytes,
+ * `out` H x rowbytes; bpp = bytes a pixel (the filters' left neighbour). SV_E_ARG
+ * on a filter type above 4 (a corrupt stream). No device work. */
+int sv_png_unfilter(const uint8_t* in, int H, int rowbytes, int bpp, uint8_t* out);
+
 /* ---- multi-GPU: RCCL over xGMI ----------------------------- */
 /* Frames shard by contiguous global-id ranges (one sv_batch per GPU); the only
  * device-data collective is the broadcast of the plane. Two drivers:

@@ -115,6 +115,7 @@ SIGNATURES = {
     "sv_hue_lut": [I, P],
     "sv_delta_tables": [I, I, I, ctypes.POINTER(Camera), P, P],
     "sv_synth_frame": [I, I64, I, I, P, P],
+    "sv_png_unfilter": [P, I, I, I, P],
     "sv_loop_create": [I, ctypes.POINTER(LoopParams), ctypes.POINTER(Camera), P, ctypes.POINTER(P)],
     "sv_loop_destroy": [P],
     "sv_loop_acquire": [P, ctypes.POINTER(P)],

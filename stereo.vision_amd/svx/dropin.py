@@ -229,6 +229,7 @@ from .ransac import RANSAC  # noqa: E402  (functions.py:278-298)
 from .stages import (calculateColourHistogram, calculatePointErrors, computePlanarThreshold,  # noqa: E402,F401
                      filterPointsByHistogram)
 from .disparity import disparity, gammaChange, greyscale, preProcessImages  # noqa: E402,F401 (functions.py:61-128)
+from .io import getImagePaths, loadImages  # noqa: E402,F401 (functions.py:41-55, PNG ingest without cv2)
 
 # Functions whose GPU results are pinned against the reference itself (fixtures made by running the reference's
 # own code, tests/golden/): installed by default.
@@ -237,8 +238,10 @@ PINNED = ("projectDisparityTo3d", "project3DPointsTo2DImagePoints", "fillAltDisp
           "calculateColourHistogram", "filterPointsByHistogram", "gammaChange", "preProcessImages")
 # Functions that restate OpenCV calls (cv2 is absent here, so nothing pins them to the reference's OpenCV 3.x):
 # StereoSGBM + filterSpeckles (functions.py:104-128), cvtColor + equalizeHist (:88-96), cv2.threshold / bitwise /
-# add (:140-147) and bitwise_and with the carmask (:169-171). Installed only on request (install(.., unpinned=True)).
-UNPINNED = ("disparity", "greyscale", "fillDisparity", "maskDisparity")
+# add (:140-147), bitwise_and with the carmask (:169-171) and cv2.imread's PNG decode behind getImagePaths /
+# loadImages (:41-55; lossless, but OpenCV's channel handling is restated, svx/io.py). Installed only on request
+# (install(.., unpinned=True)).
+UNPINNED = ("disparity", "greyscale", "fillDisparity", "maskDisparity", "getImagePaths", "loadImages")
 PATCHED = PINNED + UNPINNED
 ALIASES = {"project_disparity_to_3d": "projectDisparityTo3d",
            "project_3D_points_to_2D": "project3DPointsTo2DImagePoints"}

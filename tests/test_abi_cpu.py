@@ -106,16 +106,18 @@ def test_install_patches_module_attributes():
 
 
 def test_install_default_is_the_pinned_set():
-    """install(functions) replaces only the functions pinned against the reference's own outputs; the four
-    restatements of OpenCV (disparity, greyscale, fillDisparity, maskDisparity: functions.py:88-96,104-128,
-    140-147,169-171) stay the module's originals unless install(.., unpinned=True)."""
+    """install(functions) replaces only the functions pinned against the reference's own outputs; the
+    restatements of OpenCV (disparity, greyscale, fillDisparity, maskDisparity, and the PNG ingest getImagePaths /
+    loadImages: functions.py:41-55,88-96,104-128,140-147,169-171) stay the module's originals unless
+    install(.., unpinned=True)."""
     import types
 
     from svx import dropin
     orig = {name: (lambda *a, _n=name: _n) for name in dropin.PATCHED}
     m = types.SimpleNamespace(camera_focal_length_px=1.0, stereo_camera_baseline_m=2.0,
                               image_centre_w=3.0, image_centre_h=4.0, **orig)
-    assert set(dropin.UNPINNED) == {"disparity", "greyscale", "fillDisparity", "maskDisparity"}
+    assert set(dropin.UNPINNED) == {"disparity", "greyscale", "fillDisparity", "maskDisparity", "getImagePaths",
+                                    "loadImages"}
     dropin.install(m)
     try:
         for name in dropin.UNPINNED:
