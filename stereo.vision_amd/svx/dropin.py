@@ -99,7 +99,7 @@ def project_frame(disparity, rgb=None, step=REFERENCE_STEP, camera=None):
     return xyz[:k], (out_rgb[:k] if out_rgb is not None else None)
 
 
-from .points import PointList, as_points_array  # noqa: E402,F401  (re-exported)
+from .points import PointList, as_points_array, gather_columns  # noqa: E402,F401  (re-exported)
 
 
 def projectDisparityTo3d(disparity, max_disparity, rgb=[]):  # noqa: N802,B006 (reference signature)
@@ -119,7 +119,7 @@ def project3DPointsTo2DImagePoints(points):  # noqa: N802
     n = len(points)
     if n == 0:
         return np.zeros((0, 2), np.float64)
-    arr = as_points_array(points)
+    arr = gather_columns(points, 0, 3)   # X, Y, Z only (a selection: one C pass, svx/points.py)
     if arr.ndim != 2 or arr.shape[1] < 3:
         raise ValueError(f"points must be rows of at least [X, Y, Z], got shape {arr.shape}")
     out = np.empty((n, 2), np.float64)

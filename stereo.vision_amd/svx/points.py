@@ -12,9 +12,12 @@ stages take the array itself and never create rows. A mutation turns the
 sequence into a plain list of its rows (created then) and it forgets the array.
 """
 import collections.abc
+import ctypes
 import operator
 
 import numpy as np
+
+from . import _abi
 
 
 def select_rows(seq, idx):
@@ -119,6 +122,16 @@ class PointList(collections.abc.MutableSequence):
 
     __hash__ = None
 
+    def rows_spec(self):
+        """(base, idx or None) when the rows are an index selection of a C-contiguous float64 array (what
+        projectDisparityTo3d returns), for the C gathers below; None after a mutation or for another base."""
+        if self._rows is not None:
+            return None
+        b = self._base
+        if not (isinstance(b, np.ndarray) and b.dtype == np.float64 and b.ndim == 2 and b.flags.c_contiguous):
+            return None
+        return b, (None if self._idx is None else np.ascontiguousarray(self._idx, np.int64))
+
     def array(self):
         if self._rows is not None:
             return None
@@ -134,3 +147,46 @@ def as_points_array(points):
     arr = points if isinstance(points, np.ndarray) else np.asarray(list(points) if isinstance(points, PointList)
                                                                    else points)
     return np.ascontiguousarray(arr, dtype=np.float64)
+
+
+def _spec(points, min_cols):
+    if isinstance(points, PointList):
+        spec = points.rows_spec()
+        if spec is not None and spec[0].shape[1] >= min_cols:
+            return spec
+    return None
+
+
+def gather_columns(points, c0, nc):
+    """(n, nc) float64 C-contiguous columns c0..c0+nc-1 of a point sequence (n >= 1, rows of >= c0 + nc values).
+    A PointList over an array is gathered by libsvx in one pass over the selected rows (sv_gather_f64): reads
+    through rows and writes through them are both seen, as with as_points_array, at a fraction of numpy's whole-row
+    gather (bench extras.dropin_frame_chain)."""
+    spec = _spec(points, c0 + nc)
+    if spec is None:
+        arr = as_points_array(points)
+        if arr.ndim != 2 or arr.shape[1] < c0 + nc:
+            return arr   # the caller's shape check reports it
+        return np.ascontiguousarray(arr[:, c0:c0 + nc])
+    base, idx = spec
+    n = len(points)
+    out = np.empty((n, nc), np.float64)
+    _abi.call("sv_gather_f64", _abi.ptr(base), base.shape[1], _abi.ptr(idx), n, c0, nc, _abi.ptr(out))
+    return out
+
+
+def gather_rgb_u8(points):
+    """(n, 3) uint8 R, G, B (columns 3..5) of a point sequence of >= 6-value rows, or None when the rows are not a
+    PointList over an array (the caller converts them itself). ValueError if a colour is not an integer in
+    [0, 255] (sv_gather_rgb_u8)."""
+    spec = _spec(points, 6)
+    if spec is None:
+        return None
+    base, idx = spec
+    n = len(points)
+    out = np.empty((n, 3), np.uint8)
+    rc = _abi.lib().sv_gather_rgb_u8(_abi.ptr(base), ctypes.c_int64(base.shape[1]), _abi.ptr(idx),
+                                     ctypes.c_int64(n), _abi.ptr(out))
+    if rc != 0:
+        raise ValueError("colour stages: R, G, B must be integers in [0, 255]")
+    return out

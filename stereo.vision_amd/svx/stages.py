@@ -31,7 +31,7 @@ import math
 import numpy as np
 
 from . import _abi
-from .points import PointList, as_points_array, select_rows
+from .points import PointList, as_points_array, gather_rgb_u8, select_rows
 
 BINS = 1000
 
@@ -53,6 +53,9 @@ def _rows_array(points, min_cols, what):
 
 
 def _rgb_u8(points):
+    u8 = gather_rgb_u8(points)   # a PointList over the projection's array: one C pass over the selected rows
+    if u8 is not None:
+        return u8
     arr = _rows_array(points, 6, "colour stages")
     rgb = arr[:, 3:6]
     u8 = rgb.astype(np.uint8)
