@@ -433,8 +433,12 @@ int sv_loop_timeline(sv_loop* L, int64_t seq, double* out);
 int sv_batch_digest(sv_batch* b, const sv_camera* cam, int which, uint64_t* out);
 
 
-/* Hue bin of all 2^24 colours, index R<<16|G<<8|B (for exhaustive tests). */
+/* Hue bin of all 2^24 colours, index R<<16|G<<8|B (for exhaustive tests):
+ * sv_hue_lut the exact device function (stage kernels, tiled pipeline);
+ * sv_hue_lut_variant 0 the same, 1 the resident pipeline's fp32 path
+ * (hue_bin_sel: rcp + rint, the exact path in the tie band). */
 int sv_hue_lut(int device, int16_t* out_lut);
+int sv_hue_lut_variant(int device, int variant, int16_t* out_lut);
 /* Back-projection delta tables as computed on the device: dx[d][x], dy[d][y]. */
 int sv_delta_tables(int device, int H, int W, const sv_camera* cam, int8_t* dx, int8_t* dy);
 /* Regenerate one synthetic frame on the device and copy it back. */

@@ -305,24 +305,9 @@ __device__ __forceinline__ uint32_t r_nvalid(const uint32_t (&dw)[RCfg<STEP, QP,
     return n;
 }
 
-// Hue bin as hue_bin_fast (svx_device.h), with the sector select written as
-// value selects so that no lane mask is branched on; the +-4e-4 band around a
-// half-integer takes the exact integer/fp64 path (hue_bin). (A 392 KB
+// The hue bin of a kept colour: hue_bin_sel (svx_device.h), fp32 with the exact path in the tie band. (A 392 KB
 // (rng, n) -> bin table gather instead: 7.40 vs 6.32 ms per call)
-__device__ __forceinline__ uint32_t r_bin_sel(uint32_t col) {
-    const int b = (int)(col & 0xFF), g = (int)((col >> 8) & 0xFF), r = (int)((col >> 16) & 0xFF);
-    const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
-    const int rng = mx - mn;
-    const int nr = g - b, ng = 2 * rng + b - r, nb = 4 * rng + r - g;
-    const int n = (r == mx) ? nr : ((g == mx) ? ng : nb);
-    const float t = ((float)n * __builtin_amdgcn_rcpf((float)rng)) * (500.0f / 3.0f);
-    const float rt = __builtin_rintf(t);
-    const bool near = __builtin_fabsf(t - rt) > 0.5f - 4e-4f;
-    int bin = (int)rt + (n < 0 ? 1000 : 0);
-    bin = rng == 0 ? 0 : bin;
-    if (__builtin_expect(near, 0)) bin = hue_bin(r, g, b);
-    return (uint32_t)bin;
-}
+__device__ __forceinline__ uint32_t r_bin_sel(uint32_t col) { return hue_bin_sel(col); }
 
 // Pack the colours of the keep bits into this wave's LDS region, (lane, bit)
 // order, without branching on lane masks: a point that is not kept writes its

@@ -13,14 +13,17 @@
 
 namespace svx {
 
-__global__ __launch_bounds__(256) void hue_lut_kernel(int16_t* __restrict__ lut) {
+// variant 0: hue_bin (exact; the stage kernels and the tiled pipeline), 1: hue_bin_sel (the resident pipeline's
+// fp32 path). Colour i = R << 16 | G << 8 | B.
+__global__ __launch_bounds__(256) void hue_lut_kernel(int16_t* __restrict__ lut, int variant) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= (1u << 24)) return;
-    lut[i] = (int16_t)hue_bin((int)(i >> 16), (int)((i >> 8) & 255), (int)(i & 255));
+    lut[i] = variant ? (int16_t)hue_bin_sel(i)
+                     : (int16_t)hue_bin((int)(i >> 16), (int)((i >> 8) & 255), (int)(i & 255));
 }
 
-hipError_t launch_hue_lut(int16_t* lut, hipStream_t s) {
-    hipLaunchKernelGGL(hue_lut_kernel, dim3((1u << 24) / 256), dim3(256), 0, s, lut);
+hipError_t launch_hue_lut(int16_t* lut, int variant, hipStream_t s) {
+    hipLaunchKernelGGL(hue_lut_kernel, dim3((1u << 24) / 256), dim3(256), 0, s, lut, variant);
     return hipGetLastError();
 }
 

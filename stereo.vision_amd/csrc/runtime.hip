@@ -1804,14 +1804,17 @@ int sv_select_bins(const int16_t* bins, int64_t n, const uint8_t* ok, int64_t* o
 // ---------------------------------------------------------------------------
 // verification helpers
 // ---------------------------------------------------------------------------
-int sv_hue_lut(int device, int16_t* out_lut) {
+int sv_hue_lut(int device, int16_t* out_lut) { return sv_hue_lut_variant(device, 0, out_lut); }
+
+int sv_hue_lut_variant(int device, int variant, int16_t* out_lut) {
     if (!out_lut) return fail(SV_E_ARG, "null");
+    if (variant != 0 && variant != 1) return fail(SV_E_ARG, "sv_hue_lut_variant: variant %d not 0 or 1", variant);
     Device* d;
     if (int rc = dev_get(device, &d)) return rc;
     std::lock_guard<std::mutex> lk(d->mu);
     DevBuf buf;
     HIP_TRY(buf.ensure(sizeof(int16_t) << 24));
-    hipError_t e = launch_hue_lut(buf.as<int16_t>(), d->stream);
+    hipError_t e = launch_hue_lut(buf.as<int16_t>(), variant, d->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(out_lut, buf.p, sizeof(int16_t) << 24, hipMemcpyDeviceToHost, d->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
     (void)hipFree(buf.p);

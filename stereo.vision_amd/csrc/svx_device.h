@@ -261,20 +261,24 @@ __device__ __forceinline__ bool keep1_lean(float xf, float beta, float df, const
     return e < 0.0f && df != 0.0f;
 }
 
-// Hue bin in fp32 with one rcp: |t - t_exact| <= 2.5 * 2^-23 * |t| < 3e-4,
-// while a non-tie t is >= 1/(2*3*rng) >= 6.5e-4 from a half-integer. *near
-// flags the +-4e-4 band around .5 where the caller must use hue_bin().
-// col = B | G << 8 | R << 16 (bits 24..31 ignored).
-__device__ __forceinline__ int hue_bin_fast(uint32_t col, bool& near) {
+// Hue bin in fp32 with one rcp (the resident pipeline's binning): |t - t_exact| <= 2.5 * 2^-23 * |t| < 3e-4,
+// while a non-tie t is >= 1/(2*3*rng) >= 6.5e-4 from a half-integer, so outside the +-4e-4 band around .5 the
+// fp32 rounding is the exact one; inside it (and at exact ties) the exact integer/fp64 path hue_bin() decides.
+// The sector select is written as value selects. col = B | G << 8 | R << 16 (bits 24..31 ignored). Checked
+// against the reference over all 2^24 colours (sv_hue_lut_variant 1, tests/test_gpu_parity.py).
+__device__ __forceinline__ uint32_t hue_bin_sel(uint32_t col) {
     const int b = (int)(col & 0xFF), g = (int)((col >> 8) & 0xFF), r = (int)((col >> 16) & 0xFF);
     const int mx = max(r, max(g, b)), mn = min(r, min(g, b));
     const int rng = mx - mn;
-    const int n = (r == mx) ? (g - b) : ((g == mx) ? (2 * rng + b - r) : (4 * rng + r - g));
+    const int nr = g - b, ng = 2 * rng + b - r, nb = 4 * rng + r - g;
+    const int n = (r == mx) ? nr : ((g == mx) ? ng : nb);
     const float t = ((float)n * __builtin_amdgcn_rcpf((float)rng)) * (500.0f / 3.0f);
     const float rt = __builtin_rintf(t);
-    near = __builtin_fabsf(t - rt) > 0.5f - 4e-4f;   // NaN (grey) -> false
-    const int bin = (int)rt + (n < 0 ? 1000 : 0);    // (h mod 1): rint(t + 1000) = rint(t) + 1000
-    return rng == 0 ? 0 : bin;
+    const bool near = __builtin_fabsf(t - rt) > 0.5f - 4e-4f;   // NaN (grey) -> false
+    int bin = (int)rt + (n < 0 ? 1000 : 0);                     // (h mod 1): rint(t + 1000) = rint(t) + 1000
+    bin = rng == 0 ? 0 : bin;
+    if (__builtin_expect(near, 0)) bin = hue_bin(r, g, b);
+    return (uint32_t)bin;
 }
 
 // ---------------------------------------------------------------------------

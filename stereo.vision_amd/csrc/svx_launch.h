@@ -24,7 +24,7 @@ hipError_t launch_backproject_f64(const double* xyz, int64_t n, int64_t ld, doub
 int project_compact_tiles(const KParams& p);
 
 // kernels/tables.hip --------------------------------------------------------
-hipError_t launch_hue_lut(int16_t* lut, hipStream_t s);
+hipError_t launch_hue_lut(int16_t* lut, int variant, hipStream_t s);
 // dx bits [256][dx_words], dy bits [256][dy_words]; optional int8 tables.
 // dxT / dyT (PipeBuffers) from dxbits / dybits: 8 x 32 dx_words + 8 x 32 dy_words words
 hipError_t launch_delta_transpose(const KParams& p, const uint32_t* dxbits, const uint32_t* dybits, uint32_t* dxT,

@@ -113,6 +113,7 @@ SIGNATURES = {
     "sv_batch_read_points": [P, I, P, P, I64, PI64],
     "sv_batch_digest": [P, ctypes.POINTER(Camera), I, P],
     "sv_hue_lut": [I, P],
+    "sv_hue_lut_variant": [I, I, P],
     "sv_delta_tables": [I, I, I, ctypes.POINTER(Camera), P, P],
     "sv_synth_frame": [I, I64, I, I, P, P],
     "sv_png_unfilter": [P, I, I, I, P],

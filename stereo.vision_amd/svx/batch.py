@@ -359,9 +359,11 @@ def pipeline_frame(disp, bgr, step=2, plane=None, point_thr=0.05, hist_thr=10, c
     return dict(counts=tuple(int(v) for v in counts), hist=hist, xyz2=xyz[:n2], pts=pts[:n2])
 
 
-def hue_lut(device=0):
+def hue_lut(device=0, variant=0):
+    """The device's hue bin of every colour R << 16 | G << 8 | B: variant 0 the exact function, 1 the resident
+    pipeline's fp32 path (sv_hue_lut_variant)."""
     lut = np.empty(1 << 24, np.int16)
-    _abi.call("sv_hue_lut", device, _abi.ptr(lut))
+    _abi.call("sv_hue_lut_variant", device, int(variant), _abi.ptr(lut))
     return lut
 
 

@@ -32,8 +32,11 @@ def _bits(a):
 # ---------------------------------------------------------------------------
 # exhaustive tables
 # ---------------------------------------------------------------------------
-def test_hue_lut_exhaustive(svx_mod, golden):
-    lut = svx_mod.batch.hue_lut()
+@pytest.mark.parametrize("variant", [0, 1])
+def test_hue_lut_exhaustive(svx_mod, golden, variant):
+    """every colour's bin: the exact device function (0) and the resident pipeline's fp32 path with its tie-band
+    fallback (1, hue_bin_sel) both equal the reference-run LUT digest (functions.py:73-78, 215-226)"""
+    lut = svx_mod.batch.hue_lut(variant=variant)
     ref = oracle.hue_lut()
     bad = np.flatnonzero(lut != ref)
     assert bad.size == 0, f"{bad.size} colours differ, first {bad[:5]}"
