@@ -455,15 +455,17 @@ int sv_png_unfilter(const uint8_t* in, int H, int rowbytes, int bpp, uint8_t* ou
 /* ---- stage drop-ins: host-side row gathers (no device work) ---------------
  * The one-by-one drop-ins of stereovision.py:97-113 hold their points as an index
  * selection of projectDisparityTo3d's (N, ld) float64 rows (svx/points.py); these
- * gather the columns a stage uploads. idx NULL = rows 0..n-1.
+ * gather the columns a stage uploads from rows[0..nrows); idx NULL = rows 0..n-1;
+ * an index outside [0, nrows) is SV_E_ARG (nothing read).
  * sv_gather_rgb_u8: columns 3..5 (R, G, B) as uint8, n x 3; SV_E_ARG if a value is
  *   not an integer in [0, 255] (the colour stages' input check, svx/stages.py).
  *   Replaces the row conversion inside calculateColourHistogram /
  *   filterPointsByHistogram (functions.py:215-230).
  * sv_gather_f64: columns c0..c0+nc-1, n x nc (project3DPointsTo2DImagePoints'
  *   X, Y, Z, functions.py:201-209). */
-int sv_gather_rgb_u8(const double* rows, int64_t ld, const int64_t* idx, int64_t n, uint8_t* out);
-int sv_gather_f64(const double* rows, int64_t ld, const int64_t* idx, int64_t n, int c0, int nc, double* out);
+int sv_gather_rgb_u8(const double* rows, int64_t nrows, int64_t ld, const int64_t* idx, int64_t n, uint8_t* out);
+int sv_gather_f64(const double* rows, int64_t nrows, int64_t ld, const int64_t* idx, int64_t n, int c0, int nc,
+                  double* out);
 
 /* ---- multi-GPU: RCCL over xGMI ----------------------------- */
 /* Frames shard by contiguous global-id ranges (one sv_batch per GPU); the only

@@ -8,8 +8,17 @@
 
 #include "../../include/svx.h"
 
-extern "C" int sv_gather_rgb_u8(const double* rows, int64_t ld, const int64_t* idx, int64_t n, uint8_t* out) {
-    if (!rows || !out || ld < 6 || n < 0) return SV_E_ARG;
+// every index must name one of the nrows rows (idx NULL: rows 0..n-1, n <= nrows)
+static bool rows_ok(int64_t nrows, const int64_t* idx, int64_t n) {
+    if (!idx) return n <= nrows;
+    for (int64_t i = 0; i < n; ++i)
+        if ((uint64_t)idx[i] >= (uint64_t)nrows) return false;
+    return true;
+}
+
+extern "C" int sv_gather_rgb_u8(const double* rows, int64_t nrows, int64_t ld, const int64_t* idx, int64_t n,
+                                uint8_t* out) {
+    if (!rows || !out || ld < 6 || n < 0 || !rows_ok(nrows, idx, n)) return SV_E_ARG;
     for (int64_t i = 0; i < n; ++i) {
         const double* r = rows + (idx ? idx[i] : i) * ld + 3;
         for (int c = 0; c < 3; ++c) {
@@ -22,9 +31,9 @@ extern "C" int sv_gather_rgb_u8(const double* rows, int64_t ld, const int64_t* i
     return SV_OK;
 }
 
-extern "C" int sv_gather_f64(const double* rows, int64_t ld, const int64_t* idx, int64_t n, int c0, int nc,
-                             double* out) {
-    if (!rows || !out || n < 0 || c0 < 0 || nc < 1 || c0 + nc > ld) return SV_E_ARG;
+extern "C" int sv_gather_f64(const double* rows, int64_t nrows, int64_t ld, const int64_t* idx, int64_t n, int c0,
+                             int nc, double* out) {
+    if (!rows || !out || n < 0 || c0 < 0 || nc < 1 || c0 + nc > ld || !rows_ok(nrows, idx, n)) return SV_E_ARG;
     for (int64_t i = 0; i < n; ++i) {
         const double* r = rows + (idx ? idx[i] : i) * ld + c0;
         double* o = out + i * nc;

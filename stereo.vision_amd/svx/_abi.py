@@ -117,8 +117,8 @@ SIGNATURES = {
     "sv_delta_tables": [I, I, I, ctypes.POINTER(Camera), P, P],
     "sv_synth_frame": [I, I64, I, I, P, P],
     "sv_png_unfilter": [P, I, I, I, P],
-    "sv_gather_rgb_u8": [P, I64, P, I64, P],
-    "sv_gather_f64": [P, I64, P, I64, I, I, P],
+    "sv_gather_rgb_u8": [P, I64, I64, P, I64, P],
+    "sv_gather_f64": [P, I64, I64, P, I64, I, I, P],
     "sv_loop_create": [I, ctypes.POINTER(LoopParams), ctypes.POINTER(Camera), P, ctypes.POINTER(P)],
     "sv_loop_destroy": [P],
     "sv_loop_acquire": [P, ctypes.POINTER(P)],

@@ -9,12 +9,15 @@ handling:
 * IMREAD_COLOR -> H x W x 3 BGR (alpha stripped, not composited; grey replicated; palette expanded);
 * IMREAD_GRAYSCALE -> H x W (alpha stripped; a colour image through libpng's rgb_to_gray with OpenCV's
   coefficients 0.299 / 0.587, i.e. (9797 R + 19234 G + 3737 B) >> 15 where R, G, B differ, else R);
-* IMREAD_UNCHANGED -> the file's channels, colour in BGR(A) order.
+* IMREAD_UNCHANGED -> 1, 3 or 4 channels as OpenCV's decoder chooses them: grey 1; RGB and palette 3, or 4 with
+  a tRNS chunk (alpha from it); grey + alpha 4 (BGRA, the grey replicated); RGBA 4; colour in BGR(A) order;
+  uint16 for 16-bit files.
 
-Parity: exact for the lossless decode (tests/test_io_cpu.py round-trips every filter type and colour type);
-the grey conversion restates libpng's published arithmetic and is unpinned against OpenCV itself (absent; the
-reference's masks are black and white, where every formula gives the same bytes). 16-bit and interlaced PNGs
-raise ValueError.
+Parity: exact for the lossless decode (tests/test_io_cpu.py round-trips every filter type, colour type, bit
+depth and Adam7 interlacing); the grey conversion restates libpng's published arithmetic and is unpinned against
+OpenCV itself (absent; the reference's masks are black and white, where every formula gives the same bytes). A
+corrupt file gives None, as cv2.imread does; a 16-bit colour file read as IMREAD_GRAYSCALE raises
+NotImplementedError.
 """
 import os
 import struct
@@ -30,23 +33,65 @@ IMREAD_COLOR = 1
 
 _SIG = b"\x89PNG\r\n\x1a\n"
 _CHANNELS = {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}   # PNG colour type -> samples a pixel
+_DEPTHS = {0: (1, 2, 4, 8, 16), 2: (8, 16), 3: (1, 2, 4, 8), 4: (8, 16), 6: (8, 16)}
+_CRITICAL = (b"IHDR", b"PLTE", b"IDAT", b"IEND")
+# Adam7 passes: (x0, y0, dx, dy)
+_ADAM7 = ((0, 0, 8, 8), (4, 0, 8, 8), (0, 4, 4, 8), (2, 0, 4, 4), (0, 2, 2, 4), (1, 0, 2, 2), (0, 1, 1, 2))
+
+
+class PngCorrupt(ValueError):
+    """The file is not a decodable PNG (cv2.imread returns None for it)."""
+
+
+def _samples(raw, h, w, ch, depth):
+    """unfiltered scanlines (h x rowbytes) -> (h, w, ch) samples: uint8 for depth <= 8, uint16 for 16."""
+    if depth == 8:
+        return raw.reshape(h, w, ch)
+    if depth == 16:
+        return raw.reshape(h, w * ch, 2).view(">u2").reshape(h, w, ch).astype(np.uint16)
+    per = 8 // depth   # samples a byte, the first in the high bits
+    bits = np.unpackbits(raw, axis=1).reshape(h, -1, depth)
+    vals = (bits * (1 << np.arange(depth - 1, -1, -1, dtype=np.uint8))).sum(axis=2, dtype=np.uint16)
+    assert vals.shape[1] == raw.shape[1] * per
+    return vals[:, : w * ch].astype(np.uint8).reshape(h, w, ch)
+
+
+def _unfilter(data, h, rowbytes, bpp):
+    if len(data) < h * (rowbytes + 1):
+        raise PngCorrupt("truncated image data")
+    src = np.ascontiguousarray(np.frombuffer(data, np.uint8, count=h * (rowbytes + 1)))
+    out = np.empty((h, rowbytes), np.uint8)
+    if h:
+        rc = _abi.lib().sv_png_unfilter(_abi.ptr(src), h, rowbytes, bpp, _abi.ptr(out))
+        if rc != 0:
+            raise PngCorrupt("bad scanline filter type")
+    return out
 
 
 def _read_png(path):
-    """(H x W x C uint8 samples as stored: grey, grey+alpha, RGB, RGBA, or palette-expanded RGB(A))."""
+    """(samples H x W x C as stored — uint8, or uint16 at depth 16 — with sub-byte grey scaled to 8 bits and
+    palette indices expanded to RGB(A), colour type of the result, tRNS key or None, depth). Raises PngCorrupt."""
     with open(path, "rb") as fh:
         data = fh.read()
     if data[:8] != _SIG:
-        raise ValueError(f"{path}: not a PNG file")
+        raise PngCorrupt(f"{path}: not a PNG file")
     pos, ihdr, idat, plte, trns = 8, None, [], None, None
-    while pos + 8 <= len(data):
+    while True:
+        if pos + 12 > len(data):
+            raise PngCorrupt(f"{path}: truncated chunk")
         ln, typ = struct.unpack(">I4s", data[pos:pos + 8])
         body = data[pos + 8:pos + 8 + ln]
+        if len(body) < ln or pos + 12 + ln > len(data):
+            raise PngCorrupt(f"{path}: truncated chunk")
+        crc = struct.unpack(">I", data[pos + 8 + ln:pos + 12 + ln])[0]
+        good = zlib.crc32(typ + body) & 0xFFFFFFFF == crc
+        if not good and typ in _CRITICAL:   # libpng: an error for critical chunks, ancillary ones are dropped
+            raise PngCorrupt(f"{path}: CRC error in {typ.decode('latin-1')}")
         if typ == b"IHDR":
             ihdr = struct.unpack(">IIBBBBB", body)
         elif typ == b"PLTE":
-            plte = np.frombuffer(body, np.uint8).reshape(-1, 3)
-        elif typ == b"tRNS":
+            plte = np.frombuffer(body, np.uint8)[: len(body) // 3 * 3].reshape(-1, 3)
+        elif typ == b"tRNS" and good:
             trns = np.frombuffer(body, np.uint8)
         elif typ == b"IDAT":
             idat.append(body)
@@ -54,33 +99,45 @@ def _read_png(path):
             break
         pos += 12 + ln
     if ihdr is None:
-        raise ValueError(f"{path}: no IHDR chunk")
+        raise PngCorrupt(f"{path}: no IHDR chunk")
     W, H, depth, ctype, _comp, _filt, interlace = ihdr
-    if ctype not in _CHANNELS:
-        raise ValueError(f"{path}: unknown PNG colour type {ctype}")
-    if depth != 8:
-        raise ValueError(f"{path}: {depth}-bit PNG not supported (8-bit only)")
-    if interlace:
-        raise ValueError(f"{path}: interlaced PNG not supported")
+    if ctype not in _CHANNELS or depth not in _DEPTHS[ctype] or interlace > 1 or W == 0 or H == 0:
+        raise PngCorrupt(f"{path}: bad IHDR (colour type {ctype}, depth {depth}, interlace {interlace})")
     ch = _CHANNELS[ctype]
-    raw = zlib.decompress(b"".join(idat))
-    rowbytes = W * ch
-    if len(raw) < H * (rowbytes + 1):
-        raise ValueError(f"{path}: truncated image data")
-    src = np.frombuffer(raw, np.uint8, count=H * (rowbytes + 1))
-    out = np.empty((H, W, ch), np.uint8)
-    _abi.call("sv_png_unfilter", _abi.ptr(np.ascontiguousarray(src)), H, rowbytes, ch, _abi.ptr(out))
+    try:
+        raw = zlib.decompress(b"".join(idat))
+    except zlib.error as e:
+        raise PngCorrupt(f"{path}: {e}") from None
+    bpp = max(1, ch * depth // 8)   # the filters' left neighbour, in bytes
+    px = np.zeros((H, W, ch), np.uint16 if depth == 16 else np.uint8)
+    passes = _ADAM7 if interlace else ((0, 0, 1, 1),)
+    off = 0
+    for x0, y0, dx, dy in passes:
+        pw, ph = (W - x0 + dx - 1) // dx, (H - y0 + dy - 1) // dy
+        if pw <= 0 or ph <= 0:
+            continue   # an empty pass has no scanlines (and no filter bytes)
+        rowbytes = (pw * ch * depth + 7) // 8
+        rows = _unfilter(raw[off:], ph, rowbytes, bpp)
+        off += ph * (rowbytes + 1)
+        px[y0::dy, x0::dx] = _samples(rows, ph, pw, ch, depth)
+    if ctype == 0 and depth < 8:   # png_set_expand_gray_1_2_4_to_8: 0..2^b - 1 scaled to 0..255
+        px = (px.astype(np.uint16) * (255 // ((1 << depth) - 1))).astype(np.uint8)
+    key = None
     if ctype == 3:   # palette: indices -> RGB, or RGBA when the file gives palette alpha
-        if plte is None:
-            raise ValueError(f"{path}: palette image without PLTE")
-        idx = out[..., 0]
-        rgb = plte[np.minimum(idx, len(plte) - 1)]
-        if trns is not None:
+        if plte is None or len(plte) == 0:
+            raise PngCorrupt(f"{path}: palette image without PLTE")
+        idx = np.minimum(px[..., 0], len(plte) - 1)
+        rgb = plte[idx]
+        if trns is not None and len(trns):
             alpha = np.full(len(plte), 255, np.uint8)
             alpha[:min(len(trns), len(plte))] = trns[:len(plte)]
-            return np.dstack([rgb, alpha[np.minimum(idx, len(plte) - 1)]]), 6
-        return rgb, 2
-    return out, ctype
+            return np.dstack([rgb, alpha[idx]]), 6, None, 8
+        return rgb, 2, None, 8
+    if trns is not None and ctype in (0, 2) and len(trns) >= 2 * ch:
+        key = np.frombuffer(trns[: 2 * ch].tobytes(), ">u2").astype(np.uint16)   # the transparent sample value(s)
+        if depth < 8:
+            key = key * (255 // ((1 << depth) - 1))
+    return px, ctype, key, depth
 
 
 def _rgb_to_gray(rgb):
@@ -94,18 +151,37 @@ def _rgb_to_gray(rgb):
 
 
 def imread(path, flags=IMREAD_COLOR):
-    """cv2.imread(path, flags) for 8-bit PNG files (functions.py:29-34, :55). A missing or unreadable file
-    returns None, as cv2.imread does."""
+    """cv2.imread(path, flags) for PNG files (functions.py:29-34, :55), with OpenCV's PNG decoder's rules
+    (grfmt_png.cpp): a missing, unreadable or corrupt file (bad signature, CRC error in a critical chunk, truncated
+    or undecodable data) returns None. Colour types, bit depths 1-16 and Adam7 interlacing are decoded; 16-bit
+    samples are kept by IMREAD_UNCHANGED (uint16) and cut to their high byte otherwise (png_set_strip_16), except a
+    16-bit colour file read as IMREAD_GRAYSCALE (libpng's 16-bit grey conversion is not restated:
+    NotImplementedError)."""
     if not os.path.isfile(path):
         return None
-    px, ctype = _read_png(path)
+    try:
+        px, ctype, key, depth = _read_png(path)
+    except (PngCorrupt, OSError):
+        return None
     has_alpha = ctype in (4, 6)
     colour = ctype in (2, 6)
     if flags == IMREAD_UNCHANGED:
+        # OpenCV's m_type: 4 channels for colour or grey with alpha and for RGB / palette with tRNS, else 3 or 1
+        if ctype == 2 and key is not None:   # png_set_tRNS_to_alpha: 0 where the pixel equals the key
+            a = np.where(np.all(px == key.astype(px.dtype), axis=2), 0, 255 if depth != 16 else 65535)
+            px = np.dstack([px, a.astype(px.dtype)])
+            has_alpha = True
         if colour:
-            bgr = px[..., [2, 1, 0] + ([3] if has_alpha else [])]
-            return np.ascontiguousarray(bgr)
-        return np.ascontiguousarray(px[..., 0] if not has_alpha else px)
+            out = px[..., [2, 1, 0] + ([3] if has_alpha else [])]
+        elif has_alpha:   # grey + alpha -> BGRA (png_set_gray_to_rgb)
+            out = px[..., [0, 0, 0, 1]]
+        else:
+            out = px[..., 0]
+        return np.ascontiguousarray(out)
+    if depth == 16:
+        if flags == IMREAD_GRAYSCALE and colour:
+            raise NotImplementedError(f"{path}: 16-bit colour PNG as IMREAD_GRAYSCALE (libpng's 16-bit rgb_to_gray)")
+        px = (px >> 8).astype(np.uint8)   # png_set_strip_16
     if flags == IMREAD_GRAYSCALE:
         if colour:
             return np.ascontiguousarray(_rgb_to_gray(px[..., :3]))

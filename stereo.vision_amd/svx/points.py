@@ -171,7 +171,7 @@ def gather_columns(points, c0, nc):
     base, idx = spec
     n = len(points)
     out = np.empty((n, nc), np.float64)
-    _abi.call("sv_gather_f64", _abi.ptr(base), base.shape[1], _abi.ptr(idx), n, c0, nc, _abi.ptr(out))
+    _abi.call("sv_gather_f64", _abi.ptr(base), base.shape[0], base.shape[1], _abi.ptr(idx), n, c0, nc, _abi.ptr(out))
     return out
 
 
@@ -185,8 +185,8 @@ def gather_rgb_u8(points):
     base, idx = spec
     n = len(points)
     out = np.empty((n, 3), np.uint8)
-    rc = _abi.lib().sv_gather_rgb_u8(_abi.ptr(base), ctypes.c_int64(base.shape[1]), _abi.ptr(idx),
-                                     ctypes.c_int64(n), _abi.ptr(out))
+    rc = _abi.lib().sv_gather_rgb_u8(_abi.ptr(base), ctypes.c_int64(base.shape[0]), ctypes.c_int64(base.shape[1]),
+                                     _abi.ptr(idx), ctypes.c_int64(n), _abi.ptr(out))
     if rc != 0:
         raise ValueError("colour stages: R, G, B must be integers in [0, 255]")
     return out

@@ -34,26 +34,53 @@ def _filter_row(ft, row, prev, bpp):
     return bytes([ft]) + bytes(out)
 
 
-def write_png(path, samples, ctype, palette=None, trns=None, filters=(0, 1, 2, 3, 4)):
-    """samples: H x W x C uint8 as the file stores them (C per colour type); rows cycle through `filters`."""
+ADAM7 = ((0, 0, 8, 8), (4, 0, 8, 8), (0, 4, 4, 8), (2, 0, 4, 4), (0, 2, 2, 4), (1, 0, 2, 2), (0, 1, 1, 2))
+
+
+def _row_bytes(row, depth):
+    """one scanline's samples (1-D, uint8 or uint16) as the file stores them"""
+    if depth == 16:
+        return row.astype(">u2").tobytes()
+    if depth == 8:
+        return row.astype(np.uint8).tobytes()
+    per = 8 // depth
+    v = np.zeros(-(-len(row) // per) * per, np.uint8)
+    v[: len(row)] = row
+    v = v.reshape(-1, per)
+    return bytes((v << (8 - depth * (np.arange(per) + 1))).sum(axis=1, dtype=np.uint16).astype(np.uint8).tolist())
+
+
+def write_png(path, samples, ctype, palette=None, trns=None, filters=(0, 1, 2, 3, 4), depth=8, interlace=0,
+              corrupt=None):
+    """samples: H x W x C as the file stores them (C per colour type; uint16 values at depth 16); rows cycle
+    through `filters`; interlace 1 = Adam7; corrupt: "crc" (IDAT CRC) or "trunc" (data cut short)."""
     H, W, C = samples.shape
+    bpp = max(1, C * depth // 8)
     raw = b""
-    prev = None
-    for y in range(H):
-        row = samples[y].reshape(-1).tobytes()
-        raw += _filter_row(filters[y % len(filters)], row, prev, C)
-        prev = row
+    passes = ADAM7 if interlace else ((0, 0, 1, 1),)
+    for x0, y0, dx, dy in passes:
+        sub = samples[y0::dy, x0::dx]
+        prev = None
+        for y in range(sub.shape[0]):
+            if sub.shape[1] == 0:
+                break
+            row = _row_bytes(sub[y].reshape(-1), depth)
+            raw += _filter_row(filters[y % len(filters)], row, prev, bpp)
+            prev = row
 
-    def chunk(t, body):
-        return struct.pack(">I", len(body)) + t + body + struct.pack(">I", zlib.crc32(t + body) & 0xFFFFFFFF)
+    def chunk(t, body, bad=False):
+        crc = zlib.crc32(t + body) & 0xFFFFFFFF
+        return struct.pack(">I", len(body)) + t + body + struct.pack(">I", crc ^ (1 if bad else 0))
 
-    data = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", W, H, 8, ctype, 0, 0, 0))
+    data = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", W, H, depth, ctype, 0, 0, interlace))
     if palette is not None:
         data += chunk(b"PLTE", palette.astype(np.uint8).tobytes())
     if trns is not None:
-        data += chunk(b"tRNS", trns.astype(np.uint8).tobytes())
+        data += chunk(b"tRNS", np.asarray(trns).astype(">u2" if ctype in (0, 2) else np.uint8).tobytes())
     z = zlib.compress(raw, 6)
-    data += chunk(b"IDAT", z[: len(z) // 2]) + chunk(b"IDAT", z[len(z) // 2:])   # split over two IDATs
+    if corrupt == "trunc":
+        z = z[: len(z) // 2]
+    data += chunk(b"IDAT", z[: len(z) // 2]) + chunk(b"IDAT", z[len(z) // 2:], bad=corrupt == "crc")
     data += chunk(b"IEND", b"")
     with open(path, "wb") as fh:
         fh.write(data)
@@ -72,8 +99,8 @@ def test_every_filter_and_colour_type_round_trips(tmp_path, ctype, C):
     un = sio.imread(p, sio.IMREAD_UNCHANGED)
     if colour:
         exp = px[..., [2, 1, 0] + ([3] if alpha else [])]
-    else:
-        exp = px if alpha else px[..., 0]
+    else:   # OpenCV's decoder: grey + alpha comes back as 4 channels, BGRA
+        exp = px[..., [0, 0, 0, 1]] if alpha else px[..., 0]
     np.testing.assert_array_equal(un, exp)
     bgr = sio.imread(p)
     np.testing.assert_array_equal(bgr, px[..., [2, 1, 0]] if colour else np.repeat(px[..., :1], 3, axis=2))
@@ -103,12 +130,70 @@ def test_palette_with_and_without_alpha(tmp_path):
     np.testing.assert_array_equal(un[..., 3], alpha[idx[..., 0]])
 
 
-def test_missing_file_is_none_and_bad_files_raise(tmp_path):
-    assert sio.imread(str(tmp_path / "absent.png")) is None   # cv2.imread returns None
+def test_missing_and_corrupt_files_are_none(tmp_path):
+    """cv2.imread returns None (it does not raise) for a file it cannot decode"""
+    assert sio.imread(str(tmp_path / "absent.png")) is None
     bad = tmp_path / "bad.png"
     bad.write_bytes(b"not a png")
-    with pytest.raises(ValueError):
-        sio.imread(str(bad))
+    assert sio.imread(str(bad)) is None
+    px = np.random.default_rng(9).integers(0, 256, (7, 9, 3), dtype=np.uint8)
+    for how in ("crc", "trunc"):
+        p = str(tmp_path / f"{how}.png")
+        write_png(p, px, 2, corrupt=how)
+        assert sio.imread(p) is None, how
+    ok = str(tmp_path / "ok.png")
+    write_png(ok, px, 2)
+    data = open(ok, "rb").read()
+    open(ok, "wb").write(data[: len(data) - 20])   # cut inside the last chunks
+    assert sio.imread(ok) is None
+
+
+@pytest.mark.parametrize("depth", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("interlace", [0, 1])
+def test_grey_bit_depths_and_interlacing(tmp_path, depth, interlace):
+    """png_set_expand_gray_1_2_4_to_8 (v * 255 / (2^b - 1)), 16-bit kept by IMREAD_UNCHANGED and cut to the high
+    byte otherwise (png_set_strip_16), Adam7 interlacing on an odd size (empty passes included)"""
+    rng = np.random.default_rng(depth + 10 * interlace)
+    px = rng.integers(0, 1 << depth, (11, 13, 1)).astype(np.uint16 if depth == 16 else np.uint8)
+    p = str(tmp_path / f"g{depth}.png")
+    write_png(p, px, 0, depth=depth, interlace=interlace)
+    un = sio.imread(p, sio.IMREAD_UNCHANGED)
+    grey8 = (px[..., 0] >> 8).astype(np.uint8) if depth == 16 else (px[..., 0] * (255 // ((1 << depth) - 1))).astype(np.uint8)
+    np.testing.assert_array_equal(un, px[..., 0] if depth == 16 else grey8)
+    assert un.dtype == (np.uint16 if depth == 16 else np.uint8)
+    np.testing.assert_array_equal(sio.imread(p, sio.IMREAD_GRAYSCALE), grey8)
+    np.testing.assert_array_equal(sio.imread(p), np.repeat(grey8[..., None], 3, axis=2))
+
+
+@pytest.mark.parametrize("depth", [1, 2, 4, 8])
+def test_palette_bit_depths_interlaced(tmp_path, depth):
+    rng = np.random.default_rng(depth)
+    pal = rng.integers(0, 256, (1 << depth, 3), dtype=np.uint8)
+    idx = rng.integers(0, 1 << depth, (9, 10, 1), dtype=np.uint8)
+    p = str(tmp_path / f"p{depth}.png")
+    write_png(p, idx, 3, palette=pal, depth=depth, interlace=1)
+    np.testing.assert_array_equal(sio.imread(p), pal[idx[..., 0]][..., ::-1])
+
+
+def test_rgb16_and_rgb_trns(tmp_path):
+    rng = np.random.default_rng(4)
+    px = rng.integers(0, 65536, (6, 7, 3)).astype(np.uint16)
+    p = str(tmp_path / "rgb16.png")
+    write_png(p, px, 2, depth=16, interlace=1)
+    np.testing.assert_array_equal(sio.imread(p, sio.IMREAD_UNCHANGED), px[..., ::-1])
+    np.testing.assert_array_equal(sio.imread(p), (px[..., ::-1] >> 8).astype(np.uint8))
+    with pytest.raises(NotImplementedError):   # libpng's 16-bit grey conversion is not restated
+        sio.imread(p, sio.IMREAD_GRAYSCALE)
+    # an RGB tRNS key: IMREAD_UNCHANGED gives BGRA with alpha 0 exactly where the pixel is the key
+    q8 = rng.integers(0, 4, (6, 7, 3), dtype=np.uint8) * 60
+    key = q8[2, 3].astype(np.uint16)
+    q = str(tmp_path / "rgb_trns.png")
+    write_png(q, q8, 2, trns=key)
+    un = sio.imread(q, sio.IMREAD_UNCHANGED)
+    assert un.shape == (6, 7, 4)
+    np.testing.assert_array_equal(un[..., :3], q8[..., ::-1])
+    np.testing.assert_array_equal(un[..., 3], np.where(np.all(q8 == key, axis=2), 0, 255))
+    np.testing.assert_array_equal(sio.imread(q), q8[..., ::-1])   # IMREAD_COLOR strips it
 
 
 def test_image_pairing(tmp_path):
@@ -146,3 +231,34 @@ def test_reference_masks_decode():
     # the carmask fixture the pre-pass and loop tests use (tests/golden/carmask.npz) is this mask, bit for bit
     from test_prepass_cpu import carmask
     np.testing.assert_array_equal(m["carmask"] != 0, carmask() != 0)
+
+
+def test_against_pil_encoder_and_decoder(tmp_path):
+    """An independent codec where one is importable (PIL, this container): files PIL writes (its own adaptive
+    filters; modes 1, L, LA, P, RGB, RGBA) decode to PIL's pixels, and PIL decodes this file's Adam7-interlaced
+    writer's files to the same pixels as svx.io."""
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(21)
+    H, W = 37, 53
+    smooth = (np.add.outer(np.arange(H), np.arange(W)) * 3 % 256).astype(np.uint8)   # filters other than None pay
+    imgs = {
+        "1": Image.fromarray(rng.integers(0, 2, (H, W)).astype(bool)),
+        "L": Image.fromarray(smooth),
+        "LA": Image.fromarray(np.dstack([smooth, rng.integers(0, 256, (H, W), dtype=np.uint8)]), "LA"),
+        "RGB": Image.fromarray(np.dstack([smooth, smooth[::-1], rng.integers(0, 256, (H, W), dtype=np.uint8)])),
+        "RGBA": Image.fromarray(rng.integers(0, 256, (H, W, 4), dtype=np.uint8)),
+    }
+    imgs["P"] = imgs["RGB"].quantize(colors=37)
+    for mode, im in imgs.items():
+        p = str(tmp_path / f"pil_{mode}.png")
+        im.save(p)
+        rgb = np.asarray(Image.open(p).convert("RGB"))
+        np.testing.assert_array_equal(sio.imread(p), rgb[..., ::-1], err_msg=mode)
+        if mode in ("1", "L"):
+            np.testing.assert_array_equal(sio.imread(p, sio.IMREAD_GRAYSCALE), np.asarray(Image.open(p).convert("L")))
+    for ctype, C in ((0, 1), (2, 3), (4, 2), (6, 4)):
+        px = rng.integers(0, 256, (H, W, C), dtype=np.uint8)
+        p = str(tmp_path / f"adam7_{ctype}.png")
+        write_png(p, px, ctype, interlace=1)
+        ref = np.asarray(Image.open(p).convert("RGB"))
+        np.testing.assert_array_equal(sio.imread(p), ref[..., ::-1], err_msg=str(ctype))

@@ -69,3 +69,20 @@ def test_mutated_and_foreign_sequences_use_the_numpy_path():
     np.testing.assert_array_equal(gather_columns(rows, 0, 3), base[:9, :3])
     xyz = PointList(np.ascontiguousarray(base[:, :3]))   # rows of 3 values: no colours to gather
     assert gather_rgb_u8(xyz) is None
+
+
+def test_indices_outside_the_rows_are_refused():
+    """the C ABI checks every index against the row count before reading (no out-of-bounds read)"""
+    import ctypes
+    from svx import _abi
+    base = _base(10)
+    out8 = np.empty((2, 3), np.uint8)
+    out64 = np.empty((2, 3), np.float64)
+    for bad in ([0, 10], [-1, 2]):
+        idx = np.array(bad, np.int64)
+        assert _abi.lib().sv_gather_rgb_u8(_abi.ptr(base), ctypes.c_int64(10), ctypes.c_int64(6), _abi.ptr(idx),
+                                           ctypes.c_int64(2), _abi.ptr(out8)) != 0
+        assert _abi.lib().sv_gather_f64(_abi.ptr(base), ctypes.c_int64(10), ctypes.c_int64(6), _abi.ptr(idx),
+                                        ctypes.c_int64(2), 0, 3, _abi.ptr(out64)) != 0
+    assert _abi.lib().sv_gather_f64(_abi.ptr(base), ctypes.c_int64(1), ctypes.c_int64(6), None, ctypes.c_int64(2),
+                                    0, 3, _abi.ptr(out64)) != 0   # n > nrows without indices
