@@ -255,8 +255,9 @@ def install(functions_module, unpinned=False):
 
     By default only the PINNED functions are replaced: the ones whose outputs equal the
     reference's own on its fixtures. unpinned=True also replaces the UNPINNED ones, the
-    restatements of OpenCV (SGBM, grey + equalizeHist, fillDisparity, maskDisparity) whose
-    equality with the reference's cv2 cannot be checked here."""
+    restatements of OpenCV (SGBM, grey + equalizeHist, fillDisparity, maskDisparity, and
+    getImagePaths / loadImages: cv2.imread of the PNG pairs, svx.io) whose equality with the
+    reference's cv2 cannot be checked here."""
     global _module
     _abi.lib()  # fail loudly now if libsvx is missing
     _module = functions_module

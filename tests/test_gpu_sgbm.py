@@ -271,3 +271,35 @@ def test_dropin_installed_module(sv):
         assert gl.shape == L.shape and gl.dtype == np.uint8
     finally:
         sv.dropin.uninstall()
+
+
+def test_front_end_from_png_files(sv, tmp_path):
+    """loop.py:70-76 then stereovision.py:44-56 from files, through the installed drop-ins: getImagePaths ->
+    loadImages (svx.io, PNG ingest) -> preProcessImages -> greyscale -> disparity, against the oracle on the pixels
+    the files hold (the PNG round trip is lossless; one file interlaced, the other not)."""
+    from test_io_cpu import write_png
+    L, R = osg.synth_pair(4, 96, 320)
+    rng = np.random.default_rng(4)
+    bgr_l = np.clip(np.dstack([L] * 3).astype(np.int32) + rng.integers(0, 40, 3), 0, 255).astype(np.uint8)
+    bgr_r = np.clip(np.dstack([R] * 3).astype(np.int32) + rng.integers(0, 40, 3), 0, 255).astype(np.uint8)
+    dl, dr = tmp_path / "left", tmp_path / "right"
+    dl.mkdir()
+    dr.mkdir()
+    write_png(str(dl / "1506942473.484027_L.png"), bgr_l[..., ::-1], 2, filters=(4, 1, 2, 3, 0), interlace=1)
+    write_png(str(dr / "1506942473.484027_R.png"), bgr_r[..., ::-1], 2)
+    mod = types.SimpleNamespace(camera_focal_length_px=399.9745178222656, stereo_camera_baseline_m=0.2090607502,
+                                image_centre_w=474.5, image_centre_h=262.0)
+    sv.dropin.install(mod, unpinned=True)   # the PNG readers and the cv2 restatements are opt-in
+    try:
+        paths = mod.getImagePaths("1506942473.484027_L.png", str(dl), str(dr))
+        img_l, img_r = mod.loadImages(paths)
+        assert np.array_equal(img_l, bgr_l) and np.array_equal(img_r, bgr_r)
+        img_l, img_r = mod.preProcessImages(img_l, img_r)
+        gray_l, gray_r = mod.greyscale(img_l, img_r)
+        disp = mod.disparity(gray_l, gray_r, 128, False)
+        t = np.asarray(META["gamma"]["1.4"], np.uint8)
+        exp = osg.disparity(osg.grey_equalize(t[bgr_l]), osg.grey_equalize(t[bgr_r]))
+        assert np.array_equal(disp, exp)
+        assert disp.any()
+    finally:
+        sv.dropin.uninstall()
