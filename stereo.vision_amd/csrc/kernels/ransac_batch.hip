@@ -861,6 +861,35 @@ __device__ double rb_np_pairwise(int k, LoadF load, TermF term) {
     return rb_readlane(vst, 0);
 }
 
+// One DPP step of an fp64 wave scan (both 32-bit halves moved with the same control; a lane whose source is
+// outside its row or row mask reads 0.0) and the two-value wave sum built from six of them — the wave_scan_dpp
+// pattern of svx_device.h (row_shr 1/2/4/8, then row_bcast 15 and 31; lane 63 ends with the total), the two
+// chains interleaved. One VALU op a move instead of a ds_bpermute round trip: the xor butterfly of __shfl_xor had
+// put six dependent LDS round trips on every trial's chain. All 64 lanes must be active. The additions run in
+// another order than the butterfly's; the screen's sums are bounded approximations (64 fp64 lane sums round by
+// ~2^-47 of their magnitude, far inside the screen's 4x margin) and the decision is taken on exact fp64 errors.
+template <int CTL, int RM>
+__device__ __forceinline__ double rb_dpp_f64(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTL, RM, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTL, RM, 0xf, false);
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+__device__ __forceinline__ void rb_wave_sum2_f64(double& a, double& b) {
+#define SVX_RB_SUM2_STEP(ctl, rm)        \
+    a += rb_dpp_f64<ctl, rm>(a);         \
+    b += rb_dpp_f64<ctl, rm>(b)
+    SVX_RB_SUM2_STEP(0x111, 0xf);   // row_shr:1
+    SVX_RB_SUM2_STEP(0x112, 0xf);   // row_shr:2
+    SVX_RB_SUM2_STEP(0x114, 0xf);   // row_shr:4
+    SVX_RB_SUM2_STEP(0x118, 0xf);   // row_shr:8
+    SVX_RB_SUM2_STEP(0x142, 0xa);   // row_bcast:15
+    SVX_RB_SUM2_STEP(0x143, 0xc);   // row_bcast:31
+#undef SVX_RB_SUM2_STEP
+    a = rb_readlane_f64(a, 63);
+    b = rb_readlane_f64(b, 63);
+}
+
 // Screen + decision. LDS: the frame's packed points (LDS_PTS) or none, then
 // per trial the screened mean and its bound (2 doubles).
 template <class IdxT, bool LDS_PTS>
@@ -974,15 +1003,11 @@ __global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
             bnd = __builtin_fmaf(rr, live ? q : 0.0f, bnd);
         };
         const auto finish = [&](int t, const double (&rec)[kRBTri], double sum, double bnd) {
-#pragma unroll
-            for (int o = kWave / 2; o > 0; o >>= 1) {
-                sum += __shfl_xor(sum, o, kWave);
-                bnd += __shfl_xor(bnd, o, kWave);
-            }
+            rb_wave_sum2_f64(sum, bnd);
             if (lane == 0) {   // the screened mean and its bound; bound -1 marks a singular trial
-                const double d = rec[3];
-                scr[2 * t] = sum / (d * k);
-                scr[2 * t + 1] = rec[4] == 1.0 ? -1.0 : (bnd + (double)k) * 0x1p-18 / (d * k);
+                const double inv = 1.0 / (rec[3] * k);   // (one more rounding each: inside the margin)
+                scr[2 * t] = sum * inv;
+                scr[2 * t + 1] = rec[4] == 1.0 ? -1.0 : (bnd + (double)k) * 0x1p-18 * inv;
             }
         };
         {

@@ -1123,18 +1123,13 @@ __global__ __launch_bounds__(256) void sgbm_cc_count_kernel(SgbmK k, const int16
         if (end && root != y * W + s) __hip_atomic_store(par + y * W + s, root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int len = x - s + 1;
         const bool mine = end && root == acc_root;
-        int add = mine ? len : 0;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o, 64);
-        acc += add;
+        acc += (int)wave_sum(mine ? (uint32_t)len : 0u);   // (uniform loop: every lane active)
         const uint64_t rest = __ballot(end && !mine);
         if (rest) {
             // the first remaining run's root becomes the running root (flush the old one)
             const int r1 = __shfl(root, (int)__builtin_ctzll(rest), 64);
             const bool take = end && !mine && root == r1;
-            int add1 = take ? len : 0;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) add1 += __shfl_xor(add1, o, 64);
+            const int add1 = (int)wave_sum(take ? (uint32_t)len : 0u);   // (`rest` is uniform: every lane active)
             if (lane == 0 && acc_root >= 0 && acc) atomicAdd(sz + acc_root, acc);
             acc_root = r1;
             acc = add1;

@@ -315,10 +315,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return wave_scan_dpp(v, [](uint32_t a, uint32_t b) { return a + b; });
 }
 
+// Wave64 sum, uniform: the DPP scan's total (lane 63) read back — six VALU steps instead of the xor butterfly's six
+// dependent ds_bpermute round trips. Integer addition, so any order gives the same sum. All 64 lanes must be active.
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
 }
 
 // ---------------------------------------------------------------------------
