@@ -278,7 +278,7 @@ def test_front_end_from_png_files(sv, tmp_path):
     loadImages (svx.io, PNG ingest) -> preProcessImages -> greyscale -> disparity, against the oracle on the pixels
     the files hold (the PNG round trip is lossless; one file interlaced, the other not)."""
     from test_io_cpu import write_png
-    L, R = osg.synth_pair(4, 96, 320)
+    L, R = osg.synth_pair(4)   # a whole 544 x 1024 frame: its regions outlast filterSpeckles' 4000 pixels
     rng = np.random.default_rng(4)
     bgr_l = np.clip(np.dstack([L] * 3).astype(np.int32) + rng.integers(0, 40, 3), 0, 255).astype(np.uint8)
     bgr_r = np.clip(np.dstack([R] * 3).astype(np.int32) + rng.integers(0, 40, 3), 0, 255).astype(np.uint8)

@@ -17,21 +17,25 @@ from svx import io as sio
 REF_MASKS = "/root/reference/masks"
 
 
-def _paeth(a, b, c):
-    p = a + b - c
-    pa, pb, pc = abs(p - a), abs(p - b), abs(p - c)
-    return a if pa <= pb and pa <= pc else (b if pb <= pc else c)
-
-
 def _filter_row(ft, row, prev, bpp):
-    out = bytearray(len(row))
-    for i, x in enumerate(row):
-        a = row[i - bpp] if i >= bpp else 0
-        b = prev[i] if prev is not None else 0
-        c = prev[i - bpp] if (prev is not None and i >= bpp) else 0
-        pred = [0, a, b, (a + b) >> 1, _paeth(a, b, c)][ft]
-        out[i] = (x - pred) & 0xFF
-    return bytes([ft]) + bytes(out)
+    """one scanline filtered with type ft (PNG 1.2 §6), vectorised: every predictor reads raw bytes only"""
+    x = np.frombuffer(row, np.uint8).astype(np.int16)
+    b = np.frombuffer(prev, np.uint8).astype(np.int16) if prev is not None else np.zeros_like(x)
+    a = np.concatenate([np.zeros(bpp, np.int16), x[:-bpp]])[: len(x)]
+    c = np.concatenate([np.zeros(bpp, np.int16), b[:-bpp]])[: len(x)]
+    if ft == 0:
+        pred = np.zeros_like(x)
+    elif ft == 1:
+        pred = a
+    elif ft == 2:
+        pred = b
+    elif ft == 3:
+        pred = (a + b) >> 1
+    else:   # Paeth: the neighbour nearest a + b - c, ties a, b, c
+        p = a + b - c
+        pa, pb, pc = np.abs(p - a), np.abs(p - b), np.abs(p - c)
+        pred = np.where((pa <= pb) & (pa <= pc), a, np.where(pb <= pc, b, c))
+    return bytes([ft]) + ((x - pred) & 0xFF).astype(np.uint8).tobytes()
 
 
 ADAM7 = ((0, 0, 8, 8), (4, 0, 8, 8), (0, 4, 4, 8), (2, 0, 4, 4), (0, 2, 2, 4), (1, 0, 2, 2), (0, 1, 1, 2))
