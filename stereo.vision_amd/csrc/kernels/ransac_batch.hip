@@ -893,7 +893,14 @@ __device__ __forceinline__ void rb_wave_sum2_f64(double& a, double& b) {
 // Screen + decision. LDS: the frame's packed points (LDS_PTS) or none, then
 // per trial the screened mean and its bound (2 doubles).
 template <class IdxT, bool LDS_PTS>
-__global__ __launch_bounds__(kRBEvalThreads) void ransac_eval_kernel(
+// 96 VGPRs (five waves' worth a SIMD, no spills) instead of the 123 the kernel takes unconstrained: its 1024-lane
+// workgroup is four waves a SIMD, and at 123 they filled the register file, so nothing else ran on a CU beside an
+// evaluation workgroup — in the frame loop the next batch's pre-pass waited for whole CUs (loop 15.30 -> 15.01 ms,
+// four alternations, profiles/r05/ab_eval_vgpr_s19.txt).
+#ifndef SVX_EVAL_WPE
+#define SVX_EVAL_WPE 5
+#endif
+__global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(SVX_EVAL_WPE))) void ransac_eval_kernel(
     const uint32_t* __restrict__ packed, RbTables tb, int64_t cap, KParams cp,
     const int64_t* __restrict__ counts, int trials, int k, const IdxT* __restrict__ sidx,
     double* __restrict__ tri, const int32_t* __restrict__ fstat, double* __restrict__ out_abc,
