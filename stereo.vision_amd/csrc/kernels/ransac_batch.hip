@@ -336,28 +336,34 @@ __device__ __forceinline__ void rb_twist_level(uint32_t* mt, uint32_t* dummy) {
 // pos + span > G; a level moves G by at most 227, so the positions it drops
 // (below the new G - 624 < pos + span - 397) were consumed already.
 struct RbStream {   // wave 0's view of the frame's output stream (uniform)
-    uint32_t pos;     // next unconsumed output
-    uint32_t T;       // whole twists done
-    int lev;          // levels of twist T + 1 done (0..2)
-    __device__ uint32_t G() const { return 624u * T + (lev == 0 ? 0u : lev == 1 ? 227u : 454u); }
+    uint32_t pos = 0;   // next unconsumed output
+    uint32_t pm = 0;    // pos % 624, kept as pos moves (a step is < 624)
+    uint32_t G = 0;     // 624 (whole twists done) + the level boundary (0, 227, 454) of the next one
+    int lev = 0;        // levels of the next twist done (0..2)
+    __device__ void step(uint32_t d) {
+        pos += d;
+        pm += d;
+        pm -= pm >= 624u ? 624u : 0u;
+    }
 };
 
 template <class IdxT>
 __device__ __forceinline__ void rb_advance(RansacShared<IdxT>& sh, RbStream& st, uint32_t span) {
-    while (st.pos + span > st.G()) {
+    while (st.pos + span > st.G) {
         if (st.lev == 0) rb_twist_level<0>(sh.mt, sh.dummy);
         else if (st.lev == 1) rb_twist_level<1>(sh.mt, sh.dummy);
         else rb_twist_level<2>(sh.mt, sh.dummy);
-        if (++st.lev == 3) {
-            st.lev = 0;
-            ++st.T;
-        }
+        st.G += st.lev == 2 ? 170u : 227u;
+        st.lev = st.lev == 2 ? 0 : st.lev + 1;
     }
 }
 
+// output pos + lane (lane < 64): state word (pm + lane) mod 624
 template <class IdxT>
-__device__ __forceinline__ uint32_t rb_word(const RansacShared<IdxT>& sh, uint32_t q) {
-    return rb_temper(sh.mt[q % 624]);
+__device__ __forceinline__ uint32_t rb_word_at(const RansacShared<IdxT>& sh, const RbStream& st, uint32_t lane) {
+    uint32_t i = st.pm + lane;
+    i -= i >= 624u ? 624u : 0u;
+    return rb_temper(sh.mt[i]);
 }
 
 // numpy.cross(P1 - P2, P2 - P3) all zero (functions.py:255-258); products rounded first
@@ -375,7 +381,7 @@ __device__ void rb_draw_below(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
     int got = 0;
     while (got < m && st.pos < kRBMaxDraws) {
         rb_advance(sh, st, 64u);
-        const uint32_t r = rb_word(sh, st.pos + lane) >> (32 - kb);
+        const uint32_t r = rb_word_at(sh, st, (uint32_t)lane) >> (32 - kb);
         uint64_t acc = rb_ballot(r < n);
         int last = 63;
         while (acc && got < m) {
@@ -384,7 +390,7 @@ __device__ void rb_draw_below(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
             out[got++] = __builtin_amdgcn_readlane(r, l);   // l is wave-uniform: a scalar read
             last = l;
         }
-        st.pos += (got == m) ? (uint32_t)(last + 1) : 64u;
+        st.step((got == m) ? (uint32_t)(last + 1) : 64u);
     }
 }
 
@@ -413,7 +419,7 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
     uint32_t r[kRBWin];
     while (have < k && st.pos < kRBMaxDraws) {
         rb_advance(sh, st, 64u * kRBWin);
-        const uint32_t base = st.pos % 624;
+        const uint32_t base = st.pm;
         uint32_t old[kRBWin];
 #pragma unroll
         for (int w = 0; w < kRBWin; ++w) {
@@ -434,36 +440,39 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
         int q0 = have;
 #pragma unroll
         for (int w = 0; w < kRBWin; ++w) {
-            const bool acc = r[w] < n;
-            const uint32_t bit = 1u << (r[w] & 31);
-            uint64_t hm = rb_ballot(acc && (old[w] & bit));
+            // lane masks from single compares, combined in scalar registers (a ballot of a compound condition
+            // costs a select and a compare more): accepted draws, draws whose bit was already set
+            const uint64_t accm = rb_ballot(r[w] < n);
+            const uint64_t setm = rb_ballot((old[w] & (1u << (r[w] & 31))) != 0u);
+            uint64_t hm = accm & setm;
             uint64_t rej = hm;
             while (hm) {   // rare
                 const int l = __builtin_ctzll(hm);
                 const uint32_t v = __builtin_amdgcn_readlane(r[w], l);   // uniform lane: no LDS round trip
-                const uint64_t eq = rb_ballot(acc && r[w] == v);
-                const uint64_t fresh = rb_ballot(acc && r[w] == v && !(old[w] & bit));
+                const uint64_t eq = accm & rb_ballot(r[w] == v);
+                const uint64_t fresh = eq & ~setm;
                 hm &= ~eq;
                 rej = fresh ? ((rej & ~eq) | (eq & (eq - 1))) : (rej | eq);
             }
-            const bool sel = acc && !((rej >> lane) & 1ull);
-            const uint64_t sm = rb_ballot(sel);
-            const int q = q0 + (int)__builtin_popcountll(sm & ((1ull << lane) - 1));
+            const uint64_t sm = accm & ~rej;   // the window's selections (rej is inside accm)
+            const bool sel = (sm >> lane) & 1ull;
+            const uint32_t q = (uint32_t)q0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
             // picks numbered >= k keep their claims: no later draw of this sample can see them (they are
             // past its end in stream order) and the whole bitmap is cleared after the sample
-            if (sel && q < k) {
+            if (sel && q < (uint32_t)k) {
                 idx[q] = (IdxT)r[w];
                 if (TR && tr) tr[q] = (int32_t)r[w];
             }
             const int nsel = (int)__builtin_popcountll(sm);
             if (q0 < k && q0 + nsel >= k) {   // (uniform) the sample's last pick is in this window
-                const uint64_t lastm = rb_ballot(sel && q == k - 1);
+                const uint64_t lastm = sm & rb_ballot(q == (uint32_t)(k - 1));
                 consumed = 64u * w + (uint32_t)__builtin_ctzll(lastm) + 1u;
             }
             q0 += nsel;
         }
         have = q0 < k ? q0 : k;
-        st.pos += consumed;
+        st.step(consumed);
         rb_wave_lds_sync();   // the next round reads bits set/cleared by other lanes
     }
     // clear the sample's bits (the whole bitmap, 16 bytes a store: the launch rounds it to 4 words)
@@ -689,7 +698,7 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
     for (int q = lane; q < bitmap_words; q += 64) sh.bitmap[q] = 0;
     if (lane == 0) rb_seed(sh.mt, seed_base + (uint64_t)(first_frame + frame));
     __syncthreads();   // one wave: orders lane 0's seeding before every lane's reads
-    RbStream st{0, 0, 0};
+    RbStream st;
     const int g_pt = lane % 3, g_co = min(lane / 3, 2);   // the triple gather: point, coordinate (rb_point's tables)
     int status = 0, s = 0;
     for (; s < trials; ++s) {
