@@ -427,9 +427,11 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
             i -= i >= 624 ? 624 : 0;
             r[w] = rb_temper(sh.mt[i]) >> (32 - kb);
         }
+        uint64_t accm[kRBWin];   // the accepted draws of each window (ballot of the compare the claim selects on)
 #pragma unroll
         for (int w = 0; w < kRBWin; ++w) {   // claims issued in window order; rejected draws or a lane's dummy word
             const bool acc = r[w] < n;
+            accm[w] = rb_ballot(acc);
             uint32_t* a = acc ? &sh.bitmap[r[w] >> 5] : &sh.dummy[lane];
             old[w] = atomicOr(a, acc ? 1u << (r[w] & 31) : 0u);
         }
@@ -442,20 +444,19 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
         for (int w = 0; w < kRBWin; ++w) {
             // lane masks from single compares, combined in scalar registers (a ballot of a compound condition
             // costs a select and a compare more): accepted draws, draws whose bit was already set
-            const uint64_t accm = rb_ballot(r[w] < n);
             const uint64_t setm = rb_ballot((old[w] & (1u << (r[w] & 31))) != 0u);
-            uint64_t hm = accm & setm;
+            uint64_t hm = accm[w] & setm;
             uint64_t rej = hm;
             while (hm) {   // rare
                 const int l = __builtin_ctzll(hm);
                 const uint32_t v = __builtin_amdgcn_readlane(r[w], l);   // uniform lane: no LDS round trip
-                const uint64_t eq = accm & rb_ballot(r[w] == v);
+                const uint64_t eq = accm[w] & rb_ballot(r[w] == v);
                 const uint64_t fresh = eq & ~setm;
                 hm &= ~eq;
                 rej = fresh ? ((rej & ~eq) | (eq & (eq - 1))) : (rej | eq);
             }
-            const uint64_t sm = accm & ~rej;   // the window's selections (rej is inside accm)
-            const bool sel = (sm >> lane) & 1ull;
+            const uint64_t sm = accm[w] & ~rej;   // the window's selections (rej is inside accm)
+            const bool sel = __builtin_amdgcn_inverse_ballot_w64(sm);   // this lane's bit, as an exec-style mask
             const uint32_t q = (uint32_t)q0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
             // picks numbered >= k keep their claims: no later draw of this sample can see them (they are
