@@ -724,6 +724,9 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
             // lane 3 c + i (< 9) gathers coordinate c of point i: one load of the packed words, one of the
             // tables (two memory round trips); every lane then takes the nine values from lanes 0..8
             const uint32_t pk = fpk[g_pt == 0 ? t3[0] : g_pt == 1 ? t3[1] : t3[2]];
+            // while the packed words are in flight: the next twist level, once the stream has consumed the
+            // state words it replaces (a level drops positions below G - 397; pos >= G - 397 has read them all)
+            if (st.pos + 397u >= st.G) rb_advance(sh, st, st.G + 1u - st.pos);
             const uint32_t x2 = (pk & 0xFFF) >> 1, y2 = ((pk >> 12) & 0xFFF) >> 1, dd = pk >> 24;
             const double v = g_co == 0 ? tb.X[x2 * 256 + dd] : g_co == 1 ? tb.Y[y2 * 256 + dd] : tb.Z[dd];
 #pragma unroll
