@@ -338,7 +338,7 @@ __device__ __forceinline__ void rb_twist_level(uint32_t* mt, uint32_t* dummy) {
 struct RbStream {   // wave 0's view of the frame's output stream (uniform)
     uint32_t pos = 0;   // next unconsumed output
     uint32_t pm = 0;    // pos % 624, kept as pos moves (a step is < 624)
-    uint32_t G = 0;     // 624 (whole twists done) + the level boundary (0, 227, 454) of the next one
+    uint32_t G = 0;     // 624 x (whole twists done) + the level boundary (0, 227, 454) of the next one
     int lev = 0;        // levels of the next twist done (0..2)
     __device__ void step(uint32_t d) {
         pos += d;
