@@ -212,11 +212,8 @@ def cpu_baseline(budget_s):
         frames1 += 1
     s1 = time.perf_counter() - t1
     return {"value": round(ng2 / med["a1_project_rgb"] / 1e3, 4), "unit": "Mpoints/s", "cores": 1, "kind": "port",
-            "port": "oracle/cpu_loop.py + oracle/ransac.py: nested-loop restatement of functions.py:178-323 and "
-                    ":240-298 (numpy-scalar fp64 semantics), pinned to the reference-run fixtures in tests/golden/",
-            "sample": f"configs[0]: synthetic frame 0, step 2 ({ng2} grid points), stereovision.py:84-113 per stage, "
-                      f"median of {reps} runs on one pinned core; value = grid points / the port's "
-                      f"projectDisparityTo3d time",
+            "port": "oracle/cpu_loop.py+oracle/ransac.py",
+            "sample": f"configs[0]: frame 0, step 2 ({ng2} pts), stereovision.py:84-113, median of {reps}",
             "config1_stage_ms": med, "config1_chain_ms_per_frame": round(sum(med.values()), 1),
             "step1_projection": {"Mpoints_per_s": round(pts1 / s1 / 1e6, 4), "frames": frames1,
                                  "seconds": round(s1, 1)},
@@ -253,6 +250,37 @@ def profile_traffic(path, frames, step, kernel, kind):
     if have != src:
         return None, f"profile built from sources {have}, the timed kernel from {src}"
     return tj.get("k1_hbm_bytes_per_launch" if kind == "k1" else "pipeline_hbm_bytes_per_call"), None
+
+
+LINE_LIMIT = 6144   # bytes of the JSON line: the driver keeps the last 8 KB of stdout + stderr
+
+
+def finalize(out, limit=LINE_LIMIT):
+    """Order the line (the driver's contract fields, then the headline's sub-records, extras last) and hold it
+    within `limit` bytes: the prose lives in DESIGN.md §6, the line carries numbers and short keys. If it is still
+    too long, the least important records go first (placements, then extras' stage breakdowns), so the contract
+    fields, roofline, cpu_baseline, pipeline and parity always survive."""
+    order = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "latency_1frame_us", "pipeline",
+             "parity"]
+    o = {k: out[k] for k in order if k in out}
+    o.update((k, v) for k, v in out.items() if k not in o)
+    o["doc"] = "DESIGN.md §6"
+
+    def size():
+        return len(json.dumps(o, separators=(",", ":")).encode())
+    drops = [("roofline", "placement"), ("pipeline", "placement"), ("extras", "sgbm_disparity", "placement"),
+             ("extras", "device_frame_loop_serial", "stage_ms"), ("extras", "device_frame_loop_with_input", "stage_ms"),
+             ("cpu_baseline", "step1_projection"), ("extras", "road_from_bitmap"), ("extras", "road_raster_nonzero")]
+    for path in drops:
+        if size() <= limit:
+            break
+        d = o
+        for k in path[:-1]:
+            d = d.get(k, {}) if isinstance(d, dict) else {}
+        if isinstance(d, dict):
+            d.pop(path[-1], None)
+    return o
 
 
 def ramp(fn, syncs, ms):
@@ -342,8 +370,7 @@ def dropin_chain(fmod, disp, bgr, reps=5):
                 st.setdefault(k, []).append(v * 1e3)
     random.setstate(state)
     med = {k: round(float(np.median(v)), 2) for k, v in st.items()}
-    return {"ms_per_frame": round(sum(med.values()), 2), "stage_ms": med, "plane_points": n_pp,
-            "stages": "stereovision.py:84-113 via installed drop-ins, step 2, RANSAC 600"}
+    return {"ms_per_frame": round(sum(med.values()), 2), "stage_ms": med, "plane_points": n_pp}
 
 
 def check_plane_parity(b, first):
@@ -391,15 +418,14 @@ def extras(b, args, with_cpu, first=0):
     # point, so approx_GBps is an upper bound)
     byts = 8 * n2 + px + 4 * n2
     ex["road_raster_nonzero"] = {"ms_per_batch": round(ms, 3), "approx_GBps": round(byts / ms / 1e6, 1),
-                                 "points": n2, "kernels": "road_kernel (raster + non-zero walk in one pass)"}
+                                 "points": n2}
     mask = carmask()
     b.set_mask(mask)
     ms = _timed(b, lambda: b.prepass("previous", sync=False), 3, ramp_ms=args.ramp_ms / 3)
     # fillDisparity's recurrence: the disparity read, the cleaned frame written in place (maskDisparity is applied
     # by maskpoints as it reads the cleaned frame, not materialised)
     ex["prepass_fill_previous"] = {"ms_per_batch": round(ms, 3), "GBps": round(2 * px / ms / 1e6, 1),
-                                   "bytes_per_pixel": 2, "kernel": "fill_prev_kernel",
-                                   "mask": "carmask applied inside maskpoints_kernel"}
+                                   "frac": round(2 * px / ms / 1e6 / PEAK_HBM_GBS, 4)}
     # the per-frame-plane workload below is pinned end to end (tests/golden/plane_digests.npz): fresh frames,
     # ONE pre-pass over the batch in frame order (the timing above cleaned them four times), RANSAC with
     # random.seed(F), the pipeline with each frame's plane
@@ -415,8 +441,7 @@ def extras(b, args, with_cpu, first=0):
         random.seed(s)
         ransac.RANSAC(pts, 600)
     gpu_ms = (time.perf_counter() - t0) / 5 * 1e3
-    r = {"points": len(pts), "trials": 600, "ms_per_call": round(gpu_ms, 2),
-         "path": "host CPython-random replay + ransac_eval_kernel + numpy re-decision of the winner"}
+    r = {"points": len(pts), "trials": 600, "ms_per_call": round(gpu_ms, 2)}
     if with_cpu:
         t0 = time.perf_counter()
         random.seed(0)
@@ -428,8 +453,7 @@ def extras(b, args, with_cpu, first=0):
     # pipeline driven by each frame's own plane: stereovision.py:84-113 for the whole batch
     ms = _timed(b, lambda: b.ransac(seed_base=0, trials=600, sync=False), 2, ramp_ms=args.ramp_ms / 3)
     rb = {"frames": b.frames, "trials": 600, "ms_per_batch": round(ms, 2),
-          "us_per_frame": round(ms / b.frames * 1e3, 2), "kernels": "maskpoints_kernel + ransac_draw_kernel + ransac_eval_kernel",
-          "rng": "random.seed(frame) per frame"}
+          "us_per_frame": round(ms / b.frames * 1e3, 2)}
     if "cpu_restatement_ms_per_call" in r:
         rb["cpu_restatement_ms_per_frame"] = r["cpu_restatement_ms_per_call"]
     ex["ransac_batch"] = rb
@@ -444,18 +468,14 @@ def extras(b, args, with_cpu, first=0):
                                    "frames": b.frames, "kept_points": kept,
                                    "algorithmic_bytes_per_call": fp_bytes,
                                    "frac": round(fp_bytes / fp_s / 1e9 / PEAK_HBM_GBS, 4) if fp_s > 0 else None,
-                                   "survey_bytes_per_call": fp_bytes + 4 * kept,
                                    "frac_at_survey_bytes": round((fp_bytes + 4 * kept) / fp_s / 1e9 / PEAK_HBM_GBS, 4)
-                                   if fp_s > 0 else None,
-                                   "workload": "the prepass-cleaned frames (fill previous + carmask), each with its "
-                                               "own RANSAC plane (threshold 0.05, hist thr 10)",
-                                   "kernels": "frame_planes_kernel + resident_fused_kernel (each frame's plane)"
-                                   if b.frames >= 512 else "frame_planes_kernel + tiled kernels",
-                                   "kernel": b.kernel_name("pipeline")}
+                                   if fp_s > 0 else None}
     fp_tr, fp_why = profile_traffic(args.traffic_planes, b.frames, args.step, b.kernel_name("pipeline"), "pipeline")
     ex["pipeline_frame_planes"]["traffic"] = fp_tr
+    ex["pipeline_frame_planes"]["traffic_src"] = "profiles/traffic_planes.json" if fp_tr else None
     if fp_tr:
-        ex["pipeline_frame_planes"]["frac_of_traffic"] = round(fp_tr / fp_s / 1e9 / PEAK_HBM_GBS, 4)
+        ex["pipeline_frame_planes"]["frac_of_traffic"] = round(fp_tr / fp_s / 1e9 / PEAK_HBM_GBS, 4) \
+            if fp_s > 0 else None
     else:
         ex["pipeline_frame_planes"]["traffic_note"] = fp_why
     if not args.no_parity:
@@ -479,11 +499,7 @@ def extras(b, args, with_cpu, first=0):
         "pipeline_with_bitmap_gpu_ms_per_call": round(kb_ms / max(kb_n, 1), 4),
         "pipeline_gpu_ms_per_call": ex["pipeline_frame_planes"]["gpu_ms_per_call"],
         "points": n2p, "bytes_from_bitmap": 4 * 32 * H * b.frames + px_all + 4 * n2p,
-        "bytes_from_points": 8 * n2p + px_all + 4 * n2p,
-        "note": "per-frame-plane points; bytes count one 4-byte walk entry (x | y << 16) per point (an upper "
-                "bound); the bitmap is "
-                "written by the pipeline (+0.28 GB per 4096 frames, counted in its time above)",
-        "kernels": "road_rowscan_kernel + road_rows_kernel (from the bitmap) vs road_kernel (from the points)"}
+        "bytes_from_points": 8 * n2p + px_all + 4 * n2p}
 
     fmod = types.SimpleNamespace(camera_focal_length_px=399.9745178222656, stereo_camera_baseline_m=0.2090607502,
                                  image_centre_w=474.5, image_centre_h=262.0, carmask=mask)
@@ -528,16 +544,7 @@ def loop_extra(args, device, first, mask):
             tls = [loop.timeline(q) for q in range(seq - slots + 1, seq + 1)]
         stage_ms = {name: round(float(np.mean([tl[name][1] - tl[name][0] for tl in tls])), 3) for name in STAGES}
         r = {"ms_per_batch": round(ms, 2), "frames": frames, "frames_per_s": round(frames / ms * 1e3, 1),
-             "slots": slots, "batches_timed": reps, "input": "synthetic frames generated per batch on the device"
-             if source == "synth" else "resident raw frames (generated once per slot and kept; every batch "
-                                       "cleans them again)",
-             "stage_ms": stage_ms,
-             "stages": ("synthetic input (global ids) -> " if source == "synth" else "") +
-                       "prepass(previous+carmask) -> maskpoints -> RANSAC(600, random.seed(g)): draw, eval -> "
-                       "pipeline(per-frame planes) -> road raster + walk",
-             "api": "svx.loop.FrameLoop / sv_loop_create + sv_loop_submit"
-                    + (" (two slots, one stream each)" if slots == 2 else
-                       " with slots=1 (one batch at a time)")}
+             "slots": slots, "batches_timed": reps, "stage_ms": stage_ms}
         if slots == 2:
             a, b = tls[0], tls[1]   # batch k and k + 1: how much of k + 1's draw ran beside k's pipeline + road
             lo, hi = max(b["draw"][0], a["pipeline"][0]), min(b["draw"][1], a["road"][1])
@@ -588,14 +595,9 @@ def sgbm_extra(sb, device, with_cpu, frames=128, chunk=128):
         r = {"frames": frames, "chunk": chunk, "ms_per_batch": round(ms, 2),
              "us_per_frame": round(k_ms / max(k_n, 1) / frames * 1e3, 1),
              "frame0_matches_oracle": bool(np.array_equal(b.read_disp(0), ref)),
-             "kernels": "sgbm_hsum + sgbm_vertical + sgbm_diag + sgbm_row + sgbm_median3 + cc_rows/union/count + out",
-             "parity": "unpinned vs OpenCV (absent); bit-exact vs oracle/sgbm_oracle.c",
-             "placement": dict(b.placement("sgbm"), note="sgbm_place: on the batch's first SGBM call up to 2 "
-                               "contiguous sets of the four cost volumes, the first chunk's compute timed on each, "
-                               "the fastest kept (outside the timed region; DESIGN §7.4)")}
+             "placement": b.placement("sgbm")}
         if with_cpu:
             r["cpu_restatement_ms_per_frame"] = round(cpu_ms, 1)
-            r["cpu_note"] = "oracle/sgbm_oracle.c, 1 thread, scalar C (not OpenCV's SIMD build)"
         out["sgbm_disparity"] = r
         b.set_mask(carmask())
         b.synth_bgr_pair(0)        # BGR stereo pairs: the loop starts at stereovision.py:44
@@ -610,11 +612,7 @@ def sgbm_extra(sb, device, with_cpu, frames=128, chunk=128):
             b.nonzero(sync=False)
         ms = _timed(b, loop, 2)
         out["device_frame_loop_from_pairs"] = {
-            "ms_per_batch": round(ms, 2), "frames": frames, "frames_per_s": round(frames / ms * 1e3, 1),
-            "stages": "BGR pairs: gamma 1.4 + grey/equalizeHist -> SGBM disparity -> prepass(previous+mask) -> "
-                      "maskpoints+RANSAC(600) -> pipeline(per-frame planes, the corrected left image's colours) -> "
-                      "road raster -> non-zero walk (stereovision.py:40-136 minus the cv2 drawing and minus "
-                      "sanitiseRoadImage's morphology, functions.py:350-358: the walk is of the raw raster)"}
+            "ms_per_batch": round(ms, 2), "frames": frames, "frames_per_s": round(frames / ms * 1e3, 1)}
     return out
 
 
@@ -730,30 +728,25 @@ def main(argv=None):
 
     frames_gpu = batches[0].frames
     global_frames = int(ctrl.sum([sum(b.frames for b in batches)])[0])
-    par = {"ranks": f"one process per GPU (torchrun), RCCL communicator per rank",
-           "multi": f"one process, {pl['n_gpus']} GPUs (ncclCommInitAll)",
-           "single": "one process, one GPU"}[pl["mode"]]
+    par = {"ranks": "torchrun ranks, RCCL", "multi": "one process, ncclCommInitAll",
+           "single": "one process"}[pl["mode"]]
     out = {
         "metric": METRIC, "value": round(agg["value"], 1), "unit": "Mpoints/s", "n_gpus": pl["n_gpus"],
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(agg["ms_per_step"], 4),
         "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8->f32",
-        "data": "synthetic (counter-based generator of SURVEY §8d, generated on device)",
-        "config": {"workload": f"configs[2]: batch={frames_gpu}/GPU synthetic {W}x{H} disparity maps, "
-                               f"step {args.step}, dense fp32 XYZ planes (K1)"
+        "data": "synthetic (SURVEY §8d generator, on device)",
+        "config": {"workload": f"configs[2]: {frames_gpu}/GPU x {W}x{H}, step {args.step}, dense fp32 XYZ (K1)"
                                + (f"; configs[4]: {global_frames} frames over {pl['n_gpus']} GPUs"
                                   + (" (strong scaling)" if strong else "") if pl["n_gpus"] > 1 or strong else ""),
                    "frames_per_gpu": frames_gpu, "global_frames": global_frames, "H": H, "W": W,
                    "step": args.step, "grid_points_per_frame": ng,
-                   "parallelism": f"frame-sharded x{pl['n_gpus']} (no data-path collective); {par}"},
+                   "parallelism": f"frame-sharded x{pl['n_gpus']}; {par}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                      "kernel": k1_name, "kernel_ms": round(k_avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_point": K1_BYTES_PER_POINT,
-                     "placement": dict(batches[0].placement("project"),
-                                       note="k1_place: on the batch's first projection up to 3 contiguous sets of "
-                                            "X/Y/Z planes, one K1 launch timed on each, the fastest kept "
-                                            "(outside the timed region; DESIGN §4)")},
+                     "placement": batches[0].placement("project")},
     }
     if traffic_why:
         out["roofline"]["traffic_note"] = traffic_why
@@ -798,43 +791,28 @@ def main(argv=None):
         kept2_gpu0 = int(batches[0].read_counts()[:, 2].sum())
         pbytes = 4 * ng * frames_gpu + 16 * kept2_gpu0 + 4096 * frames_gpu
         survey_bytes = pbytes + 4 * kept2_gpu0   # SURVEY 8d's 20 B per kept point (int32 x and y stored apart)
+        # bytes: 4 B read a grid point + 16 B a kept point as stored (fp32 X, Y, Z + the int32 pair as
+        # int16 halves of one word) + 4 KB of histogram a frame; survey_bytes: SURVEY §8d's 20 B a kept point (an
+        # effective rate, frac_at_survey_bytes); traffic: PMC bytes a call of this kernel instance and sources
         out["pipeline"] = {
-            "workload": "configs[3]/[4]: same batch, plane threshold 0.05 + hue histogram (thr 10) "
-                        "+ ordered compaction + int32 back-projection",
+            "gpu_ms_per_call": round(p_avg_s * 1e3, 4), "frac": round(pbytes / p_avg_s / 1e9 / PEAK_HBM_GBS, 4),
             "value": round(pagg["value"], 1), "unit": "Mpoints/s",
-            "ms_per_step": round(pagg["ms_per_step"], 4), "gpu_ms_per_call": round(p_avg_s * 1e3, 4),
+            "ms_per_step": round(pagg["ms_per_step"], 4),
             "achieved_GBps": round(pbytes / p_avg_s / 1e9, 1),
-            "frac": round(pbytes / p_avg_s / 1e9 / PEAK_HBM_GBS, 4),
             "algorithmic_bytes_per_call": pbytes,
-            "bytes_note": "algorithmic = SURVEY 8d config 4 per GPU with the outputs as stored: 4 B read per grid point "
-                          "(disparity + BGR) + 16 B per kept point (fp32 X, Y, Z + the int32 (x, y) back-projection as "
-                          "int16 halves of one word, lossless: -1 <= x, y < 32768, widened on read-back; SURVEY counts "
-                          "20 B: survey_bytes_per_call, frac_at_survey_bytes) + 4 KB histogram per frame; the resident "
-                          "kernel does not read the BGR (nor, in pass 2, the disparity) of chunks the plane rules out, "
-                          "so it moves fewer bytes (traffic = PMC bytes per call of the timed kernel instance, "
-                          "frac_of_traffic = traffic / time / peak; null with traffic_note when no profile of that "
-                          "instance and its sources is committed). frac_at_survey_bytes is an EFFECTIVE rate: it credits "
-                          "4 B per kept point that SURVEY counts and the kernel does not store; frac is the real one",
-            "survey_bytes_per_call": survey_bytes,
             "frac_at_survey_bytes": round(survey_bytes / p_avg_s / 1e9 / PEAK_HBM_GBS, 4),
             "counts_total": {"valid": int(counts[0]), "kept": int(counts[1]), "kept2": int(counts[2])},
-            "plane_broadcast": comm_note or {
-                "ranks": "RCCL ncclBroadcast into device memory every step (sv_comm_broadcast_plane_dev)",
-                "multi": "RCCL grouped ncclBroadcast to every device every step (sv_multi_pipeline)",
-                "single": "host plane (single GPU)"}[pl["mode"]],
-            "kernels": "resident_fused_kernel (one workgroup per frame, keep1 from the plane in device memory)"
-                       if frames_gpu >= 512 else "tiled: stage_kernel + offsets_kernel",
-            "placement": dict(batches[0].placement("pipeline"),
-                              note="pipe_place: on the first resident call the current set of the five output "
-                                   "planes and up to two more, each timed (the faster of two passes), the fastest "
-                                   "kept (outside the timed region; DESIGN §4.1)"),
+            "plane_broadcast": comm_note or {"ranks": "RCCL ncclBroadcast to device memory",
+                                             "multi": "RCCL grouped ncclBroadcast", "single": "host plane"}[pl["mode"]],
+            "placement": batches[0].placement("pipeline"),
         }
         pname = batches[0].kernel_name("pipeline")
         out["pipeline"]["kernel"] = pname
         ptraffic, pwhy = profile_traffic(args.traffic_pipeline, frames_gpu, args.step, pname, "pipeline")
         out["pipeline"]["traffic"] = ptraffic
         if ptraffic:
-            out["pipeline"]["frac_of_traffic"] = round(ptraffic / p_avg_s / 1e9 / PEAK_HBM_GBS, 4)
+            out["pipeline"]["frac_of_traffic"] = round(ptraffic / p_avg_s / 1e9 / PEAK_HBM_GBS, 4) \
+                if p_avg_s > 0 else None
         else:
             out["pipeline"]["traffic_note"] = pwhy
         if not args.no_parity:
@@ -864,10 +842,6 @@ def main(argv=None):
         keys = list(parity)
         out["parity"] = {k: {"frames_checked": int(tot[2 * i]), "mismatched_frames": int(tot[2 * i + 1])}
                          for i, k in enumerate(keys)}
-        out["parity"]["vs"] = "device per-frame digests vs tests/golden/frame_digests.npz (pinned C oracle, " \
-                              "global frame ids), every frame of every GPU; pipeline_frame_planes and frame_loop " \
-                              "(two 2048-frame batches in flight) vs tests/golden/plane_digests.npz (oracle " \
-                              "pre-pass -> maskpoints -> RANSAC with random.seed(F) -> pipeline, every frame)"
         out["parity"]["pass"] = all(v["mismatched_frames"] == 0 and v["frames_checked"] > 0
                                     for k, v in out["parity"].items() if isinstance(v, dict))
     if comm:
@@ -875,8 +849,9 @@ def main(argv=None):
     if mcomm:
         mcomm.close()
     ctrl.barrier()
+    out = finalize(out)
     if pl["rank"] == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out, separators=(",", ":")), flush=True)
     ctrl.close()
     return out
 

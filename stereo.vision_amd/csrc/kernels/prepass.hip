@@ -62,6 +62,79 @@ __global__ __launch_bounds__(256) void fill_prev_kernel(const uint32_t* raw, uin
     }
 }
 
+// The same recurrence with loads and stores in different waves. gfx9's vmcnt counts a wave's loads and stores
+// together, in issue order, so in fill_prev_kernel every wait for the next frames' loads also waits for the
+// acknowledgements of the stores issued before them: the store latency sits on the load chain. Here each
+// 128-lane workgroup owns 64 words of the frame: wave 0 only loads (F frames of its 64 words, waits for them, puts
+// them in an LDS slot), wave 1 only computes and stores (its 64 words' recurrence in registers, the cleaned words
+// out), two LDS slots of F frames alternating, one barrier per F frames. Wave 1 never waits on vmcnt (the barrier
+// here is s_barrier with an LDS wait only, no global fence), and wave 0's next F frames are in flight while wave 1
+// works through the previous slot. disp may equal out (in place): a frame's word is loaded before it is written.
+template <int F>
+__global__ __launch_bounds__(128) void fill_prev_split_kernel(const uint32_t* raw, uint32_t* out, uint32_t* masked,
+                                                              const uint32_t* __restrict__ mask,
+                                                              const uint32_t* prev0, int frames, int64_t words) {
+    __shared__ uint32_t ring[2][F][64];
+    const int lane = threadIdx.x & 63;
+    const bool loader = threadIdx.x < 64;
+    const int64_t i = blockIdx.x * 64ll + lane;
+    const bool in = i < words;
+    const int64_t ic = in ? i : words - 1;   // lanes past the frame load a valid word and store nothing
+    const int phases = (frames + F - 1) / F;
+    const auto sync = [] {   // LDS writes complete, then the workgroup barrier; no wait on global stores
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    if (loader) {
+        uint32_t r[F];
+        const auto load = [&](int f0) {   // phase f0 / F: whole phases unconditionally, the last one clamped
+            if (f0 + F <= frames) {
+#pragma unroll
+                for (int u = 0; u < F; ++u) r[u] = __builtin_nontemporal_load(raw + (int64_t)(f0 + u) * words + ic);
+            } else {
+#pragma unroll
+                for (int u = 0; u < F; ++u)
+                    r[u] = __builtin_nontemporal_load(raw + (int64_t)min(f0 + u, frames - 1) * words + ic);
+            }
+        };
+        load(0);
+        for (int ph = 0; ph < phases; ++ph) {
+#pragma unroll
+            for (int u = 0; u < F; ++u) ring[ph & 1][u][lane] = r[u];
+            if (ph + 1 < phases) load((ph + 1) * F);
+            sync();   // slot ph & 1 holds phase ph; the writer has finished phase ph - 1
+        }
+    } else {
+        // fill4(v, 0) = v: without a previous frame the first frame passes through unchanged
+        uint32_t c = prev0 ? prev0[ic] : 0u;
+        const uint32_t m = masked && mask ? mask[ic] : 0u;
+        for (int ph = 0; ph < phases; ++ph) {
+            sync();
+            const int f0 = ph * F, nf = min(F, frames - f0);
+            uint32_t* o = out + (int64_t)f0 * words + i;
+            if (nf == F && !masked) {   // uniform: a whole phase, every read issued before the first wait
+                uint32_t v[F];
+#pragma unroll
+                for (int u = 0; u < F; ++u) v[u] = ring[ph & 1][u][lane];
+#pragma unroll
+                for (int u = 0; u < F; ++u) {
+                    c = fill4(v[u], c);
+                    if (in) o[(int64_t)u * words] = c;
+                }
+            } else {   // the batch's last, partial phase, or a masked copy too
+                for (int u = 0; u < nf; ++u) {
+                    c = fill4(ring[ph & 1][u][lane], c);
+                    if (in) {
+                        o[(int64_t)u * words] = c;
+                        if (masked) masked[(int64_t)(f0 + u) * words + i] = c & m;
+                    }
+                }
+            }
+        }
+    }
+}
+
 // One wave per row of W bytes (W % 4 == 0); rows = frames * H.
 __global__ __launch_bounds__(256) void fill_mean_kernel(uint8_t* disp, uint8_t* masked, const uint8_t* __restrict__ mask,
                                                         int64_t rows, int H, int W, int Wrow) {
@@ -117,6 +190,8 @@ hipError_t launch_mask_bytes(const uint8_t* m, uint8_t* out, int64_t n, hipStrea
     return hipGetLastError();
 }
 
+constexpr int kFillSplitFrames = 16;
+
 hipError_t launch_fill_prev(const uint8_t* raw, uint8_t* out, uint8_t* masked, const uint8_t* mask_ff,
                             const uint8_t* prev0, int frames, int64_t frame_px, hipStream_t s) {
     if (frames <= 0 || frame_px <= 0) return hipSuccess;
@@ -134,6 +209,17 @@ hipError_t launch_fill_prev(const uint8_t* raw, uint8_t* out, uint8_t* masked, c
     auto* m = reinterpret_cast<uint32_t*>(masked);
     const auto* k = reinterpret_cast<const uint32_t*>(mask_ff);
     const auto* p = reinterpret_cast<const uint32_t*>(prev0);
+    // the loader / writer split (fill_prev_split_kernel), F frames a phase; SVX_FILL_SPLIT=0 (diagnostic build)
+    // keeps the one-wave kernel below for A/B
+    int F = kFillSplitFrames;
+    if (const char* e = svx_knob("SVX_FILL_SPLIT")) F = std::atoi(e);
+    if (F > 0) {
+        const dim3 g2((unsigned)((words + 63) / 64)), b2(128);
+        if (F >= 32) hipLaunchKernelGGL(fill_prev_split_kernel<32>, g2, b2, 0, s, r, o, m, k, p, frames, words);
+        else if (F >= 16) hipLaunchKernelGGL(fill_prev_split_kernel<16>, g2, b2, 0, s, r, o, m, k, p, frames, words);
+        else hipLaunchKernelGGL(fill_prev_split_kernel<8>, g2, b2, 0, s, r, o, m, k, p, frames, words);
+        return hipGetLastError();
+    }
     if (U >= 32) hipLaunchKernelGGL(fill_prev_kernel<32>, grid, block, 0, s, r, o, m, k, p, frames, words);
     else if (U >= 16) hipLaunchKernelGGL(fill_prev_kernel<16>, grid, block, 0, s, r, o, m, k, p, frames, words);
     else hipLaunchKernelGGL(fill_prev_kernel<8>, grid, block, 0, s, r, o, m, k, p, frames, words);

@@ -32,30 +32,42 @@ namespace svx {
 struct PyMT {
     uint32_t mt[624];
     int index;
+    // the tempered outputs of the current state (out[i] = temper(mt[i])), made once per twist: the twist and the
+    // tempering run as straight loops over the 624 words (vectorised), and a draw is one load
+    uint32_t out[624];
+    bool out_valid = false;
 
-    uint32_t genrand() {
+    void twist() {
         constexpr uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, A = 0x9908b0dfu;
-        if (index >= 624) {
-            int kk;
-            uint32_t y;
-            for (kk = 0; kk < 624 - 397; kk++) {
-                y = (mt[kk] & UPPER) | (mt[kk + 1] & LOWER);
-                mt[kk] = mt[kk + 397] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
-            }
-            for (; kk < 623; kk++) {
-                y = (mt[kk] & UPPER) | (mt[kk + 1] & LOWER);
-                mt[kk] = mt[kk + (397 - 624)] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
-            }
-            y = (mt[623] & UPPER) | (mt[0] & LOWER);
-            mt[623] = mt[396] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
-            index = 0;
+        int kk;
+        for (kk = 0; kk < 624 - 397; kk++) {
+            const uint32_t y = (mt[kk] & UPPER) | (mt[kk + 1] & LOWER);
+            mt[kk] = mt[kk + 397] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
         }
-        uint32_t y = mt[index++];
-        y ^= (y >> 11);
-        y ^= (y << 7) & 0x9d2c5680u;
-        y ^= (y << 15) & 0xefc60000u;
-        y ^= (y >> 18);
-        return y;
+        for (; kk < 623; kk++) {
+            const uint32_t y = (mt[kk] & UPPER) | (mt[kk + 1] & LOWER);
+            mt[kk] = mt[kk + (397 - 624)] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+        }
+        const uint32_t y = (mt[623] & UPPER) | (mt[0] & LOWER);
+        mt[623] = mt[396] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+        index = 0;
+        out_valid = false;
+    }
+    void temper_all() {
+        for (int i = 0; i < 624; ++i) {
+            uint32_t y = mt[i];
+            y ^= (y >> 11);
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= (y >> 18);
+            out[i] = y;
+        }
+        out_valid = true;
+    }
+    uint32_t genrand() {   // CPython's genrand_uint32
+        if (index >= 624) twist();
+        if (!out_valid) temper_all();
+        return out[index++];
     }
     uint32_t getrandbits(int k) { return k == 0 ? 0u : genrand() >> (32 - k); }   // k <= 32
     uint32_t randbelow(uint32_t n) {

@@ -1031,10 +1031,15 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
             }
         };
         {
+            // every sample index is clamped to the frame's points before it addresses anything: the indices come
+            // from memory another kernel wrote, and a word past the frame's n points (a stale LDS word or another
+            // frame's) would send rb_point's table gathers (12-bit x, y fields) past the tables
+            const uint32_t nm1 = (uint32_t)n64 - 1;
             auto load = [&](int t, uint32_t (&ix)[kRBGather], double (&rec)[kRBTri]) {
                 const IdxT* idx = fidx + (int64_t)t * k;
 #pragma unroll
-                for (int v = 0; v < kRBGather; ++v) ix[v] = (uint32_t)idx[min(lane + kWave * v, k - 1)];   // no branch
+                for (int v = 0; v < kRBGather; ++v)
+                    ix[v] = min((uint32_t)idx[min(lane + kWave * v, k - 1)], nm1);   // no branch
 #pragma unroll
                 for (int q = 0; q < kRBTri; ++q) rec[q] = ftri[(int64_t)t * kRBTri + q];
             };
@@ -1060,7 +1065,7 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
                         if (g > 0) {   // k > 640: the rest of the sample (same order as the first batch)
 #pragma unroll
                             for (int v = 0; v < kRBGather; ++v)
-                                ix[v] = (uint32_t)fidx[(int64_t)t * k + min(j0 + kWave * v, k - 1)];
+                                ix[v] = min((uint32_t)fidx[(int64_t)t * k + min(j0 + kWave * v, k - 1)], nm1);
                         }
 #pragma unroll
                         for (int v = 0; v < kRBGather; ++v) u[v] = P[ix[v]];
@@ -1123,7 +1128,7 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
         }
     }
     __syncthreads();
-    const uint32_t nc = ncand_s;
+    const uint32_t nc = ncand_s, nm1 = (uint32_t)n64 - 1;
     for (uint32_t ci = wave; ci < nc; ci += kRBEvalThreads / 64) {
         const int t = cand[ci];
         const double* tr = ftri + (int64_t)t * kRBTri;
@@ -1134,7 +1139,7 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
         // (3, 1) product, numpy's ddot: fma(z, c, fma(y, b, x a))); np.mean (:289) =
         // the pairwise sum / k. Bit-identical to numpy (tests/test_ransac_cpu.py).
         const double sum = rb_np_pairwise(
-            k, [&](int i) { return P[(uint32_t)idx[i]]; },   // the packed point (LDS, or memory when it did not fit)
+            k, [&](int i) { return P[min((uint32_t)idx[i], nm1)]; },   // the packed point (LDS, or memory), clamped
             [&](uint32_t u) {
                 double qx, qy, qz;
                 rb_point(u, tb, qx, qy, qz);

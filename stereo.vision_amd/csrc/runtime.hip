@@ -1480,11 +1480,14 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 // ---------------------------------------------------------------------------
 
 // DIAGNOSTIC ONLY (env SVX_RANSAC_ABLATE, diagnostic build, documented in DESIGN.md): 1 skips the trial
-// evaluation, 2 draws only the first two trials (results invalid); 4 evaluates every trial in fp64 (no fp32
-// screen; results valid, for A/B); draw kernel (results invalid): 8 no collinearity test, 16 no random.sample.
+// evaluation (results invalid); 4 evaluates every trial in fp64 (no fp32 screen; results valid, for A/B); draw
+// kernel (results invalid): 8 no collinearity test, 16 no random.sample (both also skip the evaluation). Any other
+// bit is refused (-1): an undocumented bit once rode along in an A/B run that faulted.
+static constexpr int kRansacAblateBits = 1 | 4 | 8 | 16;
 static int ransac_ablate() {
     const char* e = svx_knob("SVX_RANSAC_ABLATE");
-    return e ? std::atoi(e) : 0;
+    const int v = e ? std::atoi(e) : 0;
+    return (v & ~kRansacAblateBits) ? -1 : v;
 }
 
 // Batched RANSAC in two phases, so that a caller with other streams to feed (the frame loop) is not held by the
@@ -1577,6 +1580,9 @@ static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_
         b->rmax_pool_n = max_pool_n;
     }
     const int64_t max_n = b->rmax_n, max_pool_n = b->rmax_pool_n;
+    const int ablate = ransac_ablate();
+    if (ablate < 0)
+        return fail(SV_E_ARG, "SVX_RANSAC_ABLATE: only the documented bits 1, 4, 8 and 16 (diagnostic build)");
     HIP_TRY(b->rsidx.ensure(std::max<size_t>(ransac_sidx_bytes(max_n, b->frames, trials, k), 4)));
     HIP_TRY(b->rtri.ensure(sizeof(double) * 5 * F * (size_t)std::max(trials, 1) + sizeof(int32_t) * 2 * F));
     const RansacScratch rs{b->rsidx.p, b->rtri.as<double>(),
@@ -1584,7 +1590,7 @@ static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_
     HIP_TRY(launch_ransac_batch(b->mpk.as<uint32_t>(), b->rtab.as<double>(), b->H, b->W, mcap, p, r.mcount, max_n,
                                 max_pool_n,
                                 seed_base, first_frame, b->frames, trials, k, rs, r.abc, r.err, r.trial, r.flags, trace,
-                                b->trace_trials, ransac_ablate(), phases, started, epoch, stream));
+                                b->trace_trials, ablate, phases, started, epoch, stream));
     return SV_OK;
 }
 
@@ -2499,7 +2505,8 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     // pre-pass (stereovision.py:53-76): frame 0 cleaned with the previous batch's last cleaned frame
     HIP_TRY(begin(kLsPrepass));
     bool carried = false;
-    if (q.prepass) {
+    {   // option 0 (no pre-pass) still runs: a caller-fed slot (keep_input) holds its frames in `raw`, and the
+        // impl copies them into `disp`, which every later stage reads
         const uint8_t* prev = q.prepass == 1 && L->carry_valid ? L->carry[L->carry_cur].as<uint8_t>() : nullptr;
         if (int rc = batch_prepass_impl(b, q.prepass, prev)) return rc;
         if (q.prepass == 1) {

@@ -126,11 +126,14 @@ def _read_png(path):
     if ctype == 3:   # palette: indices -> RGB, or RGBA when the file gives palette alpha
         if plte is None or len(plte) == 0:
             raise PngCorrupt(f"{path}: palette image without PLTE")
-        idx = np.minimum(px[..., 0], len(plte) - 1)
-        rgb = plte[idx]
+        # libpng keeps a zero-filled 256-entry palette (alpha 255 past tRNS), so an index past PLTE decodes black
+        pal = np.zeros((256, 3), np.uint8)
+        pal[:min(len(plte), 256)] = plte[:256]
+        idx = px[..., 0]
+        rgb = pal[idx]
         if trns is not None and len(trns):
-            alpha = np.full(len(plte), 255, np.uint8)
-            alpha[:min(len(trns), len(plte))] = trns[:len(plte)]
+            alpha = np.full(256, 255, np.uint8)
+            alpha[:min(len(trns), len(plte), 256)] = trns[:min(len(plte), 256)]
             return np.dstack([rgb, alpha[idx]]), 6, None, 8
         return rgb, 2, None, 8
     if trns is not None and ctype in (0, 2) and len(trns) >= 2 * ch:

@@ -152,3 +152,45 @@ def test_committed_profiles_name_their_kernel():
         tj = json.load(open(os.path.join(REPO, "profiles", f)))
         assert tj.get(key), f
         assert tj.get("source_ids"), f
+
+
+def _record(extra_bytes=0):
+    """A line with every record bench.py emits at N = 1 (numbers and short keys only), optionally bloated."""
+    stage = {k: 1.234 for k in ("input", "prepass", "maskpoints", "draw", "eval", "pipeline", "road")}
+    pl = {"tried_ms": [4.2345, 4.3456, 4.4567], "kept": 1}
+    loop = {"ms_per_batch": 14.38, "frames": 4096, "frames_per_s": 284840.1, "slots": 2, "batches_timed": 4,
+            "stage_ms": stage, "draw_overlap_ms": 5.123}
+    out = {"metric": bench.METRIC, "value": 534406.4, "unit": "Mpoints/s", "n_gpus": 1, "steps": 20, "warmup": 3,
+           "ms_per_step": 4.2576, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8->f32",
+           "data": "synthetic", "config": {"workload": "configs[2]", "frames_per_gpu": 4096, "parallelism": "x1"},
+           "roofline": {"bound": "hbm", "achieved": 6972.5, "peak": 8000.0, "unit": "GB/s", "frac": 0.8716,
+                        "traffic": 29607724672.0, "kernel": "svx::project_dense_kernel<1, true, 1, 0>",
+                        "kernel_ms": 4.2422, "placement": dict(pl, junk="x" * extra_bytes)},
+           "cpu_baseline": {"value": 1.52, "unit": "Mpoints/s", "cores": 1, "kind": "port", "sample": "configs[0]"},
+           "latency_1frame_us": 6.8,
+           "pipeline": {"gpu_ms_per_call": 5.256, "frac": 0.649, "value": 432900.1, "placement": pl,
+                        "kernel": "svx::resident_fused_kernel<1, 4, true, true, true, false>", "traffic": 2.7e10},
+           "parity": {"k1": {"frames_checked": 4096, "mismatched_frames": 0}, "pass": True},
+           "extras": {"device_frame_loop": loop, "device_frame_loop_serial": dict(loop),
+                      "device_frame_loop_with_input": dict(loop),
+                      "sgbm_disparity": {"us_per_frame": 236.4, "placement": dict(pl, junk="y" * extra_bytes)}}}
+    return out
+
+
+def test_json_line_within_limit():
+    """The driver keeps the last 8 KB of the run's output: the line is at most LINE_LIMIT bytes, the contract fields
+    come first, and an over-long line loses placements and stage breakdowns before any contract or headline
+    field (the pipeline's own figures had fallen out of the driver's record)."""
+    import json
+    for extra in (0, 3000, 9000):
+        o = bench.finalize(_record(extra))
+        line = json.dumps(o, separators=(",", ":"))
+        assert len(line.encode()) <= bench.LINE_LIMIT, (extra, len(line))
+        assert line.startswith('{"metric":')
+        for k in ("value", "unit", "ms_per_step", "roofline", "cpu_baseline", "pipeline", "parity",
+                  "latency_1frame_us"):
+            assert k in o, (extra, k)
+        assert o["pipeline"]["gpu_ms_per_call"] == 5.256 and o["pipeline"]["frac"] == 0.649
+        assert o["extras"]["device_frame_loop"]["ms_per_batch"] == 14.38
+    # the unbloated line needs no drop at all
+    assert bench.finalize(_record(0)) == bench.finalize(_record(0), limit=10 ** 9)

@@ -151,10 +151,23 @@ def test_caller_slot_keeps_its_raw_frames(mask, prepass):
     """A caller-fed slot keeps the frames the caller wrote: the pre-pass reads them there and writes the cleaned
     frames elsewhere, so submitting the slot again without refilling it processes the same raw frames (with a
     per-frame pre-pass, fillAltDisparity or none, the results are identical), and the raw frames are never
-    overwritten by a clean."""
+    overwritten by a clean. The first submit must also equal a plain batch given the same uploads (with
+    prepass="none" the stages read frames the loop copied from the raw buffer, not a buffer never written)."""
     import oracle
+    from svx import batch
     from svx.loop import FrameLoop
     frames = [oracle.synth_frame(g) for g in range(40, 44)]
+    with batch.Batch(4, with_bgr=True, with_points=True) as one:
+        for f, (d, c) in enumerate(frames):
+            one.upload(f, d, c)
+        one.set_mask(mask)
+        if prepass != "none":
+            one.prepass(prepass)
+        one.ransac(seed_base=3, trials=600, first_frame=40)
+        one.pipeline_planes()
+        ref = one.digest("pipeline")
+        ref_r = [one.read_ransac(f)["trial"] for f in range(4)]
+    assert np.all(ref[:, 2] > 0)   # the frames keep points: a batch of zeros would not
     with FrameLoop(4, slots=1, source="caller", prepass=prepass, seed_base=3, carmask=mask) as loop:
         b = loop.acquire()
         for f, (d, c) in enumerate(frames):
@@ -164,6 +177,7 @@ def test_caller_slot_keeps_its_raw_frames(mask, prepass):
         b0, _ = loop.batch(s0)
         want = b0.digest("pipeline")
         want_r = [b0.read_ransac(f)["trial"] for f in range(4)]
+        assert np.array_equal(want, ref) and want_r == ref_r
         for rep in range(2):
             loop.acquire()   # not refilled
             s1 = loop.submit(40)

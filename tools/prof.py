@@ -84,6 +84,10 @@ def _run(b, w, chunk=0, sync=False):
 
 
 def cmd_workload(a):
+    if a.srcid_out:   # the sources of the library THIS process profiles (traffic_json reads them back)
+        import bench
+        with open(a.srcid_out, "w") as fh:
+            json.dump({k: bench.kernel_source_id(k) for k in ("k1", "pipeline")}, fh)
     b = _batch(a.frames, a.what, a.mode)
     if "planes" in a.what:
         b.ransac(seed_base=0, trials=600)
@@ -231,13 +235,18 @@ def traffic_json(root, frames, step):
     v = _load_pmc(root)
     out = {"frames": frames, "step": step, "source": root,
            "correction": "fetched = 2 x FETCH_SIZE (gfx950, calibrated on K1's loads); written = WRITE_SIZE"}
-    # the sources the profiled kernels were built from: bench.py uses a profile only for the same instance name
-    # AND the same sources (bench.kernel_source_id)
-    import bench
+    # the sources the profiled kernels were built from, as the profiled `workload` process recorded them from the
+    # library it loaded (source_ids.json beside each pass): bench.py uses a profile only for the same instance name
+    # AND the same sources. Without that record (an older profile) no id is written and bench.py reports null.
+    ids = {}
+    for f in sorted(glob.glob(f"{root}/**/source_ids.json", recursive=True)):
+        for kind, sid in json.load(open(f)).items():
+            if ids.setdefault(kind, sid) != sid:
+                ids[kind] = None   # passes of one profile from different libraries: no id
     kinds = {"k1": "project_dense_kernel", "pipeline": "resident_fused_kernel"}
     for kind, pat in kinds.items():
-        if any(pat in k for k in v):
-            out.setdefault("source_ids", {})[kind] = bench.kernel_source_id(kind)
+        if any(pat in k for k in v) and ids.get(kind):
+            out.setdefault("source_ids", {})[kind] = ids[kind]
     for k, cs in v.items():
         if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
@@ -264,8 +273,9 @@ def cmd_traffic(a):
 
 def _profile(args, out, workload):
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+    os.makedirs(out, exist_ok=True)
     cmd = ["rocprofv3", *args, "--output-format", "csv", "-d", out, "-o", "run", "--",
-           sys.executable, __file__, "workload", *workload]
+           sys.executable, __file__, "workload", "--srcid-out", os.path.join(out, "source_ids.json"), *workload]
     with open(out + ".log", "w") as log:
         # no placement probes: counted bytes are per launch of the measured call
         p = subprocess.run(["timeout", "-s", "KILL", "180", *cmd], stdout=log, stderr=subprocess.STDOUT,
@@ -370,7 +380,9 @@ def main():
         p.add_argument("--reps", type=int, default=3)
         p.add_argument("--mode", default="auto")
         p.add_argument("--chunk", type=int, default=0)
-    common(sp.add_parser("workload"), "k1,pipe")
+    p = sp.add_parser("workload")
+    common(p, "k1,pipe")
+    p.add_argument("--srcid-out", default="", help="write the loaded library's source ids here (JSON)")
     p = sp.add_parser("time")
     common(p)
     p.add_argument("--sizes", default="4096")
