@@ -59,6 +59,18 @@ int sv_project_frame(const uint8_t* disp, int H, int W, int64_t ld_disp,
                      const uint8_t* bgr, int64_t ld_bgr, int step, const sv_camera* cam,
                      double* out_xyz, uint8_t* out_rgb, int64_t cap, int64_t* out_n);
 
+/* projectDisparityTo3d's rows as the drop-in returns them (functions.py:178-198, the same points and bits as
+ * sv_project_frame): out_rows holds cap rows of `cols` doubles — X, Y, Z (cols 3; bgr may be NULL) or X, Y, Z, R,
+ * G, B (cols 6, bgr required) — laid out on the device and copied back in one transfer, a direct DMA when out_rows
+ * is page-locked (sv_host_alloc). *out_n = rows written. */
+int sv_project_rows(const uint8_t* disp, int H, int W, int64_t ld_disp, const uint8_t* bgr, int64_t ld_bgr,
+                    int step, const sv_camera* cam, double* out_rows, int cols, int64_t cap, int64_t* out_n);
+
+/* Page-locked host memory for drop-in outputs (hipHostMalloc / hipHostFree): the Python binding pools these blocks
+ * and hands them out as numpy arrays that return to the pool when the last view is gone (svx/_abi.py). */
+int sv_host_alloc(int64_t bytes, void** out);
+int sv_host_free(void* p);
+
 /* Replaces functions.py:201-209 project3DPointsTo2DImagePoints(points):
  * x = ((X*f)/Z)+cw, y = ((Y*f)/Z)+ch in fp64, bit-identical. xyz rows have
  * stride ld (>= 3) doubles; out_xy is n x 2. */

@@ -335,6 +335,28 @@ hipError_t launch_project_compact_f64(const KParams& p, const uint8_t* disp, int
     return hipGetLastError();
 }
 
+// The drop-in's rows (sv_project_rows): X, Y, Z and the colour bytes as doubles, 6 a row, so the host receives
+// the array it returns in one copy (no numpy assembly of two arrays).
+__global__ __launch_bounds__(256) void rows6_kernel(const double* __restrict__ xyz, const uint8_t* __restrict__ rgb,
+                                                    int64_t n, double* __restrict__ rows) {
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        double* r = rows + 6 * i;
+        r[0] = xyz[3 * i];
+        r[1] = xyz[3 * i + 1];
+        r[2] = xyz[3 * i + 2];
+        r[3] = (double)rgb[3 * i];
+        r[4] = (double)rgb[3 * i + 1];
+        r[5] = (double)rgb[3 * i + 2];
+    }
+}
+
+hipError_t launch_rows6(const double* xyz, const uint8_t* rgb, int64_t n, double* rows, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(rows6_kernel, dim3(g), dim3(256), 0, s, xyz, rgb, n, rows);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // Drop-in back-projection (functions.py:201-209), fp64, bit-identical.
 // ---------------------------------------------------------------------------

@@ -96,14 +96,33 @@ static void py_sample(PyMT& rng, uint32_t n, int k, int32_t* out, std::vector<ui
             pool[j] = pool[n - i - 1];
         }
     } else {
-        if (selected.size() < (n + 63) / 64) selected.assign((n + 63) / 64, 0);
-        for (int i = 0; i < k; ++i) {
-            uint32_t j = rng.randbelow(n);
-            while ((selected[j >> 6] >> (j & 63)) & 1) j = rng.randbelow(n);
-            selected[j >> 6] |= 1ull << (j & 63);
-            out[i] = (int32_t)j;
+        // `j = randbelow(n); while j in selected: j = randbelow(n)` consumes the stream one word at a time and
+        // keeps a word iff its top n.bit_length() bits are < n and not selected yet: one flat, branch-free loop
+        // over the tempered words (a rejected word writes its bit into a spare word past the bitmap)
+        const uint32_t nw = (n + 63) / 64;
+        if (selected.size() < nw + 1) selected.assign(nw + 1, 0);
+        const int sh = __builtin_clz(n);   // 32 - n.bit_length()
+        uint64_t* __restrict__ sel = selected.data();
+        int32_t* __restrict__ dst = out;   // (distinct from the state and the bitmap: no reload after each store)
+        int cnt = 0;
+        while (cnt < k) {
+            if (rng.index >= 624) rng.twist();
+            if (!rng.out_valid) rng.temper_all();
+            const uint32_t* __restrict__ src = rng.out;
+            int i = rng.index;
+            for (; i < 624 && cnt < k; ++i) {
+                const uint32_t j = src[i] >> sh;
+                const uint32_t jj = j < n ? j : 64u * nw;   // the spare word
+                const uint64_t w = sel[jj >> 6], bit = 1ull << (jj & 63);
+                const uint32_t take = (uint32_t)(j < n) & (uint32_t)((w & bit) == 0);
+                sel[jj >> 6] = w | (take ? bit : 0ull);
+                dst[cnt] = (int32_t)j;
+                cnt += (int)take;
+            }
+            rng.index = i;
         }
-        for (int i = 0; i < k; ++i) selected[(uint32_t)out[i] >> 6] = 0;   // every word that got a bit
+        for (int i = 0; i < k; ++i) sel[(uint32_t)out[i] >> 6] = 0;   // every word that got a bit
+        sel[nw] = 0;
     }
 }
 

@@ -984,6 +984,15 @@ __device__ __forceinline__ void fused_body(const PipeBuffers& bf, const RParams&
     const int frame = blockIdx.x;
     const FramePlane* Lp = bf.planes + (int64_t)frame * bf.plane_stride;
     const RLean L{Lp->al32, Lp->bb32, Lp->b032, Lp->tn32, Lp->g32};
+#ifdef SVX_DIAG
+    // DIAGNOSTIC A/B (diagnostic build; outputs unchanged): ablate bits 20-30 = a start delay in us per slot group,
+    // workgroup w of the first round waiting (w / 256) x that, so the five workgroups a CU holds do not run pass 1
+    // and pass 2 in phase (the phase-lock probe)
+    if (const uint32_t us = (uint32_t)p.ablate >> 20; us && blockIdx.x < 5 * 256) {
+        const uint64_t t0 = wall_clock64(), wait = (uint64_t)(blockIdx.x >> 8) * us * 100u;   // 100 MHz ticks
+        while (wall_clock64() - t0 < wait) __builtin_amdgcn_s_sleep(32);
+    }
+#endif
     frame_pass1<STEP, QP, LC, PF1>(frame, sh, bf, L, Lp, p);
     // pass 2 (store-bound) issues ahead of other workgroups' pass-1 waves on the SIMD: -0.2 to -0.4 %
     // (5.78 vs 5.80 ms, 6.81 vs 6.82 with per-frame planes; ten and eight in-process alternations)

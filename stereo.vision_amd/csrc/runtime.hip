@@ -439,20 +439,11 @@ int sv_init(int device) {
 // ---------------------------------------------------------------------------
 // drop-in: projectDisparityTo3d (functions.py:178-198)
 // ---------------------------------------------------------------------------
-int sv_project_frame(const uint8_t* disp, int H, int W, int64_t ld_disp, const uint8_t* bgr,
-                     int64_t ld_bgr, int step, const sv_camera* cam, double* out_xyz, uint8_t* out_rgb,
-                     int64_t cap, int64_t* out_n) {
-    if (!disp || !cam || !out_n || H < 0 || W < 0 || step < 1 || ld_disp < W)
-        return fail(SV_E_ARG, "sv_project_frame: bad arguments (H=%d W=%d step=%d)", H, W, step);
-    if (bgr && ld_bgr < 3ll * W) return fail(SV_E_ARG, "sv_project_frame: ld_bgr < 3*W");
-    *out_n = 0;
-    const KParams p = make_params(H, W, step, *cam);
-    if ((int64_t)p.Hg * p.Wg == 0) return SV_OK;
-    int dev;
-    if (int rc = current_device(&dev)) return rc;
-    Device* d;
-    if (int rc = dev_get(dev, &d)) return rc;
-    std::lock_guard<std::mutex> lk(d->mu);
+// The drop-in projection on the device: the frame (and its colours) up, the compact fp64 kernel, the point count
+// back (one sync). On success *n is the count and d's xyz / rgb buffers hold the points; the device mutex is held
+// by the caller.
+static int project_on_device(Device* d, const uint8_t* disp, int H, int W, int64_t ld_disp, const uint8_t* bgr,
+                             int64_t ld_bgr, bool want_rgb, const KParams& p, int64_t* n) {
     hipStream_t s = d->stream;
     const int tiles = project_compact_tiles(p);
     const int64_t ng = (int64_t)p.Hg * p.Wg;
@@ -460,7 +451,6 @@ int sv_project_frame(const uint8_t* disp, int H, int W, int64_t ld_disp, const u
     HIP_TRY(d->xyz.ensure(sizeof(double) * 3 * ng));
     HIP_TRY(d->ctrl.ensure(sizeof(uint64_t) * (tiles + 2)));
     HIP_TRY(hipMemcpy2DAsync(d->disp.p, W, disp, ld_disp, W, H, hipMemcpyHostToDevice, s));
-    const bool want_rgb = bgr && out_rgb;
     if (want_rgb) {
         HIP_TRY(d->bgr.ensure((size_t)H * W * 3));
         HIP_TRY(d->rgb.ensure(3 * ng));
@@ -477,7 +467,28 @@ int sv_project_frame(const uint8_t* disp, int H, int W, int64_t ld_disp, const u
     HIP_TRY(hipMemcpyAsync(hs, small, sizeof hs, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (hs[2]) return fail(SV_E_DEVICE, "projection look-back timed out");
-    const int64_t n = hs[1];
+    *n = hs[1];
+    return SV_OK;
+}
+
+int sv_project_frame(const uint8_t* disp, int H, int W, int64_t ld_disp, const uint8_t* bgr,
+                     int64_t ld_bgr, int step, const sv_camera* cam, double* out_xyz, uint8_t* out_rgb,
+                     int64_t cap, int64_t* out_n) {
+    if (!disp || !cam || !out_n || H < 0 || W < 0 || step < 1 || ld_disp < W)
+        return fail(SV_E_ARG, "sv_project_frame: bad arguments (H=%d W=%d step=%d)", H, W, step);
+    if (bgr && ld_bgr < 3ll * W) return fail(SV_E_ARG, "sv_project_frame: ld_bgr < 3*W");
+    *out_n = 0;
+    const KParams p = make_params(H, W, step, *cam);
+    if ((int64_t)p.Hg * p.Wg == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    const bool want_rgb = bgr && out_rgb;
+    int64_t n = 0;
+    if (int rc = project_on_device(d, disp, H, W, ld_disp, bgr, ld_bgr, want_rgb, p, &n)) return rc;
     if (n > cap) return fail(SV_E_CAP, "output capacity %lld < %lld points", (long long)cap, (long long)n);
     if (n) {
         HIP_TRY(hipMemcpyAsync(out_xyz, d->xyz.p, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, s));
@@ -485,6 +496,52 @@ int sv_project_frame(const uint8_t* disp, int H, int W, int64_t ld_disp, const u
         HIP_TRY(hipStreamSynchronize(s));
     }
     *out_n = n;
+    return SV_OK;
+}
+
+int sv_project_rows(const uint8_t* disp, int H, int W, int64_t ld_disp, const uint8_t* bgr, int64_t ld_bgr,
+                    int step, const sv_camera* cam, double* out_rows, int cols, int64_t cap, int64_t* out_n) {
+    if (!disp || !cam || !out_n || H < 0 || W < 0 || step < 1 || ld_disp < W || (cols != 3 && cols != 6) ||
+        (cols == 6 && !bgr))
+        return fail(SV_E_ARG, "sv_project_rows: bad arguments (H=%d W=%d step=%d cols=%d)", H, W, step, cols);
+    if (bgr && ld_bgr < 3ll * W) return fail(SV_E_ARG, "sv_project_rows: ld_bgr < 3*W");
+    *out_n = 0;
+    const KParams p = make_params(H, W, step, *cam);
+    if ((int64_t)p.Hg * p.Wg == 0) return SV_OK;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    Device* d;
+    if (int rc = dev_get(dev, &d)) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t s = d->stream;
+    int64_t n = 0;
+    if (int rc = project_on_device(d, disp, H, W, ld_disp, bgr, ld_bgr, cols == 6, p, &n)) return rc;
+    if (n > cap) return fail(SV_E_CAP, "output capacity %lld < %lld points", (long long)cap, (long long)n);
+    if (!n) return SV_OK;
+    if (!out_rows) return fail(SV_E_ARG, "sv_project_rows: null out_rows");
+    const double* src = d->xyz.as<double>();
+    if (cols == 6) {
+        HIP_TRY(d->aux2.ensure(sizeof(double) * 6 * (size_t)n));
+        HIP_TRY(launch_rows6(d->xyz.as<double>(), d->rgb.as<uint8_t>(), n, d->aux2.as<double>(), s));
+        src = d->aux2.as<double>();
+    }
+    HIP_TRY(hipMemcpyAsync(out_rows, src, sizeof(double) * cols * (size_t)n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *out_n = n;
+    return SV_OK;
+}
+
+int sv_host_alloc(int64_t bytes, void** out) {
+    if (!out || bytes <= 0) return fail(SV_E_ARG, "sv_host_alloc: bad arguments");
+    *out = nullptr;
+    int dev;
+    if (int rc = current_device(&dev)) return rc;   // (no GPU: fails like every compute entry point)
+    HIP_TRY(hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault));
+    return SV_OK;
+}
+
+int sv_host_free(void* p) {
+    if (p) HIP_TRY(hipHostFree(p));
     return SV_OK;
 }
 
@@ -1669,11 +1726,17 @@ int sv_ransac_draw(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld,
     return SV_OK;
 }
 
+// The draws are replayed on the host in chunks of trials; each chunk's samples go up (asynchronously when the
+// caller's sidx / tri are page-locked, as svx/ransac.py allocates them) and are evaluated on the device while the
+// next chunk is drawn, so only the last chunk's evaluation is exposed after the replay.
 int sv_ransac(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
               int32_t* tri, double* out_abc, double* out_err, uint8_t* out_flag, int* out_trials) {
-    if (int rc = sv_ransac_draw(mt_state, pts, n, ld, trials, k, sidx, tri, out_trials)) return rc;
-    const int ran = *out_trials;
-    if (ran == 0) return SV_OK;
+    if (!mt_state || !out_trials || trials < 0 || k < 0 || ld < 3 || n < 0 || (n > 0 && !pts) ||
+        (trials > 0 && (!sidx || !tri)))
+        return fail(SV_E_ARG, "sv_ransac: bad arguments");
+    if (mt_state[624] > 624) return fail(SV_E_ARG, "sv_ransac: MT index %u > 624", mt_state[624]);
+    *out_trials = 0;
+    if (trials == 0 || n < k || n < 1 || n >= (1ll << 31)) return SV_OK;   // random.sample raises: no draw
     if (!out_abc || !out_err || !out_flag) return fail(SV_E_ARG, "sv_ransac: null outputs");
     int dev;
     if (int rc = current_device(&dev)) return rc;
@@ -1682,24 +1745,35 @@ int sv_ransac(uint32_t* mt_state, const double* pts, int64_t n, int64_t ld, int 
     std::lock_guard<std::mutex> lk(d->mu);
     hipStream_t s = d->stream;
     const size_t pbytes = sizeof(double) * (size_t)n * ld;
-    const size_t ibytes = sizeof(int32_t) * ((size_t)ran * k + 3 * (size_t)ran);
-    const size_t obytes = sizeof(double) * 4 * (size_t)ran + (size_t)ran;
+    const size_t ibytes = sizeof(int32_t) * ((size_t)trials * k + 3 * (size_t)trials);
+    const size_t obytes = sizeof(double) * 4 * (size_t)trials + (size_t)trials;
     HIP_TRY(d->xyz.ensure(pbytes));
     HIP_TRY(d->aux.ensure(ibytes));
     HIP_TRY(d->aux2.ensure(obytes));
     int32_t* dsidx = d->aux.as<int32_t>();
-    int32_t* dtri = dsidx + (size_t)ran * k;
+    int32_t* dtri = dsidx + (size_t)trials * k;
     double* dabc = d->aux2.as<double>();
-    double* derr = dabc + 3 * (size_t)ran;
-    uint8_t* dflag = reinterpret_cast<uint8_t*>(derr + ran);
+    double* derr = dabc + 3 * (size_t)trials;
+    uint8_t* dflag = reinterpret_cast<uint8_t*>(derr + trials);
     HIP_TRY(hipMemcpyAsync(d->xyz.p, pts, pbytes, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(dsidx, sidx, sizeof(int32_t) * (size_t)ran * k, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(dtri, tri, sizeof(int32_t) * 3 * (size_t)ran, hipMemcpyHostToDevice, s));
-    HIP_TRY(launch_ransac_eval(d->xyz.as<double>(), ld, dsidx, dtri, ran, k, dabc, derr, dflag, s));
-    HIP_TRY(hipMemcpyAsync(out_abc, dabc, sizeof(double) * 3 * ran, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(out_err, derr, sizeof(double) * ran, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(out_flag, dflag, (size_t)ran, hipMemcpyDeviceToHost, s));
+    constexpr int kChunks = 4;
+    const int per = (trials + kChunks - 1) / kChunks;
+    for (int t0 = 0; t0 < trials; t0 += per) {
+        const int c = std::min(per, trials - t0);
+        if (ransac_draw(mt_state, pts, n, ld, c, k, sidx + (size_t)t0 * k, tri + 3 * (size_t)t0) != c)
+            return fail(SV_E_ARG, "sv_ransac: draw replay stopped");
+        HIP_TRY(hipMemcpyAsync(dsidx + (size_t)t0 * k, sidx + (size_t)t0 * k, sizeof(int32_t) * (size_t)c * k,
+                               hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(dtri + 3 * (size_t)t0, tri + 3 * (size_t)t0, sizeof(int32_t) * 3 * (size_t)c,
+                               hipMemcpyHostToDevice, s));
+        HIP_TRY(launch_ransac_eval(d->xyz.as<double>(), ld, dsidx + (size_t)t0 * k, dtri + 3 * (size_t)t0, c, k,
+                                   dabc + 3 * (size_t)t0, derr + t0, dflag + t0, s));
+    }
+    HIP_TRY(hipMemcpyAsync(out_abc, dabc, sizeof(double) * 3 * trials, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_err, derr, sizeof(double) * trials, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_flag, dflag, (size_t)trials, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    *out_trials = trials;
     return SV_OK;
 }
 
@@ -2447,6 +2521,25 @@ static int loop_enqueue_tail(sv_loop* L, int64_t seq, uint64_t gate_epoch) {
     };
     auto end = [&](int stage) { return hipEventRecord(L->t1[s][stage], st); };
     if (gate_epoch) HIP_TRY(launch_loop_gate(L->gate.as<uint64_t>(), gate_epoch, 50.0, st));
+#ifdef SVX_DIAG
+    // DIAGNOSTIC probe (diagnostic build, SVX_LOOP_SIDE=1; results unchanged): one more fill pass over this batch's
+    // raw frames into a scratch buffer, on a side stream, beside the pipeline and the next batch's draw — how much
+    // does a pre-pass moved into that window slow them? (the three-deep front end)
+    if (const char* e = svx_knob("SVX_LOOP_SIDE"); e && e[0] == '1' && b->keep_input) {
+        static hipStream_t side = nullptr;
+        static hipEvent_t ev = nullptr;
+        static DevBuf scratch;
+        if (!side) {
+            HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        }
+        const int64_t px = (int64_t)b->H * b->W;
+        HIP_TRY(scratch.ensure((size_t)px * b->frames));
+        HIP_TRY(hipEventRecord(ev, st));
+        HIP_TRY(hipStreamWaitEvent(side, ev, 0));
+        HIP_TRY(launch_fill_prev(input_disp(b), scratch.as<uint8_t>(), nullptr, nullptr, nullptr, b->frames, px, side));
+    }
+#endif
     // the pipeline with every frame's own plane (stereovision.py:97-113)
     HIP_TRY(begin(kLsPipeline));
     if (int rc = sv_batch_pipeline_planes(b, &L->cam, q.point_thr, q.hist_thr, 0, 0)) return rc;

@@ -19,6 +19,7 @@ hipError_t launch_project_compact_f64(const KParams& p, const uint8_t* disp, int
                                       const uint8_t* bgr, int64_t ld_bgr, double* xyz, uint8_t* rgb,
                                       uint64_t* status, uint32_t* ticket, uint32_t* count,
                                       uint32_t* err, hipStream_t s);
+hipError_t launch_rows6(const double* xyz, const uint8_t* rgb, int64_t n, double* rows, hipStream_t s);
 hipError_t launch_backproject_f64(const double* xyz, int64_t n, int64_t ld, double f, double cw,
                                   double ch, double* xy, hipStream_t s);
 int project_compact_tiles(const KParams& p);

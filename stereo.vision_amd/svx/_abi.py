@@ -48,6 +48,9 @@ SIGNATURES = {
     "sv_device_count": [ctypes.POINTER(I)],
     "sv_init": [I],
     "sv_project_frame": [P, I, I, I64, P, I64, I, ctypes.POINTER(Camera), P, P, I64, PI64],
+    "sv_project_rows": [P, I, I, I64, P, I64, I, ctypes.POINTER(Camera), P, I, I64, PI64],
+    "sv_host_alloc": [I64, ctypes.POINTER(P)],
+    "sv_host_free": [P],
     "sv_backproject": [P, I64, I64, ctypes.POINTER(Camera), P],
     "sv_pipeline_frame": [P, P, I, I, I, ctypes.POINTER(Camera), ctypes.POINTER(Plane), D, I,
                           P, P, P, P, I64],
@@ -184,3 +187,58 @@ def device_count():
     n = ctypes.c_int(0)
     rc = lib().sv_device_count(ctypes.byref(n))
     return n.value if rc == 0 else 0
+
+
+class _PinnedPool:
+    """Page-locked host blocks (sv_host_alloc) for drop-in outputs, reused by size class: an array handed out by
+    pinned_empty() returns its block here when the array and every view of it are gone, so a frame loop that drops
+    each frame's points recycles the same few blocks and every device-to-host copy is a direct DMA."""
+
+    def __init__(self):
+        import threading
+        self._free = {}
+        self._lock = threading.Lock()
+        self._closed = False
+        self.allocs = 0   # blocks allocated (sv_host_alloc) so far: a steady loop stops adding to it
+
+    def take(self, nbytes):
+        size = 1 << max(16, (int(nbytes) - 1).bit_length())   # power-of-two classes from 64 KiB
+        with self._lock:
+            blocks = self._free.get(size)
+            if blocks:
+                return blocks.pop(), size
+        p = P()
+        call("sv_host_alloc", size, ctypes.byref(p))
+        self.allocs += 1
+        return p.value, size
+
+    def give(self, addr, size):
+        if self._closed:
+            return
+        with self._lock:
+            self._free.setdefault(size, []).append(addr)
+
+    def close(self):   # interpreter exit: the HIP runtime may already be gone, so the blocks are left to it
+        self._closed = True
+
+
+_pool = _PinnedPool()
+
+
+def pinned_empty(shape, dtype):
+    """An uninitialised numpy array in pooled page-locked host memory (see _PinnedPool)."""
+    import weakref
+
+    import numpy as np
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape))
+    nbytes = max(count * dt.itemsize, 1)
+    addr, size = _pool.take(nbytes)
+    buf = (ctypes.c_char * nbytes).from_address(addr)
+    weakref.finalize(buf, _pool.give, addr, size)
+    return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
+
+
+import atexit  # noqa: E402
+
+atexit.register(_pool.close)

@@ -102,16 +102,37 @@ def project_frame(disparity, rgb=None, step=REFERENCE_STEP, camera=None):
 from .points import PointList, as_points_array, gather_columns  # noqa: E402,F401  (re-exported)
 
 
+def project_rows(disparity, rgb=None, step=REFERENCE_STEP, camera=None):
+    """(N, 6) float64 rows X, Y, Z, R, G, B — or (N, 3) without colours — in reference order, laid out on the
+    device and copied straight into pooled page-locked memory (sv_project_rows, one DMA, no host assembly)."""
+    disp = _as_u8(disparity, 2, "disparity")
+    h, w = disp.shape
+    bgr = None
+    if rgb is not None and len(rgb) > 0:
+        bgr = _as_u8(rgb, 3, "rgb")
+        if bgr.shape[0] < h or bgr.shape[1] < w or bgr.shape[2] < 3:
+            raise IndexError(f"rgb shape {bgr.shape} smaller than disparity {disp.shape}")
+        if bgr.shape[2] != 3:
+            bgr = np.ascontiguousarray(bgr[:, :, :3])
+    cols = 6 if bgr is not None else 3
+    hg = (h - 1 + step - 1) // step if h > 1 else 0
+    wg = (w - 1 + step - 1) // step if w > 1 else 0
+    cap = max(hg * wg, 1)
+    cam = camera if camera is not None else _camera()
+    n = ctypes.c_int64(0)
+    if hg * wg == 0:
+        rows = np.empty((cap, cols), np.float64)
+    else:
+        rows = _abi.pinned_empty((cap, cols), np.float64)
+    _abi.call("sv_project_rows", _abi.ptr(disp), h, w, disp.strides[0], _abi.ptr(bgr),
+              bgr.strides[0] if bgr is not None else 0, step, ctypes.byref(cam), _abi.ptr(rows), cols, cap,
+              ctypes.byref(n))
+    return rows[: n.value]
+
+
 def projectDisparityTo3d(disparity, max_disparity, rgb=[]):  # noqa: N802,B006 (reference signature)
     """functions.py:178-198 on the GPU. Returns a Sequence of rows (see module doc)."""
-    xyz, rgbs = project_frame(disparity, rgb)
-    if rgbs is None:
-        rows = xyz
-    else:
-        rows = np.empty((len(xyz), 6), np.float64)
-        rows[:, :3] = xyz
-        rows[:, 3:] = rgbs
-    return PointList(rows)
+    return PointList(project_rows(disparity, rgb))
 
 
 def project3DPointsTo2DImagePoints(points):  # noqa: N802

@@ -42,8 +42,9 @@ def trials_gpu(points, trials, state=None, k=SAMPLE):
     st = state if state is not None else random.getstate()
     words = np.array(st[1], dtype=np.uint32)
     n = len(arr)
-    sidx = np.empty((max(trials, 1), k), np.int32)
-    tri = np.empty((max(trials, 1), 3), np.int32)
+    # page-locked (pooled): sv_ransac sends each chunk of drawn trials up while it draws the next
+    sidx = _abi.pinned_empty((max(trials, 1), k), np.int32)
+    tri = _abi.pinned_empty((max(trials, 1), 3), np.int32)
     abc = np.empty((max(trials, 1), 3), np.float64)
     err = np.empty(max(trials, 1), np.float64)
     flag = np.empty(max(trials, 1), np.uint8)

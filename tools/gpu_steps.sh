@@ -33,9 +33,27 @@ for step in "$@"; do
   ab_fill)
     timeout -k 10 600 python3 -u tools/prof.py ab-lib --envs "${FILL_ENVS:-SVX_FILL_SPLIT=0;SVX_FILL_SPLIT=16;SVX_FILL_SPLIT=32;SVX_FILL_SPLIT=8}" \
       --what prepass --rounds 3 --reps 5 > "$OUT/ab_fill.txt" 2>&1; rc=$?; echo "ab_fill rc=$rc"; grep variant "$OUT/ab_fill.txt"; ok $rc ab_fill ;;
+  ab_libs)   # release-flavoured variant libraries (make -C stereo.vision_amd/csrc ab NAME=..), alternating processes
+    timeout -k 10 900 python3 -u tools/prof.py ab-lib --libs "$AB_LIBS" --what "${AB_WHAT:-pipe,planes}" \
+      --rounds "${AB_ROUNDS:-4}" --reps 5 > "$OUT/ab_libs.txt" 2>&1; rc=$?; echo "ab_libs rc=$rc"
+    grep variant "$OUT/ab_libs.txt"; ok $rc ab_libs ;;
   ab_pipe)
     timeout -k 10 600 python3 -u tools/prof.py ab ${ARGS_AB_PIPE:---ablate 0} > "$OUT/ab_pipe.txt" 2>&1; rc=$?
     echo "ab_pipe rc=$rc"; cat "$OUT/ab_pipe.txt" | tail -8; ok $rc ab_pipe ;;
+  ab_loop)   # the frame loop's timelines, one process per variant (LOOP_ENVS, ';'-separated), alternating twice
+    IFS=';' read -ra VARS <<< "${LOOP_ENVS:-SVX_FILL_SPLIT=0;SVX_FILL_SPLIT=16}"
+    for r in 1 2; do for v in "${VARS[@]}"; do
+      echo "== $v (round $r)" >> "$OUT/ab_loop.txt"
+      env $v SVX_LIB="$PWD/stereo.vision_amd/svx/_lib/libsvx_diag.so" PROBE_ONLY=caller2 timeout -k 10 200 \
+        python3 -u tools/_probe_loop.py >> "$OUT/ab_loop.txt" 2>&1; rc=$?; ok $rc "ab_loop $v"
+    done; done
+    grep -A0 "==\|ms/batch" "$OUT/ab_loop.txt" ;;
+  dropin)
+    timeout -k 10 200 python3 -u tools/prof.py dropin --reps 20 > "$OUT/dropin.txt" 2>&1; rc=$?
+    echo "dropin rc=$rc"; cat "$OUT/dropin.txt"; ok $rc dropin ;;
+  probe_ransac)
+    timeout -k 10 200 python3 -u tools/_probe_ransac_dropin.py > "$OUT/probe_ransac_dropin.txt" 2>&1; rc=$?
+    echo "probe_ransac rc=$rc"; cat "$OUT/probe_ransac_dropin.txt"; ok $rc probe_ransac ;;
   loop)
     PROBE_ONLY=${PROBE_ONLY:-caller2,caller1} timeout -k 10 400 python3 -u tools/_probe_loop.py > "$OUT/loop.txt" 2>&1
     rc=$?; echo "loop rc=$rc"; grep -v "batch" "$OUT/loop.txt" | tail -6; ok $rc loop ;;
