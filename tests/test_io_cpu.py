@@ -134,6 +134,25 @@ def test_palette_with_and_without_alpha(tmp_path):
     np.testing.assert_array_equal(un[..., 3], alpha[idx[..., 0]])
 
 
+def test_palette_index_past_plte_is_black(tmp_path):
+    """An index past the PLTE entries decodes as libpng's zero-filled 256-entry palette gives it: black (and opaque
+    past tRNS), not the last entry (the decoder had clamped the index)."""
+    pal = np.array([[10, 20, 30], [40, 50, 60], [70, 80, 90]], np.uint8)
+    idx = np.array([[[0], [2], [3], [200]], [[1], [255], [0], [2]]], np.uint8)
+    p = str(tmp_path / "pal_short.png")
+    write_png(p, idx, 3, palette=pal)
+    full = np.zeros((256, 3), np.uint8)
+    full[:3] = pal
+    np.testing.assert_array_equal(sio.imread(p), full[idx[..., 0]][..., ::-1])
+    q = str(tmp_path / "pal_short_a.png")
+    write_png(q, idx, 3, palette=pal, trns=np.array([7, 8], np.uint8))
+    un = sio.imread(q, sio.IMREAD_UNCHANGED)
+    alpha = np.full(256, 255, np.uint8)
+    alpha[:2] = (7, 8)
+    np.testing.assert_array_equal(un[..., :3], full[idx[..., 0]][..., ::-1])
+    np.testing.assert_array_equal(un[..., 3], alpha[idx[..., 0]])
+
+
 def test_missing_and_corrupt_files_are_none(tmp_path):
     """cv2.imread returns None (it does not raise) for a file it cannot decode"""
     assert sio.imread(str(tmp_path / "absent.png")) is None
