@@ -79,15 +79,20 @@ struct PyMT {
     }
 };
 
+// random.sample's setsize (Lib/random.py): the pool branch for n <= setsize, the set branch above it
+static int64_t sample_setsize(int k) {
+    int64_t setsize = 21;
+    if (k > 5) setsize += (int64_t)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
+    return setsize;
+}
+
 // random.sample(range(n), k) -> out[0..k). Caller guarantees 0 <= k <= n.
 // The set branch's `selected` is a bitmap of n bits (cleared bit by bit after
 // the sample): membership is what the reference's set answers, at a fraction
 // of a hash set's cost.
 static void py_sample(PyMT& rng, uint32_t n, int k, int32_t* out, std::vector<uint32_t>& pool,
                       std::vector<uint64_t>& selected) {
-    int64_t setsize = 21;
-    if (k > 5) setsize += (int64_t)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
-    if ((int64_t)n <= setsize) {
+    if ((int64_t)n <= sample_setsize(k)) {
         pool.resize(n);
         for (uint32_t i = 0; i < n; ++i) pool[i] = i;
         for (int i = 0; i < k; ++i) {
@@ -135,12 +140,85 @@ static bool collinear(const double* p1, const double* p2, const double* p3) {
     return c0 == 0.0 && c1 == 0.0 && c2 == 0.0;
 }
 
+// set branch fast path: every draw of the call is randbelow(n) for one n (sample(points, k) with n > setsize, and
+// the triples' sample(points, 1)), i.e. a word is taken iff its top bit_length(n) bits are < n. The words of each
+// twist block are compacted into the accepted values (branch-free), then consumed in order.
+struct AccStream {
+    PyMT& rng;
+    uint32_t n;
+    int sh;
+    uint32_t vals[624];
+    uint16_t pos[624];
+    int m = 0, c = 0;
+    AccStream(PyMT& r, uint32_t n_) : rng(r), n(n_), sh(__builtin_clz(n_)) { compact(); }
+    void compact() {   // the accepted values of the current block from rng.index on
+        if (rng.index >= 624) rng.twist();
+        if (!rng.out_valid) rng.temper_all();
+        const uint32_t* __restrict__ src = rng.out;
+        uint32_t* __restrict__ v = vals;
+        uint16_t* __restrict__ p = pos;
+        int k = 0;
+        for (int i = rng.index; i < 624; ++i) {
+            const uint32_t j = src[i] >> sh;
+            v[k] = j;
+            p[k] = (uint16_t)i;
+            k += (int)(j < n);
+        }
+        m = k;
+        c = 0;
+    }
+    inline uint32_t next() {
+        while (c == m) {   // the block's remaining words are all rejected: consumed, then the next block
+            rng.index = 624;
+            compact();
+        }
+        const uint32_t v = vals[c];
+        rng.index = pos[c] + 1;
+        ++c;
+        return v;
+    }
+};
+
+static void ransac_draw_set(PyMT& rng, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
+                            int32_t* tri) {
+    std::vector<uint64_t> selected(((uint64_t)n + 63) / 64, 0);
+    uint64_t* __restrict__ sel = selected.data();
+    AccStream as(rng, (uint32_t)n);
+    for (int t = 0; t < trials; ++t) {
+        int32_t* __restrict__ dst = sidx + (int64_t)t * k;
+        for (int q = 0; q < k;) {
+            const uint32_t v = as.next();
+            uint64_t& wd = sel[v >> 6];
+            const uint64_t b = 1ull << (v & 63);
+            if (__builtin_expect((wd & b) != 0, 0)) continue;   // drawn before in this sample: rejected
+            wd |= b;
+            dst[q++] = (int32_t)v;
+        }
+        for (int q = 0; q < k; ++q) sel[(uint32_t)dst[q] >> 6] = 0;
+        uint32_t i1, i2, i3;
+        do {
+            i1 = as.next();
+            i2 = as.next();
+            i3 = as.next();
+        } while (collinear(pts + i1 * ld, pts + i2 * ld, pts + i3 * ld));
+        tri[3 * t + 0] = (int32_t)i1;
+        tri[3 * t + 1] = (int32_t)i2;
+        tri[3 * t + 2] = (int32_t)i3;
+    }
+}
+
 int ransac_draw(uint32_t* state625, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,
                 int32_t* tri) {
     if (n < k || n < 1 || n >= (1ll << 31)) return 0;   // random.sample raises before drawing: no trial runs
     PyMT rng;
     for (int i = 0; i < 624; ++i) rng.mt[i] = state625[i];
     rng.index = (int)state625[624];
+    if ((int64_t)n > sample_setsize(k)) {   // every draw of the call is randbelow(n): the compacted stream
+        ransac_draw_set(rng, pts, n, ld, trials, k, sidx, tri);
+        for (int i = 0; i < 624; ++i) state625[i] = rng.mt[i];
+        state625[624] = (uint32_t)rng.index;
+        return trials;
+    }
     std::vector<uint32_t> pool;
     std::vector<uint64_t> selected;
     for (int t = 0; t < trials; ++t) {

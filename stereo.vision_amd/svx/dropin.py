@@ -140,10 +140,10 @@ def project3DPointsTo2DImagePoints(points):  # noqa: N802
     n = len(points)
     if n == 0:
         return np.zeros((0, 2), np.float64)
-    arr = gather_columns(points, 0, 3)   # X, Y, Z only (a selection: one C pass, svx/points.py)
+    arr = gather_columns(points, 0, 3, pinned=True)   # X, Y, Z only (a selection: one C pass, svx/points.py)
     if arr.ndim != 2 or arr.shape[1] < 3:
         raise ValueError(f"points must be rows of at least [X, Y, Z], got shape {arr.shape}")
-    out = np.empty((n, 2), np.float64)
+    out = _abi.pinned_empty((n, 2), np.float64)   # page-locked: the device-to-host copy is a direct DMA
     cam = _camera()
     _abi.call("sv_backproject", _abi.ptr(arr), n, arr.shape[1], ctypes.byref(cam), _abi.ptr(out))
     return out

@@ -39,7 +39,7 @@ class PointList(collections.abc.MutableSequence):
     rows (zero-copy for a whole array; a selection gathers it on every call, so
     writes through rows are seen); None once the sequence was mutated."""
 
-    __slots__ = ("_base", "_cache", "_idx", "_rows")
+    __slots__ = ("_base", "_cache", "_idx", "_rows", "__weakref__")
 
     def __init__(self, array):
         self._base = array
@@ -157,7 +157,7 @@ def _spec(points, min_cols):
     return None
 
 
-def gather_columns(points, c0, nc):
+def gather_columns(points, c0, nc, pinned=False):
     """(n, nc) float64 C-contiguous columns c0..c0+nc-1 of a point sequence (n >= 1, rows of >= c0 + nc values).
     A PointList over an array is gathered by libsvx in one pass over the selected rows (sv_gather_f64): reads
     through rows and writes through them are both seen, as with as_points_array, at a fraction of numpy's whole-row
@@ -170,7 +170,8 @@ def gather_columns(points, c0, nc):
         return np.ascontiguousarray(arr[:, c0:c0 + nc])
     base, idx = spec
     n = len(points)
-    out = np.empty((n, nc), np.float64)
+    # pinned: the result goes to the device next, so gather it into page-locked memory (a direct DMA)
+    out = _abi.pinned_empty((n, nc), np.float64) if pinned else np.empty((n, nc), np.float64)
     _abi.call("sv_gather_f64", _abi.ptr(base), base.shape[0], base.shape[1], _abi.ptr(idx), n, c0, nc, _abi.ptr(out))
     return out
 

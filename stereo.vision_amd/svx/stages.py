@@ -64,15 +64,32 @@ def _rgb_u8(points):
     return np.ascontiguousarray(u8)
 
 
+# The last colour stage's result, for the next stage on the same points: the reference's chain
+# (stereovision.py:103-106) bins the same selection twice, calculateColourHistogram(points) then
+# filterPointsByHistogram(points, hist, thr). Kept only for a PointList (by weak reference) and reused only when the
+# colours gathered again are byte-for-byte the ones it was computed from, so a write through a row in between is seen.
+_hue_last = {"ref": None, "rgb": None, "out": None}
+
+
 def _hue(points, bins):
-    """(bins int16 or None, hist u32[1000], first i64[1000]) of the points' colours (device)."""
+    """(bins int16, hist u32[1000], first i64[1000]) of the points' colours (device)."""
+    import weakref
     rgb = _rgb_u8(points)
+    last = _hue_last
+    ref = last["ref"]
+    if ref is not None and ref() is points and last["rgb"].shape == rgb.shape and np.array_equal(last["rgb"], rgb):
+        return last["out"]
     n = len(rgb)
     hist = np.empty(BINS, np.uint32)
     first = np.empty(BINS, np.int64)
-    out_bins = np.empty(n, np.int16) if bins else None
+    out_bins = np.empty(n, np.int16)
     _abi.call("sv_hue_histogram", _abi.ptr(rgb), n, 3, _abi.ptr(out_bins), _abi.ptr(hist), _abi.ptr(first))
-    return out_bins, hist, first
+    out = (out_bins, hist, first)
+    if isinstance(points, PointList):
+        last.update(ref=weakref.ref(points), rgb=rgb, out=out)
+    else:
+        last.update(ref=None, rgb=None, out=None)
+    return out
 
 
 def _select(points, idx):

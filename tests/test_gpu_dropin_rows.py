@@ -53,3 +53,27 @@ def test_chain_reuses_pinned_blocks():
         counts.append(_abi._pool.allocs)
     assert counts[-1] == counts[2], counts
     assert len(held) > 0
+
+
+def test_colour_stages_reuse_only_unchanged_colours():
+    """filterPointsByHistogram reuses calculateColourHistogram's bins for the same points only while their colours
+    are unchanged: a write through a row in between is binned afresh (svx/stages.py _hue)."""
+    import oracle
+    from svx import dropin, stages
+    disp, bgr = oracle.synth_frame(11)
+    pts = dropin.projectDisparityTo3d(disp, 128, bgr)
+    hist = stages.calculateColourHistogram(pts)
+    kept = stages.filterPointsByHistogram(pts, hist, 10)                 # reuses the bins
+    stages._hue_last["ref"] = None
+    fresh = stages.filterPointsByHistogram(pts, hist, 10)                # bins computed again
+    assert len(kept) == len(fresh) and all(a is b for a, b in zip(kept, fresh))
+    # recolour the first point with the colour of a point whose key is rare (count <= 10): the filter must see it
+    bins = stages._hue(pts, True)[0]
+    rare = next(i for i, k in enumerate(bins.tolist()) if hist[stages.bin_key(k)] <= 10)
+    row0, src = pts[0], pts[rare]
+    row0[3], row0[4], row0[5] = src[3], src[4], src[5]
+    after = stages.filterPointsByHistogram(pts, hist, 10)
+    stages._hue_last["ref"] = None
+    want = stages.filterPointsByHistogram(pts, hist, 10)
+    assert [id(r) for r in after] == [id(r) for r in want]
+    assert all(r is not row0 for r in after)
