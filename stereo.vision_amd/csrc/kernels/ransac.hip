@@ -150,7 +150,8 @@ struct AccStream {
     uint32_t vals[624];
     uint16_t pos[624];
     int m = 0, c = 0;
-    AccStream(PyMT& r, uint32_t n_) : rng(r), n(n_), sh(__builtin_clz(n_)) { compact(); }
+    bool started = false;   // nothing is compacted (and the state not twisted) before the first value is taken
+    AccStream(PyMT& r, uint32_t n_) : rng(r), n(n_), sh(__builtin_clz(n_)) {}
     void compact() {   // the accepted values of the current block from rng.index on
         if (rng.index >= 624) rng.twist();
         if (!rng.out_valid) rng.temper_all();
@@ -167,15 +168,24 @@ struct AccStream {
         m = k;
         c = 0;
     }
-    inline uint32_t next() {
-        while (c == m) {   // the block's remaining words are all rejected: consumed, then the next block
+    __attribute__((noinline)) void refill() {
+        if (!started) {   // the first value: the current block from the caller's position
+            started = true;
+            compact();
+            if (m > 0) return;
+        }
+        do {   // the block's remaining words are all rejected: consumed, then the next block
             rng.index = 624;
             compact();
-        }
-        const uint32_t v = vals[c];
-        rng.index = pos[c] + 1;
-        ++c;
-        return v;
+        } while (m == 0);
+    }
+    inline uint32_t next() {
+        if (__builtin_expect(c == m, 0)) refill();
+        return vals[c++];
+    }
+    // the stream position after the last value taken (the words after it in the block are not consumed)
+    void finish() {
+        if (c > 0) rng.index = pos[c - 1] + 1;
     }
 };
 
@@ -205,6 +215,7 @@ static void ransac_draw_set(PyMT& rng, const double* pts, int64_t n, int64_t ld,
         tri[3 * t + 1] = (int32_t)i2;
         tri[3 * t + 2] = (int32_t)i3;
     }
+    as.finish();
 }
 
 int ransac_draw(uint32_t* state625, const double* pts, int64_t n, int64_t ld, int trials, int k, int32_t* sidx,

@@ -82,6 +82,26 @@ def test_host_draw_replay_matches_cpython(cases, n, k, trials, seed):
     assert st1 == r.getstate()
 
 
+@pytest.mark.parametrize("pre,trials", [(0, 0), (3, 4), (623, 2), (624 * 3 + 100, 3)])
+def test_host_draw_from_any_stream_position(pre, trials):
+    """The caller's stream at any position (words already drawn from the current twist block, or exactly at its
+    end) and zero trials (the state must stay untouched: no twist without a draw)."""
+    n, k = 26287, 600
+    pts = np.random.default_rng(pre).normal(0, 10, (n, 3))
+    r = random.Random(11)
+    for _ in range(pre):
+        r.getrandbits(32)
+    st0 = r.getstate()
+    ran, sidx, tri, st1 = _draw(st0, pts, trials, k)
+    _, recs = oransac.ransac(pts, trials, k, rng=r)
+    assert ran == len(recs) == trials
+    for t, rec in enumerate(recs):
+        assert list(sidx[t]) == rec["idx"] and tuple(tri[t]) == rec["tri"]
+    assert st1 == r.getstate()
+    if trials == 0:
+        assert st1 == st0
+
+
 def test_host_draw_rejects_bad_state():
     from svx import _abi
     st = list(random.Random(1).getstate()[1])
