@@ -466,7 +466,9 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
                 if (TR && tr) tr[q] = (int32_t)r[w];
             }
             const int nsel = (int)__builtin_popcountll(sm);
-            if (q0 < k && q0 + nsel >= k) {   // (uniform) the sample's last pick is in this window
+            // (uniform) the sample's last pick is in this window: q0 < k <= q0 + nsel as one unsigned compare (a
+            // q0 past k wraps high): ransac alone 6.80 vs 6.97-7.01 ms (profiles/r06/ab_draw_lastpick_s11.txt)
+            if ((uint32_t)(k - 1 - q0) < (uint32_t)nsel) {
                 const uint64_t lastm = sm & rb_ballot(q == (uint32_t)(k - 1));
                 consumed = 64u * w + (uint32_t)__builtin_ctzll(lastm) + 1u;
             }
@@ -701,6 +703,7 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
     __syncthreads();   // one wave: orders lane 0's seeding before every lane's reads
     RbStream st;
     const int g_pt = lane % 3, g_co = min(lane / 3, 2);   // the triple gather: point, coordinate (rb_point's tables)
+    const uint32_t tg_y = (uint32_t)((tb.Y - tb.X) / 256), tg_z = (uint32_t)((tb.Z - tb.X) / 256);   // table rows
     int status = 0, s = 0;
     for (; s < trials; ++s) {
         IdxT* idx = sidx + ((int64_t)frame * trials + s) * k;
@@ -728,7 +731,11 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
             // state words it replaces (a level drops positions below G - 397; pos >= G - 397 has read them all)
             if (st.pos + 397u >= st.G) rb_advance(sh, st, st.G + 1u - st.pos);
             const uint32_t x2 = (pk & 0xFFF) >> 1, y2 = ((pk >> 12) & 0xFFF) >> 1, dd = pk >> 24;
-            const double v = g_co == 0 ? tb.X[x2 * 256 + dd] : g_co == 1 ? tb.Y[y2 * 256 + dd] : tb.Z[dd];
+            // one load: the three tables are one allocation (X rows, then Y rows, then Z), so the lane's coordinate
+            // picks a row, not a pointer (no exec branches): ransac alone 6.75-6.78 vs 6.82-6.83 ms, loop 14.34-14.37
+            // vs 14.38-14.50 (profiles/r06/ab_draw_triple_gather_s12.txt)
+            const uint32_t row = g_co == 0 ? x2 : g_co == 1 ? tg_y + y2 : tg_z;
+            const double v = tb.X[row * 256 + dd];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 p1[c] = rb_readlane_f64(v, 3 * c + 0);

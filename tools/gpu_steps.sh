@@ -54,6 +54,14 @@ for step in "$@"; do
   probe_ransac)
     timeout -k 10 200 python3 -u tools/_probe_ransac_dropin.py > "$OUT/probe_ransac_dropin.txt" 2>&1; rc=$?
     echo "probe_ransac rc=$rc"; cat "$OUT/probe_ransac_dropin.txt"; ok $rc probe_ransac ;;
+  ab_loop_libs)   # the frame loop with each library of AB_LIBS (release builds), one process each, alternating twice
+    IFS=',' read -ra LIBS <<< "$AB_LIBS"
+    for r in 1 2; do for l in "${LIBS[@]}"; do
+      echo "== $l (round $r)" >> "$OUT/ab_loop_libs.txt"
+      SVX_LIB="$PWD/$l" PROBE_ONLY=caller2 PROBE_RANSAC=1 timeout -k 10 200 \
+        python3 -u tools/_probe_loop.py >> "$OUT/ab_loop_libs.txt" 2>&1; rc=$?; ok $rc "ab_loop_libs $l"
+    done; done
+    grep "==\|ms/batch\|ransac alone" "$OUT/ab_loop_libs.txt" ;;
   loop)
     PROBE_ONLY=${PROBE_ONLY:-caller2,caller1} timeout -k 10 400 python3 -u tools/_probe_loop.py > "$OUT/loop.txt" 2>&1
     rc=$?; echo "loop rc=$rc"; grep -v "batch" "$OUT/loop.txt" | tail -6; ok $rc loop ;;
