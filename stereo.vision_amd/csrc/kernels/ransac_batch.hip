@@ -540,7 +540,7 @@ __device__ void rb_sample_pool(RansacShared<IdxT>& sh, RbStream& st, uint32_t n,
     rb_wave_lds_sync();   // idx (and the trace) read by every lane next
 }
 
-constexpr int kRBGather = 10;     // screen gathers a lane keeps in flight
+[[maybe_unused]] constexpr int kRBGather = 10;     // screen gathers a lane keeps in flight
 constexpr int kRBEvalThreads = 1024;   // eval: 16 waves screen 16 trials at a time
 
 // One trial's record: the draw kernel writes the triple's three indices into
@@ -650,8 +650,8 @@ __device__ __forceinline__ void rb_solve_record(const double* r1, const double* 
     o[4] = singular ? 1.0 : 0.0;
 }
 
-template <class IdxT, bool TR>
-__global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restrict__ packed, RbTables tb, int64_t cap,
+template <class IdxT, bool TR, int WPG = 1>
+__global__ __launch_bounds__(64 * WPG) void ransac_draw_kernel(const uint32_t* __restrict__ packed, RbTables tb, int64_t cap,
                                                          const int64_t* __restrict__ counts, uint64_t seed_base,
                                                          int64_t first_frame, int trials, int k,
                                                          IdxT* __restrict__ sidx, double* __restrict__ tri,
@@ -660,23 +660,26 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
                                                          uint64_t* __restrict__ started, uint64_t epoch, int nframes) {
     // the frame loop's dispatch signal: the last workgroup of the grid is placed after every other one, so once it
     // runs, every frame's wave is resident and another stream's kernel may take the rest of the CUs (loop_gate)
-    if (started && blockIdx.x == gridDim.x - 1 && lane_id() == 0)
+    if (started && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
         __hip_atomic_store(started, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __shared__ uint32_t mt[624];
-    __shared__ uint32_t dummy[64];
-    extern __shared__ uint4 rb_dyn4[];   // [bitmap_words] bitmap / pool list (16-byte aligned, 4-word multiple)
-    uint32_t* rb_dyn = reinterpret_cast<uint32_t*>(rb_dyn4);
+    // WPG waves a workgroup, each its own frame with its own LDS (no barrier between them): fewer workgroups
+    // for the same waves (SVX_DRAW_WPG, diagnostic A/B)
+    const int wave = (int)(threadIdx.x >> 6);
+    __shared__ uint32_t mt_w[WPG][624];
+    __shared__ uint32_t dummy_w[WPG][64];
+    extern __shared__ uint4 rb_dyn4[];   // WPG x [bitmap_words] bitmap / pool list (16-byte aligned, 4-word multiple)
+    uint32_t* rb_dyn = reinterpret_cast<uint32_t*>(rb_dyn4) + (size_t)wave * bitmap_words;
     RansacShared<IdxT> sh;
-    sh.mt = mt;
+    sh.mt = mt_w[wave];
     sh.bitmap = rb_dyn;
     sh.pool_list = rb_dyn;
     sh.k = k;
-    sh.dummy = dummy;
+    sh.dummy = dummy_w[wave];
     sh.ablate = ablate;
     const int lane = lane_id();
     // one frame a wave, or (the frame loop, gridDim.x < nframes) a wave's frames one after the other: fewer
     // waves resident at once hold less LDS beside the other batch's pipeline
-    for (int frame = blockIdx.x; frame < nframes; frame += gridDim.x) {
+    for (int frame = blockIdx.x * WPG + wave; frame < nframes; frame += gridDim.x * WPG) {
     const int64_t n64 = counts[frame];
     const uint32_t* fpk = packed + (int64_t)frame * cap;
     if (n64 < k || trials <= 0) {   // every trial's random.sample raises: (None, None)
@@ -700,7 +703,7 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
     }
     for (int q = lane; q < bitmap_words; q += 64) sh.bitmap[q] = 0;
     if (lane == 0) rb_seed(sh.mt, seed_base + (uint64_t)(first_frame + frame));
-    __syncthreads();   // one wave: orders lane 0's seeding before every lane's reads
+    rb_wave_lds_sync();   // the wave's own LDS: lane 0's seeding (and the clears) before every lane's reads
     RbStream st;
     const int g_pt = lane % 3, g_co = min(lane / 3, 2);   // the triple gather: point, coordinate (rb_point's tables)
     const uint32_t tg_y = (uint32_t)((tb.Y - tb.X) / 256), tg_z = (uint32_t)((tb.Z - tb.X) / 256);   // table rows
@@ -761,7 +764,7 @@ __global__ __launch_bounds__(64) void ransac_draw_kernel(const uint32_t* __restr
         fstat[2 * frame] = status;   // 1: the reference would never return; 2: draw budget
         fstat[2 * frame + 1] = s;    // trials drawn (the failing one excluded)
     }
-    __syncthreads();   // (one wave) the next frame re-seeds mt and clears the bitmap
+    rb_wave_lds_sync();   // (the wave's own LDS) the next frame re-seeds mt and clears the bitmap
     }
 }
 
@@ -910,6 +913,26 @@ __device__ __forceinline__ void rb_wave_sum2_f64(double& a, double& b) {
     b = rb_readlane_f64(b, 63);
 }
 
+#ifdef SVX_DIAG
+// DIAGNOSTIC (diagnostic build, SVX_RANSAC_ABLATE bit 32; results valid): the evaluation's phases timed by each
+// workgroup's thread 0 at the barriers that end them (wall clock, 10 ns ticks), summed over the workgroups:
+// [0] the points' LDS fill, [1] the plane solves, [2] the screen, [3] the candidate compaction, [4] the candidates'
+// fp64 errors, [5] the decision, [6] workgroups stamped. Read by sv_diag_eval_phases.
+__device__ unsigned long long g_eval_phase[8];
+#define SVX_EVAL_STAMP(i)                                                                       \
+    do {                                                                                        \
+        if ((ablate & 32) && tid == 0) {                                                        \
+            const uint64_t now_ = wall_clock64();                                               \
+            atomicAdd(&g_eval_phase[i], (unsigned long long)(now_ - stamp_));                   \
+            stamp_ = now_;                                                                      \
+        }                                                                                       \
+    } while (0)
+#else
+#define SVX_EVAL_STAMP(i) \
+    do {                  \
+    } while (0)
+#endif
+
 // Screen + decision. LDS: the frame's packed points (LDS_PTS) or none, then
 // per trial the screened mean and its bound (2 doubles).
 template <class IdxT, bool LDS_PTS>
@@ -919,6 +942,12 @@ template <class IdxT, bool LDS_PTS>
 // four alternations, profiles/r05/ab_eval_vgpr_s19.txt).
 #ifndef SVX_EVAL_WPE
 #define SVX_EVAL_WPE 5
+#endif
+#ifndef SVX_SCREEN_RUN   // index vectors a lane loads before gathering (the grouped screen)
+#define SVX_SCREEN_RUN 5
+#endif
+#ifndef SVX_SCREEN_GROUPED   // 0: the one-wave-a-trial screen (A/B build)
+#define SVX_SCREEN_GROUPED 1
 #endif
 __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(SVX_EVAL_WPE))) void ransac_eval_kernel(
     const uint32_t* __restrict__ packed, RbTables tb, int64_t cap, KParams cp,
@@ -941,6 +970,10 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
         return;
     }
     const int status = fstat[2 * frame], T = fstat[2 * frame + 1];
+#ifdef SVX_DIAG
+    uint64_t stamp_ = (ablate & 32) ? wall_clock64() : 0;
+    if ((ablate & 32) && tid == 0) atomicAdd(&g_eval_phase[6], 1ull);
+#endif
     const uint32_t* fpk = packed + (int64_t)frame * cap;
     const uint32_t* P = fpk;
     if (LDS_PTS && n64 > lds_pts_words) {   // above the launch's LDS bound (only if its premise broke): flag 32
@@ -981,6 +1014,7 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
     double* ftri = tri + (int64_t)frame * trials * kRBTri;
     const IdxT* fidx = sidx + (int64_t)frame * trials * k;
     __syncthreads();
+    SVX_EVAL_STAMP(0);
     // every trial's plane from its triple (the draw kernel wrote the three indices
     // into the record's first words), one lane a trial: the record in place
     if (!(ablate & 1)) {
@@ -997,6 +1031,7 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
         }
         __syncthreads();   // the records are read by other waves below (same workgroup: same L1)
     }
+    SVX_EVAL_STAMP(1);
     // screen every trial in fp32 (one wave a trial): the mean distance from the
     // packed points and, per point, the bound (T' + 1) 2^-18 / |abc| on its
     // difference to the fp64 distance, T' = rcp(d) (|cx Ba| + |cy Bb| + |Cc|) (the
@@ -1029,7 +1064,7 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
             sum += live ? __builtin_fabsf(t) : 0.0f;
             bnd = __builtin_fmaf(rr, live ? q : 0.0f, bnd);
         };
-        const auto finish = [&](int t, const double (&rec)[kRBTri], double sum, double bnd) {
+        [[maybe_unused]] const auto finish = [&](int t, const double (&rec)[kRBTri], double sum, double bnd) {
             rb_wave_sum2_f64(sum, bnd);
             if (lane == 0) {   // the screened mean and its bound; bound -1 marks a singular trial
                 const double inv = 1.0 / (rec[3] * k);   // (one more rounding each: inside the margin)
@@ -1037,6 +1072,85 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
                 scr[2 * t + 1] = rec[4] == 1.0 ? -1.0 : (bnd + (double)k) * 0x1p-18 * inv;
             }
         };
+#if SVX_SCREEN_GROUPED
+        // Eight lanes a trial, eight trials a wave pass: lane gl of a trial's group takes the trial's indices in
+        // runs of VEC (one 16-byte load each; the group's eight loads are one 128-byte line), all of a pass's
+        // loads issued first (k <= kRBScreenRun: one run), then its VEC-point fp32 batches (<= 10 terms each, as
+        // the bound requires) added in fp64; the group's sums meet in three DPP steps, eight trials at once, and
+        // the group's lane 0 stores the screened mean and bound. Against one wave a trial — ten 2-byte index
+        // loads a lane waited for once a trial and a 64-lane fp64 reduction and division on every trial's chain —
+        // the screen took 91 us a frame of the evaluation's 118 (profiles/r06/probe_eval_phases_s18.txt).
+        {
+            constexpr int GL = 8, TPW = kWave / GL;     // lanes a trial, trials a wave pass
+            constexpr int VEC = 16 / (int)sizeof(IdxT);  // indices a 16-byte load holds
+            constexpr int RUN = SVX_SCREEN_RUN;          // loads a lane holds (k <= 8 x RUN x VEC in one run)
+            const int grp = lane / GL, gl = lane % GL;
+            const uint32_t nm1 = (uint32_t)n64 - 1;
+            // 16-byte loads need every trial's row 16-byte aligned (k x sizeof(IdxT) a multiple of 16); a lane past
+            // the row's end loads the row's last whole vector (k % VEC == 0 then) and its points are masked
+            const bool vec_ok = ((int64_t)k * (int64_t)sizeof(IdxT)) % 16 == 0 &&
+                                (reinterpret_cast<uintptr_t>(fidx) & 15) == 0;
+            for (int t0 = wave * TPW; t0 < T; t0 += NW * TPW) {   // uniform per wave
+                const int t = min(t0 + grp, T - 1);   // a group past T repeats the last trial (not stored)
+                double rec[kRBTri];
+#pragma unroll
+                for (int q = 0; q < kRBTri; ++q) rec[q] = ftri[(int64_t)t * kRBTri + q];
+                const IdxT* idx = fidx + (int64_t)t * k;
+                double sum = 0.0, bnd = 0.0;
+                for (int r0 = 0; r0 < k; r0 += RUN * GL * VEC) {   // uniform: one run for k <= 640 (u16)
+                    uint4 w[RUN];   // the run's index vectors, unpacked where used
+#pragma unroll
+                    for (int j = 0; j < RUN; ++j) {
+                        const int i = r0 + j * GL * VEC + gl * VEC;
+                        if (vec_ok) {
+                            w[j] = *reinterpret_cast<const uint4*>(idx + min(i, k - VEC));
+                        } else {   // element loads packed the same way
+                            uint32_t ww[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                            for (int e = 0; e < VEC; ++e) {
+                                const uint32_t v = (uint32_t)idx[min(i + e, k - 1)];
+                                if (sizeof(IdxT) == 2) ww[e / 2] |= v << (16 * (e % 2));
+                                else ww[e] = v;
+                            }
+                            w[j] = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+                        }
+                    }
+                    const double Ba64 = cp.B * rec[0], Bb64 = cp.B * rec[1];
+                    const float Ba = (float)Ba64, Bb = (float)Bb64;
+                    const float Cc = (float)(cp.fB * rec[2] - (double)cp.cw_lo * Ba64 - (double)cp.ch_lo * Bb64);
+#pragma unroll
+                    for (int j = 0; j < RUN; ++j) {
+                        const int i = r0 + j * GL * VEC + gl * VEC;
+                        const uint32_t ww[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+                        uint32_t u[VEC];
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e) {
+                            const uint32_t ix = sizeof(IdxT) == 2 ? (ww[e / 2] >> (16 * (e % 2))) & 0xFFFFu : ww[e];
+                            u[e] = P[min(ix, nm1)];
+                        }
+                        float s32 = 0.0f, b32 = 0.0f;
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e) point(u[e], i + e < k, Ba, Bb, Cc, s32, b32);
+                        sum += (double)s32;
+                        bnd += (double)b32;
+                    }
+                }
+                // the group's eight lane sums: quad_perm [1,0,3,2] and [2,3,0,1], then the other quad of the
+                // half row (row_half_mirror); every lane of the group ends with the same total
+                sum += rb_dpp_f64<0xB1, 0xf>(sum);
+                bnd += rb_dpp_f64<0xB1, 0xf>(bnd);
+                sum += rb_dpp_f64<0x4E, 0xf>(sum);
+                bnd += rb_dpp_f64<0x4E, 0xf>(bnd);
+                sum += rb_dpp_f64<0x141, 0xf>(sum);
+                bnd += rb_dpp_f64<0x141, 0xf>(bnd);
+                if (gl == 0 && t0 + grp < T) {   // the screened mean and its bound; bound -1 marks a singular trial
+                    const double inv = 1.0 / (rec[3] * k);
+                    scr[2 * t] = sum * inv;
+                    scr[2 * t + 1] = rec[4] == 1.0 ? -1.0 : (bnd + (double)k) * 0x1p-18 * inv;
+                }
+            }
+        }
+#else
         {
             // every sample index is clamped to the frame's points before it addresses anything: the indices come
             // from memory another kernel wrote, and a word past the frame's n points (a stale LDS word or another
@@ -1044,6 +1158,9 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
             const uint32_t nm1 = (uint32_t)n64 - 1;
             auto load = [&](int t, uint32_t (&ix)[kRBGather], double (&rec)[kRBTri]) {
                 const IdxT* idx = fidx + (int64_t)t * k;
+#if defined(SVX_SCREEN_AB) && SVX_SCREEN_AB == 1   // DIAGNOSTIC A/B build (results invalid): the first trial's indices only
+                if (t < NW)
+#endif
 #pragma unroll
                 for (int v = 0; v < kRBGather; ++v)
                     ix[v] = min((uint32_t)idx[min(lane + kWave * v, k - 1)], nm1);   // no branch
@@ -1074,21 +1191,32 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
                             for (int v = 0; v < kRBGather; ++v)
                                 ix[v] = min((uint32_t)fidx[(int64_t)t * k + min(j0 + kWave * v, k - 1)], nm1);
                         }
+#if defined(SVX_SCREEN_AB) && SVX_SCREEN_AB == 2   // DIAGNOSTIC A/B build (results invalid): no LDS gathers
+#pragma unroll
+                        for (int v = 0; v < kRBGather; ++v) u[v] = ix[v] * 0x9E3779B1u;
+#else
 #pragma unroll
                         for (int v = 0; v < kRBGather; ++v) u[v] = P[ix[v]];
+#endif
 #pragma unroll
                         for (int v = 0; v < kRBGather; ++v) point(u[v], j0 + kWave * v < k, Ba, Bb, Cc, s32, b32);
                         sum += (double)s32;
                         bnd += (double)b32;
                     }
                 }
+#if defined(SVX_SCREEN_AB) && SVX_SCREEN_AB == 3   // DIAGNOSTIC A/B build (results invalid): no wave sums
+                if (lane == 0) scr[2 * t] = sum, scr[2 * t + 1] = bnd;
+#else
                 finish(t, rec, sum, bnd);
+#endif
             }
         }
+#endif
     } else {
         for (int t = tid; t < T; t += kRBEvalThreads) scr[2 * t + 1] = ftri[(int64_t)t * kRBTri + 4] == 1.0 ? -1.0 : 0.0;
     }
     __syncthreads();
+    SVX_EVAL_STAMP(2);
     // Which trials can matter? The running best before trial t is exactly
     // min_{j<t} e_j (a trial the sequential screen skips has e_j >= LB_j >
     // best_{j-1}), and e_j <= UB_j = e32_j + eb_j, so every trial the
@@ -1135,6 +1263,7 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
         }
     }
     __syncthreads();
+    SVX_EVAL_STAMP(3);
     const uint32_t nc = ncand_s, nm1 = (uint32_t)n64 - 1;
     for (uint32_t ci = wave; ci < nc; ci += kRBEvalThreads / 64) {
         const int t = cand[ci];
@@ -1156,6 +1285,7 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
         if (lane == 0) ce[ci] = sum / k;
     }
     __syncthreads();
+    SVX_EVAL_STAMP(4);
     double best = __builtin_huge_val(), second = __builtin_huge_val();
     int best_t = -1;
     uint32_t flags = any_singular_s ? 1u : 0u;
@@ -1190,7 +1320,20 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
         out_abc[3 * frame + 1] = babc[1];
         out_abc[3 * frame + 2] = babc[2];
     }
+    SVX_EVAL_STAMP(5);
 }
+#undef SVX_EVAL_STAMP
+
+#ifdef SVX_DIAG
+hipError_t diag_eval_phases(unsigned long long* out, bool reset) {   // (diagnostic build)
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_eval_phase), sizeof(unsigned long long) * 8);
+    if (e == hipSuccess && reset) {
+        static const unsigned long long zero[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_eval_phase), zero, sizeof(zero));
+    }
+    return e;
+}
+#endif
 
 template <class IdxT>
 static hipError_t launch_ransac_typed(const uint32_t* packed, const RbTables& tb, int64_t cap, const KParams& cp,
@@ -1202,19 +1345,40 @@ static hipError_t launch_ransac_typed(const uint32_t* packed, const RbTables& tb
     IdxT* sidx = reinterpret_cast<IdxT*>(rs.sidx);
     // frames a draw wave walks: 1, or in the frame loop (started: the draw runs beside another batch's pipeline)
     // SVX_DRAW_FPW (diagnostic build, A/B)
-    int fpw = 1;
+    // eight frames' waves a workgroup (two a SIMD as the dispatcher places a workgroup's waves), each wave its own
+    // frame and LDS: the batched RANSAC 6.35 vs 6.93 ms with four against one a workgroup, the frame loop
+    // 14.48-14.68 vs 14.72-14.79 ms (profiles/r06/ab_draw_wpg_s16.txt); eight against four: RANSAC equal, the loop
+    // 14.54-14.66 vs 14.65-14.83 ms in five alternations on two boxes (ab_draw_wpg_s17.txt, _s18.txt);
+    // SVX_DRAW_WPG (diagnostic build) 1, 2, 4, 8 or 16
+    int fpw = 1, wpg = 8;
     if (started)
         if (const char* e = svx_knob("SVX_DRAW_FPW")) fpw = std::max(1, std::atoi(e));
-    const int grid = (frames + fpw - 1) / fpw;
+    if (const char* e = svx_knob("SVX_DRAW_WPG")) {
+        const int v = std::atoi(e);
+        wpg = v == 1 || v == 2 || v == 8 || v == 16 ? v : 4;
+    }
+    while (wpg > 1 && (trace || words * wpg > 16384)) wpg /= 2;   // traced: one wave a workgroup; dynamic LDS <= 64 KiB
+    const int waves = (frames + fpw - 1) / fpw, grid = (waves + wpg - 1) / wpg;
+    const size_t ddyn = sizeof(uint32_t) * (size_t)words * (size_t)wpg;
+#define SVX_DRAW(TRv, WPGv, TRP, TRN)                                                                            \
+    hipLaunchKernelGGL((ransac_draw_kernel<IdxT, TRv, WPGv>), dim3(grid), dim3(64 * WPGv), ddyn, s, packed, tb, cap, \
+                       counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, TRP, TRN, (int)words,     \
+                       ablate, started, epoch, frames)
     if (!(phases & 1)) {
-    } else if (trace)
-        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, true>), dim3(grid), dim3(64), sizeof(uint32_t) * (size_t)words,
-                           s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat, trace,
-                           trace_trials, (int)words, ablate, started, epoch, frames);
-    else
-        hipLaunchKernelGGL((ransac_draw_kernel<IdxT, false>), dim3(grid), dim3(64), sizeof(uint32_t) * (size_t)words,
-                           s, packed, tb, cap, counts, seed_base, first_frame, trials, k, sidx, rs.tri, rs.fstat,
-                           nullptr, 0, (int)words, ablate, started, epoch, frames);
+    } else if (trace) {
+        SVX_DRAW(true, 1, trace, trace_trials);
+    } else if (wpg == 2) {
+        SVX_DRAW(false, 2, nullptr, 0);
+    } else if (wpg == 4) {
+        SVX_DRAW(false, 4, nullptr, 0);
+    } else if (wpg == 8) {
+        SVX_DRAW(false, 8, nullptr, 0);
+    } else if (wpg == 16) {
+        SVX_DRAW(false, 16, nullptr, 0);
+    } else {
+        SVX_DRAW(false, 1, nullptr, 0);
+    }
+#undef SVX_DRAW
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !(phases & 2)) return e;
     if (ablate & (8 | 16)) ablate |= 1;   // DIAGNOSTIC: no samples / planes drawn -> no evaluation of them

@@ -1540,7 +1540,21 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 // evaluation (results invalid); 4 evaluates every trial in fp64 (no fp32 screen; results valid, for A/B); draw
 // kernel (results invalid): 8 no collinearity test, 16 no random.sample (both also skip the evaluation). Any other
 // bit is refused (-1): an undocumented bit once rode along in an A/B run that faulted.
-static constexpr int kRansacAblateBits = 1 | 4 | 8 | 16;
+static constexpr int kRansacAblateBits = 1 | 4 | 8 | 16 | 32;
+#ifdef SVX_DIAG
+}  // extern "C"
+namespace svx {
+hipError_t diag_eval_phases(unsigned long long* out, bool reset);
+}
+extern "C" {
+// DIAGNOSTIC (diagnostic build only, not in include/svx.h): the evaluation's phase clocks (SVX_RANSAC_ABLATE bit 32)
+extern "C" int sv_diag_eval_phases(unsigned long long* out8, int reset) {
+    if (!out8) return fail(SV_E_ARG, "sv_diag_eval_phases: null argument");
+    HIP_TRY(diag_eval_phases(out8, reset != 0));
+    return SV_OK;
+}
+#endif
+
 static int ransac_ablate() {
     const char* e = svx_knob("SVX_RANSAC_ABLATE");
     const int v = e ? std::atoi(e) : 0;
@@ -1556,6 +1570,8 @@ static int ransac_ablate() {
 // the pool branch's k-entry list) within 8 KiB and the sample indices 16-bit; otherwise the counts are read.
 static int64_t ransac_device_bound(const sv_batch* b, int k) {
     if (!b->have_mask) return -1;
+    // DIAGNOSTIC A/B (diagnostic build): SVX_RANSAC_BOUND=0 sizes the draw from the counts read back even with a mask
+    if (const char* e = svx_knob("SVX_RANSAC_BOUND"); e && e[0] == '0') return -1;
     const int64_t n = std::min(b->mask_n2, b->mcap);
     const int64_t words = std::max<int64_t>((n + 31) / 32, k);
     return (words <= 2048 && n <= 65535) ? n : -1;
@@ -1639,7 +1655,7 @@ static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_
     const int64_t max_n = b->rmax_n, max_pool_n = b->rmax_pool_n;
     const int ablate = ransac_ablate();
     if (ablate < 0)
-        return fail(SV_E_ARG, "SVX_RANSAC_ABLATE: only the documented bits 1, 4, 8 and 16 (diagnostic build)");
+        return fail(SV_E_ARG, "SVX_RANSAC_ABLATE: only the documented bits 1, 4, 8, 16 and 32 (diagnostic build)");
     HIP_TRY(b->rsidx.ensure(std::max<size_t>(ransac_sidx_bytes(max_n, b->frames, trials, k), 4)));
     HIP_TRY(b->rtri.ensure(sizeof(double) * 5 * F * (size_t)std::max(trials, 1) + sizeof(int32_t) * 2 * F));
     const RansacScratch rs{b->rsidx.p, b->rtri.as<double>(),
