@@ -689,6 +689,20 @@ __global__ __launch_bounds__(64 * WPG) void ransac_draw_kernel(const uint32_t* _
         }
         continue;
     }
+#ifdef SVX_DIAG
+    // DIAGNOSTIC (diagnostic build, SVX_RANSAC_ABLATE bit 128; results invalid): the wave holds its resources for
+    // 4 ms of wall clock and draws nothing (the evaluation then reads stale indices, clamped) — does the pipeline
+    // beside the draw slow down for the draw's resources or for its work?
+    if (ablate & 128) {
+        const uint64_t t0 = wall_clock64();
+        while (wall_clock64() - t0 < 400000u) __builtin_amdgcn_s_sleep(64);
+        if (lane == 0) {
+            fstat[2 * frame] = 0;
+            fstat[2 * frame + 1] = trials;
+        }
+        continue;
+    }
+#endif
     const uint32_t n = (uint32_t)n64;
     const int kb = 32 - __builtin_clz(n);
     const bool pool = (int64_t)n <= ransac_setsize(k);
@@ -1126,11 +1140,20 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
                         for (int e = 0; e < VEC; ++e) {
                             const uint32_t ix = sizeof(IdxT) == 2 ? (ww[e / 2] >> (16 * (e % 2))) & 0xFFFFu : ww[e];
+#if defined(SVX_SCREEN_AB) && SVX_SCREEN_AB == 2   // DIAGNOSTIC A/B build (results invalid): no LDS gathers
+                            u[e] = min(ix, nm1) * 0x9E3779B1u | 0x01000000u;
+#else
                             u[e] = P[min(ix, nm1)];
+#endif
                         }
                         float s32 = 0.0f, b32 = 0.0f;
+#if defined(SVX_SCREEN_AB) && SVX_SCREEN_AB == 4   // DIAGNOSTIC A/B build (results invalid): no point arithmetic
+#pragma unroll
+                        for (int e = 0; e < VEC; ++e) s32 += (float)u[e];
+#else
 #pragma unroll
                         for (int e = 0; e < VEC; ++e) point(u[e], i + e < k, Ba, Bb, Cc, s32, b32);
+#endif
                         sum += (double)s32;
                         bnd += (double)b32;
                     }
@@ -1388,7 +1411,9 @@ static hipError_t launch_ransac_typed(const uint32_t* packed, const RbTables& tb
                        sizeof(double) * ((size_t)trials + 1);
     const int64_t pts_words = (max_n + 1) & ~1ll;   // the doubles after the points stay 8-byte aligned
     const size_t pts_b = sizeof(uint32_t) * (size_t)pts_words;
-    const bool lds_pts = pts_b + scr <= 150 * 1024;
+    bool lds_pts = pts_b + scr <= 150 * 1024;
+    // SVX_EVAL_LDS_PTS=0 (diagnostic build, A/B): the points gathered from memory (L2) instead of LDS
+    if (const char* e = svx_knob("SVX_EVAL_LDS_PTS"); e && e[0] == '0') lds_pts = false;
     const size_t dyn = (lds_pts ? pts_b : 0) + scr;
     if (lds_pts) {
         // dynamic LDS above 64 KiB needs the per-kernel opt-in (on the current device)

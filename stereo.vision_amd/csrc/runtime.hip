@@ -1540,7 +1540,7 @@ int sv_batch_read_road(sv_batch* b, int frame, uint8_t* img, int32_t* nzpts, int
 // evaluation (results invalid); 4 evaluates every trial in fp64 (no fp32 screen; results valid, for A/B); draw
 // kernel (results invalid): 8 no collinearity test, 16 no random.sample (both also skip the evaluation). Any other
 // bit is refused (-1): an undocumented bit once rode along in an A/B run that faulted.
-static constexpr int kRansacAblateBits = 1 | 4 | 8 | 16 | 32;
+static constexpr int kRansacAblateBits = 1 | 4 | 8 | 16 | 32 | 128;
 #ifdef SVX_DIAG
 }  // extern "C"
 namespace svx {
@@ -1655,7 +1655,7 @@ static int batch_ransac_launch(sv_batch* b, const sv_camera* cam, uint64_t seed_
     const int64_t max_n = b->rmax_n, max_pool_n = b->rmax_pool_n;
     const int ablate = ransac_ablate();
     if (ablate < 0)
-        return fail(SV_E_ARG, "SVX_RANSAC_ABLATE: only the documented bits 1, 4, 8, 16 and 32 (diagnostic build)");
+        return fail(SV_E_ARG, "SVX_RANSAC_ABLATE: only the documented bits 1, 4, 8, 16, 32 and 128 (diagnostic build)");
     HIP_TRY(b->rsidx.ensure(std::max<size_t>(ransac_sidx_bytes(max_n, b->frames, trials, k), 4)));
     HIP_TRY(b->rtri.ensure(sizeof(double) * 5 * F * (size_t)std::max(trials, 1) + sizeof(int32_t) * 2 * F));
     const RansacScratch rs{b->rsidx.p, b->rtri.as<double>(),

@@ -3,14 +3,8 @@ set -o pipefail
 OUT=gpurun_out/${SESSION:-r6sX}; mkdir -p $OUT
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_ransac_batch.py tests/test_gpu_loop.py tests/test_gpu_digests.py > $OUT/pytest_ransac.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_ransac.log; exit 1; }
 tail -1 $OUT/pytest_ransac.log
-for r in 1 2; do for L in stereo.vision_amd/svx/_lib/libsvx_diag.so _ab/libsvx_scr_old.so _ab/libsvx_scr_run3.so; do
-  echo "== $L (round $r)" >> $OUT/probe_eval_screen_ab.txt
-  SVX_LIB=$PWD/$L timeout -k 10 200 python3 -u tools/_probe_eval_phases.py >> $OUT/probe_eval_screen_ab.txt 2>&1 || { echo "$L failed"; tail $OUT/probe_eval_screen_ab.txt; exit 1; }
+for r in 1 2 3; do for L in stereo.vision_amd/svx/_lib/libsvx_diag.so _ab/libsvx_qb0.so; do
+  echo "== $L (round $r)" >> $OUT/ab_eval_screen_qbound.txt
+  SVX_LIB=$PWD/$L timeout -k 10 200 python3 -u tools/_probe_eval_phases.py >> $OUT/ab_eval_screen_qbound.txt 2>&1 || { echo "$L failed"; tail $OUT/ab_eval_screen_qbound.txt; exit 1; }
 done; done
-grep "==\|screen\|total\|per call" $OUT/probe_eval_screen_ab.txt
-D=$PWD/stereo.vision_amd/svx/_lib/libsvx_diag.so
-for r in 1 2; do for L in stereo.vision_amd/svx/_lib/libsvx_diag.so _ab/libsvx_scr_old.so; do
-  echo "== $L (round $r)" >> $OUT/ab_loop_screen.txt
-  SVX_LIB=$PWD/$L SVX_DRAW_WPG=8 PROBE_ONLY=caller2 PROBE_RANSAC=1 timeout -k 10 200 python3 -u tools/_probe_loop.py >> $OUT/ab_loop_screen.txt 2>&1 || { echo "loop $L failed"; tail $OUT/ab_loop_screen.txt; exit 1; }
-done; done
-grep "==\|ms/batch\|alone" $OUT/ab_loop_screen.txt
+grep "==\|screen\|candidates\|per call" $OUT/ab_eval_screen_qbound.txt

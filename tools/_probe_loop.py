@@ -23,12 +23,17 @@ for source, slots in (("caller", 2), ("caller", 1), ("synth", 2), ("caller", 3),
         for i in range(6):
             if i == 2:
                 loop.wait(s)
+                # PROBE_ABLATE (diagnostic build): SVX_RANSAC_ABLATE for the timed batches only, so their evaluation
+                # reads the first batches' (valid) scratch
+                if os.environ.get("PROBE_ABLATE"):
+                    os.environ["SVX_RANSAC_ABLATE"] = os.environ["PROBE_ABLATE"]
                 t0 = time.perf_counter()
             if source == "caller" and i < slots:
                 loop.acquire().synth(i * F)
             s = loop.submit(i * F)
         loop.wait(s)
         dt = (time.perf_counter() - t0) / 4 * 1e3
+        os.environ.pop("SVX_RANSAC_ABLATE", None) if os.environ.get("PROBE_ABLATE") else None
         print(f"source={source} slots={slots}: {dt:.2f} ms/batch", flush=True)
         show(loop, range(s - slots + 1, s + 1))
 
