@@ -912,6 +912,20 @@ __device__ __forceinline__ double rb_dpp_f64(double v) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTL, RM, 0xf, false);
     return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
 }
+// The DPP move of an fp64 value where a lane with no source (or outside the row mask) reads +inf, and the min-scan
+// step built from it.
+template <int CTL, int RM = 0xf>
+__device__ __forceinline__ double rb_dpp_inf_f64(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    constexpr uint64_t kInf = 0x7FF0000000000000ull;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)kInf, (int)(uint32_t)u, CTL, RM, 0xf, false);
+    const uint32_t hi =
+        (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(kInf >> 32), (int)(uint32_t)(u >> 32), CTL, RM, 0xf, false);
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+template <int CTL, int RM>
+__device__ __forceinline__ double rb_dpp_min_f64(double v) { return fmin(v, rb_dpp_inf_f64<CTL, RM>(v)); }
+
 __device__ __forceinline__ void rb_wave_sum2_f64(double& a, double& b) {
 #define SVX_RB_SUM2_STEP(ctl, rm)        \
     a += rb_dpp_f64<ctl, rm>(a);         \
@@ -1263,13 +1277,16 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
             const double e32 = in ? scr[2 * t] : 0.0, eb = in ? scr[2 * t + 1] : -1.0;
             const bool singular = in && eb < 0.0;
             const double ub = (in && !singular) ? e32 + eb : __builtin_huge_val();
-            double inc = ub;   // inclusive min-scan over the wave
-#pragma unroll
-            for (int o = 1; o < kWave; o <<= 1) {
-                const double v = __shfl_up(inc, o, kWave);
-                if (lane >= o) inc = fmin(inc, v);
-            }
-            double ex = __shfl_up(inc, 1, kWave);
+            // inclusive min-scan over the wave by DPP (row_shr 1/2/4/8, row_bcast 15/31; a lane with no source keeps
+            // +inf), then the exclusive one by wave_shr:1 — six VALU moves instead of six ds_bpermute round trips
+            double inc = ub;
+            inc = rb_dpp_min_f64<0x111, 0xf>(inc);
+            inc = rb_dpp_min_f64<0x112, 0xf>(inc);
+            inc = rb_dpp_min_f64<0x114, 0xf>(inc);
+            inc = rb_dpp_min_f64<0x118, 0xf>(inc);
+            inc = rb_dpp_min_f64<0x142, 0xa>(inc);
+            inc = rb_dpp_min_f64<0x143, 0xc>(inc);
+            double ex = rb_dpp_inf_f64<0x138>(inc);
             ex = lane == 0 ? carry : fmin(ex, carry);   // min over j < t
             bool c = in && !singular && !(e32 - eb > ex * (1.0 + 2e-9));   // NaN / inf: a candidate
             if (ablate & 4) c = in && !singular;
@@ -1278,7 +1295,7 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
             if (c) cand[nc + __builtin_popcountll(m & ((1ull << lane) - 1))] = t;
             nc += (uint32_t)__builtin_popcountll(m);
             sing |= rb_ballot(singular) != 0 ? 1u : 0u;
-            carry = fmin(carry, __shfl(inc, kWave - 1, kWave));
+            carry = fmin(carry, rb_readlane_f64(inc, kWave - 1));
         }
         if (lane == 0) {
             ncand_s = nc;
