@@ -60,6 +60,19 @@ def test_release_library_reads_no_knobs():
         assert b"SVX_ABLATE" in dblob and b"SVX_RANSAC_ABLATE" in dblob
 
 
+def test_diagnostic_library_loads_with_its_probes():
+    """The diagnostic build loads (every symbol it uses resolves) and exports the evaluation's phase clocks
+    (tools/_probe_eval_phases.py); the release build does not export them."""
+    import ctypes
+    from svx import _abi
+    diag = os.path.join(os.path.dirname(_abi.LIB_PATH), "libsvx_diag.so")
+    if not os.path.exists(diag):
+        pytest.skip("diagnostic library not built")
+    d = ctypes.CDLL(diag)
+    assert hasattr(d, "sv_diag_eval_phases") and hasattr(d, "sv_batch_create")
+    assert not hasattr(_abi.lib(), "sv_diag_eval_phases")
+
+
 def test_no_device_errors_are_raised_not_faked():
     """Without a GPU every compute entry point must fail loudly (no CPU fallback)."""
     import svx
