@@ -522,12 +522,14 @@ def loop_extra(args, device, first, mask):
     every batch cleans the same raw frames), so a batch's time is the stages' alone;
     `device_frame_loop_with_input`: every batch first generates its synthetic frames on the device (global ids).
     Steady state: `warm` batches first (buffers, tables, clocks), then `reps` batches timed host-side from the end
-    of the last warm-up batch to the end of the last one. Then the parity leg: frames 0..4095 as two 2048-frame
+    of the last warm-up batch to the end of the last one. The timed region starts from a drained loop (the first
+    timed batch's stages run with nothing beside them, the last one's pipeline and road with no next draw), so
+    `reps` is 16: four batches read 13.86 ms a batch where 32 read 13.50 on the same box. Then the parity leg: frames 0..4095 as two 2048-frame
     batches in flight, every frame against tests/golden/plane_digests.npz. Run after the headline batch is freed
     (two slots hold ~200 GB)."""
     from svx.loop import STAGES, FrameLoop
     out = {}
-    frames, warm, reps = args.frames, 2, 4
+    frames, warm, reps = args.frames, 2, 16
     for key, slots, source in (("device_frame_loop", 2, "caller"), ("device_frame_loop_serial", 1, "caller"),
                                ("device_frame_loop_with_input", 2, "synth")):
         with FrameLoop(frames, slots=slots, source=source, carmask=mask, device=device) as loop:

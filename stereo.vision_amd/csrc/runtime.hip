@@ -2645,10 +2645,11 @@ int sv_loop_submit(sv_loop* L, int64_t first_frame_id, int64_t* out_seq) {
     }
     // RANSAC evaluation, after the previous batch's road pass (SVX_LOOP_EVAL_AFTER=pipeline, diagnostic build:
     // after its pipeline, beside the road pass)
-    {
+    {   // (SVX_LOOP_EVAL_AFTER=none, diagnostic build: after this batch's draw only, so its workgroups take the CUs
+        // the previous batch's pipeline drains, beside that batch's road pass)
         const char* ea = svx_knob("SVX_LOOP_EVAL_AFTER");
-        const int dep = ea && ea[0] == 'p' ? kLsPipeline : kLsRoad;
-        if (seq > 0 && ps != s) HIP_TRY(hipStreamWaitEvent(st, L->t1[ps][dep], 0));
+        const int dep = ea && ea[0] == 'p' ? kLsPipeline : ea && ea[0] == 'n' ? -1 : kLsRoad;
+        if (seq > 0 && ps != s && dep >= 0) HIP_TRY(hipStreamWaitEvent(st, L->t1[ps][dep], 0));
     }
     HIP_TRY(begin(kLsEval));
     if (int rc = batch_ransac_launch(b, &L->cam, q.seed_base, first_frame_id, q.trials, q.k, st, 2)) return rc;

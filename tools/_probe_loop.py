@@ -20,7 +20,8 @@ for source, slots in (("caller", 2), ("caller", 1), ("synth", 2), ("caller", 3),
     if ONLY and f"{source}{slots}" not in ONLY.split(","):
         continue
     with FrameLoop(F, slots=slots, source=source, carmask=mask) as loop:
-        for i in range(6):
+        NB = int(os.environ.get("PROBE_BATCHES", 6))   # batches submitted: 2 warm-up, NB - 2 timed
+        for i in range(NB):
             if i == 2:
                 loop.wait(s)
                 # PROBE_ABLATE (diagnostic build): SVX_RANSAC_ABLATE for the timed batches only, so their evaluation
@@ -32,7 +33,7 @@ for source, slots in (("caller", 2), ("caller", 1), ("synth", 2), ("caller", 3),
                 loop.acquire().synth(i * F)
             s = loop.submit(i * F)
         loop.wait(s)
-        dt = (time.perf_counter() - t0) / 4 * 1e3
+        dt = (time.perf_counter() - t0) / (NB - 2) * 1e3
         os.environ.pop("SVX_RANSAC_ABLATE", None) if os.environ.get("PROBE_ABLATE") else None
         print(f"source={source} slots={slots}: {dt:.2f} ms/batch", flush=True)
         show(loop, range(s - slots + 1, s + 1))
