@@ -1,9 +1,5 @@
 # ad-hoc GPU session steps (kept with the session's records under profiles/r06/scripts when used)
 set -o pipefail
 OUT=gpurun_out/${SESSION:-r6sX}; mkdir -p $OUT
-D=$PWD/stereo.vision_amd/svx/_lib/libsvx_diag.so
-for r in 1 2; do for a in road none pipeline; do
-  echo "== SVX_LOOP_EVAL_AFTER=$a (round $r)" >> $OUT/ab_loop_eval_after_18.txt
-  SVX_LIB=$D SVX_LOOP_EVAL_AFTER=$a PROBE_BATCHES=18 PROBE_ONLY=caller2 timeout -k 10 200 python3 -u tools/_probe_loop.py >> $OUT/ab_loop_eval_after_18.txt 2>&1 || { echo "loop $a failed"; tail $OUT/ab_loop_eval_after_18.txt; exit 1; }
-done; done
-grep "==\|ms/batch\|batch 16" $OUT/ab_loop_eval_after_18.txt
+SVX_LIB=$PWD/stereo.vision_amd/svx/_lib/libsvx_diag.so timeout -k 10 300 python3 -u tools/prof.py ab --modes resident --ablate 0,262144 --what pipe --rounds 8 > $OUT/ab_pipe_late_prio.txt 2>&1; rc=$?; cat $OUT/ab_pipe_late_prio.txt; [ $rc -eq 0 ] || exit 1
+SVX_LIB=$PWD/stereo.vision_amd/svx/_lib/libsvx_diag.so timeout -k 10 300 python3 -u tools/prof.py ab --modes resident --ablate 0,262144 --what planes --rounds 6 > $OUT/ab_planes_late_prio.txt 2>&1; rc=$?; cat $OUT/ab_planes_late_prio.txt; exit $rc
