@@ -145,6 +145,8 @@ def _sparse_frame(n, seed):
     ((599, 600, 601, 20000), 600, 2**32 + 3),   # n < k (no trial), n == k, two-word seeds
     ((20, 21, 22, 300), 5, 11),             # k <= 5: setsize 21
     ((50, 3, 4, 9), 1, 2**40),              # k = 1 (n = 3: collinear redraws of repeated points)
+    ((70000, 66000), 600, 21),              # n > 65535: 32-bit sample indices; points past the LDS (from memory)
+    ((70000, 1000), 598, 5),                # 32-bit indices with k x 4 B not a multiple of 16 (element loads)
 ])
 def test_batch_sample_branches(svb, ns, k, seed_base):
     trials = 25

@@ -1,5 +1,4 @@
 # ad-hoc GPU session steps (kept with the session's records under profiles/r06/scripts when used)
 set -o pipefail
 OUT=gpurun_out/${SESSION:-r6sX}; mkdir -p $OUT
-SVX_LIB=$PWD/stereo.vision_amd/svx/_lib/libsvx_diag.so timeout -k 10 300 python3 -u tools/prof.py ab --modes resident --ablate 0,262144 --what pipe --rounds 8 > $OUT/ab_pipe_late_prio.txt 2>&1; rc=$?; cat $OUT/ab_pipe_late_prio.txt; [ $rc -eq 0 ] || exit 1
-SVX_LIB=$PWD/stereo.vision_amd/svx/_lib/libsvx_diag.so timeout -k 10 300 python3 -u tools/prof.py ab --modes resident --ablate 0,262144 --what planes --rounds 6 > $OUT/ab_planes_late_prio.txt 2>&1; rc=$?; cat $OUT/ab_planes_late_prio.txt; exit $rc
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_ransac_batch.py -k "sample_branches" > $OUT/pytest_branches.log 2>&1; rc=$?; tail -15 $OUT/pytest_branches.log; exit $rc
