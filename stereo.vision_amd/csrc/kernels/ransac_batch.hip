@@ -1102,12 +1102,14 @@ __global__ __launch_bounds__(kRBEvalThreads) __attribute__((amdgpu_waves_per_eu(
         };
 #if SVX_SCREEN_GROUPED
         // Eight lanes a trial, eight trials a wave pass: lane gl of a trial's group takes the trial's indices in
-        // runs of VEC (one 16-byte load each; the group's eight loads are one 128-byte line), all of a pass's
-        // loads issued first (k <= kRBScreenRun: one run), then its VEC-point fp32 batches (<= 10 terms each, as
-        // the bound requires) added in fp64; the group's sums meet in three DPP steps, eight trials at once, and
-        // the group's lane 0 stores the screened mean and bound. Against one wave a trial — ten 2-byte index
-        // loads a lane waited for once a trial and a 64-lane fp64 reduction and division on every trial's chain —
-        // the screen took 91 us a frame of the evaluation's 118 (profiles/r06/probe_eval_phases_s18.txt).
+        // vectors of VEC (one 16-byte load each; the group's eight loads are one 128-byte line), RUN vectors a lane
+        // loaded before any is used (two runs for k = 600 at 16-bit indices), then its VEC-point fp32 batches
+        // (<= 10 terms each, as the bound requires) added in fp64; the group's sums meet in three DPP steps, eight
+        // trials at once, and the group's lane 0 stores the screened mean and bound. Against one wave a trial —
+        // ten 2-byte index loads a lane waited for once a trial and a 64-lane fp64 reduction and division on every
+        // trial's chain — the screen took 91 us a frame of the evaluation's 118, now 57 (RUN = 5: more spills
+        // VGPRs at the kernel's 96; RUN = 3: 70 us) (profiles/r06/probe_eval_phases_s18.txt,
+        // ab_eval_screen_grouped_s20.txt).
         {
             constexpr int GL = 8, TPW = kWave / GL;     // lanes a trial, trials a wave pass
             constexpr int VEC = 16 / (int)sizeof(IdxT);  // indices a 16-byte load holds
