@@ -228,7 +228,7 @@ struct RansacShared {
     uint32_t* bitmap;                         // set branch: selected indices of the current sample
     uint32_t* pool_list;                      // pool branch: the virtual pool's entries (same words, <= k)
     int k;
-    uint32_t* dummy;                          // claims of rejected draws (one word a lane)
+    uint32_t spread;                          // (a power of two, <= the bitmap's words) - 1: rejected claims' words
     int ablate;                               // DIAGNOSTIC (SVX_RANSAC_ABLATE, diag build)
 };
 
@@ -298,9 +298,10 @@ __device__ __forceinline__ uint32_t rb_temper(uint32_t y) {
 // (word 623 also reads new[0]). Within a level every lane reads all its inputs
 // (up to 4 words a lane) before any lane writes, so no read sees a word of its
 // own level already replaced. Branch-free: a lane's slot past the level's end
-// computes from a clamped word and writes its lane's dummy word instead.
+// computes from the clamped word hi - 1 and stores that word's new value again (the same value its owner stores:
+// no LDS word is spent on a dump).
 template <int LEV>
-__device__ __forceinline__ void rb_twist_level(uint32_t* mt, uint32_t* dummy) {
+__device__ __forceinline__ void rb_twist_level(uint32_t* mt) {
     constexpr uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, A = 0x9908b0dfu;
     constexpr int lo = LEV == 0 ? 0 : LEV == 1 ? 227 : 454;
     constexpr int hi = LEV == 0 ? 227 : LEV == 1 ? 454 : 624;
@@ -319,9 +320,9 @@ __device__ __forceinline__ void rb_twist_level(uint32_t* mt, uint32_t* dummy) {
     rb_wave_lds_sync();   // every read of this level before any write of it
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-        const int kk = lo + lane + 64 * j;
-        uint32_t* dst = (lo + 64 * j + 63 < hi || kk < hi) ? &mt[kk] : &dummy[lane];
-        *dst = nv[j];
+        int kk = lo + lane + 64 * j;
+        if (lo + 64 * j + 63 >= hi) kk = min(kk, hi - 1);
+        mt[kk] = nv[j];
     }
     rb_wave_lds_sync();   // the next level reads this one's words
 }
@@ -350,9 +351,9 @@ struct RbStream {   // wave 0's view of the frame's output stream (uniform)
 template <class IdxT>
 __device__ __forceinline__ void rb_advance(RansacShared<IdxT>& sh, RbStream& st, uint32_t span) {
     while (st.pos + span > st.G) {
-        if (st.lev == 0) rb_twist_level<0>(sh.mt, sh.dummy);
-        else if (st.lev == 1) rb_twist_level<1>(sh.mt, sh.dummy);
-        else rb_twist_level<2>(sh.mt, sh.dummy);
+        if (st.lev == 0) rb_twist_level<0>(sh.mt);
+        else if (st.lev == 1) rb_twist_level<1>(sh.mt);
+        else rb_twist_level<2>(sh.mt);
         st.G += st.lev == 2 ? 170u : 227u;
         st.lev = st.lev == 2 ? 0 : st.lev + 1;
     }
@@ -429,10 +430,11 @@ __device__ void rb_sample_set(RansacShared<IdxT>& sh, RbStream& st, uint32_t n, 
         }
         uint64_t accm[kRBWin];   // the accepted draws of each window (ballot of the compare the claim selects on)
 #pragma unroll
-        for (int w = 0; w < kRBWin; ++w) {   // claims issued in window order; rejected draws or a lane's dummy word
+        for (int w = 0; w < kRBWin; ++w) {   // claims issued in window order; a rejected draw ORs 0 into a word of
+            // the bitmap (spread by lane: no bank conflict), which changes nothing and whose return is not used
             const bool acc = r[w] < n;
             accm[w] = rb_ballot(acc);
-            uint32_t* a = acc ? &sh.bitmap[r[w] >> 5] : &sh.dummy[lane];
+            uint32_t* a = acc ? &sh.bitmap[r[w] >> 5] : &sh.bitmap[lane & sh.spread];
             old[w] = atomicOr(a, acc ? 1u << (r[w] & 31) : 0u);
         }
         // Selections are numbered in stream order from `have`; number q < k is the
@@ -666,7 +668,6 @@ __global__ __launch_bounds__(64 * WPG) void ransac_draw_kernel(const uint32_t* _
     // for the same waves (SVX_DRAW_WPG, diagnostic A/B)
     const int wave = (int)(threadIdx.x >> 6);
     __shared__ uint32_t mt_w[WPG][624];
-    __shared__ uint32_t dummy_w[WPG][64];
     extern __shared__ uint4 rb_dyn4[];   // WPG x [bitmap_words] bitmap / pool list (16-byte aligned, 4-word multiple)
     uint32_t* rb_dyn = reinterpret_cast<uint32_t*>(rb_dyn4) + (size_t)wave * bitmap_words;
     RansacShared<IdxT> sh;
@@ -674,7 +675,7 @@ __global__ __launch_bounds__(64 * WPG) void ransac_draw_kernel(const uint32_t* _
     sh.bitmap = rb_dyn;
     sh.pool_list = rb_dyn;
     sh.k = k;
-    sh.dummy = dummy_w[wave];
+    sh.spread = bitmap_words >= 64 ? 63u : bitmap_words >= 32 ? 31u : bitmap_words >= 16 ? 15u : bitmap_words >= 8 ? 7u : 3u;
     sh.ablate = ablate;
     const int lane = lane_id();
     // one frame a wave, or (the frame loop, gridDim.x < nframes) a wave's frames one after the other: fewer
