@@ -3,10 +3,15 @@ set -o pipefail
 OUT=gpurun_out/${SESSION:-r6sX}; mkdir -p $OUT
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_ransac_batch.py tests/test_gpu_loop.py tests/test_gpu_digests.py > $OUT/pytest_ransac.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_ransac.log; exit 1; }
 tail -1 $OUT/pytest_ransac.log
-PROBE_LOOP_PIPE=1 timeout -k 10 300 python3 -u tools/_probe_pipe_beside_draw.py > $OUT/probe_loop_pipe_beside_draw.txt 2>&1 || exit 1; cat $OUT/probe_loop_pipe_beside_draw.txt
-D=$PWD/stereo.vision_amd/svx/_lib/libsvx_diag.so
-for r in 1 2; do for a in 1 0; do
-  echo "== SVX_RANSAC_BOUND=$a (round $r)" >> $OUT/ab_loop_bound.txt
-  SVX_LIB=$D SVX_RANSAC_BOUND=$a PROBE_BATCHES=18 PROBE_ONLY=caller2 timeout -k 10 200 python3 -u tools/_probe_loop.py >> $OUT/ab_loop_bound.txt 2>&1 || { echo "loop $a failed"; tail $OUT/ab_loop_bound.txt; exit 1; }
+for r in 1 2 3; do for L in stereo.vision_amd/svx/_lib/libsvx_diag.so _ab/libsvx_mpold.so; do
+  echo "== $L (round $r)" >> $OUT/ab_maskpoints.txt
+  SVX_LIB=$PWD/$L timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$r_$(basename $L .so) -o run -- python3 -u tools/prof.py workload --what ransac --frames 4096 --reps 10 >> $OUT/ab_maskpoints.txt 2>&1 || { echo "$L failed"; tail $OUT/ab_maskpoints.txt; exit 1; }
+  python3 - "$OUT/prof_$r_$(basename $L .so)" >> $OUT/ab_maskpoints.txt <<'PY'
+import csv, glob, sys
+f = sorted(glob.glob(f"{sys.argv[1]}/**/run_kernel_stats.csv", recursive=True))[-1]
+for r in csv.DictReader(open(f)):
+    if any(k in r["Name"] for k in ("maskpoints_kernel", "ransac_draw", "ransac_eval")):
+        print(f'  {r["Name"][:50]:52s} {r["Calls"]:>4s} {float(r["AverageNs"]) / 1e3:9.1f} us')
+PY
 done; done
-grep "==\|ms/batch\|batch 1[67]" $OUT/ab_loop_bound.txt
+grep "==\|  " $OUT/ab_maskpoints.txt | grep -v "^\s*$"
